@@ -1,0 +1,97 @@
+/*
+ * hs_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement ("oracle") of the HSLabs control-loop hot path
+ * (pergen -> lik -> FK -> dynrec -> ftsolver -> motor torques), used as the
+ * parity checker for the HIP product path and as the bench's cpu_baseline leg.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may load it.
+ * The product (hslabs_amd/, include/hslabs.h) never links or calls this code.
+ *
+ * Parity status: the reference (ODE + Eigen + rapidxml)
+ * cannot be built in this image, so this restatement is pinned by the
+ * reference's own self-checks restated as known-answer tests (IK round trip
+ * lik.cpp:371-404, rot_ztov check visualization.cpp:24, Euler round trip
+ * pergen.cpp:377-383, rank-loop residual ftsolver.cpp:228-232, static-stance
+ * force balance) and by an independent numpy/scipy formulation in tests/.
+ * Against the reference binary itself: "parity unpinned".
+ */
+#ifndef HS_ORACLE_H
+#define HS_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Gait setup parameters: the fields of pgsconfigparams (pergen.h:137-146),
+ * same meaning as a pgs_config.txt line (player.cpp:170-208). */
+typedef struct {
+  double torso_pos[3];
+  double torso_angles[3];
+  double step_duration;
+  double period, step_length, step_height;
+  double curvature;
+  double foot_shift;       /* value of lateral/radial foot shift */
+  int32_t foot_shift_type; /* -1 none, 0 lateral, 1 radial (pergen.h:143) */
+  int32_t reserved;
+} hso_gait;
+
+/* null-space basis modes */
+enum { HSO_BASIS_ORTHO = 0, /* reference-faithful: orthonormal Q of QR(B^T) (ftsolver.cpp:187-202) */
+       HSO_BASIS_TREE = 1   /* tree-built basis [-B0^-1 Bc; I] (same basis the HIP kernel uses) */ };
+
+/* flag bits per step (also used by the product, see include/hslabs.h) */
+#define HSO_FLAG_RANK_RETRY   1u  /* adaptive-rank loop ran more than once (ftsolver.cpp:279-303) */
+#define HSO_FLAG_FULL_RANK    2u  /* zeroth-order Gram full rank: reference would assert in comma init */
+#define HSO_FLAG_LOOP_EXHAUST 4u  /* rank loop reached rank 0 without converging */
+#define HSO_FLAG_NAN          8u  /* NaN in torques / contact forces */
+#define HSO_FLAG_UNREACH     16u  /* an IK target was clamped (ignore_reach, lik.cpp:250-253) */
+#define HSO_FLAG_NO_CONTACT  32u  /* k == 0 */
+
+typedef struct hso_model hso_model;
+
+int hso_model_load(const char* xml_path, hso_model** out);
+void hso_model_free(hso_model* m);
+/* n_parts, nmj, nfeet, config_dim, lik variant, n_limbs */
+void hso_model_dims(const hso_model* m, int* dims6);
+
+/*
+ * One rollout, processing steps k = k0 .. k0+H-1, i.e. trajectory samples
+ * i = k+2 (periodic.cpp:377-391 uses i in [2, n_t+2) with k0=0, H=n_t).
+ * Outputs (any pointer may be NULL):
+ *   q    [(k0+H+4) x config_dim]  trajectory records (periodic.cpp:166-185)
+ *   tau  [H x nmj]                motor torques (periodic.cpp:328-343)
+ *   cf   [H x 3*nfeet]            contact forces z (ftsolver.cpp:163)
+ *   x    [H x 6n]                 joint force/torque vector (ftsolver.cpp:166)
+ *   flags[H]
+ *   work_cot[2]                   positive work over the processed steps and
+ *                                 work/(sum m * step_length) (player.cpp:269-285)
+ *   diag [H x 4]                  k, final rank0, loop iterations, rel_error
+ * ignore_reach: lik.cpp:142 global (main.cpp:41 sets it).
+ */
+int hso_rollout(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, int basis,
+                int ignore_reach, double* q, double* tau, double* cf, double* x,
+                uint32_t* flags, double* work_cot, double* diag);
+
+/* Batched CPU baseline: B rollouts (params[B]), same k0/H for all, tree basis,
+ * n_threads std::threads over rollouts. Outputs tau[B][H][nmj], cf[B][H][3nf],
+ * work_cot[B][2]. Returns 0 on success. */
+int hso_batch(const hso_model* m, const hso_gait* params, int B, int n_t, int k0, int H,
+              int basis, int ignore_reach, int n_threads, double* tau, double* cf,
+              double* work_cot, uint32_t* flags);
+
+/* Known-answer helpers (restated reference self-checks). */
+/* lik.cpp:371-404: bend_solver o limb_solver round trip; returns max error over n tries */
+double hso_lik_roundtrip(const hso_model* m, int n, uint64_t seed);
+/* visualization.cpp:62-101: affine_from_orientation o euler_angles_from_affine */
+void hso_euler_roundtrip(const double* angles3, double* out3);
+/* rot_ztov (visualization.cpp:11-25): R (affine column-major 3x3 part, 9 doubles) */
+void hso_rot_ztov(const double* v3, double* R9);
+/* FK after IK: foot positions vs pergen targets for record at time t; out: max |err| */
+double hso_fk_ik_check(const hso_model* m, const hso_gait* g, double t, int ignore_reach);
+/* static residual checks for one step: |B0 x0 - f|, |[B0 Bc] N| (both bases) */
+int hso_residuals(const hso_model* m, const hso_gait* g, int n_t, int step, int basis, double* out2);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,252 @@
+"""ctypes wrapper around the oracle (TEST INFRASTRUCTURE ONLY).
+
+The oracle is the CPU restatement of the HSLabs hot path (see hs_oracle.h for
+what it restates and how parity is pinned). Only tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg may import this module; the product package
+``hslabs_amd`` never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass, field
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libhs_oracle.so")
+
+BASIS_ORTHO = 0
+BASIS_TREE = 1
+
+FLAG_RANK_RETRY = 1
+FLAG_FULL_RANK = 2
+FLAG_LOOP_EXHAUST = 4
+FLAG_NAN = 8
+FLAG_UNREACH = 16
+FLAG_NO_CONTACT = 32
+
+
+class Gait(ctypes.Structure):
+    """pgsconfigparams (pergen.h:137-146)."""
+
+    _fields_ = [
+        ("torso_pos", ctypes.c_double * 3),
+        ("torso_angles", ctypes.c_double * 3),
+        ("step_duration", ctypes.c_double),
+        ("period", ctypes.c_double),
+        ("step_length", ctypes.c_double),
+        ("step_height", ctypes.c_double),
+        ("curvature", ctypes.c_double),
+        ("foot_shift", ctypes.c_double),
+        ("foot_shift_type", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+@dataclass
+class GaitParams:
+    xml_file: str = "hexapod.xml"
+    torso_pos: tuple = (0.0, 0.0, 0.0)
+    torso_angles: tuple = (0.0, 0.0, 0.0)
+    step_duration: float = 1.0
+    period: float = 3.0
+    step_length: float = 0.5
+    step_height: float = 0.1
+    curvature: float = 0.0
+    foot_shift_type: int = -1
+    foot_shift: float = 0.0
+
+    def to_c(self) -> Gait:
+        g = Gait()
+        for i in range(3):
+            g.torso_pos[i] = self.torso_pos[i]
+            g.torso_angles[i] = self.torso_angles[i]
+        g.step_duration = self.step_duration
+        g.period = self.period
+        g.step_length = self.step_length
+        g.step_height = self.step_height
+        g.curvature = self.curvature
+        g.foot_shift = self.foot_shift
+        g.foot_shift_type = self.foot_shift_type
+        return g
+
+
+def parse_pgs_line(rest: str) -> GaitParams:
+    """modelplayer::get_pgs_config_params (player.cpp:170-208)."""
+    toks = rest.split()
+    p = GaitParams()
+    i = 0
+    while i < len(toks):
+        key = toks[i]
+        i += 1
+        if key == "xml_file":
+            p.xml_file = toks[i]; i += 1
+        elif key == "torso_pos":
+            p.torso_pos = tuple(float(t) for t in toks[i:i + 3]); i += 3
+        elif key == "torso_angles":
+            p.torso_angles = tuple(float(t) for t in toks[i:i + 3]); i += 3
+        elif key == "step_duration":
+            p.step_duration = float(toks[i]); i += 1
+        elif key == "period":
+            p.period = float(toks[i]); i += 1
+        elif key == "step_length":
+            p.step_length = float(toks[i]); i += 1
+        elif key == "step_height":
+            p.step_height = float(toks[i]); i += 1
+        elif key == "curvature":
+            p.curvature = float(toks[i]); i += 1
+        elif key == "lateral_foot_shift":
+            p.foot_shift_type, p.foot_shift = 0, float(toks[i]); i += 1
+        elif key == "radial_foot_shift":
+            p.foot_shift_type, p.foot_shift = 1, float(toks[i]); i += 1
+        else:
+            raise ValueError(f"unknown key {key}")
+    return p
+
+
+def load_pgs_config(path: str, setup_id: int) -> GaitParams:
+    """modelplayer::get_rec_str (player.cpp:230-244) + get_pgs_config_params."""
+    with open(path) as f:
+        for line in f:
+            parts = line.split(None, 1)
+            if parts and parts[0].lstrip("-").isdigit() and int(parts[0]) == setup_id:
+                return parse_pgs_line(parts[1] if len(parts) > 1 else "")
+    raise KeyError(f"no string with rec_id = {setup_id}")
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        dp = ctypes.POINTER(ctypes.c_double)
+        L.hso_model_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+        L.hso_model_free.argtypes = [ctypes.c_void_p]
+        L.hso_model_dims.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        L.hso_rollout.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, dp, dp, dp, dp,
+                                  ctypes.POINTER(ctypes.c_uint32), dp, dp]
+        L.hso_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, dp,
+                                ctypes.POINTER(ctypes.c_uint32)]
+        L.hso_lik_roundtrip.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]
+        L.hso_lik_roundtrip.restype = ctypes.c_double
+        L.hso_euler_roundtrip.argtypes = [dp, dp]
+        L.hso_rot_ztov.argtypes = [dp, dp]
+        L.hso_fk_ik_check.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_double, ctypes.c_int]
+        L.hso_fk_ik_check.restype = ctypes.c_double
+        L.hso_residuals.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, dp]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+@dataclass
+class Model:
+    path: str
+    handle: ctypes.c_void_p = field(default=None)
+    n: int = 0
+    nmj: int = 0
+    nf: int = 0
+    cfg: int = 0
+    lik_index: int = -1
+    n_limbs: int = 0
+
+    def __post_init__(self):
+        h = ctypes.c_void_p()
+        rc = lib().hso_model_load(self.path.encode(), ctypes.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"oracle: cannot load {self.path} (rc={rc})")
+        self.handle = h
+        d = (ctypes.c_int * 6)()
+        lib().hso_model_dims(h, d)
+        self.n, self.nmj, self.nf, self.cfg, self.lik_index, self.n_limbs = list(d)
+
+    def __del__(self):
+        try:
+            if self.handle:
+                lib().hso_model_free(self.handle)
+        except Exception:
+            pass
+
+
+def rollout(model: Model, gait: GaitParams, n_t: int = 20, k0: int = 0, H: int | None = None,
+            basis: int = BASIS_ORTHO, ignore_reach: bool = True) -> dict:
+    """One rollout through the oracle: returns q, tau, cf, x, flags, work, cot, diag."""
+    if H is None:
+        H = n_t
+    ns = k0 + H + 4
+    q = np.zeros((ns, model.cfg))
+    tau = np.zeros((H, model.nmj))
+    cf = np.zeros((H, 3 * model.nf))
+    x = np.zeros((H, 6 * model.n))
+    flags = np.zeros(H, dtype=np.uint32)
+    wc = np.zeros(2)
+    diag = np.zeros((H, 4))
+    g = gait.to_c()
+    rc = lib().hso_rollout(model.handle, ctypes.byref(g), n_t, k0, H, basis, int(ignore_reach),
+                           _ptr(q), _ptr(tau), _ptr(cf), _ptr(x),
+                           flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), _ptr(wc), _ptr(diag))
+    if rc != 0:
+        raise RuntimeError(f"oracle rollout failed rc={rc}")
+    return dict(q=q, tau=tau, cf=cf, x=x, flags=flags, work=wc[0], cot=wc[1], diag=diag)
+
+
+def batch(model: Model, gaits: list, n_t: int, k0: int, H: int, basis: int = BASIS_TREE,
+          ignore_reach: bool = True, n_threads: int = 1) -> dict:
+    B = len(gaits)
+    arr = (Gait * B)(*[g.to_c() for g in gaits])
+    tau = np.zeros((B, H, model.nmj))
+    cf = np.zeros((B, H, 3 * model.nf))
+    wc = np.zeros((B, 2))
+    flags = np.zeros((B, H), dtype=np.uint32)
+    rc = lib().hso_batch(model.handle, arr, B, n_t, k0, H, basis, int(ignore_reach), n_threads,
+                         _ptr(tau), _ptr(cf), _ptr(wc), flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    if rc != 0:
+        raise RuntimeError(f"oracle batch failed rc={rc}")
+    return dict(tau=tau, cf=cf, work=wc[:, 0], cot=wc[:, 1], flags=flags)
+
+
+def lik_roundtrip(model: Model, n: int = 1000, seed: int = 1) -> float:
+    return lib().hso_lik_roundtrip(model.handle, n, seed)
+
+
+def euler_roundtrip(angles) -> np.ndarray:
+    a = np.ascontiguousarray(angles, dtype=np.float64)
+    out = np.zeros(3)
+    lib().hso_euler_roundtrip(_ptr(a), _ptr(out))
+    return out
+
+
+def rot_ztov(v) -> np.ndarray:
+    a = np.ascontiguousarray(v, dtype=np.float64)
+    out = np.zeros(9)
+    lib().hso_rot_ztov(_ptr(a), _ptr(out))
+    return out.reshape(3, 3).T  # stored column-major
+
+
+def fk_ik_check(model: Model, gait: GaitParams, t: float, ignore_reach: bool = True) -> float:
+    g = gait.to_c()
+    return lib().hso_fk_ik_check(model.handle, ctypes.byref(g), t, int(ignore_reach))
+
+
+def residuals(model: Model, gait: GaitParams, n_t: int, step: int, basis: int):
+    g = gait.to_c()
+    out = np.zeros(2)
+    k = lib().hso_residuals(model.handle, ctypes.byref(g), n_t, step, basis, _ptr(out))
+    return k, out[0], out[1]
