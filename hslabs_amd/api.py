@@ -1,0 +1,274 @@
+"""Python host mirror of the reference's interface for the hot path.
+
+Names follow the reference classes so caller code reads the same:
+``KinematicModel`` (kinematicmodel, model.h:96-137), ``PgsConfigParams``
+(pgsconfigparams, pergen.h:137-146), ``Periodic`` (periodic, periodic.h:27-87),
+``ModelPlayer.measure_cot`` / ``measure_cot_sweep`` (player.cpp:269-321).
+Everything runs through the C ABI (include/hslabs.h) on the GPU; there is no
+CPU fallback. Errors raise ``HSError`` instead of exit(1).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import capi
+
+# numpy view of hs_gait_params (128 bytes)
+GAIT_DTYPE = np.dtype([
+    ("torso_pos", "<f8", (3,)), ("torso_angles", "<f8", (3,)), ("step_duration", "<f8"),
+    ("period", "<f8"), ("step_length", "<f8"), ("step_height", "<f8"), ("curvature", "<f8"),
+    ("foot_shift", "<f8"), ("foot_shift_type", "<i4"), ("reserved0", "<i4"), ("reserved", "<f8", (3,)),
+])
+assert GAIT_DTYPE.itemsize == 128
+
+SWEEP_NAMES = ("step_duration", "period", "step_length", "step_height")  # pergen.cpp:423
+
+
+@dataclass
+class PgsConfigParams:
+    """pgsconfigparams (pergen.h:137-146)."""
+
+    fname: str = ""
+    torso_pos: tuple = (0.0, 0.0, 0.0)
+    torso_angles: tuple = (0.0, 0.0, 0.0)
+    step_duration: float = 1.0
+    period: float = 3.0
+    step_length: float = 0.5
+    step_height: float = 0.1
+    curvature: float = 0.0
+    foot_shift: tuple = (-1, 0.0)  # (type, value): -1 none, 0 lateral, 1 radial
+
+    def to_record(self) -> np.ndarray:
+        r = np.zeros((), GAIT_DTYPE)
+        r["torso_pos"] = self.torso_pos
+        r["torso_angles"] = self.torso_angles
+        r["step_duration"] = self.step_duration
+        r["period"] = self.period
+        r["step_length"] = self.step_length
+        r["step_height"] = self.step_height
+        r["curvature"] = self.curvature
+        r["foot_shift_type"] = self.foot_shift[0]
+        r["foot_shift"] = self.foot_shift[1]
+        return r
+
+    @staticmethod
+    def from_record(r) -> "PgsConfigParams":
+        return PgsConfigParams(
+            torso_pos=tuple(float(v) for v in r["torso_pos"]),
+            torso_angles=tuple(float(v) for v in r["torso_angles"]),
+            step_duration=float(r["step_duration"]), period=float(r["period"]),
+            step_length=float(r["step_length"]), step_height=float(r["step_height"]),
+            curvature=float(r["curvature"]), foot_shift=(int(r["foot_shift_type"]), float(r["foot_shift"])))
+
+
+def read_pgs_config(path: str, setup_id: int) -> PgsConfigParams:
+    """modelplayer::get_rec_str + get_pgs_config_params (player.cpp:170-244)."""
+    L = capi.load()
+    c = capi.GaitParamsC()
+    buf = ctypes.create_string_buffer(256)
+    capi.check(L.hs_pgs_config_read(path.encode(), setup_id, ctypes.byref(c), buf, 256), "hs_pgs_config_read")
+    rec = np.frombuffer(bytes(c), dtype=GAIT_DTYPE)[0]
+    p = PgsConfigParams.from_record(rec)
+    p.fname = buf.value.decode()
+    return p
+
+
+@dataclass
+class KinematicModel:
+    """kinematicmodel (model.h:96-137) backed by hs_model_t."""
+
+    xml_path: str
+    lik_variant: int = -1
+    handle: ctypes.c_void_p = field(default=None, repr=False)
+
+    def __post_init__(self):
+        L = capi.load()
+        h = ctypes.c_void_p()
+        capi.check(L.hs_model_load_ex(self.xml_path.encode(), self.lik_variant, ctypes.byref(h)),
+                   f"hs_model_load({self.xml_path})")
+        self.handle = h
+        d = capi.ModelDimsC()
+        capi.check(L.hs_model_get_dims(h, ctypes.byref(d)), "hs_model_get_dims")
+        self.n_parts, self.nmj, self.nfeet = d.n_parts, d.nmj, d.nfeet
+        self.config_dim, self.n_limbs, self.lik_kind = d.config_dim, d.n_limbs, d.lik_kind
+        self.total_mass, self.rcap = d.total_mass, d.rcap
+
+    def get_config_dim(self) -> int:
+        return self.config_dim
+
+    def number_of_motor_joints(self) -> int:
+        return self.nmj
+
+    def __del__(self):
+        try:
+            if self.handle:
+                capi.load().hs_model_free(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+def params_array(params) -> np.ndarray:
+    """list[PgsConfigParams] | structured array -> contiguous GAIT_DTYPE array."""
+    if isinstance(params, np.ndarray) and params.dtype == GAIT_DTYPE:
+        return np.ascontiguousarray(params)
+    arr = np.zeros(len(params), GAIT_DTYPE)
+    for i, p in enumerate(params):
+        arr[i] = p.to_record()
+    return arr
+
+
+def run_host(model: KinematicModel, params, n_t: int = 20, k0: int = 0, horizon: int | None = None,
+             ignore_reach: bool = True, want=("q", "tau", "cf", "x", "flags", "work_cot")) -> dict:
+    """Synchronous host-buffer run of the batched path (hs_run_host)."""
+    arr = params_array(params)
+    B = len(arr)
+    H = n_t if horizon is None else horizon
+    out = {
+        "q": np.zeros((B, H, model.config_dim)) if "q" in want else None,
+        "tau": np.zeros((B, H, model.nmj)) if "tau" in want else None,
+        "cf": np.zeros((B, H, 3 * model.nfeet)) if "cf" in want else None,
+        "x": np.zeros((B, H, 6 * model.n_parts)) if "x" in want else None,
+        "flags": np.zeros((B, H), np.uint32) if "flags" in want else None,
+        "work_cot": np.zeros((B, 2)) if "work_cot" in want else None,
+    }
+    dp = ctypes.POINTER(ctypes.c_double)
+
+    def P(a, t=dp):
+        return None if a is None else a.ctypes.data_as(t)
+
+    L = capi.load()
+    rc = L.hs_run_host(model.handle, arr.ctypes.data_as(ctypes.POINTER(capi.GaitParamsC)), B, n_t, k0, H,
+                       int(ignore_reach), P(out["q"]), P(out["tau"]), P(out["cf"]), P(out["x"]),
+                       P(out["flags"], ctypes.POINTER(ctypes.c_uint32)), P(out["work_cot"]))
+    capi.check(rc, "hs_run_host")
+    return out
+
+
+class DeviceBatch:
+    """Device-resident batch (torch tensors on the current HIP device) for hs_run.
+
+    The gait parameter records and every output buffer live in HBM; ``run``
+    only enqueues the kernel on the current torch stream.
+    """
+
+    def __init__(self, model: KinematicModel, params, n_t: int = 20, k0: int = 0, horizon: int = 1,
+                 ignore_reach: bool = True, outputs=("tau", "cf", "work_cot", "flags"), device=None,
+                 rollout_id_base: int = 0):
+        import torch
+
+        self.torch = torch
+        self.model = model
+        arr = params_array(params)
+        self.B, self.H, self.n_t, self.k0 = len(arr), horizon, n_t, k0
+        self.ignore_reach = ignore_reach
+        self.rollout_id_base = rollout_id_base
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        self.params = torch.from_numpy(arr.view(np.uint8).copy()).to(dev)
+        f64 = dict(dtype=torch.float64, device=dev)
+        B, H = self.B, self.H
+        self.q = torch.empty((B, H, model.config_dim), **f64) if "q" in outputs else None
+        self.tau = torch.empty((B, H, model.nmj), **f64) if "tau" in outputs else None
+        self.cf = torch.empty((B, H, 3 * model.nfeet), **f64) if "cf" in outputs else None
+        self.x = torch.empty((B, H, 6 * model.n_parts), **f64) if "x" in outputs else None
+        self.flags = torch.empty((B, H), dtype=torch.int32, device=dev) if "flags" in outputs else None
+        self.work_cot = torch.empty((B, 2), **f64) if "work_cot" in outputs else None
+        self.best_key = torch.full((1,), -1, dtype=torch.int64, device=dev)  # UINT64_MAX bit pattern
+
+    def reset_best(self):
+        self.best_key.fill_(-1)
+
+    def run(self, stream=None, best: bool = True) -> None:
+        torch = self.torch
+        a = capi.RunArgsC()
+        a.n_rollouts, a.horizon, a.k0, a.n_t = self.B, self.H, self.k0, self.n_t
+        a.ignore_reach = int(self.ignore_reach)
+
+        def ptr(t):
+            return None if t is None else t.data_ptr()
+
+        a.params = ptr(self.params)
+        a.q, a.tau, a.cf, a.x = ptr(self.q), ptr(self.tau), ptr(self.cf), ptr(self.x)
+        a.flags, a.work_cot = ptr(self.flags), ptr(self.work_cot)
+        a.best_key = ptr(self.best_key) if best else None
+        a.rollout_id_base = self.rollout_id_base
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        a.stream = st.cuda_stream
+        capi.check(capi.load().hs_run(self.model.handle, ctypes.byref(a)), "hs_run")
+
+
+def decode_best_key(key: int):
+    """-> (cot as float32, global rollout id)"""
+    L = capi.load()
+    c = ctypes.c_float()
+    i = ctypes.c_int64()
+    L.hs_best_key_decode(ctypes.c_uint64(key & 0xFFFFFFFFFFFFFFFF), ctypes.byref(c), ctypes.byref(i))
+    return c.value, i.value
+
+
+class Periodic:
+    """periodic (periodic.h:27-87) for one gait setup, computed on the GPU."""
+
+    def __init__(self, model: KinematicModel):
+        self.model = model
+        self.n_t = 0
+        self._res = None
+
+    def record_trajectory(self, pgs: PgsConfigParams, n_t: int) -> None:  # periodic.cpp:77-96
+        self.pgs, self.n_t = pgs, n_t
+        self._res = None
+
+    def compute_torques_over_period(self) -> None:  # periodic.cpp:377-391
+        self._res = run_host(self.model, [self.pgs], n_t=self.n_t, k0=0, horizon=self.n_t)
+
+    def _ensure(self):
+        if self._res is None:
+            self.compute_torques_over_period()
+        return self._res
+
+    def get_computed_torques(self, i: int) -> np.ndarray:  # periodic.h:51 (computed_torques[i % n_t])
+        # step h solves sample h+2, stored by the reference at (h+2) % n_t
+        h = (i - 2) % self.n_t
+        return self._ensure()["tau"][0, h]
+
+    def work_over_period(self) -> float:  # periodic.cpp:285-307
+        return float(self._ensure()["work_cot"][0, 0])
+
+    def get_total_mass(self) -> float:
+        return self.model.total_mass
+
+
+class ModelPlayer:
+    """The hot-path-facing part of modelplayer (player.cpp:259-321)."""
+
+    def __init__(self, model: KinematicModel):
+        self.model = model
+
+    def measure_cot(self, pgs: PgsConfigParams, n_t: int) -> float:  # player.cpp:269-285
+        r = run_host(self.model, [pgs], n_t=n_t, k0=0, horizon=n_t, want=("work_cot",))
+        return float(r["work_cot"][0, 1])
+
+    @staticmethod
+    def sweep_params(pgs: PgsConfigParams, param_name: str, val0: float, val1: float, n_val: int):
+        """pgssweeper::sweep/next (pergen.cpp:417-449): n_val+1 values."""
+        if param_name not in SWEEP_NAMES:
+            raise capi.HSError(f"cannot sweep over {param_name}")
+        delval = (val1 - val0) / n_val
+        out = []
+        for vali in range(n_val + 1):
+            val = val0 + vali * delval
+            p = PgsConfigParams(**{k: getattr(pgs, k) for k in pgs.__dataclass_fields__})
+            setattr(p, param_name, val)
+            out.append((val, p))
+        return out
+
+    def measure_cot_sweep(self, pgs: PgsConfigParams, n_t: int, param_name: str, val0: float, val1: float,
+                          n_val: int):
+        """All sweep values in one batched launch; returns [(val, cot)] (player.cpp:311-321)."""
+        sw = self.sweep_params(pgs, param_name, val0, val1, n_val)
+        r = run_host(self.model, [p for _, p in sw], n_t=n_t, k0=0, horizon=n_t, want=("work_cot",))
+        return [(v, float(r["work_cot"][i, 1])) for i, (v, _) in enumerate(sw)]

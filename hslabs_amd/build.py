@@ -1,0 +1,54 @@
+"""Build the gfx950 shared library libhslabs.so in-tree (hslabs_amd/_build/).
+
+Only hipcc is needed (no cmake/ninja). Kernels are compiled with
+-ffp-contract=off: the reference's x86-64 ``g++ -O2`` build never fuses a*b+c,
+and keeping that rounding lets the device path match the CPU restatement to
+the last bit wherever no transcendental function is involved.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc")
+OUT_DIR = os.path.join(HERE, "_build")
+LIB = os.path.join(OUT_DIR, "libhslabs.so")
+SOURCES = ["hs_kernels.hip", "hs_capi.cpp", "hs_model.cpp"]
+HEADERS = ["hs_topo.h", "hs_math.h", "hs_internal.h", os.path.join("..", "..", "include", "hslabs.h")]
+ARCH = os.environ.get("HSLABS_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm 7.x required)")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(SRC, f) for f in SOURCES + HEADERS]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    os.makedirs(OUT_DIR, exist_ok=True)
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-ffp-contract=off", "-Wall", "-Wno-unused-function",
+           *[os.path.join(SRC, s) for s in SOURCES], "-o", LIB + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

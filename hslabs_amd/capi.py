@@ -1,0 +1,122 @@
+"""ctypes binding of include/hslabs.h (the C-ABI boundary).
+
+This module is the Python mirror of the reference-side binding a maintainer
+would write. It never falls back to a CPU path: if the
+in-tree gfx950 library is missing, loading fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from . import build as _build
+
+ABI_VERSION = 1
+
+HS_OK = 0
+HS_FLAG_RANK_RETRY = 1
+HS_FLAG_FULL_RANK = 2
+HS_FLAG_LOOP_EXHAUST = 4
+HS_FLAG_NAN = 8
+HS_FLAG_UNREACH = 16
+HS_FLAG_NO_CONTACT = 32
+
+# every symbol declared in include/hslabs.h
+EXPORTS = [
+    "hs_model_load", "hs_model_load_ex", "hs_model_free", "hs_model_get_dims", "hs_pgs_config_read",
+    "hs_run", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
+]
+
+
+class GaitParamsC(ctypes.Structure):
+    """hs_gait_params (128 bytes)."""
+
+    _fields_ = [
+        ("torso_pos", ctypes.c_double * 3),
+        ("torso_angles", ctypes.c_double * 3),
+        ("step_duration", ctypes.c_double),
+        ("period", ctypes.c_double),
+        ("step_length", ctypes.c_double),
+        ("step_height", ctypes.c_double),
+        ("curvature", ctypes.c_double),
+        ("foot_shift", ctypes.c_double),
+        ("foot_shift_type", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("reserved", ctypes.c_double * 3),
+    ]
+
+
+assert ctypes.sizeof(GaitParamsC) == 128
+
+
+class ModelDimsC(ctypes.Structure):
+    _fields_ = [
+        ("n_parts", ctypes.c_int32), ("nmj", ctypes.c_int32), ("nfeet", ctypes.c_int32),
+        ("config_dim", ctypes.c_int32), ("n_limbs", ctypes.c_int32), ("lik_kind", ctypes.c_int32),
+        ("total_mass", ctypes.c_double), ("rcap", ctypes.c_double),
+    ]
+
+
+class RunArgsC(ctypes.Structure):
+    _fields_ = [
+        ("n_rollouts", ctypes.c_int32), ("horizon", ctypes.c_int32), ("k0", ctypes.c_int32),
+        ("n_t", ctypes.c_int32), ("ignore_reach", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+        ("params", ctypes.c_void_p), ("q", ctypes.c_void_p), ("tau", ctypes.c_void_p),
+        ("cf", ctypes.c_void_p), ("x", ctypes.c_void_p), ("flags", ctypes.c_void_p),
+        ("work_cot", ctypes.c_void_p), ("best_key", ctypes.c_void_p),
+        ("rollout_id_base", ctypes.c_int64), ("stream", ctypes.c_void_p),
+    ]
+
+
+class HSError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def load(build_if_missing: bool = True) -> ctypes.CDLL:
+    """Load the in-tree libhslabs.so (building it first if allowed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.LIB
+    if not os.path.exists(path):
+        if not build_if_missing:
+            raise HSError(f"libhslabs.so not built ({path}); run `python -m hslabs_amd.build`")
+        _build.build()
+    L = ctypes.CDLL(path)
+    dp = ctypes.POINTER(ctypes.c_double)
+    vp = ctypes.c_void_p
+    L.hs_model_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
+    L.hs_model_load_ex.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(vp)]
+    L.hs_model_free.argtypes = [vp]
+    L.hs_model_free.restype = None
+    L.hs_model_get_dims.argtypes = [vp, ctypes.POINTER(ModelDimsC)]
+    L.hs_pgs_config_read.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(GaitParamsC),
+                                     ctypes.c_char_p, ctypes.c_int32]
+    L.hs_run.argtypes = [vp, ctypes.POINTER(RunArgsC)]
+    L.hs_run_host.argtypes = [vp, ctypes.POINTER(GaitParamsC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                              ctypes.c_int32, ctypes.c_int32, dp, dp, dp, dp, ctypes.POINTER(ctypes.c_uint32), dp]
+    L.hs_best_key_encode.argtypes = [ctypes.c_double, ctypes.c_int64]
+    L.hs_best_key_encode.restype = ctypes.c_uint64
+    L.hs_best_key_decode.argtypes = [ctypes.c_uint64, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64)]
+    L.hs_best_key_decode.restype = None
+    L.hs_last_error.argtypes = []
+    L.hs_last_error.restype = ctypes.c_char_p
+    L.hs_abi_version.argtypes = []
+    L.hs_abi_version.restype = ctypes.c_int
+    if L.hs_abi_version() != ABI_VERSION:
+        raise HSError("libhslabs ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != HS_OK:
+        msg = load().hs_last_error().decode(errors="replace")
+        raise HSError(f"{what}: {msg} (rc={rc})")

@@ -1,0 +1,213 @@
+// hs_capi.cpp -- implementation of include/hslabs.h (host side, HIP runtime).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "hs_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return HS_E_DEVICE;
+}
+
+std::mutex g_dev_mu;
+
+// Device copy of the topology for the current device (created once per device).
+int device_topo(hs_model_t m, const hs_topo** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  if (dev < 0 || dev >= 64) return fail(HS_E_DEVICE, "device index out of range");
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  if (!m->dev[dev]) {
+    hs_topo* d = nullptr;
+    e = hipMalloc(&d, sizeof(hs_topo));
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(topo)");
+    e = hipMemcpy(d, &m->host, sizeof(hs_topo), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { (void)hipFree(d); return hip_fail(e, "hipMemcpy(topo)"); }
+    m->dev[dev] = d;
+  }
+  *out = m->dev[dev];
+  return HS_OK;
+}
+
+int check_args(const hs_model_s* m, const hs_run_args* a) {
+  if (!m || !a) return fail(HS_E_ARG, "null model or args");
+  if (a->n_rollouts < 0) return fail(HS_E_ARG, "n_rollouts < 0");
+  if (a->horizon < 1) return fail(HS_E_ARG, "horizon must be >= 1");
+  if (a->k0 < 0) return fail(HS_E_ARG, "k0 must be >= 0");
+  if (a->n_t < 1) return fail(HS_E_ARG, "n_t must be >= 1");
+  if (a->n_rollouts > 0 && !a->params) return fail(HS_E_ARG, "params is null");
+  if (a->n_rollouts > (1 << 30)) return fail(HS_E_ARG, "too many rollouts");
+  return HS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hs_abi_version(void) { return HSLABS_ABI_VERSION; }
+
+const char* hs_last_error(void) { return g_err.c_str(); }
+
+int hs_model_load_ex(const char* xml_path, int lik_variant, hs_model_t* out) {
+  if (!xml_path || !out) return fail(HS_E_ARG, "null argument");
+  hs_model_s* m = new hs_model_s;
+  memset(m->dev, 0, sizeof(m->dev));
+  std::string err;
+  int rc = hs::load_model_file(xml_path, lik_variant, &m->host, err);
+  if (rc != HS_OK) {
+    delete m;
+    return fail(rc, err);
+  }
+  *out = m;
+  return HS_OK;
+}
+
+int hs_model_load(const char* xml_path, hs_model_t* out) { return hs_model_load_ex(xml_path, -1, out); }
+
+void hs_model_free(hs_model_t m) {
+  if (!m) return;
+  for (int d = 0; d < 64; d++)
+    if (m->dev[d]) {
+      int cur = 0;
+      if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(d) == hipSuccess) {
+        (void)hipFree(m->dev[d]);
+        (void)hipSetDevice(cur);
+      }
+    }
+  delete m;
+}
+
+int hs_model_get_dims(hs_model_t m, hs_model_dims* o) {
+  if (!m || !o) return fail(HS_E_ARG, "null argument");
+  const hs_topo& t = m->host;
+  o->n_parts = t.n;
+  o->nmj = t.nmj;
+  o->nfeet = t.nf;
+  o->config_dim = t.cfg;
+  o->n_limbs = t.n_limbs;
+  o->lik_kind = t.lik_kind;
+  o->total_mass = t.total_mass;
+  o->rcap = t.rcap;
+  return HS_OK;
+}
+
+int hs_pgs_config_read(const char* path, int setup_id, hs_gait_params* out, char* xml_file, int32_t xml_file_len) {
+  if (!path || !out) return fail(HS_E_ARG, "null argument");
+  std::string xml, err;
+  int rc = hs::read_pgs_config(path, setup_id, out, xml, err);
+  if (rc != HS_OK) return fail(rc, err);
+  if (xml_file && xml_file_len > 0) {
+    snprintf(xml_file, (size_t)xml_file_len, "%s", xml.c_str());
+  }
+  return HS_OK;
+}
+
+int hs_run(hs_model_t m, const hs_run_args* a) {
+  int rc = check_args(m, a);
+  if (rc != HS_OK) return rc;
+  if (a->n_rollouts == 0) return HS_OK;
+  const hs_topo* d = nullptr;
+  rc = device_topo(m, &d);
+  if (rc != HS_OK) return rc;
+  int e = hs::launch_rollouts(d, m->host, *a);
+  if (e != 0) return hip_fail((hipError_t)e, "kernel launch");
+  return HS_OK;
+}
+
+int hs_run_host(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n_t, int32_t k0, int32_t H,
+                int32_t ignore_reach, double* q, double* tau, double* cf, double* x, uint32_t* flags,
+                double* work_cot) {
+  if (!m || (B > 0 && !params)) return fail(HS_E_ARG, "null argument");
+  if (B <= 0 || H <= 0) return fail(HS_E_ARG, "empty batch");
+  const hs_topo& t = m->host;
+  size_t nq = (size_t)B * H * t.cfg, ntau = (size_t)B * H * t.nmj, ncf = (size_t)B * H * 3 * t.nf;
+  size_t nx = (size_t)B * H * 6 * t.n, nfl = (size_t)B * H, nwc = (size_t)B * 2;
+  hs_gait_params* dp = nullptr;
+  double *dq = nullptr, *dtau = nullptr, *dcf = nullptr, *dx = nullptr, *dwc = nullptr;
+  uint32_t* dfl = nullptr;
+  hipError_t e = hipSuccess;
+  int rc = HS_OK;
+#define HS_ALLOC(ptr, n, T)                                   \
+  if (e == hipSuccess) e = hipMalloc(&ptr, (n) * sizeof(T));
+  HS_ALLOC(dp, (size_t)B, hs_gait_params);
+  if (q) HS_ALLOC(dq, nq, double);
+  if (tau) HS_ALLOC(dtau, ntau, double);
+  if (cf) HS_ALLOC(dcf, ncf, double);
+  if (x) HS_ALLOC(dx, nx, double);
+  if (flags) HS_ALLOC(dfl, nfl, uint32_t);
+  if (work_cot) HS_ALLOC(dwc, nwc, double);
+#undef HS_ALLOC
+  if (e == hipSuccess) e = hipMemcpy(dp, params, (size_t)B * sizeof(hs_gait_params), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    rc = hip_fail(e, "alloc/copy");
+  } else {
+    hs_run_args a;
+    memset(&a, 0, sizeof(a));
+    a.n_rollouts = B;
+    a.horizon = H;
+    a.k0 = k0;
+    a.n_t = n_t;
+    a.ignore_reach = ignore_reach;
+    a.params = dp;
+    a.q = dq;
+    a.tau = dtau;
+    a.cf = dcf;
+    a.x = dx;
+    a.flags = dfl;
+    a.work_cot = dwc;
+    rc = hs_run(m, &a);
+    if (rc == HS_OK) {
+      e = hipDeviceSynchronize();
+      if (e == hipSuccess && q) e = hipMemcpy(q, dq, nq * sizeof(double), hipMemcpyDeviceToHost);
+      if (e == hipSuccess && tau) e = hipMemcpy(tau, dtau, ntau * sizeof(double), hipMemcpyDeviceToHost);
+      if (e == hipSuccess && cf) e = hipMemcpy(cf, dcf, ncf * sizeof(double), hipMemcpyDeviceToHost);
+      if (e == hipSuccess && x) e = hipMemcpy(x, dx, nx * sizeof(double), hipMemcpyDeviceToHost);
+      if (e == hipSuccess && flags) e = hipMemcpy(flags, dfl, nfl * sizeof(uint32_t), hipMemcpyDeviceToHost);
+      if (e == hipSuccess && work_cot) e = hipMemcpy(work_cot, dwc, nwc * sizeof(double), hipMemcpyDeviceToHost);
+      if (e != hipSuccess) rc = hip_fail(e, "run/copy back");
+    }
+  }
+  (void)hipFree(dp);
+  (void)hipFree(dq);
+  (void)hipFree(dtau);
+  (void)hipFree(dcf);
+  (void)hipFree(dx);
+  (void)hipFree(dfl);
+  (void)hipFree(dwc);
+  return rc;
+}
+
+uint64_t hs_best_key_encode(double cot, int64_t id) {
+  float c = (float)cot;
+  uint32_t bits;
+  memcpy(&bits, &c, 4);
+  uint32_t ord = std::isnan(c) ? 0xFFFFFFFFu : ((bits & 0x80000000u) ? ~bits : (bits | 0x80000000u));
+  return ((uint64_t)ord << 32) | (uint32_t)id;
+}
+
+void hs_best_key_decode(uint64_t key, float* cot, int64_t* id) {
+  uint32_t ord = (uint32_t)(key >> 32);
+  uint32_t bits = (ord & 0x80000000u) ? (ord & 0x7FFFFFFFu) : ~ord;
+  float c;
+  memcpy(&c, &bits, 4);
+  if (ord == 0xFFFFFFFFu) c = NAN;
+  if (cot) *cot = c;
+  if (id) *id = (int64_t)(uint32_t)key;
+}
+
+}  // extern "C"

@@ -1,0 +1,55 @@
+// hs_topo.h -- flat, device-resident description of one robot model.
+//
+// Built once on the host by hs_model_load() (hs_model.cpp) from the MuJoCo-style
+// XML and copied to HBM; every wavefront reads it through the scalar cache
+// (all addresses are wave-uniform). It replaces the pointer-linked tree of
+// reference model.h:34-137 (modelnode/modeljoint), the odepart geometry of
+// visualization.h:93-120 and the liksolver tables of lik.cpp:7-78.
+#pragma once
+#include <stdint.h>
+
+#define HS_NMAX 24  // parts (hexapod 22, spider 19, myant 17)
+#define HS_LMAX 6   // limbs / feet
+#define HS_KMAX 18  // 3 * contacts
+#define HS_CMAX 6   // children per node
+
+enum { HS_J_NONE = -1, HS_J_FREE = 0, HS_J_HINGE = 1 };
+enum { HS_LIK_YXX = 0, HS_LIK_ZXX = 1 };
+
+// 3x4 rigid transform, column-major: m[c*3 + r], c = 0..3 (c = 3 is translation).
+// The implicit bottom row is (0,0,0,1): the reference's 4x4 product
+// (matrix.cpp:78-97) adds A(j,3)*B(3,i) = A(j,3)*0 for i < 3 and A(j,3)*1 for
+// i = 3, both exact, so the 3x4 product rounds identically.
+struct hs_aff34 { double m[12]; };
+
+struct hs_node {
+  hs_aff34 J_A_parent;  // modeljoint::A_parent (model.cpp:119-174)
+  hs_aff34 A_pj_body;   // modelnode::A_pj_body
+  double com[3];        // odepart::A_body_geom translation (get_com_pos, visualization.cpp:541-545)
+  double cap[3];        // odepart::capsule_to_pos (get_foot_pos, visualization.cpp:553-568)
+  int32_t parent, jtype, depth, nkids;
+  int32_t kids[HS_CMAX];
+  int32_t foot;         // foot index (preorder) or -1
+  int32_t hinge;        // motor index (0..nmj-1) or -1
+  int32_t owner_limb;   // limb lane that computes this node's FK/features
+  int32_t limb_below;   // limb whose foot is at/below this node, -1 if none or several
+};
+
+struct hs_topo {
+  int32_t n, nf, nmj, cfg;
+  int32_t n_limbs, lik_kind, max_depth, pad0;
+  double ls[3];            // link lengths (lik.cpp:226-227)
+  double rcap;             // foot capsule radius (lik.cpp:132-140)
+  double total_mass;       // sum of part masses (periodic.cpp:320-325)
+  double mass[HS_NMAX];    // dBodyGetMass default = 1 (dynrec.cpp:62-68)
+  int32_t footis[HS_LMAX];       // foot part ids, preorder (periodic.cpp:34-58)
+  int32_t hinge_ids[HS_NMAX];    // hinge part ids, preorder (periodic.cpp:311-319)
+  int32_t limb_child[HS_LMAX];   // limb top-link node (lik.cpp:50-63)
+  int32_t limb_parent[HS_LMAX];
+  int32_t limb_foot[HS_LMAX];    // foot node of each limb (lik.cpp:453-455)
+  int32_t limb_ysign[HS_LMAX];   // lik.cpp:230-245
+  int32_t limb_pergen[HS_LMAX];  // likpergen_map (pergen.cpp:243-262)
+  int32_t limb_chain_len[HS_LMAX];      // nodes from root to limb parent (inclusive)
+  int32_t limb_chain[HS_LMAX][HS_NMAX]; // root ... limb parent
+  hs_node node[HS_NMAX];
+};

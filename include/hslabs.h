@@ -1,0 +1,140 @@
+/*
+ * hslabs.h -- C ABI of the MI355X-native HSLabs control-loop path.
+ *
+ * Drop-in boundary for the reference's pergen -> lik -> FK -> dynrec ->
+ * ftsolver -> motor-torque path. The reference exposes this path only as C++
+ * classes (no FFI); each entry point below names the reference interface it
+ * replaces (file:line in underactuated/HSLabs). Plain pointers and sizes only;
+ * no HIP or torch types. All functions return 0 on success and a negative
+ * HS_E* code on failure (never exit(), unlike lik.cpp:321-330 / pergen.cpp:12);
+ * hs_last_error() returns a thread-local message for the last failure.
+ *
+ * Threading: a model handle is immutable after load and may be shared by
+ * threads; hs_run() calls on distinct streams are independent.
+ */
+#ifndef HSLABS_H
+#define HSLABS_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HSLABS_ABI_VERSION 1
+
+enum {
+  HS_OK = 0,
+  HS_E_ARG = -1,        /* bad argument / size */
+  HS_E_IO = -2,         /* file not found / unreadable */
+  HS_E_PARSE = -3,      /* malformed XML or config line (model.cpp:224-244, player.cpp:170-208) */
+  HS_E_TOPOLOGY = -4,   /* model outside the supported topology class */
+  HS_E_NOLIK = -5,      /* no limb IK variant for this model (lik.cpp:7-20) */
+  HS_E_DEVICE = -6,     /* HIP runtime error */
+  HS_E_NOTFOUND = -7    /* config id not present (player.cpp:243) */
+};
+
+/* Per-step flag bits (hs_run_args.flags). */
+#define HS_FLAG_RANK_RETRY   1u  /* adaptive-rank loop iterated (ftsolver.cpp:279-303) */
+#define HS_FLAG_FULL_RANK    2u  /* zeroth-order Gram full rank (reference asserts in its comma initializer) */
+#define HS_FLAG_LOOP_EXHAUST 4u  /* rank loop reached rank 0 without converging */
+#define HS_FLAG_NAN          8u  /* NaN in torques or contact forces */
+#define HS_FLAG_UNREACH     16u  /* an IK target was clamped (ignore_reach, lik.cpp:250-253) */
+#define HS_FLAG_NO_CONTACT  32u  /* no foot in contact (k = 0) */
+
+/* Gait setup of one rollout: the fields of pgsconfigparams (pergen.h:137-146),
+ * same meaning and units as a pgs_config.txt line (player.cpp:170-208).
+ * 128 bytes, so one wavefront reads a rollout's record in one coalesced load. */
+typedef struct {
+  double torso_pos[3];     /* "torso_pos" */
+  double torso_angles[3];  /* "torso_angles" (Euler phi, theta, psi; model.cpp:45) */
+  double step_duration;    /* in [0,1] (pergen.cpp:30-51) */
+  double period;           /* T */
+  double step_length;      /* L */
+  double step_height;      /* h */
+  double curvature;        /* 0 = straight (pergen.cpp:160-198) */
+  double foot_shift;       /* lateral_foot_shift / radial_foot_shift value */
+  int32_t foot_shift_type; /* -1 none, 0 lateral, 1 radial */
+  int32_t reserved0;
+  double reserved[3];
+} hs_gait_params;
+
+typedef struct hs_model_s* hs_model_t;
+
+typedef struct {
+  int32_t n_parts;     /* dynparts / model nodes (periodic.h:45) */
+  int32_t nmj;         /* motor joints (model.h:114 number_of_motor_joints) */
+  int32_t nfeet;       /* periodic.h:48 get_nfeet */
+  int32_t config_dim;  /* model.h:125 get_config_dim */
+  int32_t n_limbs;     /* liksolver::get_number_of_limbs (lik.h:48) */
+  int32_t lik_kind;    /* 0 = y-x-x legs (lik.cpp:151), 1 = z-x-x legs (lik.cpp:189) */
+  double total_mass;   /* periodic::get_total_mass (periodic.cpp:320) */
+  double rcap;         /* liksolver::get_rcap (lik.h:50) */
+} hs_model_dims;
+
+/* Replaces kinematicmodel::load_fromxml (model.cpp:224-244) + liksolver ctor
+ * (lik.cpp:7-20) + periodic::set_dynparts (periodic.cpp:34-58). The IK variant
+ * is chosen by basename like lik.cpp:9-11 ("myant.xml", "hexapod.xml",
+ * "spider.xml"); hs_model_load_ex(lik_variant >= 0) selects it explicitly
+ * (0 = myant, 1 = hexapod, 2 = spider tables). */
+int hs_model_load(const char* xml_path, hs_model_t* out);
+int hs_model_load_ex(const char* xml_path, int lik_variant, hs_model_t* out);
+void hs_model_free(hs_model_t model);
+int hs_model_get_dims(hs_model_t model, hs_model_dims* out);
+
+/* Replaces modelplayer::get_rec_str + get_pgs_config_params (player.cpp:170-244):
+ * reads line `setup_id` of a pgs_config.txt. xml_file receives the model name. */
+int hs_pgs_config_read(const char* path, int setup_id, hs_gait_params* out, char* xml_file, int32_t xml_file_len);
+
+/*
+ * One batched pass of the hot path. Rollout b (0 <= b < n_rollouts) runs the
+ * gait setup (pgssweeper::setup_pergen, pergen.cpp:453-507), samples the
+ * trajectory at t_i = i * (period / n_t) for i = k0 .. k0+H+3 (record_trajectory,
+ * periodic.cpp:77-96: pergen set_rec + lik + FK), builds dynamics records
+ * (periodic.cpp:149-202, dynrec.cpp:134-224) and solves steps
+ * i = k0+2 .. k0+H+1 (compute_torques_over_period, periodic.cpp:377-391).
+ * With k0 = 0 and H = n_t this is exactly one reference cycle and work_cot[1]
+ * is the reference COT (player.cpp:269-285).
+ *
+ * All arrays are DEVICE pointers on the current HIP device, row-major. Outputs
+ * may be NULL. The call is asynchronous on `stream` (a hipStream_t, NULL =
+ * default stream).
+ */
+typedef struct {
+  int32_t n_rollouts;
+  int32_t horizon;        /* H >= 1 */
+  int32_t k0;             /* first step index (0 = reference i = 2) */
+  int32_t n_t;            /* samples per period (measure_cot n_t, main.cpp:69) */
+  int32_t ignore_reach;   /* liksolver::set_ignore_reach_flag (lik.cpp:142-147) */
+  int32_t reserved0;
+  const hs_gait_params* params; /* [n_rollouts] */
+  double* q;              /* [B][H][config_dim]: configuration at each solved sample */
+  double* tau;            /* [B][H][nmj]: motor torques (periodic.cpp:328-343) */
+  double* cf;             /* [B][H][3*nfeet]: contact forces (ftsolver.cpp:163) */
+  double* x;              /* [B][H][6*n_parts]: joint forces/torques (ftsolver.cpp:166) */
+  uint32_t* flags;        /* [B][H] */
+  double* work_cot;       /* [B][2]: positive work, work/(sum m * step_length) */
+  uint64_t* best_key;     /* scalar; atomically min-reduced (cot key, see hs_best_key_decode) */
+  int64_t rollout_id_base;/* global id of rollout 0 (shard offset) */
+  void* stream;           /* hipStream_t */
+} hs_run_args;
+
+int hs_run(hs_model_t model, const hs_run_args* args);
+
+/* Host-buffer convenience wrapper of hs_run (copies in/out, synchronous).
+ * Replaces periodic::compute_torques_over_period + get_motor_torques +
+ * work_over_period for a batch of rollouts. Output pointers may be NULL. */
+int hs_run_host(hs_model_t model, const hs_gait_params* params, int32_t n_rollouts, int32_t n_t,
+                int32_t k0, int32_t horizon, int32_t ignore_reach, double* q, double* tau, double* cf,
+                double* x, uint32_t* flags, double* work_cot);
+
+/* Best-rollout key: (order-preserving bits of (float)cot) << 32 | (uint32)rollout id.
+ * NaN COT maps to the largest key. Initial value for a reduction: UINT64_MAX. */
+uint64_t hs_best_key_encode(double cot, int64_t rollout_id);
+void hs_best_key_decode(uint64_t key, float* cot, int64_t* rollout_id);
+
+const char* hs_last_error(void);
+int hs_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

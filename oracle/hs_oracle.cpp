@@ -1154,7 +1154,7 @@ struct CPQR {
           temp = (1 + temp) * (1 - temp);
           temp = temp < 0 ? 0 : temp;
           double ratio = nu[j] / nd[j];
-          double temp2 = temp * ratio * ratio;
+          double temp2 = temp * (ratio * ratio);  // temp * abs2(nu/nd)
           if (temp2 <= norm_downdate_threshold) {
             double s = 0;
             for (int i = k + 1; i < rows; i++) s += qr(i, j) * qr(i, j);
