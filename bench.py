@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Benchmark: batched control-loop steps/s on MI355X (BASELINE.json metric).
+
+A bench "step" is one pass of the hot path over one batch: every rollout of
+the batch advances one control-loop time step (pergen -> lik -> FK -> dynrec
+-> ftsolver -> motor torques), i.e. `rollouts x horizon` control-loop steps.
+Default workload = BASELINE.json configs[1]: hexapod.xml, 4096 rollouts per
+GPU, horizon 1, fp64. Bench step s solves time step k = s mod n_t of every
+rollout and accumulates positive work on the device, so 20 timed steps cover
+exactly one reference cycle (n_t = 20, main.cpp:69) and the per-rollout COT
+is the reference's measure_cot (player.cpp:269-285). After the timed steps
+every rank min-reduces its best (COT, rollout id) key with ONE RCCL
+all_reduce(MIN) of 8 bytes; that collective is inside the timed region.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 via
+torch.distributed.run (one process per GPU, RCCL).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "batched control-loop steps/sec (hexapod.xml, 18-DoF) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFLOPS = 78.6    # MI355X vector FP64 (spec), see DESIGN.md
+# algorithmic HBM bytes per control-loop step = outputs
+# tau 18*8 + contact forces 18*8 (+ 96 B of gait parameters amortized over H)
+OUT_BYTES_PER_STEP = {"hexapod": 288, "spider": 288, "myant": 192}
+PARAM_BYTES = 96
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rollouts", type=int, default=4096, help="rollouts per GPU")
+    ap.add_argument("--horizon", type=int, default=1)
+    ap.add_argument("--model", default="hexapod", choices=["hexapod", "spider", "myant"])
+    ap.add_argument("--n_t", type=int, default=20)
+    ap.add_argument("--curved", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(model_name, n_t, horizon, seconds, threads):
+    """Oracle (CPU restatement, tree basis = same algorithm as the kernel) on a bounded sample."""
+    from oracle import oracle as O
+    from hslabs_amd import synth
+
+    om = O.Model(os.path.join(ROOT, "models", f"{model_name}.xml"))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    chunk = 256 * threads
+    arr = synth.gen_params(chunk, model_name)
+    gaits = [O.GaitParams(torso_pos=tuple(r["torso_pos"]), torso_angles=tuple(r["torso_angles"]),
+                          step_duration=float(r["step_duration"]), period=float(r["period"]),
+                          step_length=float(r["step_length"]), step_height=float(r["step_height"]),
+                          curvature=float(r["curvature"]), foot_shift_type=int(r["foot_shift_type"]),
+                          foot_shift=float(r["foot_shift"])) for r in arr]
+
+    def timed(nthr, budget):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            O.batch(om, gaits, n_t, 0, horizon, basis=O.BASIS_TREE, n_threads=nthr)
+            done += len(gaits) * horizon
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return done / el, done, el
+
+    single, _, _ = timed(1, min(2.0, seconds / 4))
+    rate, done, el = timed(threads, seconds)
+    return {"value": round(rate, 1), "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"{done} control-loop steps ({model_name}, H={horizon}, synthetic gaits) in {el:.1f}s, "
+                      f"oracle tree-basis restatement, g++ -O2, std::thread x{threads}; "
+                      f"single-thread {single:.1f} steps/s",
+            "single_thread": round(single, 1)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import hslabs_amd as H
+    from hslabs_amd import synth
+
+    model = H.KinematicModel(os.path.join(ROOT, "models", f"{args.model}.xml"))
+    B, Hh, n_t = args.rollouts, args.horizon, args.n_t
+    id0 = rank * B
+    params = synth.gen_params(B, args.model, id0=id0, curved=args.curved)
+    batch = H.DeviceBatch(model, params, n_t=n_t, k0=0, horizon=Hh, outputs=("tau", "cf", "work_cot", "flags"),
+                          device=dev, rollout_id_base=id0)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(s):
+        batch.k0 = (s * Hh) % n_t
+        batch.run(stream=stream, best=False, accumulate=True)
+
+    # warmup (untimed)
+    batch.work_cot.zero_()
+    for w in range(args.warmup):
+        step(w)
+    torch.cuda.synchronize()
+    batch.work_cot.zero_()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+
+    def best_key_local():
+        # order-preserving key of (float32 COT, id), same encoding as hs_best_key_encode
+        cot = batch.work_cot[:, 1].to(torch.float32)
+        bits = cot.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        neg = bits >= 0x80000000
+        ordk = torch.where(neg, (~bits) & 0xFFFFFFFF, bits | 0x80000000)
+        ordk = torch.where(torch.isnan(cot), torch.full_like(ordk, 0xFFFFFFFF), ordk)
+        ids = torch.arange(id0, id0 + B, device=dev, dtype=torch.int64)
+        key = (ordk << 32) | ids
+        # int64 min with the sign bit flipped == uint64 min
+        return (key ^ (-(2 ** 63))).min().reshape(1)
+
+    # warm the key computation and the collective too (first use loads code objects)
+    warm = best_key_local()
+    if world > 1:
+        dist.all_reduce(warm, op=dist.ReduceOp.MIN)
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        starts[s].record(stream)
+        step(s)
+        ends[s].record(stream)
+    key = best_key_local()
+    if world > 1:
+        dist.all_reduce(key, op=dist.ReduceOp.MIN)  # the single RCCL collective
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(starts, ends)]))
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+    best = int(key.item()) ^ (-(2 ** 63))
+    best_cot, best_id = H.decode_best_key(best & 0xFFFFFFFFFFFFFFFF)
+    nan_steps = int(((batch.flags & 8) != 0).sum().item())
+
+    if rank == 0:
+        steps_total = B * Hh * args.steps * world
+        value = steps_total / elapsed
+        ms_per_step = 1e3 * elapsed / args.steps
+        alg_bytes = B * Hh * (OUT_BYTES_PER_STEP[args.model] + PARAM_BYTES / Hh)
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tf):
+            try:
+                j = json.load(open(tf))
+                if j.get("workload") == f"{args.model} B={B} H={Hh}":
+                    traffic = j.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (splitmix64 gait parameters around pgs id 8; SURVEY.md 8d)",
+            "config": {"workload": f"{args.model}.xml B={B}/GPU H={Hh} n_t={n_t} fp64 (BASELINE configs[1])",
+                       "rollouts_per_gpu": B, "horizon": Hh, "n_t": n_t,
+                       "parallelism": f"rollout-sharded x{world}, 1 RCCL all_reduce(MIN, 8 B) per job"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "hs_rollout_kernel", "kernel_ms": round(kern_ms, 5),
+                         "alg_bytes_per_launch": alg_bytes},
+            "best_rollout": {"id": best_id, "cot": best_cot},
+            "nan_steps": nan_steps,
+        }
+        if not args.no_cpu and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args.model, n_t, Hh, args.cpu_seconds, args.cpu_threads)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

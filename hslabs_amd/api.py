@@ -182,11 +182,12 @@ class DeviceBatch:
     def reset_best(self):
         self.best_key.fill_(-1)
 
-    def run(self, stream=None, best: bool = True) -> None:
+    def run(self, stream=None, best: bool = True, accumulate: bool = False) -> None:
         torch = self.torch
         a = capi.RunArgsC()
         a.n_rollouts, a.horizon, a.k0, a.n_t = self.B, self.H, self.k0, self.n_t
         a.ignore_reach = int(self.ignore_reach)
+        a.accumulate = int(accumulate)
 
         def ptr(t):
             return None if t is None else t.data_ptr()

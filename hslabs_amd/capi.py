@@ -60,7 +60,7 @@ class ModelDimsC(ctypes.Structure):
 class RunArgsC(ctypes.Structure):
     _fields_ = [
         ("n_rollouts", ctypes.c_int32), ("horizon", ctypes.c_int32), ("k0", ctypes.c_int32),
-        ("n_t", ctypes.c_int32), ("ignore_reach", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+        ("n_t", ctypes.c_int32), ("ignore_reach", ctypes.c_int32), ("accumulate", ctypes.c_int32),
         ("params", ctypes.c_void_p), ("q", ctypes.c_void_p), ("tau", ctypes.c_void_p),
         ("cf", ctypes.c_void_p), ("x", ctypes.c_void_p), ("flags", ctypes.c_void_p),
         ("work_cot", ctypes.c_void_p), ("best_key", ctypes.c_void_p),

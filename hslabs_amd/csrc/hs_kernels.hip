@@ -68,6 +68,17 @@ struct Smem {
 
 __device__ inline void wave_sync() { __syncthreads(); }
 
+#ifdef HS_STAMPS
+// diagnostic build only: per-phase shader-clock stamps of the first 4096 rollouts
+__device__ unsigned long long g_stamps[4096][16];
+#define STAMP(slot)                                                                  \
+  do {                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][slot] += __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define STAMP(slot) do {} while (0)
+#endif
+
 __device__ inline A34 node_joint_parent(const hs_topo* T, int v) { return load34(T->node[v].J_A_parent); }
 __device__ inline A34 node_pj(const hs_topo* T, int v) { return load34(T->node[v].A_pj_body); }
 
@@ -723,7 +734,9 @@ __device__ uint32_t contact_solve(SolveL& sv, int k, int lane) {
   double rel_error = 0;
   do {
     iters++;
+    STAMP(9);
     LUInfo info = fullpiv_lu(sv, k, lane);
+    STAMP(10);
     double thr = DBL_EPSILON * (double)k;
     int r = lu_rank(sv, info, thr);
     for (int guard = 0; guard < 2100 && r > rank0; guard++) {  // setThreshold doubling
@@ -732,6 +745,7 @@ __device__ uint32_t contact_solve(SolveL& sv, int k, int lane) {
     }
     lu_solve(sv, info, k, r, lane);
     lu_kernel_image(sv, info, k, r, thr, lane);
+    STAMP(11);
     if (r == k) flags |= HS_FLAG_FULL_RANK;
     rank0 = r;
     const int dimker = k - r;
@@ -756,8 +770,11 @@ __device__ uint32_t contact_solve(SolveL& sv, int k, int lane) {
       sv.M[i + j * LD] = s;
     }
     wave_sync();
+    STAMP(12);
     int np = colpiv_qr(sv, k, lane);
+    STAMP(13);
     qr_solve(sv, k, np, lane);
+    STAMP(14);
     // rel_error = |M z - b| / |b|
     if (lane < k) {
       double s = 0.0;
@@ -797,7 +814,9 @@ __global__ __launch_bounds__(WAVE) void hs_rollout_kernel(const hs_topo* __restr
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
   const bool ignore_reach = a.ignore_reach != 0;
 
+  STAMP(0);
   gait_setup(T, g, a.n_t, sm, lane);
+  STAMP(1);
 
   // initial window: samples k0 .. k0+4, lane = (sample, limb)
   {
@@ -808,8 +827,9 @@ __global__ __launch_bounds__(WAVE) void hs_rollout_kernel(const hs_topo* __restr
     }
   }
   wave_sync();
+  STAMP(2);
 
-  double work = 0;
+  double work = (a.accumulate && a.work_cot) ? a.work_cot[2 * (size_t)b] : 0.0;
   for (int h = 0; h < a.horizon; h++) {
     const int i = a.k0 + h + 2;
     if (h > 0) {
@@ -818,10 +838,15 @@ __global__ __launch_bounds__(WAVE) void hs_rollout_kernel(const hs_topo* __restr
     }
     const int s0 = i % NS;
     const SampleL& S = sm.s[s0];
+    STAMP(3);
     dynamics(T, sm, (i - 2) % NS, (i - 1) % NS, s0, (i + 1) % NS, (i + 2) % NS, lane);
+    STAMP(4);
     particular(T, sm, S, lane);
+    STAMP(5);
     const int k = build_grams(T, sm, S, lane);
+    STAMP(6);
     uint32_t flags = contact_solve(sm.sv, k, lane);
+    STAMP(7);
 
     // S4: x = x_part + N y for the hinge torque rows, motor torques (periodic.cpp:328-343)
     if (lane < nmj) {
@@ -898,6 +923,7 @@ __global__ __launch_bounds__(WAVE) void hs_rollout_kernel(const hs_topo* __restr
     }
     if (a.flags && lane == 0) a.flags[(size_t)b * a.horizon + h] = flags;
     wave_sync();
+    STAMP(8);
   }
   if (lane == 0) {
     double cot = work / (T->total_mass * g.step_length);
@@ -910,6 +936,18 @@ __global__ __launch_bounds__(WAVE) void hs_rollout_kernel(const hs_topo* __restr
 }
 
 }  // namespace
+
+#ifdef HS_STAMPS
+extern "C" int hs_debug_read_stamps(unsigned long long* out, int n_rows) {
+  if (n_rows > 4096) n_rows = 4096;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16 * n_rows, 0,
+                                  hipMemcpyDeviceToHost);
+}
+extern "C" int hs_debug_clear_stamps() {
+  static unsigned long long zero[4096][16];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+#endif
 
 namespace hs {
 

@@ -104,7 +104,8 @@ typedef struct {
   int32_t k0;             /* first step index (0 = reference i = 2) */
   int32_t n_t;            /* samples per period (measure_cot n_t, main.cpp:69) */
   int32_t ignore_reach;   /* liksolver::set_ignore_reach_flag (lik.cpp:142-147) */
-  int32_t reserved0;
+  int32_t accumulate;     /* 1: add this call's work to work_cot[b][0] (successive H-step calls
+                             then sum work in the reference's step order, periodic.cpp:291-304) */
   const hs_gait_params* params; /* [n_rollouts] */
   double* q;              /* [B][H][config_dim]: configuration at each solved sample */
   double* tau;            /* [B][H][nmj]: motor torques (periodic.cpp:328-343) */
