@@ -126,22 +126,15 @@ def main():
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
 
+    from hslabs_amd import dist as hdist
+
     def best_key_local():
-        # order-preserving key of (float32 COT, id), same encoding as hs_best_key_encode
-        cot = batch.work_cot[:, 1].to(torch.float32)
-        bits = cot.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
-        neg = bits >= 0x80000000
-        ordk = torch.where(neg, (~bits) & 0xFFFFFFFF, bits | 0x80000000)
-        ordk = torch.where(torch.isnan(cot), torch.full_like(ordk, 0xFFFFFFFF), ordk)
-        ids = torch.arange(id0, id0 + B, device=dev, dtype=torch.int64)
-        key = (ordk << 32) | ids
-        # int64 min with the sign bit flipped == uint64 min
-        return (key ^ (-(2 ** 63))).min().reshape(1)
+        return hdist.best_key(batch.work_cot[:, 1], id0)
 
     # warm the key computation and the collective too (first use loads code objects)
     warm = best_key_local()
+    hdist.reduce_best(warm)
     if world > 1:
-        dist.all_reduce(warm, op=dist.ReduceOp.MIN)
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -149,9 +142,7 @@ def main():
         starts[s].record(stream)
         step(s)
         ends[s].record(stream)
-    key = best_key_local()
-    if world > 1:
-        dist.all_reduce(key, op=dist.ReduceOp.MIN)  # the single RCCL collective
+    key = hdist.reduce_best(best_key_local())  # the single RCCL collective (8 B)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -161,8 +152,7 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms = float(t[0]), float(t[1])
-    best = int(key.item()) ^ (-(2 ** 63))
-    best_cot, best_id = H.decode_best_key(best & 0xFFFFFFFFFFFFFFFF)
+    best_cot, best_id = hdist.decode(key)
     nan_steps = int(((batch.flags & 8) != 0).sum().item())
 
     if rank == 0:

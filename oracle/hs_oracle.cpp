@@ -1685,6 +1685,54 @@ double hso_fk_ik_check(const hso_model* m0, const hso_gait* g, double t, int ign
   return worst;
 }
 
+int hso_dynrec_dump(const hso_model* m0, const hso_gait* g, int n_t, int step, double* pos, double* jpos,
+                    double* jz, double* mom_rate, double* amr, double* fpos, int32_t* contacts,
+                    int32_t* parents, int32_t* footis, int32_t* hinge_ids) {
+  hso_model mm = *m0;
+  hso_model* m = &mm;
+  tl_ignore_reach = true;
+  PGS pgs;
+  setup_pergen(m, pgs, g);
+  int nsamp = step + 5;
+  double dt = pgs.pergen.period / n_t;
+  std::vector<DynRec> dr(nsamp);
+  std::vector<double> rec(m->cfg);
+  std::vector<std::vector<double>> traj(nsamp);
+  double t = 0;
+  for (int i = 0; i < nsamp; i++) {
+    pgs.set_rec(rec.data(), t);
+    if (!set_jvalues_with_lik(m, rec.data())) return -10;
+    traj[i].resize(m->cfg);
+    for (int j = 0; j < m->cfg; j++) traj[i][j] = jv(m, j);
+    t += dt;
+  }
+  for (int i = step; i < nsamp; i++) {
+    dr[i].init(m->n, m->nf);
+    for (int j = 0; j < m->cfg; j++) jv(m, j) = traj[i][j];
+    recompute_modelnodes(m);
+    dynrec_initialize(m, dr[i], m->rcap);
+  }
+  for (int i = step + 1; i <= nsamp - 2; i++) compute_ders(m, dr[i], 0, dr[i - 1], dr[i + 1], dt);
+  compute_ders(m, dr[step + 2], 1, dr[step + 1], dr[step + 3], dt);
+  const DynRec& d = dr[step + 2];
+  for (int i = 0; i < m->n; i++)
+    for (int j = 0; j < 3; j++) {
+      pos[3 * i + j] = d.pos[i].v[j];
+      jpos[3 * i + j] = d.jpos[i].v[j];
+      jz[3 * i + j] = d.jzaxis[i].v[j];
+      mom_rate[3 * i + j] = d.mom_rate[i].v[j];
+      amr[3 * i + j] = d.ang_mom_rate[i].v[j];
+    }
+  for (int f = 0; f < m->nf; f++) {
+    for (int j = 0; j < 3; j++) fpos[3 * f + j] = d.fpos[f].v[j];
+    contacts[f] = d.contacts[f];
+    footis[f] = m->footis[f];
+  }
+  for (int i = 0; i < m->n; i++) parents[i] = m->parentis[i];
+  for (int i = 0; i < m->nmj; i++) hinge_ids[i] = m->hinge_ids[i];
+  return 3 * d.ncontacts();
+}
+
 int hso_residuals(const hso_model* m0, const hso_gait* g, int n_t, int step, int basis, double* out2) {
   hso_model mm = *m0;
   hso_model* m = &mm;

@@ -91,6 +91,13 @@ double hso_fk_ik_check(const hso_model* m, const hso_gait* g, double t, int igno
 /* static residual checks for one step: |B0 x0 - f|, |[B0 Bc] N| (both bases) */
 int hso_residuals(const hso_model* m, const hso_gait* g, int n_t, int step, int basis, double* out2);
 
+/* Dynamics record of one step (sample i = step+2) for independent cross-checks:
+ * pos/jpos/jz/mom_rate/ang_mom_rate [n*3], fpos [nf*3], contacts [nf], parents [n], footis [nf],
+ * hinge_ids [nmj]. Returns k = 3 * #contacts. */
+int hso_dynrec_dump(const hso_model* m, const hso_gait* g, int n_t, int step, double* pos, double* jpos,
+                    double* jz, double* mom_rate, double* amr, double* fpos, int32_t* contacts,
+                    int32_t* parents, int32_t* footis, int32_t* hinge_ids);
+
 #ifdef __cplusplus
 }
 #endif

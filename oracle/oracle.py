@@ -148,6 +148,9 @@ def lib():
         L.hso_fk_ik_check.restype = ctypes.c_double
         L.hso_residuals.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, dp]
+        ip = ctypes.POINTER(ctypes.c_int32)
+        L.hso_dynrec_dump.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int,
+                                      dp, dp, dp, dp, dp, dp, ip, ip, ip, ip]
         _lib = L
     return _lib
 
@@ -250,3 +253,23 @@ def residuals(model: Model, gait: GaitParams, n_t: int, step: int, basis: int):
     out = np.zeros(2)
     k = lib().hso_residuals(model.handle, ctypes.byref(g), n_t, step, basis, _ptr(out))
     return k, out[0], out[1]
+
+
+def dynrec_dump(model: Model, gait: GaitParams, n_t: int, step: int) -> dict:
+    """Dynamics record of step `step` (sample step+2): the inputs of ftsolver."""
+    n, nf = model.n, model.nf
+    out = {k: np.zeros((n, 3)) for k in ("pos", "jpos", "jz", "mom_rate", "amr")}
+    out["fpos"] = np.zeros((nf, 3))
+    out["contacts"] = np.zeros(nf, np.int32)
+    out["parents"] = np.zeros(n, np.int32)
+    out["footis"] = np.zeros(nf, np.int32)
+    out["hinge_ids"] = np.zeros(model.nmj, np.int32)
+    ip = ctypes.POINTER(ctypes.c_int32)
+    g = gait.to_c()
+    k = lib().hso_dynrec_dump(model.handle, ctypes.byref(g), n_t, step, *[_ptr(out[k]) for k in
+                              ("pos", "jpos", "jz", "mom_rate", "amr", "fpos")],
+                              *[out[k].ctypes.data_as(ip) for k in ("contacts", "parents", "footis", "hinge_ids")])
+    if k < 0:
+        raise RuntimeError("dynrec_dump failed")
+    out["k"] = k
+    return out

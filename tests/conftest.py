@@ -1,0 +1,61 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+MODELS = os.path.join(ROOT, "models")
+PGS_CONFIG = os.path.join(MODELS, "pgs_config.txt")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+# pgs ids whose model XML ships with the reference (ids 28-32 name missing weaver*.xml)
+PGS_IDS = list(range(28))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")
+
+
+@pytest.fixture(scope="session")
+def oracle_mod():
+    from oracle import oracle as O
+
+    O.build()
+    return O
+
+
+@pytest.fixture(scope="session")
+def product():
+    """The product package with its in-tree gfx950 library (built if stale)."""
+    from hslabs_amd import build as b
+
+    b.build()
+    import hslabs_amd as H
+
+    H.capi.load(build_if_missing=False)
+    return H
+
+
+@pytest.fixture(scope="session")
+def omodels(oracle_mod):
+    return {name: oracle_mod.Model(os.path.join(MODELS, f"{name}.xml")) for name in ("hexapod", "spider", "myant")}
+
+
+def to_oracle_gait(O, p):
+    """hslabs_amd.PgsConfigParams -> oracle GaitParams"""
+    return O.GaitParams(torso_pos=tuple(p.torso_pos), torso_angles=tuple(p.torso_angles),
+                        step_duration=p.step_duration, period=p.period, step_length=p.step_length,
+                        step_height=p.step_height, curvature=p.curvature, foot_shift_type=p.foot_shift[0],
+                        foot_shift=p.foot_shift[1])
+
+
+def record_to_oracle_gait(O, r):
+    """GAIT_DTYPE record -> oracle GaitParams"""
+    return O.GaitParams(torso_pos=tuple(float(v) for v in r["torso_pos"]),
+                        torso_angles=tuple(float(v) for v in r["torso_angles"]),
+                        step_duration=float(r["step_duration"]), period=float(r["period"]),
+                        step_length=float(r["step_length"]), step_height=float(r["step_height"]),
+                        curvature=float(r["curvature"]), foot_shift_type=int(r["foot_shift_type"]),
+                        foot_shift=float(r["foot_shift"]))

@@ -1,0 +1,204 @@
+"""Oracle pinning (CPU): the reference's own self-checks restated as known-answer
+tests, analytic properties of the force/torque system, and an independent
+numpy/scipy formulation of the ftsolver problem. The reference binary cannot be
+built here, so these are what pins the oracle.
+"""
+import os
+
+import numpy as np
+import pytest
+import scipy.linalg as sla
+
+from conftest import MODELS, PGS_CONFIG, PGS_IDS
+
+
+def pgs(O, sid):
+    return O.load_pgs_config(PGS_CONFIG, sid)
+
+
+def model_for(O, omodels, g):
+    return omodels[g.xml_file.replace(".xml", "")]
+
+
+# --- visualization.cpp:24 rot_ztov built-in check: R z = v/|v| ------------------------------
+@pytest.mark.parametrize("v", [(0, 1, 0), (1, 0, 0), (0, 0, 1), (0, 0, -1), (0, 0, -0.1), (0.4, 0.2, 0),
+                               (-0.4, -0.2, 0), (0.3, -0.5, 0.7), (1e-12, 0, -1)])
+def test_rot_ztov_maps_z_to_v(oracle_mod, v):
+    R = oracle_mod.rot_ztov(v)
+    v = np.asarray(v, float)
+    # |v x z| < 1e-10 takes the (0,1,0) fallback axis: exact only to the reference's own 1e-3 check
+    tiny = np.linalg.norm(np.cross(v, [0, 0, 1])) < 1e-10
+    assert np.allclose(R @ [0, 0, 1], v / np.linalg.norm(v), atol=1e-3 if tiny else 1e-12)
+    assert np.allclose(R @ R.T, np.eye(3), atol=1e-12)
+    assert np.linalg.det(R) == pytest.approx(1.0, abs=1e-12)
+
+
+# --- pergen.cpp:377-383 Euler round trip -------------------------------------------------------
+def test_euler_roundtrip(oracle_mod):
+    rng = np.random.default_rng(0)
+    for _ in range(500):
+        a = np.array([rng.uniform(-np.pi, np.pi), rng.uniform(-1.5, 1.5), rng.uniform(-np.pi, np.pi)])
+        assert np.allclose(oracle_mod.euler_roundtrip(a), a, atol=1e-12)
+
+
+# --- lik.cpp:371-404 solver_test_yxx (tolerance of the reference: 1e-3) -----------------------
+@pytest.mark.parametrize("name", ["hexapod", "myant"])
+def test_lik_roundtrip(oracle_mod, omodels, name):
+    err = oracle_mod.lik_roundtrip(omodels[name], 2000, seed=7)
+    assert err < 1e-9
+
+
+# --- FK after IK reproduces the pergen foot targets -------------------------------------------
+@pytest.mark.parametrize("sid", [0, 8, 10, 20, 23, 24, 25, 26, 27])
+def test_fk_ik_feet_on_targets(oracle_mod, omodels, sid):
+    g = pgs(oracle_mod, sid)
+    m = model_for(oracle_mod, omodels, g)
+    for t in np.linspace(0, 2 * g.period, 13):
+        assert oracle_mod.fk_ik_check(m, g, t) < 1e-12
+
+
+# --- B0 x0 = f and [B0 Bc] N = 0 (SURVEY.md 8c KAT 2) ---------------------------------------------
+@pytest.mark.parametrize("sid", [0, 3, 8, 9, 20, 23, 24])
+@pytest.mark.parametrize("basis", [0, 1])
+def test_system_residuals(oracle_mod, omodels, sid, basis):
+    g = pgs(oracle_mod, sid)
+    m = model_for(oracle_mod, omodels, g)
+    for step in (0, 5, 11):
+        k, r0, r1 = oracle_mod.residuals(m, g, 20, step, basis)
+        assert k % 3 == 0 and k > 0
+        assert r0 < 1e-12 and r1 < 1e-12
+
+
+# --- basis invariance: tree-built basis == orthonormal QR basis (SURVEY.md 8c KAT 5) -------------
+@pytest.mark.parametrize("sid", PGS_IDS)
+def test_basis_invariance(oracle_mod, omodels, sid):
+    g = pgs(oracle_mod, sid)
+    m = model_for(oracle_mod, omodels, g)
+    ro = oracle_mod.rollout(m, g, 20, basis=oracle_mod.BASIS_ORTHO)
+    rt = oracle_mod.rollout(m, g, 20, basis=oracle_mod.BASIS_TREE)
+    assert np.abs(ro["tau"] - rt["tau"]).max() < 1e-9
+    assert np.abs(ro["cf"] - rt["cf"]).max() < 1e-9
+    assert abs(ro["cot"] - rt["cot"]) <= 1e-9 * abs(ro["cot"])
+    # the adaptive-rank loop converges first time on every shipped setup (ftsolver.cpp:228-232)
+    assert (ro["diag"][:, 2] == 1).all() and (ro["diag"][:, 3] < 1e-6).all()
+    assert (ro["flags"] == 0).all()
+
+
+# --- static stance (pgs ids 4, 5, 11): sum of contact forces = total weight (g = 1, m = 1) -------
+@pytest.mark.parametrize("sid,weight", [(4, 22.0), (11, 22.0), (5, 17.0)])
+def test_static_stance_force_balance(oracle_mod, omodels, sid, weight):
+    g = pgs(oracle_mod, sid)
+    m = model_for(oracle_mod, omodels, g)
+    r = oracle_mod.rollout(m, g, 20)
+    total = r["cf"].reshape(20, -1, 3).sum(axis=1)
+    assert np.allclose(total[:, 2], weight, rtol=1e-4)
+    assert np.abs(total[:, :2]).max() < 1e-3
+    n = m.n
+    # all feet down: torso actuation is eliminated exactly (zeroth-order solve)
+    assert np.abs(r["x"][:, :3]).max() < 1e-12 and np.abs(r["x"][:, 3 * n:3 * n + 3]).max() < 1e-12
+
+
+# --- >= 3 non-collinear feet: zero torso actuation; 2 feet (myant): rank-5 remainder ----------------
+@pytest.mark.parametrize("sid", [8, 23, 24])
+def test_torso_actuation_eliminated(oracle_mod, omodels, sid):
+    g = pgs(oracle_mod, sid)
+    m = model_for(oracle_mod, omodels, g)
+    r = oracle_mod.rollout(m, g, 20)
+    assert (r["diag"][:, 0] >= 9).all() and (r["diag"][:, 1] == 6).all()
+    n = m.n
+    assert np.abs(r["x"][:, :3]).max() < 1e-12 and np.abs(r["x"][:, 3 * n:3 * n + 3]).max() < 1e-12
+
+
+def test_two_feet_rank_five(oracle_mod, omodels):
+    g = pgs(oracle_mod, 9)  # myant, two feet down in most phases
+    r = oracle_mod.rollout(omodels["myant"], g, 20)
+    two = r["diag"][:, 0] == 6
+    assert two.any() and (r["diag"][two, 1] == 5).all()
+
+
+# --- independent numpy/scipy formulation of ftsolver (lexicographic least squares via SVD) --------
+def build_system(d, n):
+    """B0, f, Bc from a dynamics record, written from dynrec.cpp:227-344 independently of the oracle."""
+    def cross(r):
+        return np.array([[0, -r[2], r[1]], [r[2], 0, -r[0]], [-r[1], r[0], 0]])
+
+    B0 = np.zeros((6 * n, 6 * n))
+    f = np.zeros(6 * n)
+    for i in range(n):
+        p = d["parents"][i]
+        B0[3 * i:3 * i + 3, 3 * i:3 * i + 3] = np.eye(3)
+        B0[3 * (n + i):3 * (n + i) + 3, 3 * (n + i):3 * (n + i) + 3] = np.eye(3)
+        if p >= 0:
+            B0[3 * p:3 * p + 3, 3 * i:3 * i + 3] = -np.eye(3)
+            B0[3 * (n + p):3 * (n + p) + 3, 3 * (n + i):3 * (n + i) + 3] = -np.eye(3)
+            B0[3 * (n + i):3 * (n + i) + 3, 3 * i:3 * i + 3] = cross(d["jpos"][i] - d["pos"][i])
+            B0[3 * (n + p):3 * (n + p) + 3, 3 * i:3 * i + 3] = cross(d["pos"][p] - d["jpos"][i])
+        f[3 * i:3 * i + 3] = d["mom_rate"][i] + np.array([0, 0, 1.0])
+        f[3 * (n + i):3 * (n + i) + 3] = d["amr"][i]
+    cols = []
+    for fi in range(len(d["footis"])):
+        if not d["contacts"][fi]:
+            continue
+        p = d["footis"][fi]
+        c = np.zeros((6 * n, 3))
+        c[3 * p:3 * p + 3] = np.eye(3)
+        c[3 * (n + p):3 * (n + p) + 3] = cross(d["fpos"][fi] - d["pos"][p])
+        cols.append(c)
+    Bc = np.hstack(cols)
+    return B0, f, Bc
+
+
+def scipy_solve(d, n):
+    B0, f, Bc = build_system(d, n)
+    k = Bc.shape[1]
+    xp = np.linalg.solve(B0, f)
+    N = sla.null_space(np.hstack([B0, Bc]))  # (6n+k) x k, orthonormal
+    assert N.shape[1] == k
+    Nu = N[:6 * n]
+    c = np.ones(6 * n)
+    c[3:3 * n] = 0
+    c[3 * n + 3:] = d["jz"].reshape(-1)[3:]
+    m0 = np.zeros(6 * n, bool)
+    m0[[0, 1, 2, 3 * n, 3 * n + 1, 3 * n + 2]] = True
+    A0, b0 = (c[:, None] * Nu)[m0], (c * xp)[m0]
+    A1, b1 = (c[:, None] * Nu)[~m0], (c * xp)[~m0]
+    y0 = -np.linalg.lstsq(A0, b0, rcond=1e-10)[0]
+    Z = sla.null_space(A0, rcond=1e-10)
+    w = -np.linalg.lstsq(A1 @ Z, b1 + A1 @ y0, rcond=None)[0]
+    y = y0 + Z @ w
+    x = xp + Nu @ y
+    tau = np.array([d["jz"][h] @ x[3 * n + 3 * h:3 * n + 3 * h + 3] for h in d["hinge_ids"]])
+    wforce = N[6 * n:] @ y
+    cf = np.zeros(3 * len(d["footis"]))
+    ci = 0
+    for fi in range(len(d["footis"])):
+        if d["contacts"][fi]:
+            cf[3 * fi:3 * fi + 3] = wforce[3 * ci:3 * ci + 3]
+            ci += 1
+    return tau, cf
+
+
+@pytest.mark.parametrize("sid", [0, 3, 8, 9, 10, 12, 20, 23, 24, 25, 26])
+def test_independent_scipy_formulation(oracle_mod, omodels, sid):
+    g = pgs(oracle_mod, sid)
+    m = model_for(oracle_mod, omodels, g)
+    r = oracle_mod.rollout(m, g, 20)
+    for step in range(0, 20, 3):
+        d = oracle_mod.dynrec_dump(m, g, 20, step)
+        tau, cf = scipy_solve(d, m.n)
+        scale = max(1.0, np.abs(r["tau"][step]).max())
+        assert np.abs(tau - r["tau"][step]).max() < 1e-8 * scale
+        assert np.abs(cf - r["cf"][step]).max() < 1e-8 * max(1.0, np.abs(cf).max())
+
+
+# --- COT sweep shape (player.cpp:311-321, main.cpp:69) ------------------------------------------
+def test_cot_sweep_period(oracle_mod, omodels):
+    g = pgs(oracle_mod, 8)
+    cots = []
+    for vali in range(16):  # sweep period 3 -> 18 in 15 steps (n_val + 1 values)
+        g.period = 3 + vali * (18 - 3) / 15
+        cots.append(oracle_mod.rollout(omodels["hexapod"], g, 20, basis=1)["cot"])
+    cots = np.array(cots)
+    assert np.isfinite(cots).all() and (cots > 0).all()
+    # slower gaits need less positive work per distance
+    assert cots[-1] < cots[0]
