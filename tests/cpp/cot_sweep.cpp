@@ -1,0 +1,37 @@
+// Reference-shaped caller of the C++ shim: the hot-path part of main.cpp:33-89
+// (make_pergensu(8) -> measure_cot_sweep(period 3..18) -> periodic work_over_period).
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+
+#include "hslabs.hpp"
+
+using namespace hslabs;
+
+int main(int argc, char** argv) {
+  std::string models = argc > 1 ? argv[1] : "models";
+  modelplayer player0;
+  pergensetup* pgs = player0.make_pergensu(models + "/pgs_config.txt", 8, models);  // main.cpp:35
+  double cot = player0.measure_cot(pgs, 20);                                         // main.cpp:72
+  std::printf("COT = %.12f\n", cot);
+  auto sweep = player0.measure_cot_sweep(pgs, 20, "period", 3, 18, 15, false);        // main.cpp:69
+  for (auto& vc : sweep) std::printf("val = %g COT = %.12f\n", vc.first, vc.second);
+  periodic per(player0.get_model());                                                  // main.cpp:81-89
+  per.record_trajectory(pgs, 20);
+  per.compute_dynrecs();
+  per.compute_dynrec_ders();
+  per.switch_torso_penalty(1, 1);
+  double work = per.work_over_period();
+  std::printf("work = %.12f\n", work);
+  const double* tau = per.get_computed_torques(2);
+  std::printf("tau[2][0] = %.12f\n", tau[0]);
+  try {
+    player0.measure_cot_sweep(pgs, 20, "curvature", 0, 1, 2, false);
+    return 2;
+  } catch (const error& e) {
+    std::printf("error ok: %s\n", e.what());
+  }
+  delete pgs;
+  return (std::isfinite(cot) && std::fabs(cot - sweep[0].second) < 1e-12) ? 0 : 1;
+}
