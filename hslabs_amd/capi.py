@@ -20,6 +20,7 @@ HS_FLAG_LOOP_EXHAUST = 4
 HS_FLAG_NAN = 8
 HS_FLAG_UNREACH = 16
 HS_FLAG_NO_CONTACT = 32
+HS_FLAG_GENERAL = 64
 
 # every symbol declared in include/hslabs.h
 EXPORTS = [

@@ -50,9 +50,22 @@ struct SetupL {
   double t_step, max_radius, v, dt;
 };
 
+struct FastL {  // per-contact blocks exchanged through LDS
+  double A[HS_LMAX][18], D[HS_LMAX][9], g[HS_LMAX][3], Dinv[HS_LMAX][9], S[HS_LMAX][36], h[HS_LMAX][6];
+  double lam[6];
+  int ok[HS_LMAX];
+};
+
+struct GenMats {  // k x k matrices of the Eigen-style general path
+  double ntn0[HS_KMAX * LD], lu[HS_KMAX * LD], Ny[HS_KMAX * LD], M[HS_KMAX * LD], qr[HS_KMAX * LD];
+};
+
 struct SolveL {
   double f[6 * HS_NMAX], x[6 * HS_NMAX];
-  double ntn0[HS_KMAX * LD], lu[HS_KMAX * LD], Ny[HS_KMAX * LD], M[HS_KMAX * LD], qr[HS_KMAX * LD];
+  union {
+    GenMats gm;  // general path
+    FastL fl;    // fast path (dead once the general path starts)
+  };
   double n1[HS_LMAX][9];  // 3x3 diagonal blocks of the first-order Gram (column-major)
   double ntx0[HS_KMAX], ntx1[HS_KMAX], y0[HS_KMAX], b[HS_KMAX], z[HS_KMAX], y[HS_KMAX], c[HS_KMAX];
   double hc[HS_KMAX], nu[HS_KMAX], nd[HS_KMAX], tau[HS_NMAX];
@@ -391,7 +404,7 @@ __device__ int build_grams(const hs_topo* T, Smem& sm, const SampleL& S, int lan
       s = s + na * nb;
     }
     for (int r = 0; r < 3; r++) s = s + cross_e(da, ja, r) * cross_e(db, jb, r);
-    sm.sv.ntn0[ci + cj * LD] = s;
+    sm.sv.gm.ntn0[ci + cj * LD] = s;
   }
   if (lane < k) {
     int ci = lane, fa = sm.sv.cfoot[ci / 3], ja = ci % 3;
@@ -451,11 +464,11 @@ struct LUInfo {
   double maxpivot;
 };
 
-// Eigen FullPivLU::computeInPlace on sv.lu (k x k)
+// Eigen FullPivLU::computeInPlace on sv.gm.lu (k x k)
 __device__ LUInfo fullpiv_lu(SolveL& sv, int k, int lane) {
   for (int e = lane; e < k * k; e += WAVE) {
     int i = e % k, j = e / k;
-    sv.lu[i + j * LD] = sv.ntn0[i + j * LD];
+    sv.gm.lu[i + j * LD] = sv.gm.ntn0[i + j * LD];
   }
   wave_sync();
   LUInfo info{k, 0.0};
@@ -464,7 +477,7 @@ __device__ LUInfo fullpiv_lu(SolveL& sv, int k, int lane) {
     double best = -1.0;
     int bidx = 1 << 30;
     for (int e = lane; e < m * m; e += WAVE) {
-      double a = fabs(sv.lu[(p + e % m) + (p + e / m) * LD]);
+      double a = fabs(sv.gm.lu[(p + e % m) + (p + e / m) * LD]);
       if (a > best || (a == best && e < bidx)) { best = a; bidx = e; }
     }
     wave_argmax(best, bidx);
@@ -477,25 +490,25 @@ __device__ LUInfo fullpiv_lu(SolveL& sv, int k, int lane) {
     const int bi = p + bidx % m, bj = p + bidx / m;
     if (lane == 0) { sv.rowsT[p] = bi; sv.colsT[p] = bj; }
     if (bi != p && lane < k) {
-      double t = sv.lu[p + lane * LD];
-      sv.lu[p + lane * LD] = sv.lu[bi + lane * LD];
-      sv.lu[bi + lane * LD] = t;
+      double t = sv.gm.lu[p + lane * LD];
+      sv.gm.lu[p + lane * LD] = sv.gm.lu[bi + lane * LD];
+      sv.gm.lu[bi + lane * LD] = t;
     }
     wave_sync();
     if (bj != p && lane < k) {
-      double t = sv.lu[lane + p * LD];
-      sv.lu[lane + p * LD] = sv.lu[lane + bj * LD];
-      sv.lu[lane + bj * LD] = t;
+      double t = sv.gm.lu[lane + p * LD];
+      sv.gm.lu[lane + p * LD] = sv.gm.lu[lane + bj * LD];
+      sv.gm.lu[lane + bj * LD] = t;
     }
     wave_sync();
     if (p < k - 1) {
-      double piv = sv.lu[p + p * LD];
-      if (lane > p && lane < k) sv.lu[lane + p * LD] /= piv;
+      double piv = sv.gm.lu[p + p * LD];
+      if (lane > p && lane < k) sv.gm.lu[lane + p * LD] /= piv;
       wave_sync();
       const int mm = k - p - 1;
       for (int e = lane; e < mm * mm; e += WAVE) {
         int i = p + 1 + e % mm, j = p + 1 + e / mm;
-        sv.lu[i + j * LD] -= sv.lu[i + p * LD] * sv.lu[p + j * LD];
+        sv.gm.lu[i + j * LD] -= sv.gm.lu[i + p * LD] * sv.gm.lu[p + j * LD];
       }
       wave_sync();
     }
@@ -511,7 +524,7 @@ __device__ LUInfo fullpiv_lu(SolveL& sv, int k, int lane) {
 __device__ inline int lu_rank(const SolveL& sv, const LUInfo& info, double thr) {
   double pt = fabs(info.maxpivot) * thr;
   int r = 0;
-  for (int i = 0; i < info.nz; i++) r += fabs(sv.lu[i + i * LD]) > pt;
+  for (int i = 0; i < info.nz; i++) r += fabs(sv.gm.lu[i + i * LD]) > pt;
   return r;
 }
 
@@ -539,30 +552,30 @@ __device__ void lu_solve(SolveL& sv, const LUInfo& info, int k, int r, int lane)
   if (r == 0) return;
   for (int j = 0; j < k; j++) {  // unit lower
     double cj = sv.c[j];
-    if (lane > j && lane < k) sv.c[lane] -= cj * sv.lu[lane + j * LD];
+    if (lane > j && lane < k) sv.c[lane] -= cj * sv.gm.lu[lane + j * LD];
     wave_sync();
   }
-  upper_solve_shared(sv.lu, sv.c, r, lane);
+  upper_solve_shared(sv.gm.lu, sv.c, r, lane);
   if (lane < r) sv.y0[sv.q[lane]] = sv.c[lane];
   wave_sync();
 }
 
-// FullPivLU::kernel() -> sv.Ny (k x dimker); uses sv.qr as scratch; sv.piv/rycol set
+// FullPivLU::kernel() -> sv.gm.Ny (k x dimker); uses sv.gm.qr as scratch; sv.piv/rycol set
 __device__ void lu_kernel_image(SolveL& sv, const LUInfo& info, int k, int r, double thr, int lane) {
   if (lane == 0) {
     double pt = info.maxpivot * thr;
     int p = 0;
     for (int i = 0; i < info.nz; i++)
-      if (fabs(sv.lu[i + i * LD]) > pt) sv.piv[p++] = i;
+      if (fabs(sv.gm.lu[i + i * LD]) > pt) sv.piv[p++] = i;
     for (int i = 0; i < r; i++) sv.rycol[i] = sv.q[sv.piv[i]];  // image columns
   }
   wave_sync();
   const int dimker = k - r;
   if (dimker == 0) return;
-  double* mm = sv.qr;  // r x k trapezoid
+  double* mm = sv.gm.qr;  // r x k trapezoid
   for (int e = lane; e < r * k; e += WAVE) {
     int i = e % r, j = e / r;
-    mm[i + j * LD] = (j >= i) ? sv.lu[sv.piv[i] + j * LD] : 0.0;
+    mm[i + j * LD] = (j >= i) ? sv.gm.lu[sv.piv[i] + j * LD] : 0.0;
   }
   wave_sync();
   if (lane < r) {  // bring non-negligible pivots to the front (rows own a column swap each)
@@ -595,21 +608,21 @@ __device__ void lu_kernel_image(SolveL& sv, const LUInfo& info, int k, int r, do
     double v;
     if (i < r) v = -mm[i + (r + kk) * LD];
     else v = (i == r + kk) ? 1.0 : 0.0;
-    sv.Ny[row + kk * LD] = v;
+    sv.gm.Ny[row + kk * LD] = v;
   }
   wave_sync();
 }
 
-// Eigen 3.3 ColPivHouseholderQR on sv.qr (k x k, copy of M); returns nonzero pivots
+// Eigen 3.3 ColPivHouseholderQR on sv.gm.qr (k x k, copy of M); returns nonzero pivots
 __device__ int colpiv_qr(SolveL& sv, int k, int lane) {
   for (int e = lane; e < k * k; e += WAVE) {
     int i = e % k, j = e / k;
-    sv.qr[i + j * LD] = sv.M[i + j * LD];
+    sv.gm.qr[i + j * LD] = sv.gm.M[i + j * LD];
   }
   wave_sync();
   if (lane < k) {
     double s = 0;
-    for (int i = 0; i < k; i++) s += sv.qr[i + lane * LD] * sv.qr[i + lane * LD];
+    for (int i = 0; i < k; i++) s += sv.gm.qr[i + lane * LD] * sv.gm.qr[i + lane * LD];
     sv.nd[lane] = sqrt(s);
     sv.nu[lane] = sv.nd[lane];
   }
@@ -630,9 +643,9 @@ __device__ int colpiv_qr(SolveL& sv, int k, int lane) {
     if (lane == 0) sv.cperm[p] = bi;
     if (bi != p) {
       if (lane < k) {
-        double t = sv.qr[lane + p * LD];
-        sv.qr[lane + p * LD] = sv.qr[lane + bi * LD];
-        sv.qr[lane + bi * LD] = t;
+        double t = sv.gm.qr[lane + p * LD];
+        sv.gm.qr[lane + p * LD] = sv.gm.qr[lane + bi * LD];
+        sv.gm.qr[lane + bi * LD] = t;
       }
       if (lane == 0) {
         double t = sv.nu[p]; sv.nu[p] = sv.nu[bi]; sv.nu[bi] = t;
@@ -642,44 +655,44 @@ __device__ int colpiv_qr(SolveL& sv, int k, int lane) {
     wave_sync();
     // makeHouseholderInPlace on column p, rows p..k-1
     const int len = k - p;
-    double c0 = sv.qr[p + p * LD];
+    double c0 = sv.gm.qr[p + p * LD];
     double tail = 0;
-    for (int i = 1; i < len; i++) tail += sv.qr[p + i + p * LD] * sv.qr[p + i + p * LD];
+    for (int i = 1; i < len; i++) tail += sv.gm.qr[p + i + p * LD] * sv.gm.qr[p + i + p * LD];
     double tau, beta;
     if (len == 1 || tail <= DBL_MIN) {
       tau = 0;
       beta = c0;
-      if (lane >= 1 && lane < len) sv.qr[p + lane + p * LD] = 0;
+      if (lane >= 1 && lane < len) sv.gm.qr[p + lane + p * LD] = 0;
     } else {
       beta = sqrt(c0 * c0 + tail);
       if (c0 >= 0) beta = -beta;
       double den = c0 - beta;
-      if (lane >= 1 && lane < len) sv.qr[p + lane + p * LD] /= den;
+      if (lane >= 1 && lane < len) sv.gm.qr[p + lane + p * LD] /= den;
       tau = (beta - c0) / beta;
     }
     wave_sync();
-    if (lane == 0) { sv.qr[p + p * LD] = beta; sv.hc[p] = tau; }
+    if (lane == 0) { sv.gm.qr[p + p * LD] = beta; sv.hc[p] = tau; }
     // apply to columns p+1..k-1, then downdate their norms (one column per lane)
     const int j = lane;
     if (j > p && j < k) {
       if (len == 1) {
-        sv.qr[p + j * LD] *= (1 - tau);
+        sv.gm.qr[p + j * LD] *= (1 - tau);
       } else if (tau != 0) {
         double tmp = 0;
-        for (int i = 1; i < len; i++) tmp += sv.qr[p + i + p * LD] * sv.qr[p + i + j * LD];
-        tmp += sv.qr[p + j * LD];
-        sv.qr[p + j * LD] -= tau * tmp;
-        for (int i = 1; i < len; i++) sv.qr[p + i + j * LD] -= tau * sv.qr[p + i + p * LD] * tmp;
+        for (int i = 1; i < len; i++) tmp += sv.gm.qr[p + i + p * LD] * sv.gm.qr[p + i + j * LD];
+        tmp += sv.gm.qr[p + j * LD];
+        sv.gm.qr[p + j * LD] -= tau * tmp;
+        for (int i = 1; i < len; i++) sv.gm.qr[p + i + j * LD] -= tau * sv.gm.qr[p + i + p * LD] * tmp;
       }
       if (sv.nu[j] != 0) {
-        double temp = fabs(sv.qr[p + j * LD]) / sv.nu[j];
+        double temp = fabs(sv.gm.qr[p + j * LD]) / sv.nu[j];
         temp = (1 + temp) * (1 - temp);
         temp = temp < 0 ? 0 : temp;
         double ratio = sv.nu[j] / sv.nd[j];
         double temp2 = temp * (ratio * ratio);
         if (temp2 <= ndt) {
           double s = 0;
-          for (int i = p + 1; i < k; i++) s += sv.qr[i + j * LD] * sv.qr[i + j * LD];
+          for (int i = p + 1; i < k; i++) s += sv.gm.qr[i + j * LD] * sv.gm.qr[i + j * LD];
           sv.nd[j] = sqrt(s);
           sv.nu[j] = sv.nd[j];
         } else {
@@ -704,14 +717,14 @@ __device__ void qr_solve(SolveL& sv, int k, int np, int lane) {
       if (lane == p) sv.c[p] *= (1 - tau);
     } else if (tau != 0) {
       double tmp = 0;
-      for (int i = 1; i < len; i++) tmp += sv.qr[p + i + p * LD] * sv.c[p + i];
+      for (int i = 1; i < len; i++) tmp += sv.gm.qr[p + i + p * LD] * sv.c[p + i];
       tmp += sv.c[p];
       if (lane == 0) sv.c[p] -= tau * tmp;
-      if (lane >= 1 && lane < len) sv.c[p + lane] -= tau * sv.qr[p + lane + p * LD] * tmp;
+      if (lane >= 1 && lane < len) sv.c[p + lane] -= tau * sv.gm.qr[p + lane + p * LD] * tmp;
     }
     wave_sync();
   }
-  upper_solve_shared(sv.qr, sv.c, np, lane);
+  upper_solve_shared(sv.gm.qr, sv.c, np, lane);
   if (lane == 0) {
     int perm[HS_KMAX];
     for (int i = 0; i < k; i++) perm[i] = i;
@@ -762,12 +775,12 @@ __device__ uint32_t contact_solve(SolveL& sv, int k, int lane) {
       double s = 0.0;
       if (j < dimker) {
         int b0 = (i / 3) * 3;
-        for (int kk = b0; kk < b0 + 3; kk++) s = s + ntn1_at(sv, i, kk) * sv.Ny[kk + j * LD];
+        for (int kk = b0; kk < b0 + 3; kk++) s = s + ntn1_at(sv, i, kk) * sv.gm.Ny[kk + j * LD];
       } else {
         int col = sv.rycol[j - dimker];
-        for (int kk = 0; kk < k; kk++) s = s + sv.ntn0[i + kk * LD] * sv.ntn0[kk + col * LD];
+        for (int kk = 0; kk < k; kk++) s = s + sv.gm.ntn0[i + kk * LD] * sv.gm.ntn0[kk + col * LD];
       }
-      sv.M[i + j * LD] = s;
+      sv.gm.M[i + j * LD] = s;
     }
     wave_sync();
     STAMP(12);
@@ -778,7 +791,7 @@ __device__ uint32_t contact_solve(SolveL& sv, int k, int lane) {
     // rel_error = |M z - b| / |b|
     if (lane < k) {
       double s = 0.0;
-      for (int j = 0; j < k; j++) s = s + sv.M[lane + j * LD] * sv.z[j];
+      for (int j = 0; j < k; j++) s = s + sv.gm.M[lane + j * LD] * sv.z[j];
       sv.c[lane] = s - sv.b[lane];
     }
     wave_sync();
@@ -788,7 +801,7 @@ __device__ uint32_t contact_solve(SolveL& sv, int k, int lane) {
     rank0--;
     if (lane < k) {
       double s = 0.0;
-      for (int j = 0; j < dimker; j++) s = s + sv.Ny[lane + j * LD] * sv.z[j];
+      for (int j = 0; j < dimker; j++) s = s + sv.gm.Ny[lane + j * LD] * sv.z[j];
       sv.y[lane] = sv.y0[lane] + s;
     }
     wave_sync();
@@ -796,6 +809,221 @@ __device__ uint32_t contact_solve(SolveL& sv, int k, int lane) {
   } while (rel_error > 1e-6 && iters <= HS_KMAX + 1);
   if (iters > 1) flags |= HS_FLAG_RANK_RETRY;
   return flags;
+}
+
+// ---------------------------------------------------------------------------
+// S3 fast path: closed form of the same lexicographic least squares
+// (oracle/hs_oracle.cpp fast_contact_solve, identical operation order).
+// One lane per contact builds A_c, D_c, g_c; >= 3 contacts: 6x6 Schur
+// complement of the zeroth-order constraints; 1 contact: unique LS; 2 contacts:
+// rank-5 kernel along the feet line. Returns false (wave-uniform) when a
+// Cholesky pivot falls under the guard -> Eigen-style path.
+// ---------------------------------------------------------------------------
+constexpr double kFastPivotGuard = 1e-10;
+
+__device__ inline bool chol_n(double* a, int n, double guard) {  // row-major, in place
+  double mx = 0;
+  for (int i = 0; i < n; i++) mx = fmax(mx, a[i * n + i]);
+  for (int j = 0; j < n; j++) {
+    double s = a[j * n + j];
+    for (int k = 0; k < j; k++) s -= a[j * n + k] * a[j * n + k];
+    if (!(s > guard * mx)) return false;
+    double l = sqrt(s);
+    a[j * n + j] = l;
+    for (int i = j + 1; i < n; i++) {
+      double t = a[i * n + j];
+      for (int k = 0; k < j; k++) t -= a[i * n + k] * a[j * n + k];
+      a[i * n + j] = t / l;
+    }
+  }
+  return true;
+}
+
+__device__ inline void chol_solve_n(const double* L, int n, double* b) {
+  for (int i = 0; i < n; i++) {
+    double s = b[i];
+    for (int k = 0; k < i; k++) s -= L[i * n + k] * b[k];
+    b[i] = s / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double s = b[i];
+    for (int k = i + 1; k < n; k++) s -= L[k * n + i] * b[k];
+    b[i] = s / L[i * n + i];
+  }
+}
+
+__device__ inline void cross_rows(const double* d, double v[3][3]) {
+  v[0][0] = 0;     v[0][1] = -d[2]; v[0][2] = d[1];
+  v[1][0] = d[2];  v[1][1] = 0;     v[1][2] = -d[0];
+  v[2][0] = -d[1]; v[2][1] = d[0];  v[2][2] = 0;
+}
+
+
+
+__device__ bool fast_solve(const hs_topo* T, SolveL& sv, FastL& fl, const SampleL& S, int nc, int lane) {
+  const int n = T->n;
+  if (nc == 0) return true;
+  if (lane < nc) {  // A_c, D_c, g_c for contact c = lane
+    const int c = lane, fi = sv.cfoot[c];
+    const double* fp = S.fpos[fi];
+    double d0[3], v[3][3];
+    for (int r = 0; r < 3; r++) d0[r] = S.pos[0][r] - fp[r];
+    cross_rows(d0, v);
+    double* Ac = fl.A[c];
+    for (int r = 0; r < 3; r++)
+      for (int j = 0; j < 3; j++) { Ac[r * 3 + j] = (r == j) ? -1.0 : 0.0; Ac[(3 + r) * 3 + j] = v[r][j]; }
+    double D[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+    for (int p = T->footis[fi]; p >= 0 && T->node[p].parent >= 0; p = T->node[p].parent) {
+      double da[3], va[3][3];
+      for (int r = 0; r < 3; r++) da[r] = S.jpos[p][r] - fp[r];
+      cross_rows(da, va);
+      for (int r = 0; r < 3; r++) {
+        double w2 = S.jz[p][r] * S.jz[p][r];
+        if (w2 == 0) continue;
+        for (int i = 0; i < 3; i++) {
+          for (int j = 0; j < 3; j++) D[3 * i + j] += w2 * va[r][i] * va[r][j];
+          g[i] += w2 * va[r][i] * sv.x[3 * n + 3 * p + r];
+        }
+      }
+    }
+    for (int i = 0; i < 9; i++) fl.D[c][i] = D[i];
+    for (int i = 0; i < 3; i++) fl.g[c][i] = g[i];
+    int ok = 1;
+    if (nc >= 3) {
+      double L[9];
+      for (int i = 0; i < 9; i++) L[i] = D[i];
+      ok = chol_n(L, 3, kFastPivotGuard);
+      if (ok) {
+        double Dinv[9];
+        for (int j = 0; j < 3; j++) {
+          double e[3] = {0, 0, 0};
+          e[j] = 1;
+          chol_solve_n(L, 3, e);
+          for (int i = 0; i < 3; i++) Dinv[3 * i + j] = e[i];
+        }
+        double E[18];
+        for (int r = 0; r < 6; r++)
+          for (int j = 0; j < 3; j++) {
+            double s = 0;
+            for (int i = 0; i < 3; i++) s += Ac[r * 3 + i] * Dinv[3 * i + j];
+            E[r * 3 + j] = s;
+          }
+        for (int r = 0; r < 6; r++) {
+          for (int q = 0; q < 6; q++) {
+            double s = 0;
+            for (int j = 0; j < 3; j++) s += E[r * 3 + j] * Ac[q * 3 + j];
+            fl.S[c][6 * r + q] = s;
+          }
+          double s = 0;
+          for (int j = 0; j < 3; j++) s += E[r * 3 + j] * g[j];
+          fl.h[c][r] = s;
+        }
+        for (int i = 0; i < 9; i++) fl.Dinv[c][i] = Dinv[i];
+      }
+    }
+    fl.ok[c] = ok;
+  }
+  wave_sync();
+  for (int c = 0; c < nc; c++)
+    if (!fl.ok[c]) return false;
+  const double a[6] = {sv.x[0], sv.x[1], sv.x[2], sv.x[3 * n], sv.x[3 * n + 1], sv.x[3 * n + 2]};
+  int ok = 1;
+  if (nc == 1) {  // unique least-squares solution (A^T A) w = -A^T a
+    if (lane == 0) {
+      double M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+      const double* A = fl.A[0];
+      for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++)
+          for (int r = 0; r < 6; r++) M[3 * i + j] += A[r * 3 + i] * A[r * 3 + j];
+        for (int r = 0; r < 6; r++) b[i] -= A[r * 3 + i] * a[r];
+      }
+      ok = chol_n(M, 3, kFastPivotGuard);
+      if (ok) {
+        chol_solve_n(M, 3, b);
+        for (int i = 0; i < 3; i++) sv.y[i] = b[i];
+      }
+      fl.ok[0] = ok;
+    }
+  } else if (nc == 2) {  // rank 5: kernel n = (u,-u)/sqrt2 along the line between the feet
+    if (lane == 0) {
+      const double* f0 = S.fpos[sv.cfoot[0]];
+      const double* f1 = S.fpos[sv.cfoot[1]];
+      double u[3], un = 0;
+      for (int r = 0; r < 3; r++) { u[r] = f0[r] - f1[r]; un += u[r] * u[r]; }
+      un = sqrt(un);
+      ok = un > 1e-12;
+      double nv[6], M[36], b[6];
+      if (ok) {
+        for (int r = 0; r < 3; r++) { nv[r] = u[r] / un / sqrt(2.0); nv[3 + r] = -nv[r]; }
+        for (int i = 0; i < 6; i++) {
+          const double* Ai = fl.A[i / 3];
+          for (int j = 0; j < 6; j++) {
+            const double* Aj = fl.A[j / 3];
+            double s = 0;
+            for (int r = 0; r < 6; r++) s += Ai[r * 3 + i % 3] * Aj[r * 3 + j % 3];
+            M[6 * i + j] = s + nv[i] * nv[j];
+          }
+          double s = 0;
+          for (int r = 0; r < 6; r++) s += Ai[r * 3 + i % 3] * a[r];
+          b[i] = -s;
+        }
+        ok = chol_n(M, 6, kFastPivotGuard);
+      }
+      if (ok) {
+        chol_solve_n(M, 6, b);
+        double nDn = 0, nr = 0;
+        for (int c = 0; c < 2; c++)
+          for (int i = 0; i < 3; i++) {
+            double Dw = 0, Dn = 0;
+            for (int j = 0; j < 3; j++) { Dw += fl.D[c][3 * i + j] * b[3 * c + j]; Dn += fl.D[c][3 * i + j] * nv[3 * c + j]; }
+            nr += nv[3 * c + i] * (Dw + fl.g[c][i]);
+            nDn += nv[3 * c + i] * Dn;
+          }
+        ok = nDn > 0;
+        if (ok) {
+          double t = -nr / nDn;
+          for (int i = 0; i < 6; i++) sv.y[i] = b[i] + t * nv[i];
+        }
+      }
+      fl.ok[0] = ok;
+    }
+  } else {  // Schur complement of the 6 zeroth-order constraints
+    if (lane == 0) {
+      double Sm[36], h[6];
+      for (int i = 0; i < 36; i++) Sm[i] = 0;
+      for (int i = 0; i < 6; i++) h[i] = 0;
+      for (int c = 0; c < nc; c++) {
+        for (int i = 0; i < 36; i++) Sm[i] += fl.S[c][i];
+        for (int i = 0; i < 6; i++) h[i] += fl.h[c][i];
+      }
+      double lam[6];
+      for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
+      ok = chol_n(Sm, 6, kFastPivotGuard);
+      if (ok) {
+        chol_solve_n(Sm, 6, lam);
+        for (int r = 0; r < 6; r++) fl.lam[r] = lam[r];
+      }
+      fl.ok[0] = ok;
+    }
+    wave_sync();
+    if (fl.ok[0] && lane < nc) {
+      const int c = lane;
+      const double* Ac = fl.A[c];
+      double t[3];
+      for (int i = 0; i < 3; i++) {
+        double s = fl.g[c][i];
+        for (int r = 0; r < 6; r++) s += Ac[r * 3 + i] * fl.lam[r];
+        t[i] = s;
+      }
+      for (int i = 0; i < 3; i++) {
+        double s = 0;
+        for (int j = 0; j < 3; j++) s += fl.Dinv[c][3 * i + j] * t[j];
+        sv.y[3 * c + i] = -s;
+      }
+    }
+  }
+  wave_sync();
+  return fl.ok[0] != 0;
 }
 
 __device__ inline uint64_t best_key(double cot, int64_t id) {
@@ -843,9 +1071,24 @@ __global__ __launch_bounds__(WAVE) void hs_rollout_kernel(const hs_topo* __restr
     STAMP(4);
     particular(T, sm, S, lane);
     STAMP(5);
-    const int k = build_grams(T, sm, S, lane);
+    int nc = 0;
+    for (int fi = 0; fi < nf; fi++) {
+      if (S.contact[fi]) {
+        if (lane == 0) sm.sv.cfoot[nc] = fi;
+        nc++;
+      }
+    }
+    wave_sync();
+    int k = 3 * nc;
+    uint32_t flags = 0;
     STAMP(6);
-    uint32_t flags = contact_solve(sm.sv, k, lane);
+    if (fast_solve(T, sm.sv, sm.sv.fl, S, nc, lane)) {
+      if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
+      if (nc == 1) flags |= HS_FLAG_FULL_RANK;
+    } else {
+      k = build_grams(T, sm, S, lane);
+      flags = contact_solve(sm.sv, k, lane) | HS_FLAG_GENERAL;
+    }
     STAMP(7);
 
     // S4: x = x_part + N y for the hinge torque rows, motor torques (periodic.cpp:328-343)

@@ -39,6 +39,8 @@ enum {
 #define HS_FLAG_NAN          8u  /* NaN in torques or contact forces */
 #define HS_FLAG_UNREACH     16u  /* an IK target was clamped (ignore_reach, lik.cpp:250-253) */
 #define HS_FLAG_NO_CONTACT  32u  /* no foot in contact (k = 0) */
+#define HS_FLAG_GENERAL     64u  /* closed-form solve declined (conditioning guard): Eigen-style
+                                    FullPivLU/ColPivQR path used (informational) */
 
 /* Gait setup of one rollout: the fields of pgsconfigparams (pergen.h:137-146),
  * same meaning and units as a pgs_config.txt line (player.cpp:170-208).

@@ -1384,6 +1384,192 @@ void solve_contact_forces(const hso_model* m, const std::vector<double>& jz, con
   out.rel_error = rel_error;
 }
 
+// ---------------------------------------------------------------------------
+// Closed-form restatement of the two-stage least squares (the HIP kernel's fast
+// path). With the tree basis, y = w = contact forces, the zeroth-order rows are
+// A_c = [-I; [d0_c]x] (d0_c = pos_0 - fpos_c) and the first-order Gram is
+// block-diagonal, D_c = sum_a [d_a]x^T diag(jz_a^2) [d_a]x, g_c likewise with
+// the particular torques. When A has full row rank 6 (>= 3 non-collinear feet)
+// the zeroth-order minimizers are {A w = -a} and the first-order minimizer is
+// w_c = -D_c^-1 (g_c + A_c^T lam), (sum_c A_c D_c^-1 A_c^T) lam = a - sum_c A_c D_c^-1 g_c.
+// One foot: unique LS solution. Two feet: rank 5, kernel (u,-u) along the feet
+// line, t from the 1-D first-order problem. Returns false (caller falls back to
+// the Eigen-style path) when a pivot is below the conditioning guard.
+// ---------------------------------------------------------------------------
+constexpr double kFastPivotGuard = 1e-10;
+
+// in-place Cholesky of an n x n SPD matrix (row-major a[i*n+j]); false if a pivot
+// falls below guard * max diagonal
+bool chol(double* a, int n, double guard) {
+  double mx = 0;
+  for (int i = 0; i < n; i++) mx = std::max(mx, a[i * n + i]);
+  for (int j = 0; j < n; j++) {
+    double s = a[j * n + j];
+    for (int k = 0; k < j; k++) s -= a[j * n + k] * a[j * n + k];
+    if (!(s > guard * mx)) return false;
+    double l = sqrt(s);
+    a[j * n + j] = l;
+    for (int i = j + 1; i < n; i++) {
+      double t = a[i * n + j];
+      for (int k = 0; k < j; k++) t -= a[i * n + k] * a[j * n + k];
+      a[i * n + j] = t / l;
+    }
+  }
+  return true;
+}
+void chol_solve(const double* L, int n, double* b) {
+  for (int i = 0; i < n; i++) {
+    double s = b[i];
+    for (int k = 0; k < i; k++) s -= L[i * n + k] * b[k];
+    b[i] = s / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double s = b[i];
+    for (int k = i + 1; k < n; k++) s -= L[k * n + i] * b[k];
+    b[i] = s / L[i * n + i];
+  }
+}
+
+// rows of [d]x: ([d]x w)_r = v_r . w
+inline void cross_rows(const double* d, double v[3][3]) {
+  v[0][0] = 0;     v[0][1] = -d[2]; v[0][2] = d[1];
+  v[1][0] = d[2];  v[1][1] = 0;     v[1][2] = -d[0];
+  v[2][0] = -d[1]; v[2][1] = d[0];  v[2][2] = 0;
+}
+
+bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<double>& x, std::vector<double>& y) {
+  const int n = m->n;
+  std::vector<int> cf;  // contact -> foot index
+  for (int fi = 0; fi < m->nf; fi++)
+    if (d.contacts[fi]) cf.push_back(fi);
+  const int nc = (int)cf.size(), k = 3 * nc;
+  y.assign(k, 0.0);
+  if (nc == 0) return true;
+  double a[6] = {x[0], x[1], x[2], x[3 * n], x[3 * n + 1], x[3 * n + 2]};
+  // A_c (6x3), D_c (3x3), g_c (3)
+  std::vector<double> A(6 * 3 * nc), D(9 * nc, 0.0), g(3 * nc, 0.0);
+  for (int c = 0; c < nc; c++) {
+    const Vec& fp = d.fpos[cf[c]];
+    double d0[3];
+    for (int r = 0; r < 3; r++) d0[r] = d.pos[0].v[r] - fp.v[r];
+    double v[3][3];
+    cross_rows(d0, v);
+    double* Ac = &A[18 * c];  // row-major 6x3
+    for (int r = 0; r < 3; r++)
+      for (int j = 0; j < 3; j++) { Ac[r * 3 + j] = (r == j) ? -1.0 : 0.0; Ac[(3 + r) * 3 + j] = v[r][j]; }
+    for (int p = m->footis[cf[c]]; p >= 0 && m->parentis[p] >= 0; p = m->parentis[p]) {
+      double da[3];
+      for (int r = 0; r < 3; r++) da[r] = d.jpos[p].v[r] - fp.v[r];
+      double va[3][3];
+      cross_rows(da, va);
+      for (int r = 0; r < 3; r++) {
+        double w2 = d.jzaxis[p].v[r] * d.jzaxis[p].v[r];
+        if (w2 == 0) continue;
+        for (int i = 0; i < 3; i++) {
+          for (int j = 0; j < 3; j++) D[9 * c + 3 * i + j] += w2 * va[r][i] * va[r][j];
+          g[3 * c + i] += w2 * va[r][i] * x[3 * n + 3 * p + r];
+        }
+      }
+    }
+  }
+  if (nc == 1) {  // rank 3 = k: unique least-squares solution (A^T A) w = -A^T a
+    double M[9] = {0}, b[3] = {0};
+    for (int i = 0; i < 3; i++) {
+      for (int j = 0; j < 3; j++)
+        for (int r = 0; r < 6; r++) M[3 * i + j] += A[r * 3 + i] * A[r * 3 + j];
+      for (int r = 0; r < 6; r++) b[i] -= A[r * 3 + i] * a[r];
+    }
+    if (!chol(M, 3, kFastPivotGuard)) return false;
+    chol_solve(M, 3, b);
+    for (int i = 0; i < 3; i++) y[i] = b[i];
+    return true;
+  }
+  if (nc == 2) {  // rank 5: kernel n = (u, -u)/sqrt2, u along the line between the feet
+    double u[3], un = 0;
+    for (int r = 0; r < 3; r++) { u[r] = d.fpos[cf[0]].v[r] - d.fpos[cf[1]].v[r]; un += u[r] * u[r]; }
+    un = sqrt(un);
+    if (!(un > 1e-12)) return false;
+    double nv[6];
+    for (int r = 0; r < 3; r++) { nv[r] = u[r] / un / sqrt(2.0); nv[3 + r] = -nv[r]; }
+    double M[36] = {0}, b[6] = {0};
+    for (int i = 0; i < 6; i++) {
+      for (int j = 0; j < 6; j++) {
+        double s = 0;
+        for (int r = 0; r < 6; r++) s += A[18 * (i / 3) + r * 3 + i % 3] * A[18 * (j / 3) + r * 3 + j % 3];
+        M[6 * i + j] = s + nv[i] * nv[j];
+      }
+      double s = 0;
+      for (int r = 0; r < 6; r++) s += A[18 * (i / 3) + r * 3 + i % 3] * a[r];
+      b[i] = -s;
+    }
+    if (!chol(M, 6, kFastPivotGuard)) return false;
+    chol_solve(M, 6, b);
+    double nDn = 0, nr = 0;
+    for (int c = 0; c < 2; c++)
+      for (int i = 0; i < 3; i++) {
+        double Dw = 0, Dn = 0;
+        for (int j = 0; j < 3; j++) { Dw += D[9 * c + 3 * i + j] * b[3 * c + j]; Dn += D[9 * c + 3 * i + j] * nv[3 * c + j]; }
+        nr += nv[3 * c + i] * (Dw + g[3 * c + i]);
+        nDn += nv[3 * c + i] * Dn;
+      }
+    if (!(nDn > 0)) return false;
+    double t = -nr / nDn;
+    for (int i = 0; i < 6; i++) y[i] = b[i] + t * nv[i];
+    return true;
+  }
+  // nc >= 3: Schur complement on the 6 zeroth-order constraints
+  double S[36] = {0}, h[6] = {0};
+  std::vector<double> Dinv(9 * nc);
+  for (int c = 0; c < nc; c++) {
+    double L[9];
+    for (int i = 0; i < 9; i++) L[i] = D[9 * c + i];
+    if (!chol(L, 3, kFastPivotGuard)) return false;
+    for (int j = 0; j < 3; j++) {  // Dinv columns
+      double e[3] = {0, 0, 0};
+      e[j] = 1;
+      chol_solve(L, 3, e);
+      for (int i = 0; i < 3; i++) Dinv[9 * c + 3 * i + j] = e[i];
+    }
+    const double* Ac = &A[18 * c];
+    double E[18];  // A_c Dinv_c (6x3)
+    for (int r = 0; r < 6; r++)
+      for (int j = 0; j < 3; j++) {
+        double s = 0;
+        for (int i = 0; i < 3; i++) s += Ac[r * 3 + i] * Dinv[9 * c + 3 * i + j];
+        E[r * 3 + j] = s;
+      }
+    for (int r = 0; r < 6; r++) {
+      for (int q = 0; q < 6; q++) {
+        double s = 0;
+        for (int j = 0; j < 3; j++) s += E[r * 3 + j] * Ac[q * 3 + j];
+        S[6 * r + q] += s;
+      }
+      double s = 0;
+      for (int j = 0; j < 3; j++) s += E[r * 3 + j] * g[3 * c + j];
+      h[r] += s;
+    }
+  }
+  double lam[6];
+  for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
+  if (!chol(S, 6, kFastPivotGuard)) return false;
+  chol_solve(S, 6, lam);
+  for (int c = 0; c < nc; c++) {
+    const double* Ac = &A[18 * c];
+    double t[3];
+    for (int i = 0; i < 3; i++) {
+      double s = g[3 * c + i];
+      for (int r = 0; r < 6; r++) s += Ac[r * 3 + i] * lam[r];
+      t[i] = s;
+    }
+    for (int i = 0; i < 3; i++) {
+      double s = 0;
+      for (int j = 0; j < 3; j++) s += Dinv[9 * c + 3 * i + j] * t[j];
+      y[3 * c + i] = -s;
+    }
+  }
+  return true;
+}
+
 // forcetorquesolver::solve_forcetorques, ftsolver.cpp:78-102
 void solve_forcetorques(const hso_model* m, const DynRec& d, int basis, FTOut& out) {
   int n = m->n;
@@ -1417,7 +1603,16 @@ void solve_forcetorques(const hso_model* m, const DynRec& d, int basis, FTOut& o
     N = tree_null_basis(m, d);
   }
   std::vector<double> y;
-  solve_contact_forces(m, jz, x, N, y, out);
+  if (basis == HSO_BASIS_FAST && fast_contact_solve(m, d, x, y)) {
+    out.k = N.c;
+    out.iters = 1;
+    out.rank0 = -1;
+    if (N.c == 0) out.flags |= HSO_FLAG_NO_CONTACT;
+    if (N.c == 3) out.flags |= HSO_FLAG_FULL_RANK;
+  } else {
+    if (basis == HSO_BASIS_FAST) out.flags |= HSO_FLAG_GENERAL;
+    solve_contact_forces(m, jz, x, N, y, out);
+  }
   int k = N.c;
   // z = -N_cont y over all feet (ftsolver.cpp:276-284, 91)
   out.z.assign(3 * m->nf, 0.0);

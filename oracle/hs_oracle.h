@@ -37,7 +37,9 @@ typedef struct {
 
 /* null-space basis modes */
 enum { HSO_BASIS_ORTHO = 0, /* reference-faithful: orthonormal Q of QR(B^T) (ftsolver.cpp:187-202) */
-       HSO_BASIS_TREE = 1   /* tree-built basis [-B0^-1 Bc; I] (same basis the HIP kernel uses) */ };
+       HSO_BASIS_TREE = 1,  /* tree-built basis [-B0^-1 Bc; I], Eigen-style LU/QR loop */
+       HSO_BASIS_FAST = 2   /* tree basis + closed-form Schur solve (the HIP kernel's fast path),
+                               falling back to the TREE path when ill-conditioned */ };
 
 /* flag bits per step (also used by the product, see include/hslabs.h) */
 #define HSO_FLAG_RANK_RETRY   1u  /* adaptive-rank loop ran more than once (ftsolver.cpp:279-303) */
@@ -46,6 +48,7 @@ enum { HSO_BASIS_ORTHO = 0, /* reference-faithful: orthonormal Q of QR(B^T) (fts
 #define HSO_FLAG_NAN          8u  /* NaN in torques / contact forces */
 #define HSO_FLAG_UNREACH     16u  /* an IK target was clamped (ignore_reach, lik.cpp:250-253) */
 #define HSO_FLAG_NO_CONTACT  32u  /* k == 0 */
+#define HSO_FLAG_GENERAL     64u  /* FAST mode: closed form declined, Eigen-style path used */
 
 typedef struct hso_model hso_model;
 

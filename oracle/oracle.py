@@ -26,6 +26,8 @@ FLAG_LOOP_EXHAUST = 4
 FLAG_NAN = 8
 FLAG_UNREACH = 16
 FLAG_NO_CONTACT = 32
+FLAG_GENERAL = 64
+BASIS_FAST = 2
 
 
 class Gait(ctypes.Structure):

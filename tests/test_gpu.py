@@ -44,14 +44,14 @@ def test_pgs_setups_match_oracle(gpu, hmodels, oracle_mod, omodels, sid):
     name = p.fname.replace(".xml", "")
     g = gpu.run_host(hmodels[name], [p], n_t=20, k0=0, horizon=20)
     og = to_oracle_gait(oracle_mod, p)
-    for basis in (oracle_mod.BASIS_TREE, oracle_mod.BASIS_ORTHO):
+    for basis in (oracle_mod.BASIS_FAST, oracle_mod.BASIS_TREE, oracle_mod.BASIS_ORTHO):
         r = oracle_mod.rollout(omodels[name], og, 20, basis=basis)
         assert np.abs(g["tau"][0] - r["tau"]).max() < TAU_TOL * max(1, np.abs(r["tau"]).max())
         assert np.abs(g["cf"][0] - r["cf"]).max() < CF_TOL * max(1, np.abs(r["cf"]).max())
         assert np.abs(g["x"][0] - r["x"]).max() < CF_TOL * max(1, np.abs(r["x"]).max())
         assert g["work_cot"][0, 1] == pytest.approx(r["cot"], rel=1e-9, abs=1e-12)
     assert wrapdiff(g["q"][0], r["q"][2:22]).max() < 1e-12
-    assert (g["flags"][0] == r["flags"]).all()
+    assert ((g["flags"][0] & np.uint32(0xFFFFFFBF)) == r["flags"]).all()
 
 
 @pytest.mark.parametrize("path", sorted(__import__("glob").glob(os.path.join(GOLDEN, "pgs_*.npz"))),
@@ -92,7 +92,7 @@ def test_synthetic_batches_match_oracle(gpu, hmodels, oracle_mod, omodels, name,
     ok = tau_err < 1e-6 * scale  # north_star: per-joint torque error < 1e-6
     assert ok[~flagged].all(), f"{(~ok & ~flagged).sum()} steps over 1e-6"
     assert (tau_err[~flagged] < TAU_TOL * scale[~flagged]).mean() > 0.99
-    assert (g["flags"] == r["flags"]).mean() > 0.99
+    assert ((g["flags"] & np.uint32(0xFFFFFFBF)) == r["flags"]).mean() > 0.99
     fin = np.isfinite(r["cot"])
     np.testing.assert_allclose(g["work_cot"][fin, 0], r["work"][fin], rtol=1e-7, atol=1e-9)
 

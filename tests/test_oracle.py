@@ -202,3 +202,30 @@ def test_cot_sweep_period(oracle_mod, omodels):
     assert np.isfinite(cots).all() and (cots > 0).all()
     # slower gaits need less positive work per distance
     assert cots[-1] < cots[0]
+
+
+# --- the kernel's closed-form solve (oracle FAST mode) == Eigen-style two-stage LS ----------------
+@pytest.mark.parametrize("sid", PGS_IDS)
+def test_closed_form_matches_two_stage_ls(oracle_mod, omodels, sid):
+    g = pgs(oracle_mod, sid)
+    m = model_for(oracle_mod, omodels, g)
+    ro = oracle_mod.rollout(m, g, 20, basis=oracle_mod.BASIS_ORTHO)
+    rf = oracle_mod.rollout(m, g, 20, basis=oracle_mod.BASIS_FAST)
+    scale = max(1.0, np.abs(ro["tau"]).max())
+    assert np.abs(ro["tau"] - rf["tau"]).max() < 1e-12 * scale
+    assert np.abs(ro["cf"] - rf["cf"]).max() < 1e-12 * max(1.0, np.abs(ro["cf"]).max())
+    assert not (rf["flags"] & oracle_mod.FLAG_GENERAL).any()
+
+
+@pytest.mark.parametrize("name,curved", [("hexapod", False), ("hexapod", True), ("spider", True), ("myant", False)])
+def test_closed_form_synthetic(oracle_mod, omodels, name, curved):
+    from hslabs_amd import synth
+    from conftest import record_to_oracle_gait
+
+    arr = synth.gen_params(200, name, curved=curved, id0=777)
+    gs = [record_to_oracle_gait(oracle_mod, r) for r in arr]
+    rt = oracle_mod.batch(omodels[name], gs, 20, 0, 20, basis=oracle_mod.BASIS_TREE, n_threads=8)
+    rf = oracle_mod.batch(omodels[name], gs, 20, 0, 20, basis=oracle_mod.BASIS_FAST, n_threads=8)
+    err = np.abs(rt["tau"] - rf["tau"]).max(axis=2) / np.maximum(1, np.abs(rt["tau"]).max(axis=2))
+    assert err.max() < 1e-10
+    assert ((rf["flags"] & oracle_mod.FLAG_GENERAL) != 0).mean() < 0.01
