@@ -36,18 +36,28 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
-        return LIB
+def _compile(out: str, defines=(), verbose: bool = False) -> str:
     os.makedirs(OUT_DIR, exist_ok=True)
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-Wall", "-Wno-unused-function",
-           *[os.path.join(SRC, s) for s in SOURCES], "-o", LIB + ".tmp"]
+           "-ffp-contract=off", "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines],
+           *[os.path.join(SRC, s) for s in SOURCES], "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    return _compile(LIB, verbose=verbose)
+
+
+def build_variant(name: str, defines, verbose: bool = False) -> str:
+    """Tuning builds (e.g. HS_MIN_WAVES=N) next to the product library; select one with
+    HSLABS_LIB=<path> for a measurement sweep."""
+    return _compile(os.path.join(OUT_DIR, f"libhslabs_{name}.so"), defines, verbose)
 
 
 if __name__ == "__main__":

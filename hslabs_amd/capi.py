@@ -85,7 +85,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    path = _build.LIB
+    path = os.environ.get("HSLABS_LIB", _build.LIB)  # tuning-variant override (build.build_variant)
     if not os.path.exists(path):
         if not build_if_missing:
             raise HSError(f"libhslabs.so not built ({path}); run `python -m hslabs_amd.build`")

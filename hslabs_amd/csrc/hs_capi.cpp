@@ -23,15 +23,16 @@ int hip_fail(hipError_t e, const char* what) {
   return HS_E_DEVICE;
 }
 
-std::mutex g_dev_mu;
-
-// Device copy of the topology for the current device (created once per device).
-int device_topo(hs_model_t m, const hs_topo** out) {
+// Device copy of the topology for the current device (created once per device)
+// and a fallback workspace for at least n_rollouts rollouts. An outgrown
+// workspace is retired, not freed: kernels queued on other streams may still
+// use it; hs_model_free releases it.
+int device_state(hs_model_t m, int n_rollouts, const hs_topo** topo, void** ws) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
-  if (dev < 0 || dev >= 64) return fail(HS_E_DEVICE, "device index out of range");
-  std::lock_guard<std::mutex> lk(g_dev_mu);
+  if (dev < 0 || dev >= HS_MAX_DEVICES) return fail(HS_E_DEVICE, "device index out of range");
+  std::lock_guard<std::mutex> lk(m->mu);
   if (!m->dev[dev]) {
     hs_topo* d = nullptr;
     e = hipMalloc(&d, sizeof(hs_topo));
@@ -40,8 +41,25 @@ int device_topo(hs_model_t m, const hs_topo** out) {
     if (e != hipSuccess) { (void)hipFree(d); return hip_fail(e, "hipMemcpy(topo)"); }
     m->dev[dev] = d;
   }
-  *out = m->dev[dev];
+  if (m->ws_rollouts[dev] < (size_t)n_rollouts) {
+    void* w = nullptr;
+    e = hipMalloc(&w, (size_t)n_rollouts * hs::general_workspace_bytes());
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
+    if (m->ws[dev]) m->retired.emplace_back(dev, m->ws[dev]);
+    m->ws[dev] = w;
+    m->ws_rollouts[dev] = (size_t)n_rollouts;
+  }
+  *topo = m->dev[dev];
+  *ws = m->ws[dev];
   return HS_OK;
+}
+
+void free_on_device(int dev, void* p) {
+  int cur = 0;
+  if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(dev) == hipSuccess) {
+    (void)hipFree(p);
+    (void)hipSetDevice(cur);
+  }
 }
 
 int check_args(const hs_model_s* m, const hs_run_args* a) {
@@ -67,6 +85,8 @@ int hs_model_load_ex(const char* xml_path, int lik_variant, hs_model_t* out) {
   if (!xml_path || !out) return fail(HS_E_ARG, "null argument");
   hs_model_s* m = new hs_model_s;
   memset(m->dev, 0, sizeof(m->dev));
+  memset(m->ws, 0, sizeof(m->ws));
+  memset(m->ws_rollouts, 0, sizeof(m->ws_rollouts));
   std::string err;
   int rc = hs::load_model_file(xml_path, lik_variant, &m->host, err);
   if (rc != HS_OK) {
@@ -81,14 +101,11 @@ int hs_model_load(const char* xml_path, hs_model_t* out) { return hs_model_load_
 
 void hs_model_free(hs_model_t m) {
   if (!m) return;
-  for (int d = 0; d < 64; d++)
-    if (m->dev[d]) {
-      int cur = 0;
-      if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(d) == hipSuccess) {
-        (void)hipFree(m->dev[d]);
-        (void)hipSetDevice(cur);
-      }
-    }
+  for (int d = 0; d < HS_MAX_DEVICES; d++) {
+    if (m->dev[d]) free_on_device(d, m->dev[d]);
+    if (m->ws[d]) free_on_device(d, m->ws[d]);
+  }
+  for (auto& r : m->retired) free_on_device(r.first, r.second);
   delete m;
 }
 
@@ -122,9 +139,10 @@ int hs_run(hs_model_t m, const hs_run_args* a) {
   if (rc != HS_OK) return rc;
   if (a->n_rollouts == 0) return HS_OK;
   const hs_topo* d = nullptr;
-  rc = device_topo(m, &d);
+  void* ws = nullptr;
+  rc = device_state(m, a->n_rollouts + 1, &d, &ws);  // + the idle half-wave of an odd batch
   if (rc != HS_OK) return rc;
-  int e = hs::launch_rollouts(d, m->host, *a);
+  int e = hs::launch_rollouts(d, m->host, *a, ws);
   if (e != 0) return hip_fail((hipError_t)e, "kernel launch");
   return HS_OK;
 }

@@ -1,25 +1,33 @@
 // hs_kernels.hip -- the batched control-loop hot path on gfx950 (MI355X).
 //
-// One wavefront (one 64-thread workgroup) per rollout. Per rollout the wave
+// Two rollouts per wavefront (one 64-thread workgroup), 32 lanes each. Per
+// rollout the half-wave
 //   S  sets up the gait (pgssweeper::setup_pergen, pergen.cpp:453-507),
 //   K  samples the trajectory: lane = (sample, limb) runs pergen set_rec
 //      (pergen.cpp:225-239), the torso/body chain FK, limb IK (lik.cpp:151-223,
 //      316-347) and the limb FK (model.cpp:183-201), and writes the dynamic
-//      features of the parts it owns (dynrec.cpp:134-155) to an LDS ring of
-//      five samples,
+//      features of the parts it owns (dynrec.cpp:134-155) to LDS,
 //   D  lane = part: 5-point finite differences (dynrec.cpp:175-224),
 //   S1 lane = part, leaves -> root: particular solution of B0 x = f
 //      (replaces the SparseQR solve of ftsolver.cpp:107-113 by the tree
 //      back-substitution B0's block-triangular structure allows),
-//   S2 zeroth/first-order Gram matrices in the tree-built null basis
-//      [-B0^-1 Bc; I] (replaces SparseQR(B^T)'s Q, ftsolver.cpp:116-146),
-//   S3 the adaptive-rank FullPivLU / ColPivHouseholderQR loop of
-//      ftsolver.cpp:185-236 with Eigen 3.3 semantics, all 64 lanes on the
-//      k x k (k <= 18) matrices held in LDS,
+//   S3 the lexicographic least squares of ftsolver.cpp:185-236 in closed form
+//      (one lane per contact + a 6x6 Schur complement); a conditioning guard
+//      sends the step to the out-of-line Eigen-style FullPivLU/ColPivQR path
+//      (tree-built null basis, Gram matrices in a global-memory workspace),
 //   S4 motor torques, contact forces and positive work (periodic.cpp:261-343).
-// Every floating-point operation sequence matches oracle/hs_oracle.cpp's tree
-// mode (compiled with -ffp-contract=off), so the only expected differences
-// against it are ULP differences of the device sin/cos/atan2/acos/asin.
+//
+// Two LDS layouts (template parameter ONE):
+//   ONE  (horizon 1, the BASELINE configs[1] workload): the five stencil
+//        samples keep only what the step reads -- pos/ust at t-2dt, t, t+2dt,
+//        R at t+-dt, q at t-dt..t+dt, joint/foot features at t -- and the
+//        stencil-only block is reused by the fast solve once D has consumed it.
+//        ~12 KB per wave.
+//   ring (horizon > 1): five full samples in a ring, one new sample per step.
+//
+// Every floating-point operation sequence matches oracle/hs_oracle.cpp
+// (compiled with -ffp-contract=off), so the only expected differences against
+// it are ULP differences of the device sin/cos/atan2/acos/asin.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -33,15 +41,55 @@ namespace {
 using namespace hsd;
 
 constexpr int WAVE = 64;
+constexpr int HALF = 32;     // lanes per rollout: two rollouts per wavefront
 constexpr int NS = 5;        // samples in the derivative stencil (periodic.cpp:192-202)
-constexpr int LD = HS_KMAX;  // leading dimension of k x k matrices in LDS
+constexpr int LD = HS_KMAX;  // leading dimension of k x k matrices
+static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a rollout's lane maps exceed 32");
+#ifndef HS_MIN_WAVES
+#define HS_MIN_WAVES 1  // waves per SIMD the H = 1 kernel's register budget must allow
+#endif
 
-struct SampleL {
+// ---------------------------------------------------------------------------
+// LDS layouts
+// ---------------------------------------------------------------------------
+struct SampleL {  // one full sample (ring layout)
   double pos[HS_NMAX][3], jpos[HS_NMAX][3], ust[HS_NMAX][3], rot[HS_NMAX][9], jz[HS_NMAX][3];
   double fpos[HS_LMAX][3];
   double q[6 + HS_NMAX];
   int contact[HS_LMAX];
   int unreach[HS_LMAX];
+};
+
+struct FastL {  // per-contact blocks of the closed-form solve
+  double A[HS_LMAX][18], D[HS_LMAX][9], g[HS_LMAX][3], Dinv[HS_LMAX][9], S[HS_LMAX][36], h[HS_LMAX][6];
+  double lam[6];
+  int ok[HS_LMAX];
+};
+
+struct StencilL {  // ONE layout: fields only the finite differences read
+  double pos[2][HS_NMAX][3];  // t-2dt, t+2dt
+  double ust[3][HS_NMAX][3];  // t-2dt, t, t+2dt
+  double rot[2][HS_NMAX][9];  // t-dt, t+dt
+};
+
+struct CentreL {  // ONE layout: fields read after D
+  double pos[HS_NMAX][3], jpos[HS_NMAX][3], jz[HS_NMAX][3], fpos[HS_LMAX][3];
+  double q[3][6 + HS_NMAX];  // t-dt, t, t+dt
+  int contact[HS_LMAX];
+  int unreach[HS_LMAX];
+};
+
+struct RingStore {
+  SampleL s[NS];
+  FastL fl;
+};
+
+struct OneStore {
+  union {
+    StencilL sten;
+    FastL fl;  // written only after D has consumed the stencil
+  };
+  CentreL c;
 };
 
 struct SetupL {
@@ -50,55 +98,112 @@ struct SetupL {
   double t_step, max_radius, v, dt;
 };
 
-struct FastL {  // per-contact blocks exchanged through LDS
-  double A[HS_LMAX][18], D[HS_LMAX][9], g[HS_LMAX][3], Dinv[HS_LMAX][9], S[HS_LMAX][36], h[HS_LMAX][6];
-  double lam[6];
-  int ok[HS_LMAX];
-};
-
-struct GenMats {  // k x k matrices of the Eigen-style general path
-  double ntn0[HS_KMAX * LD], lu[HS_KMAX * LD], Ny[HS_KMAX * LD], M[HS_KMAX * LD], qr[HS_KMAX * LD];
-};
-
 struct SolveL {
   double f[6 * HS_NMAX], x[6 * HS_NMAX];
-  union {
-    GenMats gm;  // general path
-    FastL fl;    // fast path (dead once the general path starts)
-  };
-  double n1[HS_LMAX][9];  // 3x3 diagonal blocks of the first-order Gram (column-major)
-  double ntx0[HS_KMAX], ntx1[HS_KMAX], y0[HS_KMAX], b[HS_KMAX], z[HS_KMAX], y[HS_KMAX], c[HS_KMAX];
-  double hc[HS_KMAX], nu[HS_KMAX], nd[HS_KMAX], tau[HS_NMAX];
-  int rowsT[HS_KMAX], colsT[HS_KMAX], q[HS_KMAX], piv[HS_KMAX], rycol[HS_KMAX], cperm[HS_KMAX];
+  double y[HS_KMAX];
+  double wd[HS_NMAX];  // per-joint positive work of the step
   int cfoot[HS_LMAX];
 };
 
-struct Smem {
-  SampleL s[NS];
+template <bool ONE>
+struct Smem;
+template <>
+struct Smem<true> {
+  OneStore d;
+  SetupL st;
+  SolveL sv;
+};
+template <>
+struct Smem<false> {
+  RingStore d;
   SetupL st;
   SolveL sv;
 };
 
-__device__ inline void wave_sync() { __syncthreads(); }
+// Global-memory workspace of the out-of-line general path, one per rollout.
+struct GenWS {
+  double ntn0[HS_KMAX * LD], lu[HS_KMAX * LD], Ny[HS_KMAX * LD], M[HS_KMAX * LD], qr[HS_KMAX * LD];
+  double n1[HS_LMAX][9];  // 3x3 diagonal blocks of the first-order Gram (column-major)
+  double ntx0[HS_KMAX], ntx1[HS_KMAX], y0[HS_KMAX], b[HS_KMAX], z[HS_KMAX], c[HS_KMAX];
+  double hc[HS_KMAX], nu[HS_KMAX], nd[HS_KMAX];
+  int rowsT[HS_KMAX], colsT[HS_KMAX], q[HS_KMAX], piv[HS_KMAX], rycol[HS_KMAX], cperm[HS_KMAX];
+  double pos0[3], jpos[HS_NMAX][3], jz[HS_NMAX][3], fpos[HS_LMAX][3];  // centre-sample copy
+};
+
+// Cross-lane exchange through LDS inside the single wave of a workgroup: an
+// LDS-only workgroup fence (lgkmcnt, no vmcnt, so HBM stores stay in flight).
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+// The general path also exchanges through its global workspace.
+__device__ inline void gen_sync() { __syncthreads(); }
 
 #ifdef HS_STAMPS
 // diagnostic build only: per-phase shader-clock stamps of the first 4096 rollouts
 __device__ unsigned long long g_stamps[4096][16];
-#define STAMP(slot)                                                                  \
-  do {                                                                               \
-    if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][slot] += __builtin_amdgcn_s_memtime(); \
+#define STAMP(slot)                                                                                    \
+  do {                                                                                                 \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][slot] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define STAMP(slot) do {} while (0)
 #endif
 
+// ballot over the 32 lanes of this rollout (bit l = sub-lane l)
+__device__ inline uint32_t half_ballot(bool pred) {
+  return (uint32_t)(__ballot(pred) >> (threadIdx.x & HALF));
+}
+
 __device__ inline A34 node_joint_parent(const hs_topo* T, int v) { return load34(T->node[v].J_A_parent); }
 __device__ inline A34 node_pj(const hs_topo* T, int v) { return load34(T->node[v].A_pj_body); }
 
 // ---------------------------------------------------------------------------
+// Sample views. k = offset from the step's centre sample (-2..2).
+// ---------------------------------------------------------------------------
+struct RingWin {  // centre = sample i (ring slot i % 5)
+  SampleL* s;
+  int i;
+  __device__ SampleL& at(int k) const { return s[(i + k) % NS]; }
+  __device__ bool want_pos(int) const { return true; }
+  __device__ bool want_ust(int) const { return true; }
+  __device__ bool want_rot(int) const { return true; }
+  __device__ bool want_q(int) const { return true; }
+  __device__ bool want_centre(int) const { return true; }
+  __device__ double* pos(int k, int v) const { return at(k).pos[v]; }
+  __device__ double* ust(int k, int v) const { return at(k).ust[v]; }
+  __device__ double* rot(int k, int v) const { return at(k).rot[v]; }
+  __device__ double* q(int k) const { return at(k).q; }
+  __device__ double* jpos(int k, int v) const { return at(k).jpos[v]; }
+  __device__ double* jz(int k, int v) const { return at(k).jz[v]; }
+  __device__ double* fpos(int k, int f) const { return at(k).fpos[f]; }
+  __device__ int& contact(int k, int f) const { return at(k).contact[f]; }
+  __device__ int& unreach(int k, int L) const { return at(k).unreach[L]; }
+};
+
+struct OneWin {
+  OneStore* d;
+  __device__ bool want_pos(int k) const { return (k & 1) == 0; }
+  __device__ bool want_ust(int k) const { return (k & 1) == 0; }
+  __device__ bool want_rot(int k) const { return (k & 1) != 0; }
+  __device__ bool want_q(int k) const { return k >= -1 && k <= 1; }
+  __device__ bool want_centre(int k) const { return k == 0; }
+  __device__ double* pos(int k, int v) const { return k == 0 ? d->c.pos[v] : d->sten.pos[k > 0][v]; }
+  __device__ double* ust(int k, int v) const { return d->sten.ust[(k + 2) >> 1][v]; }
+  __device__ double* rot(int k, int v) const { return d->sten.rot[k > 0][v]; }
+  __device__ double* q(int k) const { return d->c.q[k + 1]; }
+  __device__ double* jpos(int, int v) const { return d->c.jpos[v]; }
+  __device__ double* jz(int, int v) const { return d->c.jz[v]; }
+  __device__ double* fpos(int, int f) const { return d->c.fpos[f]; }
+  __device__ int& contact(int, int f) const { return d->c.contact[f]; }
+  __device__ int& unreach(int, int L) const { return d->c.unreach[L]; }
+};
+
+// ---------------------------------------------------------------------------
 // S: gait setup, lanes L < n_limbs (pergen.cpp:453-507, 30-51, 143-153)
 // ---------------------------------------------------------------------------
-__device__ void gait_setup(const hs_topo* T, const hs_gait_params& g, int n_t, Smem& sm, int lane) {
+__device__ void gait_setup(const hs_topo* T, const hs_gait_params& g, int n_t, SetupL& st, int lane) {
   const int nl = T->n_limbs;
   if (lane < nl) {
     const int L = lane;
@@ -122,9 +227,9 @@ __device__ void gait_setup(const hs_topo* T, const hs_gait_params& g, int n_t, S
       for (int i = 0; i < 3; i++) pos[i] += d[i];
     }
     int j = T->limb_pergen[L];
-    sm.st.pos0[j][0] = pos[0];
-    sm.st.pos0[j][1] = pos[1];
-    sm.st.pos0[j][2] = T->rcap;  // set_limb_poss
+    st.pos0[j][0] = pos[0];
+    st.pos0[j][1] = pos[1];
+    st.pos0[j][2] = T->rcap;  // set_limb_poss
   }
   if (lane == 0) {  // periodicgenerator::set_step_duration
     double f = g.step_duration;
@@ -136,13 +241,13 @@ __device__ void gait_setup(const hs_topo* T, const hs_gait_params& g, int n_t, S
       for (int jj = 0; jj < jmax; jj++) {
         int k = jj + i * jmax;
         double ts = jj * (1. / 2 - t_step) / z + double(i) / 2;
-        sm.st.ts[k] = ts;
-        sm.st.xs[k] = ts + t_step / 2 - 1. / 2;
+        st.ts[k] = ts;
+        st.xs[k] = ts + t_step / 2 - 1. / 2;
       }
     }
-    sm.st.t_step = t_step;
-    sm.st.v = g.step_length / g.period;  // pergensetup::set_TLh
-    sm.st.dt = g.period / n_t;           // record_trajectory
+    st.t_step = t_step;
+    st.v = g.step_length / g.period;  // pergensetup::set_TLh
+    st.dt = g.period / n_t;           // record_trajectory
   }
   wave_sync();
   if (lane == 0) {  // compute_max_radius
@@ -150,7 +255,7 @@ __device__ void gait_setup(const hs_topo* T, const hs_gait_params& g, int n_t, S
     if (g.curvature != 0) {
       double cy = 1. / g.curvature;
       for (int j = 0; j < nl; j++) {
-        double d0 = sm.st.pos0[j][0] - 0.0, d1 = sm.st.pos0[j][1] - cy, d2 = sm.st.pos0[j][2] - 0.0;
+        double d0 = st.pos0[j][0] - 0.0, d1 = st.pos0[j][1] - cy, d2 = st.pos0[j][2] - 0.0;
         double s = 0;
         s += d0 * d0;
         s += d1 * d1;
@@ -159,7 +264,7 @@ __device__ void gait_setup(const hs_topo* T, const hs_gait_params& g, int n_t, S
         if (rad > mr) mr = rad;
       }
     }
-    sm.st.max_radius = mr;
+    st.max_radius = mr;
   }
   wave_sync();
 }
@@ -170,28 +275,44 @@ __device__ void gait_setup(const hs_topo* T, const hs_gait_params& g, int n_t, S
 __device__ inline double stepx(double t) { return (1 - cos(kPi * t)) / 2; }
 __device__ inline double stepz(double t) { double a = sin(kPi * t); return a * a; }
 
-__device__ void node_features(const hs_topo* T, int v, const A34& A, const A34* J, SampleL& S) {
+template <class W>
+__device__ void node_features(const hs_topo* T, int v, const A34& A, const A34* J, const W& w, int k) {
   const hs_node& nd = T->node[v];
-  double com[3] = {nd.com[0], nd.com[1], nd.com[2]}, p[3];
-  mulp(A, com, p);
-  for (int i = 0; i < 3; i++) S.pos[v][i] = p[i];
-  for (int i = 0; i < 3; i++) S.jpos[v][i] = J ? (*J)(i, 3) : A(i, 3);
-  S.ust[v][0] = (A(2, 1) - A(1, 2)) / 2;
-  S.ust[v][1] = (A(0, 2) - A(2, 0)) / 2;
-  S.ust[v][2] = (A(1, 0) - A(0, 1)) / 2;
-  for (int c = 0; c < 3; c++)
-    for (int r = 0; r < 3; r++) S.rot[v][c * 3 + r] = A(r, c);
-  for (int i = 0; i < 3; i++) S.jz[v][i] = J ? (*J)(i, 2) : 0.0;
-  if (nd.foot >= 0) {
-    double cap[3] = {nd.cap[0], nd.cap[1], nd.cap[2]}, fp[3];
-    mulp(A, cap, fp);
-    for (int i = 0; i < 3; i++) S.fpos[nd.foot][i] = fp[i];
-    S.contact[nd.foot] = fp[2] < T->rcap + 1e-4;
+  if (w.want_pos(k)) {
+    double com[3] = {nd.com[0], nd.com[1], nd.com[2]}, p[3];
+    mulp(A, com, p);
+    double* P = w.pos(k, v);
+    for (int i = 0; i < 3; i++) P[i] = p[i];
+  }
+  if (w.want_ust(k)) {
+    double* U = w.ust(k, v);
+    U[0] = (A(2, 1) - A(1, 2)) / 2;
+    U[1] = (A(0, 2) - A(2, 0)) / 2;
+    U[2] = (A(1, 0) - A(0, 1)) / 2;
+  }
+  if (w.want_rot(k)) {
+    double* R = w.rot(k, v);
+    for (int c = 0; c < 3; c++)
+      for (int r = 0; r < 3; r++) R[c * 3 + r] = A(r, c);
+  }
+  if (w.want_centre(k)) {
+    double* Jp = w.jpos(k, v);
+    double* Jz = w.jz(k, v);
+    for (int i = 0; i < 3; i++) Jp[i] = J ? (*J)(i, 3) : A(i, 3);
+    for (int i = 0; i < 3; i++) Jz[i] = J ? (*J)(i, 2) : 0.0;
+    if (nd.foot >= 0) {
+      double cap[3] = {nd.cap[0], nd.cap[1], nd.cap[2]}, fp[3];
+      mulp(A, cap, fp);
+      double* F = w.fpos(k, nd.foot);
+      for (int i = 0; i < 3; i++) F[i] = fp[i];
+      w.contact(k, nd.foot) = fp[2] < T->rcap + 1e-4;
+    }
   }
 }
 
+template <class W>
 __device__ void kin_sample(const hs_topo* T, const hs_gait_params& g, const SetupL& st, int isample, int L,
-                           bool ignore_reach, SampleL& S) {
+                           bool ignore_reach, const W& w, int k) {
   double t = 0;  // t accumulates dt (periodic.cpp:171-181)
   for (int i = 0; i < isample; i++) t += st.dt;
   // pergensetup::set_rec -> turn_torso (pergen.cpp:386-397)
@@ -250,16 +371,17 @@ __device__ void kin_sample(const hs_topo* T, const hs_gait_params& g, const Setu
   // set_jvalues_with_lik: torso + body chain FK, then limb IK (model.cpp:354-359, lik.cpp:89-99)
   double q6[6] = {o0[0], o0[1], o0[2], o1[0], o1[1], o1[2]};
   A34 A0 = mul(mul(node_joint_parent(T, 0), free_joint(q6)), node_pj(T, 0));
+  const bool wq = w.want_q(k);
   if (L == 0) {
-    for (int i = 0; i < 6; i++) S.q[i] = q6[i];
+    if (wq) for (int i = 0; i < 6; i++) w.q(k)[i] = q6[i];
     A34 J0 = node_joint_parent(T, 0);  // torso joint frame J = I * J_A_parent
-    node_features(T, 0, A0, &J0, S);
+    node_features(T, 0, A0, &J0, w, k);
   }
   A34 A = A0;
-  for (int k = 1; k < T->limb_chain_len[L]; k++) {
-    int v = T->limb_chain[L][k];
+  for (int kk = 1; kk < T->limb_chain_len[L]; kk++) {
+    int v = T->limb_chain[L][kk];
     A = mul(A, node_pj(T, v));
-    if (T->node[v].owner_limb == L) node_features(T, v, A, nullptr, S);
+    if (T->node[v].owner_limb == L) node_features(T, v, A, nullptr, w, k);
   }
   int c = T->limb_child[L];
   A34 J = mul(A, node_joint_parent(T, c));  // poslimb (lik.cpp:341-347)
@@ -268,45 +390,48 @@ __device__ void kin_sample(const hs_topo* T, const hs_gait_params& g, const Setu
   mulp(Jinv, target, pl);
   bool unreach = false, fail = false;
   limb_ik(T->lik_kind, T->ls, T->limb_ysign[L], pl, ja, ignore_reach, unreach, fail);
-  S.unreach[L] = (unreach || fail) ? 1 : 0;
+  if (w.want_centre(k)) w.unreach(k, L) = (unreach || fail) ? 1 : 0;
   // limb FK with the new joint values (compute_dynrecs' recompute_modelnodes)
   int v = c;
-  for (int k = 0; k < 3; k++) {
+  for (int kk = 0; kk < 3; kk++) {
     const hs_node& nd = T->node[v];
-    A34 Jv = (k == 0) ? J : mul(A, node_joint_parent(T, v));
-    A = mul(mul(Jv, hinge_joint(ja[k])), node_pj(T, v));
-    S.q[6 + nd.hinge] = ja[k];
-    node_features(T, v, A, &Jv, S);
-    if (k < 2) v = nd.kids[0];
+    A34 Jv = (kk == 0) ? J : mul(A, node_joint_parent(T, v));
+    A = mul(mul(Jv, hinge_joint(ja[kk])), node_pj(T, v));
+    if (wq) w.q(k)[6 + nd.hinge] = ja[kk];
+    node_features(T, v, A, &Jv, w, k);
+    if (kk < 2) v = nd.kids[0];
   }
 }
 
 // ---------------------------------------------------------------------------
 // D: finite differences at the centre sample, lane = part (dynrec.cpp:175-224)
 // ---------------------------------------------------------------------------
-__device__ void dynamics(const hs_topo* T, Smem& sm, int im2, int im1, int i0, int ip1, int ip2, int lane) {
+template <class W>
+__device__ void dynamics(const hs_topo* T, const SetupL& st, SolveL& sv, const W& w, int lane) {
   const int n = T->n;
   if (lane < n) {
     const int i = lane;
-    const double inv = 1. / (2 * sm.st.dt);
+    const double inv = 1. / (2 * st.dt);
     const double m = T->mass[i];
+    const double *Pp = w.pos(2, i), *P0 = w.pos(0, i), *Pm = w.pos(-2, i);
+    const double *Up = w.ust(2, i), *U0 = w.ust(0, i), *Um = w.ust(-2, i);
     double vp[3], vm[3], mr[3], wp[3], wm[3], amp[3], amm[3], amr[3];
     for (int j = 0; j < 3; j++) {
-      vp[j] = sm.s[ip2].pos[i][j] - sm.s[i0].pos[i][j];
+      vp[j] = Pp[j] - P0[j];
       vp[j] *= inv;
-      vm[j] = sm.s[i0].pos[i][j] - sm.s[im2].pos[i][j];
+      vm[j] = P0[j] - Pm[j];
       vm[j] *= inv;
       double mp = vp[j] * m, mm = vm[j] * m;
       mr[j] = mp - mm;
       mr[j] *= inv;
-      wp[j] = sm.s[ip2].ust[i][j] - sm.s[i0].ust[i][j];
+      wp[j] = Up[j] - U0[j];
       wp[j] *= inv;
-      wm[j] = sm.s[i0].ust[i][j] - sm.s[im2].ust[i][j];
+      wm[j] = U0[j] - Um[j];
       wm[j] *= inv;
     }
     // ang_mom = R (I (R^T w)), I = identity (compute_ang_mom, dynrec.cpp:205-216)
-    const double* Rp = sm.s[ip1].rot[i];
-    const double* Rm = sm.s[im1].rot[i];
+    const double* Rp = w.rot(1, i);
+    const double* Rm = w.rot(-1, i);
     double up[3], um[3];
     for (int r = 0; r < 3; r++) {
       double s = 0.0, t = 0.0;
@@ -325,10 +450,10 @@ __device__ void dynamics(const hs_topo* T, Smem& sm, int im2, int im1, int i0, i
       amr[j] *= inv;
     }
     for (int j = 0; j < 3; j++) {
-      sm.sv.f[3 * i + j] = mr[j];
-      sm.sv.f[3 * (n + i) + j] = amr[j];
+      sv.f[3 * i + j] = mr[j];
+      sv.f[3 * (n + i) + j] = amr[j];
     }
-    sm.sv.f[3 * i + 2] += m * 1.0;  // gravity, g = 1 (dynrec.cpp:291-295)
+    sv.f[3 * i + 2] += m * 1.0;  // gravity, g = 1 (dynrec.cpp:291-295)
   }
   wave_sync();
 }
@@ -336,34 +461,38 @@ __device__ void dynamics(const hs_topo* T, Smem& sm, int im2, int im1, int i0, i
 // ---------------------------------------------------------------------------
 // S1: tree back-substitution B0 x = f, level by level (deepest first)
 // ---------------------------------------------------------------------------
-__device__ void particular(const hs_topo* T, Smem& sm, const SampleL& S, int lane) {
+template <class W>
+__device__ void particular(const hs_topo* T, SolveL& sv, const W& w, int lane) {
   const int n = T->n;
   for (int level = T->max_depth; level >= 0; level--) {
     if (lane < n && T->node[lane].depth == level) {
       const int i = lane;
       const hs_node& nd = T->node[i];
+      const double* Pi = w.pos(0, i);
       double F[3], Tq[3];
-      for (int j = 0; j < 3; j++) { F[j] = sm.sv.f[3 * i + j]; Tq[j] = sm.sv.f[3 * (n + i) + j]; }
+      for (int j = 0; j < 3; j++) { F[j] = sv.f[3 * i + j]; Tq[j] = sv.f[3 * (n + i) + j]; }
       for (int kk = 0; kk < nd.nkids; kk++) {
         int c = nd.kids[kk];
-        for (int j = 0; j < 3; j++) F[j] += sm.sv.x[3 * c + j];
+        const double* Jc = w.jpos(0, c);
+        for (int j = 0; j < 3; j++) F[j] += sv.x[3 * c + j];
         double r[3];
-        for (int j = 0; j < 3; j++) r[j] = S.pos[i][j] - S.jpos[c][j];
-        const double* Fc = &sm.sv.x[3 * c];
+        for (int j = 0; j < 3; j++) r[j] = Pi[j] - Jc[j];
+        const double* Fc = &sv.x[3 * c];
         Tq[0] -= r[1] * Fc[2] - r[2] * Fc[1];
         Tq[1] -= r[2] * Fc[0] - r[0] * Fc[2];
         Tq[2] -= r[0] * Fc[1] - r[1] * Fc[0];
-        for (int j = 0; j < 3; j++) Tq[j] += sm.sv.x[3 * (n + c) + j];
+        for (int j = 0; j < 3; j++) Tq[j] += sv.x[3 * (n + c) + j];
       }
-      for (int j = 0; j < 3; j++) sm.sv.x[3 * i + j] = F[j];
+      for (int j = 0; j < 3; j++) sv.x[3 * i + j] = F[j];
       if (nd.parent >= 0) {
+        const double* Ji = w.jpos(0, i);
         double r[3];
-        for (int j = 0; j < 3; j++) r[j] = S.jpos[i][j] - S.pos[i][j];
+        for (int j = 0; j < 3; j++) r[j] = Ji[j] - Pi[j];
         Tq[0] -= r[1] * F[2] - r[2] * F[1];
         Tq[1] -= r[2] * F[0] - r[0] * F[2];
         Tq[2] -= r[0] * F[1] - r[1] * F[0];
       }
-      for (int j = 0; j < 3; j++) sm.sv.x[3 * (n + i) + j] = Tq[j];
+      for (int j = 0; j < 3; j++) sv.x[3 * (n + i) + j] = Tq[j];
     }
     wave_sync();
   }
@@ -377,52 +506,48 @@ __device__ inline double cross_e(const double* d, int jj, int row) {
   return row == 0 ? d[1] : (row == 1 ? -d[0] : 0.0);
 }
 
-// ---------------------------------------------------------------------------
+// ===========================================================================
+// General path (out of line; rare): Gram matrices of the tree-built null basis
+// and the Eigen 3.3 FullPivLU / ColPivHouseholderQR rank loop. Operates on the
+// rollout's global workspace G (centre features copied in) and on sv (LDS).
+// ===========================================================================
+
 // S2: Gram matrices of the masked, penalty-weighted null basis (ftsolver.cpp:185-207)
-// ---------------------------------------------------------------------------
-__device__ int build_grams(const hs_topo* T, Smem& sm, const SampleL& S, int lane) {
-  const int n = T->n, nf = T->nf;
-  int nc = 0;
-  for (int fi = 0; fi < nf; fi++) {
-    if (S.contact[fi]) {
-      if (lane == 0) sm.sv.cfoot[nc] = fi;
-      nc++;
-    }
-  }
-  const int k = 3 * nc;
-  wave_sync();
+__device__ void build_grams(const hs_topo* T, const SolveL& sv, GenWS& G, int k, int lane) {
+  const int n = T->n;
+  const int nc = k / 3;
   // zeroth order: rows {0,1,2} = -I, rows {3n..3n+2} = (pos_0 - fpos) x e_jj, weight 1
-  for (int e = lane; e < k * k; e += WAVE) {
+  for (int e = lane; e < k * k; e += HALF) {
     int ci = e % k, cj = e / k;
-    int fa = sm.sv.cfoot[ci / 3], fb = sm.sv.cfoot[cj / 3];
+    int fa = sv.cfoot[ci / 3], fb = sv.cfoot[cj / 3];
     int ja = ci % 3, jb = cj % 3;
     double da[3], db[3];
-    for (int r = 0; r < 3; r++) { da[r] = S.pos[0][r] - S.fpos[fa][r]; db[r] = S.pos[0][r] - S.fpos[fb][r]; }
+    for (int r = 0; r < 3; r++) { da[r] = G.pos0[r] - G.fpos[fa][r]; db[r] = G.pos0[r] - G.fpos[fb][r]; }
     double s = 0.0;
     for (int r = 0; r < 3; r++) {
       double na = (r == ja) ? -1.0 : 0.0, nb = (r == jb) ? -1.0 : 0.0;
       s = s + na * nb;
     }
     for (int r = 0; r < 3; r++) s = s + cross_e(da, ja, r) * cross_e(db, jb, r);
-    sm.sv.gm.ntn0[ci + cj * LD] = s;
+    G.ntn0[ci + cj * LD] = s;
   }
   if (lane < k) {
-    int ci = lane, fa = sm.sv.cfoot[ci / 3], ja = ci % 3;
+    int ci = lane, fa = sv.cfoot[ci / 3], ja = ci % 3;
     double da[3];
-    for (int r = 0; r < 3; r++) da[r] = S.pos[0][r] - S.fpos[fa][r];
+    for (int r = 0; r < 3; r++) da[r] = G.pos0[r] - G.fpos[fa][r];
     double s = 0.0;
-    for (int r = 0; r < 3; r++) s = s + ((r == ja) ? -1.0 : 0.0) * (1.0 * sm.sv.x[r]);
-    for (int r = 0; r < 3; r++) s = s + cross_e(da, ja, r) * (1.0 * sm.sv.x[3 * n + r]);
-    sm.sv.ntx0[ci] = s;
+    for (int r = 0; r < 3; r++) s = s + ((r == ja) ? -1.0 : 0.0) * (1.0 * sv.x[r]);
+    for (int r = 0; r < 3; r++) s = s + cross_e(da, ja, r) * (1.0 * sv.x[3 * n + r]);
+    G.ntx0[ci] = s;
   }
   // first order: torque rows of the non-root ancestors of each contact foot,
   // weighted by the joint-axis components (set_action_penalties, ftsolver.cpp:239-246)
-  for (int e = lane; e < nc * 9 + k; e += WAVE) {
+  for (int e = lane; e < nc * 9 + k; e += HALF) {
     bool is_vec = e >= nc * 9;
     int cc = is_vec ? (e - nc * 9) / 3 : e / 9;
     int a_col = is_vec ? (e - nc * 9) % 3 : (e % 9) % 3;
     int b_col = is_vec ? 0 : (e % 9) / 3;
-    int foot = T->footis[sm.sv.cfoot[cc]];
+    int foot = T->footis[sv.cfoot[cc]];
     // ancestors of foot below the root, in ascending part order (top of the chain first)
     int chain[HS_NMAX], len = 0;
     for (int a = foot; a >= 0 && T->node[a].parent >= 0; a = T->node[a].parent) chain[len++] = a;
@@ -430,29 +555,28 @@ __device__ int build_grams(const hs_topo* T, Smem& sm, const SampleL& S, int lan
     for (int t = len - 1; t >= 0; t--) {
       int a = chain[t];
       double d[3];
-      for (int r = 0; r < 3; r++) d[r] = S.jpos[a][r] - S.fpos[sm.sv.cfoot[cc]][r];
+      for (int r = 0; r < 3; r++) d[r] = G.jpos[a][r] - G.fpos[sv.cfoot[cc]][r];
       for (int r = 0; r < 3; r++) {
-        double w = S.jz[a][r];
+        double w = G.jz[a][r];
         double na = w * cross_e(d, a_col, r);
-        double nb = is_vec ? w * sm.sv.x[3 * n + 3 * a + r] : w * cross_e(d, b_col, r);
+        double nb = is_vec ? w * sv.x[3 * n + 3 * a + r] : w * cross_e(d, b_col, r);
         s = s + na * nb;
       }
     }
-    if (is_vec) sm.sv.ntx1[3 * cc + a_col] = s;
-    else sm.sv.n1[cc][b_col * 3 + a_col] = s;
+    if (is_vec) G.ntx1[3 * cc + a_col] = s;
+    else G.n1[cc][b_col * 3 + a_col] = s;
   }
-  wave_sync();
-  return k;
+  gen_sync();
 }
 
 // first-order Gram entry (block diagonal)
-__device__ inline double ntn1_at(const SolveL& sv, int i, int j) {
-  return (i / 3 == j / 3) ? sv.n1[i / 3][(j % 3) * 3 + (i % 3)] : 0.0;
+__device__ inline double ntn1_at(const GenWS& G, int i, int j) {
+  return (i / 3 == j / 3) ? G.n1[i / 3][(j % 3) * 3 + (i % 3)] : 0.0;
 }
 
-// wave-wide argmax with first-index tie break
+// half-wave argmax with first-index tie break
 __device__ inline void wave_argmax(double& v, int& idx) {
-  for (int off = 32; off >= 1; off >>= 1) {
+  for (int off = HALF / 2; off >= 1; off >>= 1) {
     double ov = __shfl_xor(v, off);
     int oi = __shfl_xor(idx, off);
     if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
@@ -464,71 +588,71 @@ struct LUInfo {
   double maxpivot;
 };
 
-// Eigen FullPivLU::computeInPlace on sv.gm.lu (k x k)
-__device__ LUInfo fullpiv_lu(SolveL& sv, int k, int lane) {
-  for (int e = lane; e < k * k; e += WAVE) {
+// Eigen FullPivLU::computeInPlace on G.lu (k x k)
+__device__ LUInfo fullpiv_lu(GenWS& G, int k, int lane) {
+  for (int e = lane; e < k * k; e += HALF) {
     int i = e % k, j = e / k;
-    sv.gm.lu[i + j * LD] = sv.gm.ntn0[i + j * LD];
+    G.lu[i + j * LD] = G.ntn0[i + j * LD];
   }
-  wave_sync();
+  gen_sync();
   LUInfo info{k, 0.0};
   for (int p = 0; p < k; p++) {
     const int m = k - p;
     double best = -1.0;
     int bidx = 1 << 30;
-    for (int e = lane; e < m * m; e += WAVE) {
-      double a = fabs(sv.gm.lu[(p + e % m) + (p + e / m) * LD]);
+    for (int e = lane; e < m * m; e += HALF) {
+      double a = fabs(G.lu[(p + e % m) + (p + e / m) * LD]);
       if (a > best || (a == best && e < bidx)) { best = a; bidx = e; }
     }
     wave_argmax(best, bidx);
     if (best == 0) {
       info.nz = p;
-      for (int i = p + lane; i < k; i += WAVE) { sv.rowsT[i] = i; sv.colsT[i] = i; }
+      for (int i = p + lane; i < k; i += HALF) { G.rowsT[i] = i; G.colsT[i] = i; }
       break;
     }
     if (best > info.maxpivot) info.maxpivot = best;
     const int bi = p + bidx % m, bj = p + bidx / m;
-    if (lane == 0) { sv.rowsT[p] = bi; sv.colsT[p] = bj; }
+    if (lane == 0) { G.rowsT[p] = bi; G.colsT[p] = bj; }
     if (bi != p && lane < k) {
-      double t = sv.gm.lu[p + lane * LD];
-      sv.gm.lu[p + lane * LD] = sv.gm.lu[bi + lane * LD];
-      sv.gm.lu[bi + lane * LD] = t;
+      double t = G.lu[p + lane * LD];
+      G.lu[p + lane * LD] = G.lu[bi + lane * LD];
+      G.lu[bi + lane * LD] = t;
     }
-    wave_sync();
+    gen_sync();
     if (bj != p && lane < k) {
-      double t = sv.gm.lu[lane + p * LD];
-      sv.gm.lu[lane + p * LD] = sv.gm.lu[lane + bj * LD];
-      sv.gm.lu[lane + bj * LD] = t;
+      double t = G.lu[lane + p * LD];
+      G.lu[lane + p * LD] = G.lu[lane + bj * LD];
+      G.lu[lane + bj * LD] = t;
     }
-    wave_sync();
+    gen_sync();
     if (p < k - 1) {
-      double piv = sv.gm.lu[p + p * LD];
-      if (lane > p && lane < k) sv.gm.lu[lane + p * LD] /= piv;
-      wave_sync();
+      double piv = G.lu[p + p * LD];
+      if (lane > p && lane < k) G.lu[lane + p * LD] /= piv;
+      gen_sync();
       const int mm = k - p - 1;
-      for (int e = lane; e < mm * mm; e += WAVE) {
+      for (int e = lane; e < mm * mm; e += HALF) {
         int i = p + 1 + e % mm, j = p + 1 + e / mm;
-        sv.gm.lu[i + j * LD] -= sv.gm.lu[i + p * LD] * sv.gm.lu[p + j * LD];
+        G.lu[i + j * LD] -= G.lu[i + p * LD] * G.lu[p + j * LD];
       }
-      wave_sync();
+      gen_sync();
     }
   }
   if (lane == 0) {
-    for (int i = 0; i < k; i++) sv.q[i] = i;
-    for (int p = 0; p < k; p++) { int t = sv.q[p]; sv.q[p] = sv.q[sv.colsT[p]]; sv.q[sv.colsT[p]] = t; }
+    for (int i = 0; i < k; i++) G.q[i] = i;
+    for (int p = 0; p < k; p++) { int t = G.q[p]; G.q[p] = G.q[G.colsT[p]]; G.q[G.colsT[p]] = t; }
   }
-  wave_sync();
+  gen_sync();
   return info;
 }
 
-__device__ inline int lu_rank(const SolveL& sv, const LUInfo& info, double thr) {
+__device__ inline int lu_rank(const GenWS& G, const LUInfo& info, double thr) {
   double pt = fabs(info.maxpivot) * thr;
   int r = 0;
-  for (int i = 0; i < info.nz; i++) r += fabs(sv.gm.lu[i + i * LD]) > pt;
+  for (int i = 0; i < info.nz; i++) r += fabs(G.lu[i + i * LD]) > pt;
   return r;
 }
 
-// column-oriented upper-triangular solve of vec[0..r) against U = mat (ld LD), all lanes
+// column-oriented upper-triangular solve of vec[0..r) against U (ld LD), all lanes
 __device__ void upper_solve_shared(const double* U, double* vec, int r, int lane) {
   for (int i = r - 1; i >= 0; i--) {
     double ci = vec[i];
@@ -537,54 +661,54 @@ __device__ void upper_solve_shared(const double* U, double* vec, int r, int lane
       if (lane < i) vec[lane] -= xi * U[lane + i * LD];
       if (lane == i) vec[i] = xi;
     }
-    wave_sync();
+    gen_sync();
   }
 }
 
-// FullPivLU::solve(-ntx0) -> sv.y0
-__device__ void lu_solve(SolveL& sv, const LUInfo& info, int k, int r, int lane) {
+// FullPivLU::solve(-ntx0) -> G.y0
+__device__ void lu_solve(GenWS& G, const LUInfo& info, int k, int r, int lane) {
   if (lane == 0) {
-    for (int i = 0; i < k; i++) sv.c[i] = -sv.ntx0[i];
-    for (int p = 0; p < k; p++) { double t = sv.c[p]; sv.c[p] = sv.c[sv.rowsT[p]]; sv.c[sv.rowsT[p]] = t; }
+    for (int i = 0; i < k; i++) G.c[i] = -G.ntx0[i];
+    for (int p = 0; p < k; p++) { double t = G.c[p]; G.c[p] = G.c[G.rowsT[p]]; G.c[G.rowsT[p]] = t; }
   }
-  if (lane < k) sv.y0[lane] = 0.0;
-  wave_sync();
+  if (lane < k) G.y0[lane] = 0.0;
+  gen_sync();
   if (r == 0) return;
   for (int j = 0; j < k; j++) {  // unit lower
-    double cj = sv.c[j];
-    if (lane > j && lane < k) sv.c[lane] -= cj * sv.gm.lu[lane + j * LD];
-    wave_sync();
+    double cj = G.c[j];
+    if (lane > j && lane < k) G.c[lane] -= cj * G.lu[lane + j * LD];
+    gen_sync();
   }
-  upper_solve_shared(sv.gm.lu, sv.c, r, lane);
-  if (lane < r) sv.y0[sv.q[lane]] = sv.c[lane];
-  wave_sync();
+  upper_solve_shared(G.lu, G.c, r, lane);
+  if (lane < r) G.y0[G.q[lane]] = G.c[lane];
+  gen_sync();
 }
 
-// FullPivLU::kernel() -> sv.gm.Ny (k x dimker); uses sv.gm.qr as scratch; sv.piv/rycol set
-__device__ void lu_kernel_image(SolveL& sv, const LUInfo& info, int k, int r, double thr, int lane) {
+// FullPivLU::kernel() -> G.Ny (k x dimker); uses G.qr as scratch; G.piv/rycol set
+__device__ void lu_kernel_image(GenWS& G, const LUInfo& info, int k, int r, double thr, int lane) {
   if (lane == 0) {
     double pt = info.maxpivot * thr;
     int p = 0;
     for (int i = 0; i < info.nz; i++)
-      if (fabs(sv.gm.lu[i + i * LD]) > pt) sv.piv[p++] = i;
-    for (int i = 0; i < r; i++) sv.rycol[i] = sv.q[sv.piv[i]];  // image columns
+      if (fabs(G.lu[i + i * LD]) > pt) G.piv[p++] = i;
+    for (int i = 0; i < r; i++) G.rycol[i] = G.q[G.piv[i]];  // image columns
   }
-  wave_sync();
+  gen_sync();
   const int dimker = k - r;
   if (dimker == 0) return;
-  double* mm = sv.gm.qr;  // r x k trapezoid
-  for (int e = lane; e < r * k; e += WAVE) {
+  double* mm = G.qr;  // r x k trapezoid
+  for (int e = lane; e < r * k; e += HALF) {
     int i = e % r, j = e / r;
-    mm[i + j * LD] = (j >= i) ? sv.gm.lu[sv.piv[i] + j * LD] : 0.0;
+    mm[i + j * LD] = (j >= i) ? G.lu[G.piv[i] + j * LD] : 0.0;
   }
-  wave_sync();
+  gen_sync();
   if (lane < r) {  // bring non-negligible pivots to the front (rows own a column swap each)
     for (int i = 0; i < r; i++) {
-      int pc = sv.piv[i];
+      int pc = G.piv[i];
       if (pc != i) { double t = mm[lane + i * LD]; mm[lane + i * LD] = mm[lane + pc * LD]; mm[lane + pc * LD] = t; }
     }
   }
-  wave_sync();
+  gen_sync();
   if (lane < dimker) {  // solve U11 X = U12, one right-hand column per lane
     double* col = &mm[(r + lane) * LD];
     for (int i = r - 1; i >= 0; i--) {
@@ -594,152 +718,149 @@ __device__ void lu_kernel_image(SolveL& sv, const LUInfo& info, int k, int r, do
       }
     }
   }
-  wave_sync();
+  gen_sync();
   if (lane < r) {
     for (int i = r - 1; i >= 0; i--) {
-      int pc = sv.piv[i];
+      int pc = G.piv[i];
       if (pc != i) { double t = mm[lane + i * LD]; mm[lane + i * LD] = mm[lane + pc * LD]; mm[lane + pc * LD] = t; }
     }
   }
-  wave_sync();
-  for (int e = lane; e < k * dimker; e += WAVE) {
+  gen_sync();
+  for (int e = lane; e < k * dimker; e += HALF) {
     int i = e % k, kk = e / k;
-    int row = sv.q[i];
+    int row = G.q[i];
     double v;
     if (i < r) v = -mm[i + (r + kk) * LD];
     else v = (i == r + kk) ? 1.0 : 0.0;
-    sv.gm.Ny[row + kk * LD] = v;
+    G.Ny[row + kk * LD] = v;
   }
-  wave_sync();
+  gen_sync();
 }
 
-// Eigen 3.3 ColPivHouseholderQR on sv.gm.qr (k x k, copy of M); returns nonzero pivots
-__device__ int colpiv_qr(SolveL& sv, int k, int lane) {
-  for (int e = lane; e < k * k; e += WAVE) {
+// Eigen 3.3 ColPivHouseholderQR on G.qr (k x k, copy of M); returns nonzero pivots
+__device__ int colpiv_qr(GenWS& G, int k, int lane) {
+  for (int e = lane; e < k * k; e += HALF) {
     int i = e % k, j = e / k;
-    sv.gm.qr[i + j * LD] = sv.gm.M[i + j * LD];
+    G.qr[i + j * LD] = G.M[i + j * LD];
   }
-  wave_sync();
+  gen_sync();
   if (lane < k) {
     double s = 0;
-    for (int i = 0; i < k; i++) s += sv.gm.qr[i + lane * LD] * sv.gm.qr[i + lane * LD];
-    sv.nd[lane] = sqrt(s);
-    sv.nu[lane] = sv.nd[lane];
+    for (int i = 0; i < k; i++) s += G.qr[i + lane * LD] * G.qr[i + lane * LD];
+    G.nd[lane] = sqrt(s);
+    G.nu[lane] = G.nd[lane];
   }
-  wave_sync();
+  gen_sync();
   double mx = 0;
-  for (int j = 0; j < k; j++) mx = fmax(mx, sv.nu[j]);
+  for (int j = 0; j < k; j++) mx = fmax(mx, G.nu[j]);
   const double th = mx * DBL_EPSILON;
   const double threshold_helper = th * th / (double)k;
   const double ndt = sqrt(DBL_EPSILON);
   int np = k;
   for (int p = 0; p < k; p++) {
     int bi = p;
-    double bv = sv.nu[p];
+    double bv = G.nu[p];
     for (int j = p + 1; j < k; j++)
-      if (sv.nu[j] > bv) { bv = sv.nu[j]; bi = j; }
+      if (G.nu[j] > bv) { bv = G.nu[j]; bi = j; }
     if (np == k && bv * bv < threshold_helper * (double)(k - p)) np = p;
-    wave_sync();
-    if (lane == 0) sv.cperm[p] = bi;
+    gen_sync();
+    if (lane == 0) G.cperm[p] = bi;
     if (bi != p) {
       if (lane < k) {
-        double t = sv.gm.qr[lane + p * LD];
-        sv.gm.qr[lane + p * LD] = sv.gm.qr[lane + bi * LD];
-        sv.gm.qr[lane + bi * LD] = t;
+        double t = G.qr[lane + p * LD];
+        G.qr[lane + p * LD] = G.qr[lane + bi * LD];
+        G.qr[lane + bi * LD] = t;
       }
       if (lane == 0) {
-        double t = sv.nu[p]; sv.nu[p] = sv.nu[bi]; sv.nu[bi] = t;
-        t = sv.nd[p]; sv.nd[p] = sv.nd[bi]; sv.nd[bi] = t;
+        double t = G.nu[p]; G.nu[p] = G.nu[bi]; G.nu[bi] = t;
+        t = G.nd[p]; G.nd[p] = G.nd[bi]; G.nd[bi] = t;
       }
     }
-    wave_sync();
+    gen_sync();
     // makeHouseholderInPlace on column p, rows p..k-1
     const int len = k - p;
-    double c0 = sv.gm.qr[p + p * LD];
+    double c0 = G.qr[p + p * LD];
     double tail = 0;
-    for (int i = 1; i < len; i++) tail += sv.gm.qr[p + i + p * LD] * sv.gm.qr[p + i + p * LD];
+    for (int i = 1; i < len; i++) tail += G.qr[p + i + p * LD] * G.qr[p + i + p * LD];
     double tau, beta;
     if (len == 1 || tail <= DBL_MIN) {
       tau = 0;
       beta = c0;
-      if (lane >= 1 && lane < len) sv.gm.qr[p + lane + p * LD] = 0;
+      if (lane >= 1 && lane < len) G.qr[p + lane + p * LD] = 0;
     } else {
       beta = sqrt(c0 * c0 + tail);
       if (c0 >= 0) beta = -beta;
       double den = c0 - beta;
-      if (lane >= 1 && lane < len) sv.gm.qr[p + lane + p * LD] /= den;
+      if (lane >= 1 && lane < len) G.qr[p + lane + p * LD] /= den;
       tau = (beta - c0) / beta;
     }
-    wave_sync();
-    if (lane == 0) { sv.gm.qr[p + p * LD] = beta; sv.hc[p] = tau; }
+    gen_sync();
+    if (lane == 0) { G.qr[p + p * LD] = beta; G.hc[p] = tau; }
     // apply to columns p+1..k-1, then downdate their norms (one column per lane)
     const int j = lane;
     if (j > p && j < k) {
       if (len == 1) {
-        sv.gm.qr[p + j * LD] *= (1 - tau);
+        G.qr[p + j * LD] *= (1 - tau);
       } else if (tau != 0) {
         double tmp = 0;
-        for (int i = 1; i < len; i++) tmp += sv.gm.qr[p + i + p * LD] * sv.gm.qr[p + i + j * LD];
-        tmp += sv.gm.qr[p + j * LD];
-        sv.gm.qr[p + j * LD] -= tau * tmp;
-        for (int i = 1; i < len; i++) sv.gm.qr[p + i + j * LD] -= tau * sv.gm.qr[p + i + p * LD] * tmp;
+        for (int i = 1; i < len; i++) tmp += G.qr[p + i + p * LD] * G.qr[p + i + j * LD];
+        tmp += G.qr[p + j * LD];
+        G.qr[p + j * LD] -= tau * tmp;
+        for (int i = 1; i < len; i++) G.qr[p + i + j * LD] -= tau * G.qr[p + i + p * LD] * tmp;
       }
-      if (sv.nu[j] != 0) {
-        double temp = fabs(sv.gm.qr[p + j * LD]) / sv.nu[j];
+      if (G.nu[j] != 0) {
+        double temp = fabs(G.qr[p + j * LD]) / G.nu[j];
         temp = (1 + temp) * (1 - temp);
         temp = temp < 0 ? 0 : temp;
-        double ratio = sv.nu[j] / sv.nd[j];
+        double ratio = G.nu[j] / G.nd[j];
         double temp2 = temp * (ratio * ratio);
         if (temp2 <= ndt) {
           double s = 0;
-          for (int i = p + 1; i < k; i++) s += sv.gm.qr[i + j * LD] * sv.gm.qr[i + j * LD];
-          sv.nd[j] = sqrt(s);
-          sv.nu[j] = sv.nd[j];
+          for (int i = p + 1; i < k; i++) s += G.qr[i + j * LD] * G.qr[i + j * LD];
+          G.nd[j] = sqrt(s);
+          G.nu[j] = G.nd[j];
         } else {
-          sv.nu[j] *= sqrt(temp);
+          G.nu[j] *= sqrt(temp);
         }
       }
     }
-    wave_sync();
+    gen_sync();
   }
   return np;
 }
 
-// QR solve M z = b (least squares, basic solution) -> sv.z
-__device__ void qr_solve(SolveL& sv, int k, int np, int lane) {
-  if (lane < k) { sv.c[lane] = sv.b[lane]; sv.z[lane] = 0.0; }
-  wave_sync();
+// QR solve M z = b (least squares, basic solution) -> G.z
+__device__ void qr_solve(GenWS& G, int k, int np, int lane) {
+  if (lane < k) { G.c[lane] = G.b[lane]; G.z[lane] = 0.0; }
+  gen_sync();
   if (np == 0) return;
   for (int p = 0; p < np; p++) {
     const int len = k - p;
-    const double tau = sv.hc[p];
+    const double tau = G.hc[p];
     if (len == 1) {
-      if (lane == p) sv.c[p] *= (1 - tau);
+      if (lane == p) G.c[p] *= (1 - tau);
     } else if (tau != 0) {
       double tmp = 0;
-      for (int i = 1; i < len; i++) tmp += sv.gm.qr[p + i + p * LD] * sv.c[p + i];
-      tmp += sv.c[p];
-      if (lane == 0) sv.c[p] -= tau * tmp;
-      if (lane >= 1 && lane < len) sv.c[p + lane] -= tau * sv.gm.qr[p + lane + p * LD] * tmp;
+      for (int i = 1; i < len; i++) tmp += G.qr[p + i + p * LD] * G.c[p + i];
+      tmp += G.c[p];
+      gen_sync();
+      if (lane == 0) G.c[p] -= tau * tmp;
+      if (lane >= 1 && lane < len) G.c[p + lane] -= tau * G.qr[p + lane + p * LD] * tmp;
     }
-    wave_sync();
+    gen_sync();
   }
-  upper_solve_shared(sv.gm.qr, sv.c, np, lane);
+  upper_solve_shared(G.qr, G.c, np, lane);
   if (lane == 0) {
     int perm[HS_KMAX];
     for (int i = 0; i < k; i++) perm[i] = i;
-    for (int p = 0; p < k; p++) { int t = perm[p]; perm[p] = perm[sv.cperm[p]]; perm[sv.cperm[p]] = t; }
-    for (int i = 0; i < np; i++) sv.z[perm[i]] = sv.c[i];
+    for (int p = 0; p < k; p++) { int t = perm[p]; perm[p] = perm[G.cperm[p]]; perm[G.cperm[p]] = t; }
+    for (int i = 0; i < np; i++) G.z[perm[i]] = G.c[i];
   }
-  wave_sync();
+  gen_sync();
 }
 
-struct StepResult {
-  uint32_t flags;
-};
-
-// S3: adaptive-rank two-stage least squares (ftsolver.cpp:277-303) -> sv.y
-__device__ uint32_t contact_solve(SolveL& sv, int k, int lane) {
+// S3 general: adaptive-rank two-stage least squares (ftsolver.cpp:277-303) -> sv.y
+__device__ uint32_t contact_solve(SolveL& sv, GenWS& G, int k, int lane) {
   uint32_t flags = 0;
   if (k == 0) return HS_FLAG_NO_CONTACT;
   int rank0 = k;
@@ -747,18 +868,15 @@ __device__ uint32_t contact_solve(SolveL& sv, int k, int lane) {
   double rel_error = 0;
   do {
     iters++;
-    STAMP(9);
-    LUInfo info = fullpiv_lu(sv, k, lane);
-    STAMP(10);
+    LUInfo info = fullpiv_lu(G, k, lane);
     double thr = DBL_EPSILON * (double)k;
-    int r = lu_rank(sv, info, thr);
+    int r = lu_rank(G, info, thr);
     for (int guard = 0; guard < 2100 && r > rank0; guard++) {  // setThreshold doubling
       thr = 2 * thr;
-      r = lu_rank(sv, info, thr);
+      r = lu_rank(G, info, thr);
     }
-    lu_solve(sv, info, k, r, lane);
-    lu_kernel_image(sv, info, k, r, thr, lane);
-    STAMP(11);
+    lu_solve(G, info, k, r, lane);
+    lu_kernel_image(G, info, k, r, thr, lane);
     if (r == k) flags |= HS_FLAG_FULL_RANK;
     rank0 = r;
     const int dimker = k - r;
@@ -766,49 +884,51 @@ __device__ uint32_t contact_solve(SolveL& sv, int k, int lane) {
     if (lane < k) {
       int i = lane, b0 = (i / 3) * 3;
       double t = 0.0;
-      for (int kk = b0; kk < b0 + 3; kk++) t = t + ntn1_at(sv, i, kk) * sv.y0[kk];
-      sv.b[i] = -(sv.ntx1[i] + t);
+      for (int kk = b0; kk < b0 + 3; kk++) t = t + ntn1_at(G, i, kk) * G.y0[kk];
+      G.b[i] = -(G.ntx1[i] + t);
     }
     // M = [ntn1 Ny, ntn0 Ry]
-    for (int e = lane; e < k * k; e += WAVE) {
+    for (int e = lane; e < k * k; e += HALF) {
       int i = e % k, j = e / k;
       double s = 0.0;
       if (j < dimker) {
         int b0 = (i / 3) * 3;
-        for (int kk = b0; kk < b0 + 3; kk++) s = s + ntn1_at(sv, i, kk) * sv.gm.Ny[kk + j * LD];
+        for (int kk = b0; kk < b0 + 3; kk++) s = s + ntn1_at(G, i, kk) * G.Ny[kk + j * LD];
       } else {
-        int col = sv.rycol[j - dimker];
-        for (int kk = 0; kk < k; kk++) s = s + sv.gm.ntn0[i + kk * LD] * sv.gm.ntn0[kk + col * LD];
+        int col = G.rycol[j - dimker];
+        for (int kk = 0; kk < k; kk++) s = s + G.ntn0[i + kk * LD] * G.ntn0[kk + col * LD];
       }
-      sv.gm.M[i + j * LD] = s;
+      G.M[i + j * LD] = s;
     }
-    wave_sync();
-    STAMP(12);
-    int np = colpiv_qr(sv, k, lane);
-    STAMP(13);
-    qr_solve(sv, k, np, lane);
-    STAMP(14);
+    gen_sync();
+    int np = colpiv_qr(G, k, lane);
+    qr_solve(G, k, np, lane);
     // rel_error = |M z - b| / |b|
     if (lane < k) {
       double s = 0.0;
-      for (int j = 0; j < k; j++) s = s + sv.gm.M[lane + j * LD] * sv.z[j];
-      sv.c[lane] = s - sv.b[lane];
+      for (int j = 0; j < k; j++) s = s + G.M[lane + j * LD] * G.z[j];
+      G.c[lane] = s - G.b[lane];
     }
-    wave_sync();
+    gen_sync();
     double rn = 0, bn = 0;
-    for (int i = 0; i < k; i++) { rn += sv.c[i] * sv.c[i]; bn += sv.b[i] * sv.b[i]; }
+    for (int i = 0; i < k; i++) { rn += G.c[i] * G.c[i]; bn += G.b[i] * G.b[i]; }
     rel_error = sqrt(rn) / sqrt(bn);
     rank0--;
     if (lane < k) {
       double s = 0.0;
-      for (int j = 0; j < dimker; j++) s = s + sv.gm.Ny[lane + j * LD] * sv.z[j];
-      sv.y[lane] = sv.y0[lane] + s;
+      for (int j = 0; j < dimker; j++) s = s + G.Ny[lane + j * LD] * G.z[j];
+      sv.y[lane] = G.y0[lane] + s;
     }
-    wave_sync();
+    gen_sync();
     if (rel_error > 1e-6 && rank0 <= 0) { flags |= HS_FLAG_LOOP_EXHAUST; break; }
   } while (rel_error > 1e-6 && iters <= HS_KMAX + 1);
   if (iters > 1) flags |= HS_FLAG_RANK_RETRY;
   return flags;
+}
+
+__device__ __noinline__ uint32_t general_solve(const hs_topo* T, SolveL* sv, GenWS* G, int k, int lane) {
+  build_grams(T, *sv, *G, k, lane);
+  return contact_solve(*sv, *G, k, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -817,38 +937,49 @@ __device__ uint32_t contact_solve(SolveL& sv, int k, int lane) {
 // One lane per contact builds A_c, D_c, g_c; >= 3 contacts: 6x6 Schur
 // complement of the zeroth-order constraints; 1 contact: unique LS; 2 contacts:
 // rank-5 kernel along the feet line. Returns false (wave-uniform) when a
-// Cholesky pivot falls under the guard -> Eigen-style path.
+// Cholesky pivot falls under the guard -> general path.
 // ---------------------------------------------------------------------------
 constexpr double kFastPivotGuard = 1e-10;
 
-__device__ inline bool chol_n(double* a, int n, double guard) {  // row-major, in place
+template <int N>
+__device__ inline bool chol_n(double* a, double guard) {  // row-major, in place
   double mx = 0;
-  for (int i = 0; i < n; i++) mx = fmax(mx, a[i * n + i]);
-  for (int j = 0; j < n; j++) {
-    double s = a[j * n + j];
-    for (int k = 0; k < j; k++) s -= a[j * n + k] * a[j * n + k];
+#pragma unroll
+  for (int i = 0; i < N; i++) mx = fmax(mx, a[i * N + i]);
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    double s = a[j * N + j];
+#pragma unroll
+    for (int k = 0; k < j; k++) s -= a[j * N + k] * a[j * N + k];
     if (!(s > guard * mx)) return false;
     double l = sqrt(s);
-    a[j * n + j] = l;
-    for (int i = j + 1; i < n; i++) {
-      double t = a[i * n + j];
-      for (int k = 0; k < j; k++) t -= a[i * n + k] * a[j * n + k];
-      a[i * n + j] = t / l;
+    a[j * N + j] = l;
+#pragma unroll
+    for (int i = j + 1; i < N; i++) {
+      double t = a[i * N + j];
+#pragma unroll
+      for (int k = 0; k < j; k++) t -= a[i * N + k] * a[j * N + k];
+      a[i * N + j] = t / l;
     }
   }
   return true;
 }
 
-__device__ inline void chol_solve_n(const double* L, int n, double* b) {
-  for (int i = 0; i < n; i++) {
+template <int N>
+__device__ inline void chol_solve_n(const double* L, double* b) {
+#pragma unroll
+  for (int i = 0; i < N; i++) {
     double s = b[i];
-    for (int k = 0; k < i; k++) s -= L[i * n + k] * b[k];
-    b[i] = s / L[i * n + i];
+#pragma unroll
+    for (int k = 0; k < i; k++) s -= L[i * N + k] * b[k];
+    b[i] = s / L[i * N + i];
   }
-  for (int i = n - 1; i >= 0; i--) {
+#pragma unroll
+  for (int i = N - 1; i >= 0; i--) {
     double s = b[i];
-    for (int k = i + 1; k < n; k++) s -= L[k * n + i] * b[k];
-    b[i] = s / L[i * n + i];
+#pragma unroll
+    for (int k = i + 1; k < N; k++) s -= L[k * N + i] * b[k];
+    b[i] = s / L[i * N + i];
   }
 }
 
@@ -858,27 +989,30 @@ __device__ inline void cross_rows(const double* d, double v[3][3]) {
   v[2][0] = -d[1]; v[2][1] = d[0];  v[2][2] = 0;
 }
 
-
-
-__device__ bool fast_solve(const hs_topo* T, SolveL& sv, FastL& fl, const SampleL& S, int nc, int lane) {
+template <class W>
+__device__ bool fast_solve(const hs_topo* T, SolveL& sv, FastL& fl, const W& w, int nc, int lane) {
   const int n = T->n;
   if (nc == 0) return true;
+  const double* P0 = w.pos(0, 0);
   if (lane < nc) {  // A_c, D_c, g_c for contact c = lane
     const int c = lane, fi = sv.cfoot[c];
-    const double* fp = S.fpos[fi];
+    const double* fp = w.fpos(0, fi);
     double d0[3], v[3][3];
-    for (int r = 0; r < 3; r++) d0[r] = S.pos[0][r] - fp[r];
+    for (int r = 0; r < 3; r++) d0[r] = P0[r] - fp[r];
     cross_rows(d0, v);
-    double* Ac = fl.A[c];
+    double Ac[18];
     for (int r = 0; r < 3; r++)
       for (int j = 0; j < 3; j++) { Ac[r * 3 + j] = (r == j) ? -1.0 : 0.0; Ac[(3 + r) * 3 + j] = v[r][j]; }
+    for (int i = 0; i < 18; i++) fl.A[c][i] = Ac[i];
     double D[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
     for (int p = T->footis[fi]; p >= 0 && T->node[p].parent >= 0; p = T->node[p].parent) {
+      const double* Jp = w.jpos(0, p);
+      const double* Jz = w.jz(0, p);
       double da[3], va[3][3];
-      for (int r = 0; r < 3; r++) da[r] = S.jpos[p][r] - fp[r];
+      for (int r = 0; r < 3; r++) da[r] = Jp[r] - fp[r];
       cross_rows(da, va);
       for (int r = 0; r < 3; r++) {
-        double w2 = S.jz[p][r] * S.jz[p][r];
+        double w2 = Jz[r] * Jz[r];
         if (w2 == 0) continue;
         for (int i = 0; i < 3; i++) {
           for (int j = 0; j < 3; j++) D[3 * i + j] += w2 * va[r][i] * va[r][j];
@@ -892,13 +1026,13 @@ __device__ bool fast_solve(const hs_topo* T, SolveL& sv, FastL& fl, const Sample
     if (nc >= 3) {
       double L[9];
       for (int i = 0; i < 9; i++) L[i] = D[i];
-      ok = chol_n(L, 3, kFastPivotGuard);
+      ok = chol_n<3>(L, kFastPivotGuard);
       if (ok) {
         double Dinv[9];
         for (int j = 0; j < 3; j++) {
           double e[3] = {0, 0, 0};
           e[j] = 1;
-          chol_solve_n(L, 3, e);
+          chol_solve_n<3>(L, e);
           for (int i = 0; i < 3; i++) Dinv[3 * i + j] = e[i];
         }
         double E[18];
@@ -937,17 +1071,17 @@ __device__ bool fast_solve(const hs_topo* T, SolveL& sv, FastL& fl, const Sample
           for (int r = 0; r < 6; r++) M[3 * i + j] += A[r * 3 + i] * A[r * 3 + j];
         for (int r = 0; r < 6; r++) b[i] -= A[r * 3 + i] * a[r];
       }
-      ok = chol_n(M, 3, kFastPivotGuard);
+      ok = chol_n<3>(M, kFastPivotGuard);
       if (ok) {
-        chol_solve_n(M, 3, b);
+        chol_solve_n<3>(M, b);
         for (int i = 0; i < 3; i++) sv.y[i] = b[i];
       }
       fl.ok[0] = ok;
     }
   } else if (nc == 2) {  // rank 5: kernel n = (u,-u)/sqrt2 along the line between the feet
     if (lane == 0) {
-      const double* f0 = S.fpos[sv.cfoot[0]];
-      const double* f1 = S.fpos[sv.cfoot[1]];
+      const double* f0 = w.fpos(0, sv.cfoot[0]);
+      const double* f1 = w.fpos(0, sv.cfoot[1]);
       double u[3], un = 0;
       for (int r = 0; r < 3; r++) { u[r] = f0[r] - f1[r]; un += u[r] * u[r]; }
       un = sqrt(un);
@@ -967,10 +1101,10 @@ __device__ bool fast_solve(const hs_topo* T, SolveL& sv, FastL& fl, const Sample
           for (int r = 0; r < 6; r++) s += Ai[r * 3 + i % 3] * a[r];
           b[i] = -s;
         }
-        ok = chol_n(M, 6, kFastPivotGuard);
+        ok = chol_n<6>(M, kFastPivotGuard);
       }
       if (ok) {
-        chol_solve_n(M, 6, b);
+        chol_solve_n<6>(M, b);
         double nDn = 0, nr = 0;
         for (int c = 0; c < 2; c++)
           for (int i = 0; i < 3; i++) {
@@ -998,9 +1132,9 @@ __device__ bool fast_solve(const hs_topo* T, SolveL& sv, FastL& fl, const Sample
       }
       double lam[6];
       for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
-      ok = chol_n(Sm, 6, kFastPivotGuard);
+      ok = chol_n<6>(Sm, kFastPivotGuard);
       if (ok) {
-        chol_solve_n(Sm, 6, lam);
+        chol_solve_n<6>(Sm, lam);
         for (int r = 0; r < 6; r++) fl.lam[r] = lam[r];
       }
       fl.ok[0] = ok;
@@ -1033,142 +1167,150 @@ __device__ inline uint64_t best_key(double cot, int64_t id) {
   return ((uint64_t)ord << 32) | (uint32_t)id;
 }
 
-__global__ __launch_bounds__(WAVE) void hs_rollout_kernel(const hs_topo* __restrict__ T, hs_run_args a) {
-  __shared__ Smem sm;
-  const int lane = threadIdx.x;
-  const int b = blockIdx.x;
-  if (b >= a.n_rollouts) return;
-  const hs_gait_params g = a.params[b];
+// ---------------------------------------------------------------------------
+// One control-loop step at centre sample i (row = b * H + h of the outputs)
+// ---------------------------------------------------------------------------
+template <class W>
+__device__ void step(const hs_topo* T, const hs_run_args& a, const SetupL& st, SolveL& sv, FastL& fl, const W& w,
+                     GenWS* gws, int b, bool live, int h, double& work, int lane) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
+  STAMP(3);
+  dynamics(T, st, sv, w, lane);
+  STAMP(4);
+  particular(T, sv, w, lane);
+  STAMP(5);
+  // contact list in foot order (ftsolver contact columns)
+  const uint32_t cmask = half_ballot(lane < nf && w.contact(0, lane));
+  const int nc = __popc(cmask);
+  if (lane < nf && ((cmask >> lane) & 1)) sv.cfoot[__popc(cmask & ((1u << lane) - 1))] = lane;
+  wave_sync();
+  int k = 3 * nc;
+  uint32_t flags = 0;
+  STAMP(6);
+  if (fast_solve(T, sv, fl, w, nc, lane)) {
+    if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
+    if (nc == 1) flags |= HS_FLAG_FULL_RANK;
+  } else {
+    GenWS* G = gws + b;
+    for (int e = lane; e < 3 * n; e += HALF) {
+      G->jpos[e / 3][e % 3] = w.jpos(0, e / 3)[e % 3];
+      G->jz[e / 3][e % 3] = w.jz(0, e / 3)[e % 3];
+    }
+    if (lane < 3 * nf) G->fpos[lane / 3][lane % 3] = w.fpos(0, lane / 3)[lane % 3];
+    if (lane < 3) G->pos0[lane] = w.pos(0, 0)[lane];
+    gen_sync();
+    flags = general_solve(T, &sv, G, k, lane) | HS_FLAG_GENERAL;
+  }
+  STAMP(7);
+
+  // S4: x = x_part + N y for the hinge torque rows, motor torques (periodic.cpp:328-343),
+  // and the step's positive work (compute_vel_traj + work_over_period, periodic.cpp:261-307)
+  const size_t row = (size_t)b * a.horizon + h;
+  double tq = 0.0;
+  if (lane < nmj) {
+    int h_id = T->hinge_ids[lane];
+    int fi = T->node[h_id].limb_below;
+    int cc = -1;
+    for (int c = 0; c < nc; c++) if (sv.cfoot[c] == fi) cc = c;
+    const double* Jp = w.jpos(0, h_id);
+    const double* Jz = w.jz(0, h_id);
+    double d[3];
+    if (cc >= 0) {
+      const double* fp = w.fpos(0, fi);
+      for (int rr = 0; rr < 3; rr++) d[rr] = Jp[rr] - fp[rr];
+    }
+    for (int r = 0; r < 3; r++) {
+      double s = 0.0;
+      if (cc >= 0)
+        for (int jj = 0; jj < 3; jj++) s = s + cross_e(d, jj, r) * sv.y[3 * cc + jj];
+      double xr = sv.x[3 * n + 3 * h_id + r] + s;
+      tq = tq + Jz[r] * xr;
+    }
+    if (live && a.tau) a.tau[row * nmj + lane] = tq;
+    double dd = w.q(1)[6 + lane] - w.q(-1)[6 + lane];
+    if (dd > kPi) dd -= 2 * kPi;
+    else if (dd < -kPi) dd += 2 * kPi;
+    double jvel = dd / (2 * st.dt);
+    double dw = tq * jvel;
+    sv.wd[lane] = (dw > 0) ? dw : 0;
+  }
+  if (half_ballot(lane < nmj && tq != tq) || half_ballot(lane < k && sv.y[lane] != sv.y[lane])) flags |= HS_FLAG_NAN;
+  if (half_ballot(lane < nl && w.unreach(0, lane))) flags |= HS_FLAG_UNREACH;
+  // contact forces z = -N_cont y (ftsolver.cpp:91, 276-284)
+  if (live && a.cf && lane < 3 * nf) {
+    int fi = lane / 3, j = lane % 3;
+    double zv = -0.0;
+    for (int c = 0; c < nc; c++) if (sv.cfoot[c] == fi) zv = -(0.0 + (-1.0) * sv.y[3 * c + j]);
+    a.cf[row * 3 * nf + lane] = zv;
+  }
+  if (live && a.x) {  // full joint force/torque vector x += N y
+    for (int rI = lane; rI < 6 * n; rI += HALF) {
+      int part = (rI < 3 * n) ? rI / 3 : (rI - 3 * n) / 3, comp = rI % 3;
+      double s = 0.0;
+      for (int c = 0; c < nc; c++) {
+        int foot = T->footis[sv.cfoot[c]];
+        bool anc = false;
+        for (int aa = foot; aa >= 0; aa = T->node[aa].parent) anc |= (aa == part);
+        if (!anc) continue;
+        if (rI < 3 * n) {
+          s = s + (-1.0) * sv.y[3 * c + comp];
+        } else {
+          const double* ref = (T->node[part].parent >= 0) ? w.jpos(0, part) : w.pos(0, part);
+          const double* fp = w.fpos(0, sv.cfoot[c]);
+          double d[3];
+          for (int rr = 0; rr < 3; rr++) d[rr] = ref[rr] - fp[rr];
+          for (int jj = 0; jj < 3; jj++) s = s + cross_e(d, jj, comp) * sv.y[3 * c + jj];
+        }
+      }
+      a.x[row * 6 * n + rI] = sv.x[rI] + s;
+    }
+  }
+  if (live && a.q && lane < cfg) a.q[row * cfg + lane] = w.q(0)[lane];
+  if (live && a.flags && lane == 0) a.flags[row] = flags;
+  wave_sync();
+  double work_dt = 0;  // summed in joint order like work_over_period
+  for (int jj = 0; jj < nmj; jj++) work_dt += sv.wd[jj];
+  work_dt *= st.dt;
+  work += work_dt;
+  STAMP(8);
+}
+
+template <bool ONE>
+__global__ __launch_bounds__(WAVE, ONE ? HS_MIN_WAVES : 1) void hs_rollout_kernel(const hs_topo* __restrict__ T,
+                                                                                 hs_run_args a, GenWS* __restrict__ gws) {
+  __shared__ Smem<ONE> smem[2];
+  const int sub = threadIdx.x / HALF;  // rollout slot within the wave
+  const int lane = threadIdx.x % HALF; // lane within the rollout
+  const int b = blockIdx.x * 2 + sub;
+  const bool live = b < a.n_rollouts;  // an odd batch leaves the last half computing a copy, storing nothing
+  const int bb = live ? b : a.n_rollouts - 1;
+  Smem<ONE>& sm = smem[sub];
+  double work = (live && a.accumulate && a.work_cot) ? a.work_cot[2 * (size_t)b] : 0.0;
+  const hs_gait_params g = a.params[bb];
+  const int nl = T->n_limbs;
   const bool ignore_reach = a.ignore_reach != 0;
 
   STAMP(0);
-  gait_setup(T, g, a.n_t, sm, lane);
+  gait_setup(T, g, a.n_t, sm.st, lane);
   STAMP(1);
 
-  // initial window: samples k0 .. k0+4, lane = (sample, limb)
-  {
-    int sl = lane / nl, L = lane % nl;
-    if (sl < NS) {
-      int i = a.k0 + sl;
-      kin_sample(T, g, sm.st, i, L, ignore_reach, sm.s[i % NS]);
-    }
-  }
-  wave_sync();
-  STAMP(2);
-
-  double work = (a.accumulate && a.work_cot) ? a.work_cot[2 * (size_t)b] : 0.0;
   for (int h = 0; h < a.horizon; h++) {
-    const int i = a.k0 + h + 2;
-    if (h > 0) {
-      if (lane < nl) kin_sample(T, g, sm.st, i + 2, lane, ignore_reach, sm.s[(i + 2) % NS]);
+    const int i = a.k0 + h + 2;  // centre sample of this step
+    // K: the whole window on the first step, then the newest sample (lane = (sample, limb))
+    {
+      const int sl = (h == 0) ? lane / nl : NS - 1;
+      const int L = (h == 0) ? lane % nl : lane;
+      if (sl < NS && L < nl) {
+        if constexpr (ONE) kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin{&sm.d}, sl - 2);
+        else kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, RingWin{sm.d.s, i - 2 + sl}, 0);
+      }
       wave_sync();
     }
-    const int s0 = i % NS;
-    const SampleL& S = sm.s[s0];
-    STAMP(3);
-    dynamics(T, sm, (i - 2) % NS, (i - 1) % NS, s0, (i + 1) % NS, (i + 2) % NS, lane);
-    STAMP(4);
-    particular(T, sm, S, lane);
-    STAMP(5);
-    int nc = 0;
-    for (int fi = 0; fi < nf; fi++) {
-      if (S.contact[fi]) {
-        if (lane == 0) sm.sv.cfoot[nc] = fi;
-        nc++;
-      }
-    }
-    wave_sync();
-    int k = 3 * nc;
-    uint32_t flags = 0;
-    STAMP(6);
-    if (fast_solve(T, sm.sv, sm.sv.fl, S, nc, lane)) {
-      if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
-      if (nc == 1) flags |= HS_FLAG_FULL_RANK;
-    } else {
-      k = build_grams(T, sm, S, lane);
-      flags = contact_solve(sm.sv, k, lane) | HS_FLAG_GENERAL;
-    }
-    STAMP(7);
-
-    // S4: x = x_part + N y for the hinge torque rows, motor torques (periodic.cpp:328-343)
-    if (lane < nmj) {
-      int h_id = T->hinge_ids[lane];
-      int fi = T->node[h_id].limb_below;
-      int cc = -1;
-      for (int c = 0; c < k / 3; c++) if (sm.sv.cfoot[c] == fi) cc = c;
-      double tq = 0.0;
-      for (int r = 0; r < 3; r++) {
-        double s = 0.0;
-        if (cc >= 0) {
-          double d[3];
-          for (int rr = 0; rr < 3; rr++) d[rr] = S.jpos[h_id][rr] - S.fpos[fi][rr];
-          for (int jj = 0; jj < 3; jj++) s = s + cross_e(d, jj, r) * sm.sv.y[3 * cc + jj];
-        }
-        double xr = sm.sv.x[3 * n + 3 * h_id + r] + s;
-        tq = tq + S.jz[h_id][r] * xr;
-      }
-      sm.sv.tau[lane] = tq;
-    }
-    wave_sync();
-    // contact forces z = -N_cont y (ftsolver.cpp:91, 276-284)
-    if (a.cf && lane < 3 * nf) {
-      int fi = lane / 3, j = lane % 3;
-      double zv = -0.0;
-      for (int c = 0; c < k / 3; c++) if (sm.sv.cfoot[c] == fi) zv = -(0.0 + (-1.0) * sm.sv.y[3 * c + j]);
-      a.cf[((size_t)b * a.horizon + h) * 3 * nf + lane] = zv;
-    }
-    if (a.x) {  // full joint force/torque vector x += N y
-      for (int rI = lane; rI < 6 * n; rI += WAVE) {
-        int part = (rI < 3 * n) ? rI / 3 : (rI - 3 * n) / 3, comp = rI % 3;
-        double s = 0.0;
-        for (int c = 0; c < k / 3; c++) {
-          int foot = T->footis[sm.sv.cfoot[c]];
-          bool anc = false;
-          for (int aa = foot; aa >= 0; aa = T->node[aa].parent) anc |= (aa == part);
-          if (!anc) continue;
-          if (rI < 3 * n) {
-            s = s + (-1.0) * sm.sv.y[3 * c + comp];
-          } else {
-            const double* ref = (T->node[part].parent >= 0) ? S.jpos[part] : S.pos[part];
-            double d[3];
-            for (int rr = 0; rr < 3; rr++) d[rr] = ref[rr] - S.fpos[sm.sv.cfoot[c]][rr];
-            for (int jj = 0; jj < 3; jj++) s = s + cross_e(d, jj, comp) * sm.sv.y[3 * c + jj];
-          }
-        }
-        a.x[((size_t)b * a.horizon + h) * 6 * n + rI] = sm.sv.x[rI] + s;
-      }
-    }
-    if (a.tau && lane < nmj) a.tau[((size_t)b * a.horizon + h) * nmj + lane] = sm.sv.tau[lane];
-    if (a.q && lane < cfg) a.q[((size_t)b * a.horizon + h) * cfg + lane] = S.q[lane];
-    // positive work over this step (compute_vel_traj + work_over_period)
-    {
-      const SampleL& Sp = sm.s[(i + 1) % NS];
-      const SampleL& Sm = sm.s[(i - 1) % NS];
-      double work_dt = 0;
-      for (int jj = 0; jj < nmj; jj++) {
-        double dd = Sp.q[6 + jj] - Sm.q[6 + jj];
-        if (dd > kPi) dd -= 2 * kPi;
-        else if (dd < -kPi) dd += 2 * kPi;
-        double jvel = dd / (2 * sm.st.dt);
-        double dw = sm.sv.tau[jj] * jvel;
-        dw = (dw > 0) ? dw : 0;
-        work_dt += dw;
-      }
-      work_dt *= sm.st.dt;
-      work += work_dt;
-      for (int jj = 0; jj < nmj; jj++) {
-        double v = sm.sv.tau[jj];
-        if (v != v) flags |= HS_FLAG_NAN;
-      }
-      for (int c = 0; c < 3 * (k / 3); c++) if (sm.sv.y[c] != sm.sv.y[c]) flags |= HS_FLAG_NAN;
-      for (int L = 0; L < nl; L++) if (S.unreach[L]) flags |= HS_FLAG_UNREACH;
-    }
-    if (a.flags && lane == 0) a.flags[(size_t)b * a.horizon + h] = flags;
-    wave_sync();
-    STAMP(8);
+    STAMP(2);
+    if constexpr (ONE) step(T, a, sm.st, sm.sv, sm.d.fl, OneWin{&sm.d}, gws, b, live, h, work, lane);
+    else step(T, a, sm.st, sm.sv, sm.d.fl, RingWin{sm.d.s, i}, gws, b, live, h, work, lane);
   }
-  if (lane == 0) {
+  if (lane == 0 && live) {
     double cot = work / (T->total_mass * g.step_length);
     if (a.work_cot) {
       a.work_cot[2 * (size_t)b] = work;
@@ -1194,11 +1336,19 @@ extern "C" int hs_debug_clear_stamps() {
 
 namespace hs {
 
-int launch_rollouts(const hs_topo* d_topo, const hs_topo& h_topo, const hs_run_args& a) {
+size_t general_workspace_bytes() { return sizeof(GenWS); }
+int rollouts_per_wave() { return 2; }
+
+int launch_rollouts(const hs_topo* d_topo, const hs_topo& h_topo, const hs_run_args& a, void* workspace) {
   (void)h_topo;
   if (a.n_rollouts <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
-  hipLaunchKernelGGL(hs_rollout_kernel, dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, a);
+  GenWS* ws = (GenWS*)workspace;
+  const dim3 grid((a.n_rollouts + 1) / 2);  // two rollouts per wavefront
+  if (a.horizon == 1)
+    hipLaunchKernelGGL(hs_rollout_kernel<true>, grid, dim3(WAVE), 0, st, d_topo, a, ws);
+  else
+    hipLaunchKernelGGL(hs_rollout_kernel<false>, grid, dim3(WAVE), 0, st, d_topo, a, ws);
   return (int)hipGetLastError();
 }
 
