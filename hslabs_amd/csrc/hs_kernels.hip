@@ -32,6 +32,7 @@
 
 #include <cfloat>
 #include <cstdint>
+#include <type_traits>
 
 #include "hs_internal.h"
 #include "hs_math.h"
@@ -46,16 +47,19 @@ constexpr int NS = 5;        // samples in the derivative stencil (periodic.cpp:
 constexpr int LD = HS_KMAX;  // leading dimension of k x k matrices
 static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a rollout's lane maps exceed 32");
 #ifndef HS_MIN_WAVES
-#define HS_MIN_WAVES 1  // waves per SIMD the H = 1 kernel's register budget must allow
+#define HS_MIN_WAVES 2  // waves per SIMD the H = 1 register budget allows (8 workgroups/CU at 19.5 KB LDS)
 #endif
 
 // ---------------------------------------------------------------------------
 // LDS layouts
 // ---------------------------------------------------------------------------
+// NM = part capacity of the LDS layouts (the host picks the smallest instantiation >= n,
+// so LDS per rollout follows the model: hexapod 9.5 KB at H = 1).
+template <int NM>
 struct SampleL {  // one full sample (ring layout)
-  double pos[HS_NMAX][3], jpos[HS_NMAX][3], ust[HS_NMAX][3], rot[HS_NMAX][9], jz[HS_NMAX][3];
+  double pos[NM][3], jpos[NM][3], ust[NM][3], rot[NM][9], jz[NM][3];
   double fpos[HS_LMAX][3];
-  double q[6 + HS_NMAX];
+  double q[6 + NM];
   int contact[HS_LMAX];
   int unreach[HS_LMAX];
 };
@@ -66,30 +70,42 @@ struct FastL {  // per-contact blocks of the closed-form solve
   int ok[HS_LMAX];
 };
 
-struct StencilL {  // ONE layout: fields only the finite differences read
-  double pos[2][HS_NMAX][3];  // t-2dt, t+2dt
-  double ust[3][HS_NMAX][3];  // t-2dt, t, t+2dt
-  double rot[2][HS_NMAX][9];  // t-dt, t+dt
+struct WorkL {  // per-joint positive work of the step (outputs phase; FastL is dead by then)
+  double wd[HS_NMAX];
 };
 
+template <int NM>
+struct StencilL {  // ONE layout: fields only the finite differences read
+  double pos[2][NM][3];  // t-2dt, t+2dt
+  double ust[3][NM][3];  // t-2dt, t, t+2dt
+  double rot[2][NM][9];  // t-dt, t+dt
+};
+
+template <int NM>
 struct CentreL {  // ONE layout: fields read after D
-  double pos[HS_NMAX][3], jpos[HS_NMAX][3], jz[HS_NMAX][3], fpos[HS_LMAX][3];
-  double q[3][6 + HS_NMAX];  // t-dt, t, t+dt
+  double pos[NM][3], jpos[NM][3], jz[NM][3], fpos[HS_LMAX][3];
+  double q[3][6 + NM];  // t-dt, t, t+dt
   int contact[HS_LMAX];
   int unreach[HS_LMAX];
 };
 
+template <int NM>
 struct RingStore {
-  SampleL s[NS];
-  FastL fl;
+  SampleL<NM> s[NS];
+  union {
+    FastL fl;
+    WorkL wk;
+  };
 };
 
+template <int NM>
 struct OneStore {
   union {
-    StencilL sten;
+    StencilL<NM> sten;
     FastL fl;  // written only after D has consumed the stencil
+    WorkL wk;
   };
-  CentreL c;
+  CentreL<NM> c;
 };
 
 struct SetupL {
@@ -98,26 +114,21 @@ struct SetupL {
   double t_step, max_radius, v, dt;
 };
 
+template <int NM>
 struct SolveL {
-  double f[6 * HS_NMAX], x[6 * HS_NMAX];
+  union {  // particular() overwrites each part's f with its x in place
+    double f[6 * NM];
+    double x[6 * NM];
+  };
   double y[HS_KMAX];
-  double wd[HS_NMAX];  // per-joint positive work of the step
   int cfoot[HS_LMAX];
 };
 
-template <bool ONE>
-struct Smem;
-template <>
-struct Smem<true> {
-  OneStore d;
+template <bool ONE, int NM>
+struct Smem {
+  typename std::conditional<ONE, OneStore<NM>, RingStore<NM>>::type d;
   SetupL st;
-  SolveL sv;
-};
-template <>
-struct Smem<false> {
-  RingStore d;
-  SetupL st;
-  SolveL sv;
+  SolveL<NM> sv;
 };
 
 // Global-memory workspace of the out-of-line general path, one per rollout.
@@ -162,10 +173,11 @@ __device__ inline A34 node_pj(const hs_topo* T, int v) { return load34(T->node[v
 // ---------------------------------------------------------------------------
 // Sample views. k = offset from the step's centre sample (-2..2).
 // ---------------------------------------------------------------------------
+template <int NM>
 struct RingWin {  // centre = sample i (ring slot i % 5)
-  SampleL* s;
+  SampleL<NM>* s;
   int i;
-  __device__ SampleL& at(int k) const { return s[(i + k) % NS]; }
+  __device__ SampleL<NM>& at(int k) const { return s[(i + k) % NS]; }
   __device__ bool want_pos(int) const { return true; }
   __device__ bool want_ust(int) const { return true; }
   __device__ bool want_rot(int) const { return true; }
@@ -182,8 +194,9 @@ struct RingWin {  // centre = sample i (ring slot i % 5)
   __device__ int& unreach(int k, int L) const { return at(k).unreach[L]; }
 };
 
+template <int NM>
 struct OneWin {
-  OneStore* d;
+  OneStore<NM>* d;
   __device__ bool want_pos(int k) const { return (k & 1) == 0; }
   __device__ bool want_ust(int k) const { return (k & 1) == 0; }
   __device__ bool want_rot(int k) const { return (k & 1) != 0; }
@@ -311,7 +324,7 @@ __device__ void node_features(const hs_topo* T, int v, const A34& A, const A34* 
 }
 
 template <class W>
-__device__ void kin_sample(const hs_topo* T, const hs_gait_params& g, const SetupL& st, int isample, int L,
+__device__ __noinline__ void kin_sample(const hs_topo* T, const hs_gait_params& g, const SetupL& st, int isample, int L,
                            bool ignore_reach, const W& w, int k) {
   double t = 0;  // t accumulates dt (periodic.cpp:171-181)
   for (int i = 0; i < isample; i++) t += st.dt;
@@ -406,8 +419,8 @@ __device__ void kin_sample(const hs_topo* T, const hs_gait_params& g, const Setu
 // ---------------------------------------------------------------------------
 // D: finite differences at the centre sample, lane = part (dynrec.cpp:175-224)
 // ---------------------------------------------------------------------------
-template <class W>
-__device__ void dynamics(const hs_topo* T, const SetupL& st, SolveL& sv, const W& w, int lane) {
+template <class W, class SV>
+__device__ void dynamics(const hs_topo* T, const SetupL& st, SV& sv, const W& w, int lane) {
   const int n = T->n;
   if (lane < n) {
     const int i = lane;
@@ -461,8 +474,8 @@ __device__ void dynamics(const hs_topo* T, const SetupL& st, SolveL& sv, const W
 // ---------------------------------------------------------------------------
 // S1: tree back-substitution B0 x = f, level by level (deepest first)
 // ---------------------------------------------------------------------------
-template <class W>
-__device__ void particular(const hs_topo* T, SolveL& sv, const W& w, int lane) {
+template <class W, class SV>
+__device__ void particular(const hs_topo* T, SV& sv, const W& w, int lane) {
   const int n = T->n;
   for (int level = T->max_depth; level >= 0; level--) {
     if (lane < n && T->node[lane].depth == level) {
@@ -513,7 +526,8 @@ __device__ inline double cross_e(const double* d, int jj, int row) {
 // ===========================================================================
 
 // S2: Gram matrices of the masked, penalty-weighted null basis (ftsolver.cpp:185-207)
-__device__ void build_grams(const hs_topo* T, const SolveL& sv, GenWS& G, int k, int lane) {
+template <class SV>
+__device__ void build_grams(const hs_topo* T, const SV& sv, GenWS& G, int k, int lane) {
   const int n = T->n;
   const int nc = k / 3;
   // zeroth order: rows {0,1,2} = -I, rows {3n..3n+2} = (pos_0 - fpos) x e_jj, weight 1
@@ -860,7 +874,8 @@ __device__ void qr_solve(GenWS& G, int k, int np, int lane) {
 }
 
 // S3 general: adaptive-rank two-stage least squares (ftsolver.cpp:277-303) -> sv.y
-__device__ uint32_t contact_solve(SolveL& sv, GenWS& G, int k, int lane) {
+template <class SV>
+__device__ uint32_t contact_solve(SV& sv, GenWS& G, int k, int lane) {
   uint32_t flags = 0;
   if (k == 0) return HS_FLAG_NO_CONTACT;
   int rank0 = k;
@@ -926,7 +941,8 @@ __device__ uint32_t contact_solve(SolveL& sv, GenWS& G, int k, int lane) {
   return flags;
 }
 
-__device__ __noinline__ uint32_t general_solve(const hs_topo* T, SolveL* sv, GenWS* G, int k, int lane) {
+template <class SV>
+__device__ __attribute__((always_inline)) inline uint32_t general_solve(const hs_topo* T, SV* sv, GenWS* G, int k, int lane) {
   build_grams(T, *sv, *G, k, lane);
   return contact_solve(*sv, *G, k, lane);
 }
@@ -989,8 +1005,8 @@ __device__ inline void cross_rows(const double* d, double v[3][3]) {
   v[2][0] = -d[1]; v[2][1] = d[0];  v[2][2] = 0;
 }
 
-template <class W>
-__device__ bool fast_solve(const hs_topo* T, SolveL& sv, FastL& fl, const W& w, int nc, int lane) {
+template <class W, class SV>
+__device__ bool fast_solve(const hs_topo* T, SV& sv, FastL& fl, const W& w, int nc, int lane) {
   const int n = T->n;
   if (nc == 0) return true;
   const double* P0 = w.pos(0, 0);
@@ -1170,8 +1186,8 @@ __device__ inline uint64_t best_key(double cot, int64_t id) {
 // ---------------------------------------------------------------------------
 // One control-loop step at centre sample i (row = b * H + h of the outputs)
 // ---------------------------------------------------------------------------
-template <class W>
-__device__ void step(const hs_topo* T, const hs_run_args& a, const SetupL& st, SolveL& sv, FastL& fl, const W& w,
+template <class W, class SV>
+__device__ void step(const hs_topo* T, const hs_run_args& a, const SetupL& st, SV& sv, FastL& fl, WorkL& wk, const W& w,
                      GenWS* gws, int b, bool live, int h, double& work, int lane) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
   STAMP(3);
@@ -1232,7 +1248,7 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const SetupL& st, S
     else if (dd < -kPi) dd += 2 * kPi;
     double jvel = dd / (2 * st.dt);
     double dw = tq * jvel;
-    sv.wd[lane] = (dw > 0) ? dw : 0;
+    wk.wd[lane] = (dw > 0) ? dw : 0;
   }
   if (half_ballot(lane < nmj && tq != tq) || half_ballot(lane < k && sv.y[lane] != sv.y[lane])) flags |= HS_FLAG_NAN;
   if (half_ballot(lane < nl && w.unreach(0, lane))) flags |= HS_FLAG_UNREACH;
@@ -1269,22 +1285,22 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const SetupL& st, S
   if (live && a.flags && lane == 0) a.flags[row] = flags;
   wave_sync();
   double work_dt = 0;  // summed in joint order like work_over_period
-  for (int jj = 0; jj < nmj; jj++) work_dt += sv.wd[jj];
+  for (int jj = 0; jj < nmj; jj++) work_dt += wk.wd[jj];
   work_dt *= st.dt;
   work += work_dt;
   STAMP(8);
 }
 
-template <bool ONE>
+template <bool ONE, int NM>
 __global__ __launch_bounds__(WAVE, ONE ? HS_MIN_WAVES : 1) void hs_rollout_kernel(const hs_topo* __restrict__ T,
                                                                                  hs_run_args a, GenWS* __restrict__ gws) {
-  __shared__ Smem<ONE> smem[2];
+  __shared__ Smem<ONE, NM> smem[2];
   const int sub = threadIdx.x / HALF;  // rollout slot within the wave
   const int lane = threadIdx.x % HALF; // lane within the rollout
   const int b = blockIdx.x * 2 + sub;
   const bool live = b < a.n_rollouts;  // an odd batch leaves the last half computing a copy, storing nothing
   const int bb = live ? b : a.n_rollouts - 1;
-  Smem<ONE>& sm = smem[sub];
+  Smem<ONE, NM>& sm = smem[sub];
   double work = (live && a.accumulate && a.work_cot) ? a.work_cot[2 * (size_t)b] : 0.0;
   const hs_gait_params g = a.params[bb];
   const int nl = T->n_limbs;
@@ -1301,14 +1317,14 @@ __global__ __launch_bounds__(WAVE, ONE ? HS_MIN_WAVES : 1) void hs_rollout_kerne
       const int sl = (h == 0) ? lane / nl : NS - 1;
       const int L = (h == 0) ? lane % nl : lane;
       if (sl < NS && L < nl) {
-        if constexpr (ONE) kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin{&sm.d}, sl - 2);
-        else kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, RingWin{sm.d.s, i - 2 + sl}, 0);
+        if constexpr (ONE) kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM>{&sm.d}, sl - 2);
+        else kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, RingWin<NM>{sm.d.s, i - 2 + sl}, 0);
       }
       wave_sync();
     }
     STAMP(2);
-    if constexpr (ONE) step(T, a, sm.st, sm.sv, sm.d.fl, OneWin{&sm.d}, gws, b, live, h, work, lane);
-    else step(T, a, sm.st, sm.sv, sm.d.fl, RingWin{sm.d.s, i}, gws, b, live, h, work, lane);
+    if constexpr (ONE) step(T, a, sm.st, sm.sv, sm.d.fl, sm.d.wk, OneWin<NM>{&sm.d}, gws, b, live, h, work, lane);
+    else step(T, a, sm.st, sm.sv, sm.d.fl, sm.d.wk, RingWin<NM>{sm.d.s, i}, gws, b, live, h, work, lane);
   }
   if (lane == 0 && live) {
     double cot = work / (T->total_mass * g.step_length);
@@ -1339,16 +1355,23 @@ namespace hs {
 size_t general_workspace_bytes() { return sizeof(GenWS); }
 int rollouts_per_wave() { return 2; }
 
+template <int NM>
+void launch_nm(const hs_topo* d_topo, const hs_run_args& a, GenWS* ws, hipStream_t st) {
+  const dim3 grid((a.n_rollouts + 1) / 2);  // two rollouts per wavefront
+  if (a.horizon == 1)
+    hipLaunchKernelGGL((hs_rollout_kernel<true, NM>), grid, dim3(WAVE), 0, st, d_topo, a, ws);
+  else
+    hipLaunchKernelGGL((hs_rollout_kernel<false, NM>), grid, dim3(WAVE), 0, st, d_topo, a, ws);
+}
+
 int launch_rollouts(const hs_topo* d_topo, const hs_topo& h_topo, const hs_run_args& a, void* workspace) {
-  (void)h_topo;
   if (a.n_rollouts <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
   GenWS* ws = (GenWS*)workspace;
-  const dim3 grid((a.n_rollouts + 1) / 2);  // two rollouts per wavefront
-  if (a.horizon == 1)
-    hipLaunchKernelGGL(hs_rollout_kernel<true>, grid, dim3(WAVE), 0, st, d_topo, a, ws);
-  else
-    hipLaunchKernelGGL(hs_rollout_kernel<false>, grid, dim3(WAVE), 0, st, d_topo, a, ws);
+  // smallest LDS layout that holds the model's parts (myant 17, spider 19, hexapod 22)
+  if (h_topo.n <= 18) launch_nm<18>(d_topo, a, ws, st);
+  else if (h_topo.n <= 22) launch_nm<22>(d_topo, a, ws, st);
+  else launch_nm<HS_NMAX>(d_topo, a, ws, st);
   return (int)hipGetLastError();
 }
 
