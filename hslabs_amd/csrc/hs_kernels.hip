@@ -324,7 +324,7 @@ __device__ void node_features(const hs_topo* T, int v, const A34& A, const A34* 
 }
 
 template <class W>
-__device__ __noinline__ void kin_sample(const hs_topo* T, const hs_gait_params& g, const SetupL& st, int isample, int L,
+__device__ void kin_sample(const hs_topo* T, const hs_gait_params& g, const SetupL& st, int isample, int L,
                            bool ignore_reach, const W& w, int k) {
   double t = 0;  // t accumulates dt (periodic.cpp:171-181)
   for (int i = 0; i < isample; i++) t += st.dt;
@@ -414,6 +414,14 @@ __device__ __noinline__ void kin_sample(const hs_topo* T, const hs_gait_params& 
     node_features(T, v, A, &Jv, w, k);
     if (kk < 2) v = nd.kids[0];
   }
+}
+
+// Out-of-line copy for the ring kernel, whose step loop would otherwise keep
+// the sampler's loop-invariant addresses live across all steps.
+template <class W>
+__device__ __noinline__ void kin_sample_ool(const hs_topo* T, const hs_gait_params& g, const SetupL& st, int isample,
+                                            int L, bool ignore_reach, const W& w, int k) {
+  kin_sample(T, g, st, isample, L, ignore_reach, w, k);
 }
 
 // ---------------------------------------------------------------------------
@@ -1310,7 +1318,8 @@ __global__ __launch_bounds__(WAVE, ONE ? HS_MIN_WAVES : 1) void hs_rollout_kerne
   gait_setup(T, g, a.n_t, sm.st, lane);
   STAMP(1);
 
-  for (int h = 0; h < a.horizon; h++) {
+  const int H = ONE ? 1 : a.horizon;  // compile-time single step for the H = 1 layout
+  for (int h = 0; h < H; h++) {
     const int i = a.k0 + h + 2;  // centre sample of this step
     // K: the whole window on the first step, then the newest sample (lane = (sample, limb))
     {
@@ -1318,7 +1327,7 @@ __global__ __launch_bounds__(WAVE, ONE ? HS_MIN_WAVES : 1) void hs_rollout_kerne
       const int L = (h == 0) ? lane % nl : lane;
       if (sl < NS && L < nl) {
         if constexpr (ONE) kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM>{&sm.d}, sl - 2);
-        else kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, RingWin<NM>{sm.d.s, i - 2 + sl}, 0);
+        else kin_sample_ool(T, g, sm.st, i - 2 + sl, L, ignore_reach, RingWin<NM>{sm.d.s, i - 2 + sl}, 0);
       }
       wave_sync();
     }
