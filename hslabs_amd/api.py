@@ -182,7 +182,7 @@ class DeviceBatch:
     def reset_best(self):
         self.best_key.fill_(-1)
 
-    def run(self, stream=None, best: bool = True, accumulate: bool = False) -> None:
+    def _args(self, stream, best: bool, accumulate: bool):
         torch = self.torch
         a = capi.RunArgsC()
         a.n_rollouts, a.horizon, a.k0, a.n_t = self.B, self.H, self.k0, self.n_t
@@ -199,7 +199,27 @@ class DeviceBatch:
         a.rollout_id_base = self.rollout_id_base
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         a.stream = st.cuda_stream
+        return a
+
+    def run(self, stream=None, best: bool = True, accumulate: bool = False) -> None:
+        a = self._args(stream, best, accumulate)
         capi.check(capi.load().hs_run(self.model.handle, ctypes.byref(a)), "hs_run")
+
+    def run_steps(self, n_calls: int, stream=None, best: bool = False, accumulate: bool = True,
+                  events=None) -> None:
+        """n_calls launches marching k0 through the cycle (hs_run_steps); the launch loop is
+        native. ``events``: 2*n_calls torch.cuda.Event(enable_timing=True), recorded around
+        each launch."""
+        a = self._args(stream, best, accumulate)
+        ev = None
+        if events is not None:
+            assert len(events) == 2 * n_calls
+            st = stream if stream is not None else self.torch.cuda.current_stream(self.device)
+            for e in events:  # torch creates the HIP event on first record
+                if not e.cuda_event:
+                    e.record(st)
+            ev = (ctypes.c_void_p * len(events))(*[e.cuda_event for e in events])
+        capi.check(capi.load().hs_run_steps(self.model.handle, ctypes.byref(a), n_calls, ev), "hs_run_steps")
 
 
 def decode_best_key(key: int):

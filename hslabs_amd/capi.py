@@ -25,7 +25,7 @@ HS_FLAG_GENERAL = 64
 # every symbol declared in include/hslabs.h
 EXPORTS = [
     "hs_model_load", "hs_model_load_ex", "hs_model_free", "hs_model_get_dims", "hs_pgs_config_read",
-    "hs_run", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
+    "hs_run", "hs_run_steps", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
 ]
 
 
@@ -101,6 +101,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_pgs_config_read.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(GaitParamsC),
                                      ctypes.c_char_p, ctypes.c_int32]
     L.hs_run.argtypes = [vp, ctypes.POINTER(RunArgsC)]
+    L.hs_run_steps.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32, ctypes.POINTER(vp)]
     L.hs_run_host.argtypes = [vp, ctypes.POINTER(GaitParamsC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                               ctypes.c_int32, ctypes.c_int32, dp, dp, dp, dp, ctypes.POINTER(ctypes.c_uint32), dp]
     L.hs_best_key_encode.argtypes = [ctypes.c_double, ctypes.c_int64]

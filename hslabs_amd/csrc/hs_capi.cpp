@@ -147,6 +147,30 @@ int hs_run(hs_model_t m, const hs_run_args* a) {
   return HS_OK;
 }
 
+int hs_run_steps(hs_model_t m, const hs_run_args* a, int32_t n_calls, void* const* kernel_events) {
+  int rc = check_args(m, a);
+  if (rc != HS_OK) return rc;
+  if (n_calls < 0) return fail(HS_E_ARG, "n_calls < 0");
+  if (a->n_rollouts == 0 || n_calls == 0) return HS_OK;
+  const hs_topo* d = nullptr;
+  void* ws = nullptr;
+  rc = device_state(m, a->n_rollouts + 1, &d, &ws);
+  if (rc != HS_OK) return rc;
+  hs_run_args c = *a;
+  hipStream_t st = (hipStream_t)a->stream;
+  for (int32_t i = 0; i < n_calls; i++) {
+    c.k0 = (int32_t)(((int64_t)a->k0 + (int64_t)i * a->horizon) % a->n_t);
+    hipError_t e = hipSuccess;
+    if (kernel_events) e = hipEventRecord((hipEvent_t)kernel_events[2 * i], st);
+    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+    int le = hs::launch_rollouts(d, m->host, c, ws);
+    if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
+    if (kernel_events) e = hipEventRecord((hipEvent_t)kernel_events[2 * i + 1], st);
+    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+  }
+  return HS_OK;
+}
+
 int hs_run_host(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n_t, int32_t k0, int32_t H,
                 int32_t ignore_reach, double* q, double* tau, double* cf, double* x, uint32_t* flags,
                 double* work_cot) {

@@ -122,6 +122,15 @@ typedef struct {
 
 int hs_run(hs_model_t model, const hs_run_args* args);
 
+/* n_calls successive hs_run launches on args->stream: call c solves steps
+ * k0_c = (args->k0 + c * horizon) mod n_t .. k0_c + horizon - 1, i.e. the
+ * control loop marching through the gait cycle (compute_torques_over_period's
+ * step order, periodic.cpp:377-391, wrapped); outputs are overwritten per call
+ * and work_cot accumulates when args->accumulate is set. kernel_events, if not
+ * NULL, holds 2 * n_calls caller-created hipEvent_t recorded immediately before
+ * and after each launch (per-launch kernel timing on the launch stream). */
+int hs_run_steps(hs_model_t model, const hs_run_args* args, int32_t n_calls, void* const* kernel_events);
+
 /* Host-buffer convenience wrapper of hs_run (copies in/out, synchronous).
  * Replaces periodic::compute_torques_over_period + get_motor_torques +
  * work_over_period for a batch of rollouts. Output pointers may be NULL. */

@@ -128,6 +128,31 @@ def test_accumulate_matches_full_cycle_work(gpu, hmodels):
     assert np.array_equal(wc[:, 1], full["work_cot"][:, 1])
 
 
+def test_run_steps_matches_launch_loop(gpu, hmodels):
+    """hs_run_steps (native launch loop, k0 wrapping the cycle) == the same launches one by one;
+    an odd batch leaves the last wavefront's second half idle."""
+    import torch
+
+    from hslabs_amd import synth
+
+    params = synth.gen_params(257, "hexapod", id0=3)
+    m = hmodels["hexapod"]
+    a = gpu.DeviceBatch(m, params, n_t=20, horizon=1)
+    b = gpu.DeviceBatch(m, params, n_t=20, horizon=1)
+    a.work_cot.zero_()
+    b.work_cot.zero_()
+    for s in range(27):
+        a.k0 = s % 20
+        a.run(best=False, accumulate=True)
+    b.k0 = 0
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(54)]
+    b.run_steps(27, best=False, accumulate=True, events=ev)
+    torch.cuda.synchronize()
+    assert torch.equal(a.work_cot, b.work_cot)
+    assert torch.equal(a.tau, b.tau) and torch.equal(a.cf, b.cf) and torch.equal(a.flags, b.flags)
+    assert all(ev[2 * i].elapsed_time(ev[2 * i + 1]) > 0 for i in range(27))
+
+
 def test_device_batch_best_key(gpu, hmodels):
     import torch
 

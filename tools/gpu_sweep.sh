@@ -6,7 +6,7 @@ R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out; mkdir -p $OUT
 cd $R
 timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -2 $OUT/pytest_gpu.log
-ARGS="${BENCH_ARGS:---steps 50 --warmup 5 --no-cpu}"
+ARGS="${BENCH_ARGS:---steps 200 --warmup 20 --no-cpu}"
 timeout -k 10 200 python bench.py $ARGS > $OUT/bench_base.json 2> $OUT/bench_base.err || { echo "bench failed"; tail -20 $OUT/bench_base.err; exit 1; }
 echo "base: $(python -c "import json;d=json.load(open('$OUT/bench_base.json'));print(d['value'], d['roofline']['kernel_ms'])")"
 for v in $VARIANTS; do
