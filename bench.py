@@ -47,32 +47,39 @@ def parse():
     ap.add_argument("--model", default="hexapod", choices=["hexapod", "spider", "myant"])
     ap.add_argument("--n_t", type=int, default=20)
     ap.add_argument("--curved", action="store_true")
+    ap.add_argument("--mixed", action="store_true",
+                    help="BASELINE configs[4]: myant.xml + hexapod.xml 50/50, interleaved, one launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(model_name, n_t, horizon, seconds, threads):
-    """Oracle (CPU restatement, tree basis = same algorithm as the kernel) on a bounded sample."""
+def cpu_baseline(model_names, n_t, horizon, seconds, threads):
+    """Oracle (CPU restatement, tree basis = same algorithm as the kernel) on a bounded sample
+    (model_names: one model, or the models of a mixed batch in equal shares)."""
     from oracle import oracle as O
     from hslabs_amd import synth
 
-    om = O.Model(os.path.join(ROOT, "models", f"{model_name}.xml"))
     threads = max(1, min(threads, os.cpu_count() or 1))
-    chunk = 256 * threads
-    arr = synth.gen_params(chunk, model_name)
-    gaits = [O.GaitParams(torso_pos=tuple(r["torso_pos"]), torso_angles=tuple(r["torso_angles"]),
-                          step_duration=float(r["step_duration"]), period=float(r["period"]),
-                          step_length=float(r["step_length"]), step_height=float(r["step_height"]),
-                          curvature=float(r["curvature"]), foot_shift_type=int(r["foot_shift_type"]),
-                          foot_shift=float(r["foot_shift"])) for r in arr]
+    chunk = 256 * threads // len(model_names)
+    work = []
+    for name in model_names:
+        om = O.Model(os.path.join(ROOT, "models", f"{name}.xml"))
+        arr = synth.gen_params(chunk, name)
+        work.append((om, [O.GaitParams(torso_pos=tuple(r["torso_pos"]), torso_angles=tuple(r["torso_angles"]),
+                                       step_duration=float(r["step_duration"]), period=float(r["period"]),
+                                       step_length=float(r["step_length"]), step_height=float(r["step_height"]),
+                                       curvature=float(r["curvature"]), foot_shift_type=int(r["foot_shift_type"]),
+                                       foot_shift=float(r["foot_shift"])) for r in arr]))
+    model_name = "+".join(model_names)
 
     def timed(nthr, budget):
         done, t0 = 0, time.perf_counter()
         while True:
-            O.batch(om, gaits, n_t, 0, horizon, basis=O.BASIS_TREE, n_threads=nthr)
-            done += len(gaits) * horizon
+            for om, gaits in work:
+                O.batch(om, gaits, n_t, 0, horizon, basis=O.BASIS_TREE, n_threads=nthr)
+                done += len(gaits) * horizon
             el = time.perf_counter() - t0
             if el >= budget:
                 return done / el, done, el
@@ -105,12 +112,28 @@ def main():
     import hslabs_amd as H
     from hslabs_amd import synth
 
-    model = H.KinematicModel(os.path.join(ROOT, "models", f"{args.model}.xml"))
     B, Hh, n_t = args.rollouts, args.horizon, args.n_t
     id0 = rank * B
-    params = synth.gen_params(B, args.model, id0=id0, curved=args.curved)
-    batch = H.DeviceBatch(model, params, n_t=n_t, k0=0, horizon=Hh, outputs=("tau", "cf", "work_cot", "flags"),
-                          device=dev, rollout_id_base=id0)
+    outs = ("tau", "cf", "work_cot", "flags")
+    if args.mixed:
+        model_names = list(synth.MIXED_MODELS)
+        models = [H.KinematicModel(os.path.join(ROOT, "models", f"{n}.xml")) for n in model_names]
+        params, midx = synth.gen_mixed(B, id0=id0, curved=args.curved)
+        batch = H.MixedBatch(models, midx, params, n_t=n_t, k0=0, horizon=Hh, outputs=outs, device=dev,
+                             rollout_id_base=id0)
+        out_bytes = float(np.mean([OUT_BYTES_PER_STEP[model_names[k]] for k in midx]))
+        workload = f"myant.xml+hexapod.xml 50/50 interleaved B={B}/GPU H={Hh} n_t={n_t} fp64 (BASELINE configs[4])"
+        traffic_key = f"mixed B={B} H={Hh}"
+    else:
+        model_names = [args.model]
+        model = H.KinematicModel(os.path.join(ROOT, "models", f"{args.model}.xml"))
+        params = synth.gen_params(B, args.model, id0=id0, curved=args.curved)
+        batch = H.DeviceBatch(model, params, n_t=n_t, k0=0, horizon=Hh, outputs=outs, device=dev,
+                              rollout_id_base=id0)
+        out_bytes = OUT_BYTES_PER_STEP[args.model]
+        cfg = "configs[1]" if args.model == "hexapod" and Hh == 1 else "custom"
+        workload = f"{args.model}.xml B={B}/GPU H={Hh} n_t={n_t} fp64 (BASELINE {cfg})"
+        traffic_key = f"{args.model} B={B} H={Hh}"
     stream = torch.cuda.current_stream(dev)
 
     # warmup (untimed): the same native launch loop as the timed region
@@ -157,14 +180,14 @@ def main():
         steps_total = B * Hh * args.steps * world
         value = steps_total / elapsed
         ms_per_step = 1e3 * elapsed / args.steps
-        alg_bytes = B * Hh * (OUT_BYTES_PER_STEP[args.model] + PARAM_BYTES / Hh)
+        alg_bytes = B * Hh * (out_bytes + PARAM_BYTES / Hh)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
         tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tf):
             try:
                 j = json.load(open(tf))
-                if j.get("workload") == f"{args.model} B={B} H={Hh}":
+                if j.get("workload") == traffic_key:
                     traffic = j.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -173,7 +196,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (splitmix64 gait parameters around pgs id 8; SURVEY.md 8d)",
-            "config": {"workload": f"{args.model}.xml B={B}/GPU H={Hh} n_t={n_t} fp64 (BASELINE configs[1])",
+            "config": {"workload": workload,
                        "rollouts_per_gpu": B, "horizon": Hh, "n_t": n_t,
                        "parallelism": f"rollout-sharded x{world}, 1 RCCL all_reduce(MIN, 8 B) per job"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -184,7 +207,7 @@ def main():
             "nan_steps": nan_steps,
         }
         if not args.no_cpu and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args.model, n_t, Hh, args.cpu_seconds, args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline(model_names, n_t, Hh, args.cpu_seconds, args.cpu_threads)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -3,9 +3,9 @@
 pergen -> lik -> FK -> dynrec -> ftsolver -> motor torques, one wavefront per
 gait rollout on gfx950, behind the C ABI in include/hslabs.h.
 """
-from .api import (DeviceBatch, KinematicModel, ModelPlayer, Periodic, PgsConfigParams, decode_best_key,
+from .api import (DeviceBatch, KinematicModel, MixedBatch, ModelPlayer, Periodic, PgsConfigParams, decode_best_key,
                   params_array, read_pgs_config, run_host, GAIT_DTYPE)
 from .capi import HSError
 
-__all__ = ["DeviceBatch", "KinematicModel", "ModelPlayer", "Periodic", "PgsConfigParams", "decode_best_key",
+__all__ = ["DeviceBatch", "KinematicModel", "MixedBatch", "ModelPlayer", "Periodic", "PgsConfigParams", "decode_best_key",
            "params_array", "read_pgs_config", "run_host", "GAIT_DTYPE", "HSError"]

@@ -162,6 +162,10 @@ class DeviceBatch:
 
         self.torch = torch
         self.model = model
+        self._alloc(model, params, n_t, k0, horizon, ignore_reach, outputs, device, rollout_id_base)
+
+    def _alloc(self, dims, params, n_t, k0, horizon, ignore_reach, outputs, device, rollout_id_base):
+        torch = self.torch
         arr = params_array(params)
         self.B, self.H, self.n_t, self.k0 = len(arr), horizon, n_t, k0
         self.ignore_reach = ignore_reach
@@ -171,10 +175,10 @@ class DeviceBatch:
         self.params = torch.from_numpy(arr.view(np.uint8).copy()).to(dev)
         f64 = dict(dtype=torch.float64, device=dev)
         B, H = self.B, self.H
-        self.q = torch.empty((B, H, model.config_dim), **f64) if "q" in outputs else None
-        self.tau = torch.empty((B, H, model.nmj), **f64) if "tau" in outputs else None
-        self.cf = torch.empty((B, H, 3 * model.nfeet), **f64) if "cf" in outputs else None
-        self.x = torch.empty((B, H, 6 * model.n_parts), **f64) if "x" in outputs else None
+        self.q = torch.empty((B, H, dims.config_dim), **f64) if "q" in outputs else None
+        self.tau = torch.empty((B, H, dims.nmj), **f64) if "tau" in outputs else None
+        self.cf = torch.empty((B, H, 3 * dims.nfeet), **f64) if "cf" in outputs else None
+        self.x = torch.empty((B, H, 6 * dims.n_parts), **f64) if "x" in outputs else None
         self.flags = torch.empty((B, H), dtype=torch.int32, device=dev) if "flags" in outputs else None
         self.work_cot = torch.empty((B, 2), **f64) if "work_cot" in outputs else None
         self.best_key = torch.full((1,), -1, dtype=torch.int64, device=dev)  # UINT64_MAX bit pattern
@@ -201,9 +205,11 @@ class DeviceBatch:
         a.stream = st.cuda_stream
         return a
 
+    def _launch(self, a, n_calls, ev):
+        capi.check(capi.load().hs_run_steps(self.model.handle, ctypes.byref(a), n_calls, ev), "hs_run_steps")
+
     def run(self, stream=None, best: bool = True, accumulate: bool = False) -> None:
-        a = self._args(stream, best, accumulate)
-        capi.check(capi.load().hs_run(self.model.handle, ctypes.byref(a)), "hs_run")
+        self._launch(self._args(stream, best, accumulate), 1, None)
 
     def run_steps(self, n_calls: int, stream=None, best: bool = False, accumulate: bool = True,
                   events=None) -> None:
@@ -219,7 +225,49 @@ class DeviceBatch:
                 if not e.cuda_event:
                     e.record(st)
             ev = (ctypes.c_void_p * len(events))(*[e.cuda_event for e in events])
-        capi.check(capi.load().hs_run_steps(self.model.handle, ctypes.byref(a), n_calls, ev), "hs_run_steps")
+        self._launch(a, n_calls, ev)
+
+
+class MixedBatch(DeviceBatch):
+    """Mixed-topology batch (BASELINE configs[4]): rollout b runs models[model_index[b]]
+    through one hs_mixed plan. Output rows use the maxima over the models
+    (``dims``); entries past a rollout's own dimensions are 0."""
+
+    def __init__(self, models, model_index, params, n_t: int = 20, k0: int = 0, horizon: int = 1,
+                 ignore_reach: bool = True, outputs=("tau", "cf", "work_cot", "flags"), device=None,
+                 rollout_id_base: int = 0):
+        import torch
+
+        self.torch = torch
+        self.models = list(models)
+        self.model_index = np.ascontiguousarray(model_index, dtype=np.int32)
+        L = capi.load()
+        if device is not None:
+            torch.cuda.set_device(device)
+        hs = (ctypes.c_void_p * len(self.models))(*[m.handle for m in self.models])
+        plan = ctypes.c_void_p()
+        capi.check(L.hs_mixed_create(hs, len(self.models),
+                                     self.model_index.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                     len(self.model_index), ctypes.byref(plan)), "hs_mixed_create")
+        self.plan = plan
+        d = capi.ModelDimsC()
+        capi.check(L.hs_mixed_get_dims(plan, ctypes.byref(d)), "hs_mixed_get_dims")
+        self.dims = d
+        self.model = self.models[0]
+        assert len(params_array(params)) == len(self.model_index)
+        self._alloc(d, params, n_t, k0, horizon, ignore_reach, outputs, device, rollout_id_base)
+
+    def _launch(self, a, n_calls, ev):
+        capi.check(capi.load().hs_run_mixed_steps(self.plan, ctypes.byref(a), n_calls, ev), "hs_run_mixed_steps")
+
+    def __del__(self):
+        plan = getattr(self, "plan", None)
+        if plan:
+            try:
+                capi.load().hs_mixed_free(plan)
+            except Exception:
+                pass
+            self.plan = None
 
 
 def decode_best_key(key: int):

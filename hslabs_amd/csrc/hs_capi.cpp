@@ -1,6 +1,7 @@
 // hs_capi.cpp -- implementation of include/hslabs.h (host side, HIP runtime).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -54,6 +55,24 @@ int device_state(hs_model_t m, int n_rollouts, const hs_topo** topo, void** ws) 
   return HS_OK;
 }
 
+// n_calls launches, k0 marching through the cycle (hs_run_steps semantics)
+int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::launch_map& mp, int32_t n_calls,
+                 void* const* kernel_events) {
+  hs_run_args c = a;
+  hipStream_t st = (hipStream_t)a.stream;
+  for (int32_t i = 0; i < n_calls; i++) {
+    c.k0 = (int32_t)(((int64_t)a.k0 + (int64_t)i * a.horizon) % a.n_t);
+    hipError_t e = hipSuccess;
+    if (kernel_events) e = hipEventRecord((hipEvent_t)kernel_events[2 * i], st);
+    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+    int le = hs::launch_rollouts(d, c, ws, mp);
+    if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
+    if (kernel_events) e = hipEventRecord((hipEvent_t)kernel_events[2 * i + 1], st);
+    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+  }
+  return HS_OK;
+}
+
 void free_on_device(int dev, void* p) {
   int cur = 0;
   if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(dev) == hipSuccess) {
@@ -74,6 +93,18 @@ int check_args(const hs_model_s* m, const hs_run_args* a) {
 }
 
 }  // namespace
+
+struct hs_mixed_s {
+  int dev = 0;
+  int32_t n_rollouts = 0, n_waves = 0;
+  std::vector<hs_model_t> models;
+  hs_model_dims max_dims;
+  int32_t st_tau = 0, st_cf = 0, st_q = 0, st_x = 0;
+  const hs_topo** d_topos = nullptr;
+  int32_t* d_wave_model = nullptr;
+  int32_t* d_wave_rollouts = nullptr;
+  void* ws = nullptr;
+};
 
 extern "C" {
 
@@ -134,18 +165,7 @@ int hs_pgs_config_read(const char* path, int setup_id, hs_gait_params* out, char
   return HS_OK;
 }
 
-int hs_run(hs_model_t m, const hs_run_args* a) {
-  int rc = check_args(m, a);
-  if (rc != HS_OK) return rc;
-  if (a->n_rollouts == 0) return HS_OK;
-  const hs_topo* d = nullptr;
-  void* ws = nullptr;
-  rc = device_state(m, a->n_rollouts + 1, &d, &ws);  // + the idle half-wave of an odd batch
-  if (rc != HS_OK) return rc;
-  int e = hs::launch_rollouts(d, m->host, *a, ws);
-  if (e != 0) return hip_fail((hipError_t)e, "kernel launch");
-  return HS_OK;
-}
+int hs_run(hs_model_t m, const hs_run_args* a) { return hs_run_steps(m, a, 1, nullptr); }
 
 int hs_run_steps(hs_model_t m, const hs_run_args* a, int32_t n_calls, void* const* kernel_events) {
   int rc = check_args(m, a);
@@ -154,21 +174,114 @@ int hs_run_steps(hs_model_t m, const hs_run_args* a, int32_t n_calls, void* cons
   if (a->n_rollouts == 0 || n_calls == 0) return HS_OK;
   const hs_topo* d = nullptr;
   void* ws = nullptr;
-  rc = device_state(m, a->n_rollouts + 1, &d, &ws);
+  rc = device_state(m, a->n_rollouts + 1, &d, &ws);  // + the idle half-wave of an odd batch
   if (rc != HS_OK) return rc;
-  hs_run_args c = *a;
-  hipStream_t st = (hipStream_t)a->stream;
-  for (int32_t i = 0; i < n_calls; i++) {
-    c.k0 = (int32_t)(((int64_t)a->k0 + (int64_t)i * a->horizon) % a->n_t);
-    hipError_t e = hipSuccess;
-    if (kernel_events) e = hipEventRecord((hipEvent_t)kernel_events[2 * i], st);
-    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
-    int le = hs::launch_rollouts(d, m->host, c, ws);
-    if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
-    if (kernel_events) e = hipEventRecord((hipEvent_t)kernel_events[2 * i + 1], st);
-    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+  return launch_steps(d, *a, ws, hs::single_model_map(m->host, a->n_rollouts), n_calls, kernel_events);
+}
+
+int hs_mixed_create(const hs_model_t* models, int32_t n_models, const int32_t* model_index, int32_t n_rollouts,
+                    hs_mixed_t* out) {
+  if (!models || !out || (n_rollouts > 0 && !model_index)) return fail(HS_E_ARG, "null argument");
+  if (n_models < 1 || n_models > 64) return fail(HS_E_ARG, "n_models must be in [1, 64]");
+  if (n_rollouts < 0 || n_rollouts > (1 << 30)) return fail(HS_E_ARG, "bad n_rollouts");
+  std::vector<std::vector<int32_t>> groups((size_t)n_models);
+  for (int32_t b = 0; b < n_rollouts; b++) {
+    int32_t k = model_index[b];
+    if (k < 0 || k >= n_models) return fail(HS_E_ARG, "model_index out of range");
+    groups[(size_t)k].push_back(b);
   }
+  hs_mixed_s* p = new hs_mixed_s;
+  p->n_rollouts = n_rollouts;
+  p->models.assign(models, models + n_models);
+  std::vector<const hs_topo*> topos;
+  std::vector<int32_t> wave_model, wave_rollouts;
+  hs_model_dims& md = p->max_dims;
+  memset(&md, 0, sizeof(md));
+  int32_t max_cf = 0, max_x = 0;
+  for (int k = 0; k < n_models; k++) {
+    if (!models[k]) { delete p; return fail(HS_E_ARG, "null model"); }
+    const hs_topo* d = nullptr;
+    void* ws = nullptr;
+    int rc = device_state(models[k], 1, &d, &ws);
+    if (rc != HS_OK) { delete p; return rc; }
+    topos.push_back(d);
+    const hs_topo& t = models[k]->host;
+    if (t.n > md.n_parts) {
+      hs_model_get_dims(models[k], &md);  // the model with the most parts, maxima patched below
+    }
+    max_cf = std::max(max_cf, 3 * t.nf);
+    max_x = std::max(max_x, 6 * t.n);
+    p->st_tau = std::max(p->st_tau, t.nmj);
+    p->st_q = std::max(p->st_q, t.cfg);
+    const std::vector<int32_t>& g = groups[(size_t)k];
+    for (size_t i = 0; i < g.size(); i += 2) {  // two rollouts of one model per wavefront
+      wave_model.push_back(k);
+      wave_rollouts.push_back(g[i]);
+      wave_rollouts.push_back(i + 1 < g.size() ? g[i + 1] : -1);
+    }
+  }
+  md.nmj = p->st_tau;
+  md.nfeet = max_cf / 3;
+  md.config_dim = p->st_q;
+  p->st_cf = max_cf;
+  p->st_x = max_x;
+  p->n_waves = (int32_t)wave_model.size();
+  hipError_t e = hipGetDevice(&p->dev);
+  size_t nt = topos.size() * sizeof(hs_topo*), nw = wave_model.size() * sizeof(int32_t);
+  if (e == hipSuccess) e = hipMalloc(&p->d_topos, nt);
+  if (e == hipSuccess && nw) e = hipMalloc(&p->d_wave_model, nw);
+  if (e == hipSuccess && nw) e = hipMalloc(&p->d_wave_rollouts, 2 * nw);
+  if (e == hipSuccess) e = hipMemcpy(p->d_topos, topos.data(), nt, hipMemcpyHostToDevice);
+  if (e == hipSuccess && nw) e = hipMemcpy(p->d_wave_model, wave_model.data(), nw, hipMemcpyHostToDevice);
+  if (e == hipSuccess && nw) e = hipMemcpy(p->d_wave_rollouts, wave_rollouts.data(), 2 * nw, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&p->ws, ((size_t)n_rollouts + 1) * hs::general_workspace_bytes());
+  if (e != hipSuccess) {
+    hs_mixed_free(p);
+    return hip_fail(e, "mixed plan upload");
+  }
+  *out = p;
   return HS_OK;
+}
+
+void hs_mixed_free(hs_mixed_t p) {
+  if (!p) return;
+  if (p->d_topos) free_on_device(p->dev, p->d_topos);
+  if (p->d_wave_model) free_on_device(p->dev, p->d_wave_model);
+  if (p->d_wave_rollouts) free_on_device(p->dev, p->d_wave_rollouts);
+  if (p->ws) free_on_device(p->dev, p->ws);
+  delete p;
+}
+
+int hs_mixed_get_dims(hs_mixed_t p, hs_model_dims* out) {
+  if (!p || !out) return fail(HS_E_ARG, "null argument");
+  *out = p->max_dims;
+  return HS_OK;
+}
+
+int hs_run_mixed(hs_mixed_t p, const hs_run_args* a) { return hs_run_mixed_steps(p, a, 1, nullptr); }
+
+int hs_run_mixed_steps(hs_mixed_t p, const hs_run_args* a, int32_t n_calls, void* const* kernel_events) {
+  if (!p) return fail(HS_E_ARG, "null plan");
+  int rc = check_args(p->models[0], a);
+  if (rc != HS_OK) return rc;
+  if (a->n_rollouts != p->n_rollouts) return fail(HS_E_ARG, "n_rollouts differs from the plan's");
+  if (n_calls < 0) return fail(HS_E_ARG, "n_calls < 0");
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  if (dev != p->dev) return fail(HS_E_DEVICE, "plan was created on another device");
+  if (a->n_rollouts == 0 || n_calls == 0) return HS_OK;
+  hs::launch_map mp{};
+  mp.topos = p->d_topos;
+  mp.wave_model = p->d_wave_model;
+  mp.wave_rollouts = p->d_wave_rollouts;
+  mp.n_waves = p->n_waves;
+  mp.max_parts = p->max_dims.n_parts;
+  mp.st_tau = p->st_tau;
+  mp.st_cf = p->st_cf;
+  mp.st_q = p->st_q;
+  mp.st_x = p->st_x;
+  return launch_steps(nullptr, *a, p->ws, mp, n_calls, kernel_events);
 }
 
 int hs_run_host(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n_t, int32_t k0, int32_t H,

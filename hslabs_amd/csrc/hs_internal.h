@@ -13,11 +13,22 @@ namespace hs {
 int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& err);
 int read_pgs_config(const char* path, int setup_id, hs_gait_params* out, std::string& xml, std::string& err);
 
+// Which rollouts a launch's wavefronts run and where their output rows go.
+struct launch_map {
+  const hs_topo* const* topos;   // mixed batches: device array of per-model topologies (null: one model)
+  const int32_t* wave_model;     // mixed: model of each wavefront
+  const int32_t* wave_rollouts;  // mixed: [2 * n_waves] rollout ids, -1 = idle half
+  int32_t n_waves;
+  int32_t max_parts;             // LDS layout class (largest model)
+  int32_t st_tau, st_cf, st_q, st_x;  // output row strides (mixed: maxima over the models)
+};
+
 // Kernel launcher (hs_kernels.hip). `workspace` holds general_workspace_bytes()
-// per rollout (global-memory scratch of the conditioning fallback). Returns a
-// hipError_t value.
+// per rollout + 1 (global-memory scratch of the conditioning fallback; the
+// extra slot serves idle half-waves). Returns a hipError_t value.
 size_t general_workspace_bytes();
-int launch_rollouts(const hs_topo* d_topo, const hs_topo& h_topo, const hs_run_args& a, void* workspace);
+int launch_rollouts(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
+launch_map single_model_map(const hs_topo& t, int32_t n_rollouts);
 
 }  // namespace hs
 

@@ -1195,8 +1195,8 @@ __device__ inline uint64_t best_key(double cot, int64_t id) {
 // One control-loop step at centre sample i (row = b * H + h of the outputs)
 // ---------------------------------------------------------------------------
 template <class W, class SV>
-__device__ void step(const hs_topo* T, const hs_run_args& a, const SetupL& st, SV& sv, FastL& fl, WorkL& wk, const W& w,
-                     GenWS* gws, int b, bool live, int h, double& work, int lane) {
+__device__ void step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st, SV& sv,
+                     FastL& fl, WorkL& wk, const W& w, GenWS* G, int b, bool live, int h, double& work, int lane) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
   STAMP(3);
   dynamics(T, st, sv, w, lane);
@@ -1215,7 +1215,6 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const SetupL& st, S
     if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
     if (nc == 1) flags |= HS_FLAG_FULL_RANK;
   } else {
-    GenWS* G = gws + b;
     for (int e = lane; e < 3 * n; e += HALF) {
       G->jpos[e / 3][e % 3] = w.jpos(0, e / 3)[e % 3];
       G->jz[e / 3][e % 3] = w.jz(0, e / 3)[e % 3];
@@ -1250,7 +1249,6 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const SetupL& st, S
       double xr = sv.x[3 * n + 3 * h_id + r] + s;
       tq = tq + Jz[r] * xr;
     }
-    if (live && a.tau) a.tau[row * nmj + lane] = tq;
     double dd = w.q(1)[6 + lane] - w.q(-1)[6 + lane];
     if (dd > kPi) dd -= 2 * kPi;
     else if (dd < -kPi) dd += 2 * kPi;
@@ -1258,14 +1256,15 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const SetupL& st, S
     double dw = tq * jvel;
     wk.wd[lane] = (dw > 0) ? dw : 0;
   }
+  if (live && a.tau && lane < mp.st_tau) a.tau[row * mp.st_tau + lane] = tq;  // 0 past nmj
   if (half_ballot(lane < nmj && tq != tq) || half_ballot(lane < k && sv.y[lane] != sv.y[lane])) flags |= HS_FLAG_NAN;
   if (half_ballot(lane < nl && w.unreach(0, lane))) flags |= HS_FLAG_UNREACH;
   // contact forces z = -N_cont y (ftsolver.cpp:91, 276-284)
-  if (live && a.cf && lane < 3 * nf) {
+  if (live && a.cf && lane < mp.st_cf) {
     int fi = lane / 3, j = lane % 3;
-    double zv = -0.0;
+    double zv = (lane < 3 * nf) ? -0.0 : 0.0;
     for (int c = 0; c < nc; c++) if (sv.cfoot[c] == fi) zv = -(0.0 + (-1.0) * sv.y[3 * c + j]);
-    a.cf[row * 3 * nf + lane] = zv;
+    a.cf[row * mp.st_cf + lane] = zv;
   }
   if (live && a.x) {  // full joint force/torque vector x += N y
     for (int rI = lane; rI < 6 * n; rI += HALF) {
@@ -1286,10 +1285,11 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const SetupL& st, S
           for (int jj = 0; jj < 3; jj++) s = s + cross_e(d, jj, comp) * sv.y[3 * c + jj];
         }
       }
-      a.x[row * 6 * n + rI] = sv.x[rI] + s;
+      a.x[row * mp.st_x + rI] = sv.x[rI] + s;
     }
+    for (int rI = 6 * n + lane; rI < mp.st_x; rI += HALF) a.x[row * mp.st_x + rI] = 0.0;
   }
-  if (live && a.q && lane < cfg) a.q[row * cfg + lane] = w.q(0)[lane];
+  if (live && a.q && lane < mp.st_q) a.q[row * mp.st_q + lane] = (lane < cfg) ? w.q(0)[lane] : 0.0;
   if (live && a.flags && lane == 0) a.flags[row] = flags;
   wave_sync();
   double work_dt = 0;  // summed in joint order like work_over_period
@@ -1300,14 +1300,26 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const SetupL& st, S
 }
 
 template <bool ONE, int NM>
-__global__ __launch_bounds__(WAVE, ONE ? HS_MIN_WAVES : 1) void hs_rollout_kernel(const hs_topo* __restrict__ T,
-                                                                                 hs_run_args a, GenWS* __restrict__ gws) {
+__global__ __launch_bounds__(WAVE, ONE ? HS_MIN_WAVES : 1) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
+                                                                                 hs_run_args a, GenWS* __restrict__ gws,
+                                                                                 hs::launch_map mp) {
   __shared__ Smem<ONE, NM> smem[2];
   const int sub = threadIdx.x / HALF;  // rollout slot within the wave
   const int lane = threadIdx.x % HALF; // lane within the rollout
-  const int b = blockIdx.x * 2 + sub;
-  const bool live = b < a.n_rollouts;  // an odd batch leaves the last half computing a copy, storing nothing
-  const int bb = live ? b : a.n_rollouts - 1;
+  // one model per wavefront: the topology pointer stays wave-uniform (scalar loads)
+  const hs_topo* __restrict__ T = mp.topos ? mp.topos[mp.wave_model[blockIdx.x]] : T0;
+  int b, bb;
+  bool live;  // an idle half (odd group) computes a copy of its neighbour and stores nothing
+  if (mp.wave_rollouts) {
+    b = mp.wave_rollouts[2 * blockIdx.x + sub];
+    live = b >= 0;
+    bb = live ? b : mp.wave_rollouts[2 * blockIdx.x];
+  } else {
+    b = blockIdx.x * 2 + sub;
+    live = b < a.n_rollouts;
+    bb = live ? b : a.n_rollouts - 1;
+  }
+  GenWS* G = gws + (live ? b : a.n_rollouts);
   Smem<ONE, NM>& sm = smem[sub];
   double work = (live && a.accumulate && a.work_cot) ? a.work_cot[2 * (size_t)b] : 0.0;
   const hs_gait_params g = a.params[bb];
@@ -1332,8 +1344,8 @@ __global__ __launch_bounds__(WAVE, ONE ? HS_MIN_WAVES : 1) void hs_rollout_kerne
       wave_sync();
     }
     STAMP(2);
-    if constexpr (ONE) step(T, a, sm.st, sm.sv, sm.d.fl, sm.d.wk, OneWin<NM>{&sm.d}, gws, b, live, h, work, lane);
-    else step(T, a, sm.st, sm.sv, sm.d.fl, sm.d.wk, RingWin<NM>{sm.d.s, i}, gws, b, live, h, work, lane);
+    if constexpr (ONE) step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.wk, OneWin<NM>{&sm.d}, G, b, live, h, work, lane);
+    else step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.wk, RingWin<NM>{sm.d.s, i}, G, b, live, h, work, lane);
   }
   if (lane == 0 && live) {
     double cot = work / (T->total_mass * g.step_length);
@@ -1362,25 +1374,35 @@ extern "C" int hs_debug_clear_stamps() {
 namespace hs {
 
 size_t general_workspace_bytes() { return sizeof(GenWS); }
-int rollouts_per_wave() { return 2; }
 
-template <int NM>
-void launch_nm(const hs_topo* d_topo, const hs_run_args& a, GenWS* ws, hipStream_t st) {
-  const dim3 grid((a.n_rollouts + 1) / 2);  // two rollouts per wavefront
-  if (a.horizon == 1)
-    hipLaunchKernelGGL((hs_rollout_kernel<true, NM>), grid, dim3(WAVE), 0, st, d_topo, a, ws);
-  else
-    hipLaunchKernelGGL((hs_rollout_kernel<false, NM>), grid, dim3(WAVE), 0, st, d_topo, a, ws);
+launch_map single_model_map(const hs_topo& t, int32_t n_rollouts) {
+  launch_map mp{};
+  mp.n_waves = (n_rollouts + 1) / 2;  // two rollouts per wavefront
+  mp.max_parts = t.n;
+  mp.st_tau = t.nmj;
+  mp.st_cf = 3 * t.nf;
+  mp.st_q = t.cfg;
+  mp.st_x = 6 * t.n;
+  return mp;
 }
 
-int launch_rollouts(const hs_topo* d_topo, const hs_topo& h_topo, const hs_run_args& a, void* workspace) {
-  if (a.n_rollouts <= 0) return 0;
+template <int NM>
+void launch_nm(const hs_topo* d_topo, const hs_run_args& a, GenWS* ws, const launch_map& mp, hipStream_t st) {
+  const dim3 grid(mp.n_waves);
+  if (a.horizon == 1)
+    hipLaunchKernelGGL((hs_rollout_kernel<true, NM>), grid, dim3(WAVE), 0, st, d_topo, a, ws, mp);
+  else
+    hipLaunchKernelGGL((hs_rollout_kernel<false, NM>), grid, dim3(WAVE), 0, st, d_topo, a, ws, mp);
+}
+
+int launch_rollouts(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp) {
+  if (a.n_rollouts <= 0 || mp.n_waves <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
   GenWS* ws = (GenWS*)workspace;
-  // smallest LDS layout that holds the model's parts (myant 17, spider 19, hexapod 22)
-  if (h_topo.n <= 18) launch_nm<18>(d_topo, a, ws, st);
-  else if (h_topo.n <= 22) launch_nm<22>(d_topo, a, ws, st);
-  else launch_nm<HS_NMAX>(d_topo, a, ws, st);
+  // smallest LDS layout that holds the (largest) model's parts: myant 17, spider 19, hexapod 22
+  if (mp.max_parts <= 18) launch_nm<18>(d_topo, a, ws, mp, st);
+  else if (mp.max_parts <= 22) launch_nm<22>(d_topo, a, ws, mp, st);
+  else launch_nm<HS_NMAX>(d_topo, a, ws, mp, st);
   return (int)hipGetLastError();
 }
 

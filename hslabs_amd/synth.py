@@ -70,3 +70,18 @@ def gen_params(n: int, model: str = "hexapod", id0: int = 0, curved: bool = Fals
     arr["foot_shift_type"] = base["foot_shift"][0]
     arr["foot_shift"] = base["foot_shift"][1]
     return arr
+
+
+MIXED_MODELS = ("myant", "hexapod")
+
+
+def gen_mixed(n: int, id0: int = 0, curved: bool = False, seed: int = SEED):
+    """BASELINE configs[4]: a 50/50 myant / hexapod batch, interleaved by rollout id
+    (even id -> myant, odd -> hexapod). Returns (params, model_index into MIXED_MODELS);
+    each rollout's parameters are those gen_params draws for its id and model."""
+    ids = np.arange(id0, id0 + n, dtype=np.int64)
+    idx = (ids % 2).astype(np.int32)
+    out = gen_params(n, MIXED_MODELS[0], id0, curved, seed)
+    other = gen_params(n, MIXED_MODELS[1], id0, curved, seed)
+    out[idx == 1] = other[idx == 1]
+    return out, idx

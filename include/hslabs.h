@@ -131,6 +131,25 @@ int hs_run(hs_model_t model, const hs_run_args* args);
  * and after each launch (per-launch kernel timing on the launch stream). */
 int hs_run_steps(hs_model_t model, const hs_run_args* args, int32_t n_calls, void* const* kernel_events);
 
+/* Mixed-topology batches (BASELINE configs[4], e.g. myant + hexapod interleaved):
+ * rollout b runs models[model_index[b]]. The reference runs one kinematicmodel
+ * per periodic object (periodic.cpp:34-58); a plan batches several in one
+ * launch. It groups each model's rollouts two per wavefront, so topology reads
+ * stay wave-uniform, and is reusable across calls on the device current at
+ * creation. Models must outlive the plan. model_index is a HOST array. */
+typedef struct hs_mixed_s* hs_mixed_t;
+int hs_mixed_create(const hs_model_t* models, int32_t n_models, const int32_t* model_index, int32_t n_rollouts,
+                    hs_mixed_t* out);
+void hs_mixed_free(hs_mixed_t plan);
+/* Output row strides of the plan's batches = the maxima over its models:
+ * tau rows hold max nmj, cf 3 * max nfeet, q max config_dim, x 6 * max n_parts
+ * (the other fields of *out are those of the model with the most parts).
+ * Entries past a rollout's own dimensions are written as 0. */
+int hs_mixed_get_dims(hs_mixed_t plan, hs_model_dims* out);
+/* hs_run / hs_run_steps over a plan (args->n_rollouts must equal the plan's). */
+int hs_run_mixed(hs_mixed_t plan, const hs_run_args* args);
+int hs_run_mixed_steps(hs_mixed_t plan, const hs_run_args* args, int32_t n_calls, void* const* kernel_events);
+
 /* Host-buffer convenience wrapper of hs_run (copies in/out, synchronous).
  * Replaces periodic::compute_torques_over_period + get_motor_torques +
  * work_over_period for a batch of rollouts. Output pointers may be NULL. */

@@ -164,3 +164,30 @@ def test_shard_ranges_cover_batch():
         assert sum(c for _, c in ranges) == n
         ids = [i for s, c in ranges for i in range(s, s + c)]
         assert ids == list(range(n))
+
+
+def test_mixed_plan_argument_validation(product):
+    """hs_mixed_create checks its host-side arguments before touching a device."""
+    L = product.capi.load()
+    ms = [product.KinematicModel(os.path.join(MODELS, f"{n}.xml")) for n in ("myant", "hexapod")]
+    hs = (ctypes.c_void_p * 2)(*[m.handle for m in ms])
+    plan = ctypes.c_void_p()
+    idx = np.array([0, 1, 2, 1], dtype=np.int32)  # 2 is out of range
+    p32 = ctypes.POINTER(ctypes.c_int32)
+    assert L.hs_mixed_create(hs, 2, idx.ctypes.data_as(p32), 4, ctypes.byref(plan)) == -1
+    assert b"model_index" in L.hs_last_error()
+    assert L.hs_mixed_create(hs, 0, idx.ctypes.data_as(p32), 4, ctypes.byref(plan)) == -1
+    assert L.hs_mixed_create(None, 2, idx.ctypes.data_as(p32), 4, ctypes.byref(plan)) == -1
+    assert L.hs_run_mixed(None, None) == -1
+    assert L.hs_mixed_get_dims(None, None) == -1
+    L.hs_mixed_free(None)  # no-op
+
+
+def test_mixed_synthetic_batch_layout(product):
+    from hslabs_amd import synth
+
+    p, idx = synth.gen_mixed(64, id0=10)
+    assert (idx == (np.arange(10, 74) % 2)).all() and idx.mean() == 0.5
+    a = synth.gen_params(64, "myant", id0=10)
+    h = synth.gen_params(64, "hexapod", id0=10)
+    assert (p[idx == 0] == a[idx == 0]).all() and (p[idx == 1] == h[idx == 1]).all()

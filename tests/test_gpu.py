@@ -224,3 +224,55 @@ def test_edge_cases(gpu, hmodels):
 
     big = gpu.run_host(m, synth.gen_params(32768, "hexapod"), n_t=20, horizon=1, want=("tau", "flags"))
     assert np.isfinite(big["tau"]).all()
+
+
+@pytest.mark.parametrize("horizon", [1, 20])
+def test_mixed_batch_matches_single_model_runs(gpu, hmodels, horizon):
+    """BASELINE configs[4]: myant + hexapod interleaved in one launch == each model's own
+    launch, bit for bit (same arithmetic; the LDS layout is sized to the larger model);
+    output rows padded to the larger model's dimensions with zeros."""
+    import torch
+
+    from hslabs_amd import synth
+
+    params, idx = synth.gen_mixed(301, id0=5)
+    ms = [hmodels[n] for n in synth.MIXED_MODELS]
+    mb = gpu.MixedBatch(ms, idx, params, n_t=20, horizon=horizon, outputs=("tau", "cf", "q", "x", "flags", "work_cot"))
+    assert (mb.dims.nmj, mb.dims.nfeet, mb.dims.config_dim, mb.dims.n_parts) == (18, 6, 24, 22)
+    mb.work_cot.zero_()
+    mb.k0 = 3
+    mb.run(best=False, accumulate=True)
+    torch.cuda.synchronize()
+    for k, m in enumerate(ms):
+        sel = np.nonzero(idx == k)[0]
+        sb = gpu.DeviceBatch(m, params[sel], n_t=20, k0=3, horizon=horizon,
+                             outputs=("tau", "cf", "q", "x", "flags", "work_cot"))
+        sb.work_cot.zero_()
+        sb.run(best=False, accumulate=True)
+        torch.cuda.synchronize()
+        t = torch.from_numpy(sel).to(mb.tau.device)
+        assert torch.equal(mb.tau[t][:, :, :m.nmj], sb.tau)
+        assert torch.equal(mb.cf[t][:, :, :3 * m.nfeet], sb.cf)
+        assert torch.equal(mb.q[t][:, :, :m.config_dim], sb.q)
+        assert torch.equal(mb.x[t][:, :, :6 * m.n_parts], sb.x)
+        assert torch.equal(mb.flags[t], sb.flags) and torch.equal(mb.work_cot[t], sb.work_cot)
+        assert (mb.tau[t][:, :, m.nmj:] == 0).all() and (mb.cf[t][:, :, 3 * m.nfeet:] == 0).all()
+        assert (mb.x[t][:, :, 6 * m.n_parts:] == 0).all()
+
+
+def test_mixed_batch_matches_oracle(gpu, hmodels, oracle_mod, omodels):
+    from hslabs_amd import synth
+
+    params, idx = synth.gen_mixed(24, id0=1000)
+    mb = gpu.MixedBatch([hmodels[n] for n in synth.MIXED_MODELS], idx, params, n_t=20, horizon=20)
+    mb.run(best=False)
+    import torch
+
+    torch.cuda.synchronize()
+    tau = mb.tau.cpu().numpy()
+    for b in range(24):
+        name = synth.MIXED_MODELS[idx[b]]
+        r = oracle_mod.rollout(omodels[name], record_to_oracle_gait(oracle_mod, params[b]), 20,
+                               basis=oracle_mod.BASIS_FAST)
+        nmj = hmodels[name].nmj
+        assert np.abs(tau[b, :, :nmj] - r["tau"]).max() < 1e-6 * max(1, np.abs(r["tau"]).max())
