@@ -20,6 +20,7 @@ struct launch_map {
   const int32_t* wave_rollouts;  // mixed: [2 * n_waves] rollout ids, -1 = idle half
   int32_t n_waves;
   int32_t max_parts;             // LDS layout class (largest model)
+  int32_t h_row;                 // output row of this launch's step within the horizon
   int32_t st_tau, st_cf, st_q, st_x;  // output row strides (mixed: maxima over the models)
 };
 

@@ -17,13 +17,13 @@
 //      (tree-built null basis, Gram matrices in a global-memory workspace),
 //   S4 motor torques, contact forces and positive work (periodic.cpp:261-343).
 //
-// Two LDS layouts (template parameter ONE):
-//   ONE  (horizon 1, the BASELINE configs[1] workload): the five stencil
-//        samples keep only what the step reads -- pos/ust at t-2dt, t, t+2dt,
-//        R at t+-dt, q at t-dt..t+dt, joint/foot features at t -- and the
-//        stencil-only block is reused by the fast solve once D has consumed it.
-//        ~12 KB per wave.
-//   ring (horizon > 1): five full samples in a ring, one new sample per step.
+// LDS layout: a launch solves one step per rollout, so the five stencil
+// samples keep only what that step reads -- pos/ust at t-2dt, t, t+2dt, R at
+// t+-dt, q at t-dt..t+dt, joint/foot features at t -- and the stencil-only
+// block is reused by the fast solve once D has consumed it (9.5 KB per
+// hexapod rollout). A horizon H > 1 is H launches (hs_capi.cpp): the sampler
+// is latency-bound, so recomputing the window on 30 lanes costs about what a
+// sliding window's one new sample on 6 lanes would, at twice the occupancy.
 //
 // Every floating-point operation sequence matches oracle/hs_oracle.cpp
 // (compiled with -ffp-contract=off), so the only expected differences against
@@ -32,7 +32,6 @@
 
 #include <cfloat>
 #include <cstdint>
-#include <type_traits>
 
 #include "hs_internal.h"
 #include "hs_math.h"
@@ -54,15 +53,7 @@ static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a
 // LDS layouts
 // ---------------------------------------------------------------------------
 // NM = part capacity of the LDS layouts (the host picks the smallest instantiation >= n,
-// so LDS per rollout follows the model: hexapod 9.5 KB at H = 1).
-template <int NM>
-struct SampleL {  // one full sample (ring layout)
-  double pos[NM][3], jpos[NM][3], ust[NM][3], rot[NM][9], jz[NM][3];
-  double fpos[HS_LMAX][3];
-  double q[6 + NM];
-  int contact[HS_LMAX];
-  int unreach[HS_LMAX];
-};
+// so LDS per rollout follows the model: hexapod 9.5 KB).
 
 struct FastL {  // per-contact blocks of the closed-form solve
   double A[HS_LMAX][18], D[HS_LMAX][9], g[HS_LMAX][3], Dinv[HS_LMAX][9], S[HS_LMAX][36], h[HS_LMAX][6];
@@ -75,27 +66,18 @@ struct WorkL {  // per-joint positive work of the step (outputs phase; FastL is 
 };
 
 template <int NM>
-struct StencilL {  // ONE layout: fields only the finite differences read
+struct StencilL {  // fields only the finite differences read
   double pos[2][NM][3];  // t-2dt, t+2dt
   double ust[3][NM][3];  // t-2dt, t, t+2dt
   double rot[2][NM][9];  // t-dt, t+dt
 };
 
 template <int NM>
-struct CentreL {  // ONE layout: fields read after D
+struct CentreL {  // fields read after D
   double pos[NM][3], jpos[NM][3], jz[NM][3], fpos[HS_LMAX][3];
   double q[3][6 + NM];  // t-dt, t, t+dt
   int contact[HS_LMAX];
   int unreach[HS_LMAX];
-};
-
-template <int NM>
-struct RingStore {
-  SampleL<NM> s[NS];
-  union {
-    FastL fl;
-    WorkL wk;
-  };
 };
 
 template <int NM>
@@ -124,9 +106,9 @@ struct SolveL {
   int cfoot[HS_LMAX];
 };
 
-template <bool ONE, int NM>
+template <int NM>
 struct Smem {
-  typename std::conditional<ONE, OneStore<NM>, RingStore<NM>>::type d;
+  OneStore<NM> d;
   SetupL st;
   SolveL<NM> sv;
 };
@@ -173,27 +155,6 @@ __device__ inline A34 node_pj(const hs_topo* T, int v) { return load34(T->node[v
 // ---------------------------------------------------------------------------
 // Sample views. k = offset from the step's centre sample (-2..2).
 // ---------------------------------------------------------------------------
-template <int NM>
-struct RingWin {  // centre = sample i (ring slot i % 5)
-  SampleL<NM>* s;
-  int i;
-  __device__ SampleL<NM>& at(int k) const { return s[(i + k) % NS]; }
-  __device__ bool want_pos(int) const { return true; }
-  __device__ bool want_ust(int) const { return true; }
-  __device__ bool want_rot(int) const { return true; }
-  __device__ bool want_q(int) const { return true; }
-  __device__ bool want_centre(int) const { return true; }
-  __device__ double* pos(int k, int v) const { return at(k).pos[v]; }
-  __device__ double* ust(int k, int v) const { return at(k).ust[v]; }
-  __device__ double* rot(int k, int v) const { return at(k).rot[v]; }
-  __device__ double* q(int k) const { return at(k).q; }
-  __device__ double* jpos(int k, int v) const { return at(k).jpos[v]; }
-  __device__ double* jz(int k, int v) const { return at(k).jz[v]; }
-  __device__ double* fpos(int k, int f) const { return at(k).fpos[f]; }
-  __device__ int& contact(int k, int f) const { return at(k).contact[f]; }
-  __device__ int& unreach(int k, int L) const { return at(k).unreach[L]; }
-};
-
 template <int NM>
 struct OneWin {
   OneStore<NM>* d;
@@ -414,14 +375,6 @@ __device__ void kin_sample(const hs_topo* T, const hs_gait_params& g, const Setu
     node_features(T, v, A, &Jv, w, k);
     if (kk < 2) v = nd.kids[0];
   }
-}
-
-// Out-of-line copy for the ring kernel, whose step loop would otherwise keep
-// the sampler's loop-invariant addresses live across all steps.
-template <class W>
-__device__ __noinline__ void kin_sample_ool(const hs_topo* T, const hs_gait_params& g, const SetupL& st, int isample,
-                                            int L, bool ignore_reach, const W& w, int k) {
-  kin_sample(T, g, st, isample, L, ignore_reach, w, k);
 }
 
 // ---------------------------------------------------------------------------
@@ -1299,11 +1252,11 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const hs::launch_ma
   STAMP(8);
 }
 
-template <bool ONE, int NM>
-__global__ __launch_bounds__(WAVE, ONE ? HS_MIN_WAVES : 1) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
+template <int NM>
+__global__ __launch_bounds__(WAVE, HS_MIN_WAVES) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
                                                                                  hs_run_args a, GenWS* __restrict__ gws,
                                                                                  hs::launch_map mp) {
-  __shared__ Smem<ONE, NM> smem[2];
+  __shared__ Smem<NM> smem[2];
   const int sub = threadIdx.x / HALF;  // rollout slot within the wave
   const int lane = threadIdx.x % HALF; // lane within the rollout
   // one model per wavefront: the topology pointer stays wave-uniform (scalar loads)
@@ -1320,7 +1273,7 @@ __global__ __launch_bounds__(WAVE, ONE ? HS_MIN_WAVES : 1) void hs_rollout_kerne
     bb = live ? b : a.n_rollouts - 1;
   }
   GenWS* G = gws + (live ? b : a.n_rollouts);
-  Smem<ONE, NM>& sm = smem[sub];
+  Smem<NM>& sm = smem[sub];
   double work = (live && a.accumulate && a.work_cot) ? a.work_cot[2 * (size_t)b] : 0.0;
   const hs_gait_params g = a.params[bb];
   const int nl = T->n_limbs;
@@ -1330,23 +1283,15 @@ __global__ __launch_bounds__(WAVE, ONE ? HS_MIN_WAVES : 1) void hs_rollout_kerne
   gait_setup(T, g, a.n_t, sm.st, lane);
   STAMP(1);
 
-  const int H = ONE ? 1 : a.horizon;  // compile-time single step for the H = 1 layout
-  for (int h = 0; h < H; h++) {
-    const int i = a.k0 + h + 2;  // centre sample of this step
-    // K: the whole window on the first step, then the newest sample (lane = (sample, limb))
-    {
-      const int sl = (h == 0) ? lane / nl : NS - 1;
-      const int L = (h == 0) ? lane % nl : lane;
-      if (sl < NS && L < nl) {
-        if constexpr (ONE) kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM>{&sm.d}, sl - 2);
-        else kin_sample_ool(T, g, sm.st, i - 2 + sl, L, ignore_reach, RingWin<NM>{sm.d.s, i - 2 + sl}, 0);
-      }
-      wave_sync();
-    }
-    STAMP(2);
-    if constexpr (ONE) step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.wk, OneWin<NM>{&sm.d}, G, b, live, h, work, lane);
-    else step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.wk, RingWin<NM>{sm.d.s, i}, G, b, live, h, work, lane);
+  // K: the five-sample window, lane = (sample, limb)
+  const int i = a.k0 + 2;  // centre sample of this launch's step
+  {
+    const int sl = lane / nl, L = lane % nl;
+    if (sl < NS) kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM>{&sm.d}, sl - 2);
+    wave_sync();
   }
+  STAMP(2);
+  step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.wk, OneWin<NM>{&sm.d}, G, b, live, mp.h_row, work, lane);
   if (lane == 0 && live) {
     double cot = work / (T->total_mass * g.step_length);
     if (a.work_cot) {
@@ -1388,22 +1333,30 @@ launch_map single_model_map(const hs_topo& t, int32_t n_rollouts) {
 
 template <int NM>
 void launch_nm(const hs_topo* d_topo, const hs_run_args& a, GenWS* ws, const launch_map& mp, hipStream_t st) {
-  const dim3 grid(mp.n_waves);
-  if (a.horizon == 1)
-    hipLaunchKernelGGL((hs_rollout_kernel<true, NM>), grid, dim3(WAVE), 0, st, d_topo, a, ws, mp);
-  else
-    hipLaunchKernelGGL((hs_rollout_kernel<false, NM>), grid, dim3(WAVE), 0, st, d_topo, a, ws, mp);
+  hipLaunchKernelGGL((hs_rollout_kernel<NM>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
 }
 
 int launch_rollouts(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp) {
   if (a.n_rollouts <= 0 || mp.n_waves <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
   GenWS* ws = (GenWS*)workspace;
-  // smallest LDS layout that holds the (largest) model's parts: myant 17, spider 19, hexapod 22
-  if (mp.max_parts <= 18) launch_nm<18>(d_topo, a, ws, mp, st);
-  else if (mp.max_parts <= 22) launch_nm<22>(d_topo, a, ws, mp, st);
-  else launch_nm<HS_NMAX>(d_topo, a, ws, mp, st);
-  return (int)hipGetLastError();
+  // one launch per step of the horizon: step h writes output row h, work accumulates in
+  // step order (periodic.cpp:291-304), the best key is taken after the last step
+  for (int h = 0; h < a.horizon; h++) {
+    hs_run_args ah = a;
+    launch_map mh = mp;
+    ah.k0 = a.k0 + h;
+    ah.accumulate = (h == 0) ? a.accumulate : 1;
+    if (h + 1 < a.horizon) ah.best_key = nullptr;
+    mh.h_row = h;
+    // smallest LDS layout that holds the (largest) model's parts: myant 17, spider 19, hexapod 22
+    if (mp.max_parts <= 18) launch_nm<18>(d_topo, ah, ws, mh, st);
+    else if (mp.max_parts <= 22) launch_nm<22>(d_topo, ah, ws, mh, st);
+    else launch_nm<HS_NMAX>(d_topo, ah, ws, mh, st);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
 }
 
 }  // namespace hs
