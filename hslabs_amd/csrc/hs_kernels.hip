@@ -43,7 +43,6 @@ using namespace hsd;
 constexpr int WAVE = 64;
 constexpr int HALF = 32;     // lanes per rollout: two rollouts per wavefront
 constexpr int NS = 5;        // samples in the derivative stencil (periodic.cpp:192-202)
-constexpr int LD = HS_KMAX;  // leading dimension of k x k matrices
 static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a rollout's lane maps exceed 32");
 #ifndef HS_MIN_WAVES
 #define HS_MIN_WAVES 2  // waves per SIMD the H = 1 register budget allows (8 workgroups/CU at 19.5 KB LDS)
@@ -55,15 +54,43 @@ static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a
 // NM = part capacity of the LDS layouts (the host picks the smallest instantiation >= n,
 // so LDS per rollout follows the model: hexapod 9.5 KB).
 
-struct FastL {  // per-contact blocks of the closed-form solve
-  double A[HS_LMAX][18], D[HS_LMAX][9], g[HS_LMAX][3], Dinv[HS_LMAX][9], S[HS_LMAX][36], h[HS_LMAX][6];
+struct SchurL {  // per-contact Schur complement (all D_c invertible)
+  double Dinv[HS_LMAX][9], S[HS_LMAX][36], h[HS_LMAX][6];
   double lam[6];
+};
+
+struct AugL {  // augmented system K = D + rho A^T A (a singular D_c)
+  double K[HS_KMAX * HS_KMAX], X[HS_KMAX * 7], St[36], lam[6];
+  int ok;
+};
+
+struct FastL {  // blocks of the closed-form solve
+  double A[HS_LMAX][18], D[HS_LMAX][9], g[HS_LMAX][3];
   int ok[HS_LMAX];
+  union {
+    SchurL sc;
+    AugL ag;
+  };
 };
 
 struct WorkL {  // per-joint positive work of the step (outputs phase; FastL is dead by then)
   double wd[HS_NMAX];
 };
+
+// Workspace of the general path (k x k matrices, leading dimension LD >= k).
+// SHARED: in LDS (the dead stencil block, k <= 12: any 4-legged model, up to 4
+// contacts of a 6-legged one); otherwise one global-memory slot per rollout.
+template <int LD_, bool SHARED_>
+struct GenMats {
+  static constexpr int LD = LD_;
+  static constexpr bool SHARED = SHARED_;
+  double ntn0[LD * LD], lu[LD * LD], Ny[LD * LD], qr[LD * LD];
+  double n1[LD / 3][9];  // 3x3 diagonal blocks of the first-order Gram (column-major)
+  double ntx0[LD], ntx1[LD], y0[LD], b[LD], z[LD], c[LD], hc[LD], nu[LD], nd[LD];
+  int8_t rowsT[LD], colsT[LD], q[LD], piv[LD], rycol[LD], cperm[LD];
+};
+using GenLDS = GenMats<12, true>;
+using GenWS = GenMats<HS_KMAX, false>;
 
 template <int NM>
 struct StencilL {  // fields only the finite differences read
@@ -85,6 +112,7 @@ struct OneStore {
   union {
     StencilL<NM> sten;
     FastL fl;  // written only after D has consumed the stencil
+    GenLDS gl;  // general path, k <= 12 (fast solve declined)
     WorkL wk;
   };
   CentreL<NM> c;
@@ -113,16 +141,6 @@ struct Smem {
   SolveL<NM> sv;
 };
 
-// Global-memory workspace of the out-of-line general path, one per rollout.
-struct GenWS {
-  double ntn0[HS_KMAX * LD], lu[HS_KMAX * LD], Ny[HS_KMAX * LD], M[HS_KMAX * LD], qr[HS_KMAX * LD];
-  double n1[HS_LMAX][9];  // 3x3 diagonal blocks of the first-order Gram (column-major)
-  double ntx0[HS_KMAX], ntx1[HS_KMAX], y0[HS_KMAX], b[HS_KMAX], z[HS_KMAX], c[HS_KMAX];
-  double hc[HS_KMAX], nu[HS_KMAX], nd[HS_KMAX];
-  int rowsT[HS_KMAX], colsT[HS_KMAX], q[HS_KMAX], piv[HS_KMAX], rycol[HS_KMAX], cperm[HS_KMAX];
-  double pos0[3], jpos[HS_NMAX][3], jz[HS_NMAX][3], fpos[HS_LMAX][3];  // centre-sample copy
-};
-
 // Cross-lane exchange through LDS inside the single wave of a workgroup: an
 // LDS-only workgroup fence (lgkmcnt, no vmcnt, so HBM stores stay in flight).
 __device__ inline void wave_sync() {
@@ -130,8 +148,12 @@ __device__ inline void wave_sync() {
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
-// The general path also exchanges through its global workspace.
-__device__ inline void gen_sync() { __syncthreads(); }
+// The general path with a global workspace also needs its HBM stores performed.
+template <class G>
+__device__ inline void gsync() {
+  if constexpr (G::SHARED) wave_sync();
+  else __syncthreads();
+}
 
 #ifdef HS_STAMPS
 // diagnostic build only: per-phase shader-clock stamps of the first 4096 rollouts
@@ -481,39 +503,44 @@ __device__ inline double cross_e(const double* d, int jj, int row) {
 }
 
 // ===========================================================================
-// General path (out of line; rare): Gram matrices of the tree-built null basis
-// and the Eigen 3.3 FullPivLU / ColPivHouseholderQR rank loop. Operates on the
-// rollout's global workspace G (centre features copied in) and on sv (LDS).
+// General path (rare: the fast solve's guard tripped): Gram matrices of the
+// tree-built null basis and the Eigen 3.3 FullPivLU / ColPivHouseholderQR rank
+// loop of ftsolver.cpp:185-303 (oracle/hs_oracle.cpp tree mode, same
+// operation order). G is the LDS or the global workspace (GenMats).
 // ===========================================================================
 
 // S2: Gram matrices of the masked, penalty-weighted null basis (ftsolver.cpp:185-207)
-template <class SV>
-__device__ void build_grams(const hs_topo* T, const SV& sv, GenWS& G, int k, int lane) {
+template <class W, class SV, class G>
+__device__ void build_grams(const hs_topo* T, const SV& sv, G& g, const W& w, int k, int lane) {
+  constexpr int LD = G::LD;
   const int n = T->n;
   const int nc = k / 3;
+  const double* P0 = w.pos(0, 0);
   // zeroth order: rows {0,1,2} = -I, rows {3n..3n+2} = (pos_0 - fpos) x e_jj, weight 1
   for (int e = lane; e < k * k; e += HALF) {
     int ci = e % k, cj = e / k;
-    int fa = sv.cfoot[ci / 3], fb = sv.cfoot[cj / 3];
+    const double* fa = w.fpos(0, sv.cfoot[ci / 3]);
+    const double* fb = w.fpos(0, sv.cfoot[cj / 3]);
     int ja = ci % 3, jb = cj % 3;
     double da[3], db[3];
-    for (int r = 0; r < 3; r++) { da[r] = G.pos0[r] - G.fpos[fa][r]; db[r] = G.pos0[r] - G.fpos[fb][r]; }
+    for (int r = 0; r < 3; r++) { da[r] = P0[r] - fa[r]; db[r] = P0[r] - fb[r]; }
     double s = 0.0;
     for (int r = 0; r < 3; r++) {
       double na = (r == ja) ? -1.0 : 0.0, nb = (r == jb) ? -1.0 : 0.0;
       s = s + na * nb;
     }
     for (int r = 0; r < 3; r++) s = s + cross_e(da, ja, r) * cross_e(db, jb, r);
-    G.ntn0[ci + cj * LD] = s;
+    g.ntn0[ci + cj * LD] = s;
   }
   if (lane < k) {
-    int ci = lane, fa = sv.cfoot[ci / 3], ja = ci % 3;
+    int ci = lane, ja = ci % 3;
+    const double* fa = w.fpos(0, sv.cfoot[ci / 3]);
     double da[3];
-    for (int r = 0; r < 3; r++) da[r] = G.pos0[r] - G.fpos[fa][r];
+    for (int r = 0; r < 3; r++) da[r] = P0[r] - fa[r];
     double s = 0.0;
     for (int r = 0; r < 3; r++) s = s + ((r == ja) ? -1.0 : 0.0) * (1.0 * sv.x[r]);
     for (int r = 0; r < 3; r++) s = s + cross_e(da, ja, r) * (1.0 * sv.x[3 * n + r]);
-    G.ntx0[ci] = s;
+    g.ntx0[ci] = s;
   }
   // first order: torque rows of the non-root ancestors of each contact foot,
   // weighted by the joint-axis components (set_action_penalties, ftsolver.cpp:239-246)
@@ -523,30 +550,34 @@ __device__ void build_grams(const hs_topo* T, const SV& sv, GenWS& G, int k, int
     int a_col = is_vec ? (e - nc * 9) % 3 : (e % 9) % 3;
     int b_col = is_vec ? 0 : (e % 9) / 3;
     int foot = T->footis[sv.cfoot[cc]];
+    const double* fp = w.fpos(0, sv.cfoot[cc]);
     // ancestors of foot below the root, in ascending part order (top of the chain first)
     int chain[HS_NMAX], len = 0;
     for (int a = foot; a >= 0 && T->node[a].parent >= 0; a = T->node[a].parent) chain[len++] = a;
     double s = 0.0;
     for (int t = len - 1; t >= 0; t--) {
       int a = chain[t];
+      const double* Ja = w.jpos(0, a);
+      const double* Za = w.jz(0, a);
       double d[3];
-      for (int r = 0; r < 3; r++) d[r] = G.jpos[a][r] - G.fpos[sv.cfoot[cc]][r];
+      for (int r = 0; r < 3; r++) d[r] = Ja[r] - fp[r];
       for (int r = 0; r < 3; r++) {
-        double w = G.jz[a][r];
-        double na = w * cross_e(d, a_col, r);
-        double nb = is_vec ? w * sv.x[3 * n + 3 * a + r] : w * cross_e(d, b_col, r);
+        double wz = Za[r];
+        double na = wz * cross_e(d, a_col, r);
+        double nb = is_vec ? wz * sv.x[3 * n + 3 * a + r] : wz * cross_e(d, b_col, r);
         s = s + na * nb;
       }
     }
-    if (is_vec) G.ntx1[3 * cc + a_col] = s;
-    else G.n1[cc][b_col * 3 + a_col] = s;
+    if (is_vec) g.ntx1[3 * cc + a_col] = s;
+    else g.n1[cc][b_col * 3 + a_col] = s;
   }
-  gen_sync();
+  gsync<G>();
 }
 
 // first-order Gram entry (block diagonal)
-__device__ inline double ntn1_at(const GenWS& G, int i, int j) {
-  return (i / 3 == j / 3) ? G.n1[i / 3][(j % 3) * 3 + (i % 3)] : 0.0;
+template <class G>
+__device__ inline double ntn1_at(const G& g, int i, int j) {
+  return (i / 3 == j / 3) ? g.n1[i / 3][(j % 3) * 3 + (i % 3)] : 0.0;
 }
 
 // half-wave argmax with first-index tie break
@@ -563,72 +594,78 @@ struct LUInfo {
   double maxpivot;
 };
 
-// Eigen FullPivLU::computeInPlace on G.lu (k x k)
-__device__ LUInfo fullpiv_lu(GenWS& G, int k, int lane) {
+// Eigen FullPivLU::computeInPlace of ntn0 into g.lu (k x k)
+template <class G>
+__device__ LUInfo fullpiv_lu(G& g, int k, int lane) {
+  constexpr int LD = G::LD;
   for (int e = lane; e < k * k; e += HALF) {
     int i = e % k, j = e / k;
-    G.lu[i + j * LD] = G.ntn0[i + j * LD];
+    g.lu[i + j * LD] = g.ntn0[i + j * LD];
   }
-  gen_sync();
+  gsync<G>();
   LUInfo info{k, 0.0};
   for (int p = 0; p < k; p++) {
     const int m = k - p;
     double best = -1.0;
     int bidx = 1 << 30;
     for (int e = lane; e < m * m; e += HALF) {
-      double a = fabs(G.lu[(p + e % m) + (p + e / m) * LD]);
+      double a = fabs(g.lu[(p + e % m) + (p + e / m) * LD]);
       if (a > best || (a == best && e < bidx)) { best = a; bidx = e; }
     }
     wave_argmax(best, bidx);
     if (best == 0) {
       info.nz = p;
-      for (int i = p + lane; i < k; i += HALF) { G.rowsT[i] = i; G.colsT[i] = i; }
+      for (int i = p + lane; i < k; i += HALF) { g.rowsT[i] = i; g.colsT[i] = i; }
       break;
     }
     if (best > info.maxpivot) info.maxpivot = best;
     const int bi = p + bidx % m, bj = p + bidx / m;
-    if (lane == 0) { G.rowsT[p] = bi; G.colsT[p] = bj; }
+    if (lane == 0) { g.rowsT[p] = bi; g.colsT[p] = bj; }
     if (bi != p && lane < k) {
-      double t = G.lu[p + lane * LD];
-      G.lu[p + lane * LD] = G.lu[bi + lane * LD];
-      G.lu[bi + lane * LD] = t;
+      double t = g.lu[p + lane * LD];
+      g.lu[p + lane * LD] = g.lu[bi + lane * LD];
+      g.lu[bi + lane * LD] = t;
     }
-    gen_sync();
+    gsync<G>();
     if (bj != p && lane < k) {
-      double t = G.lu[lane + p * LD];
-      G.lu[lane + p * LD] = G.lu[lane + bj * LD];
-      G.lu[lane + bj * LD] = t;
+      double t = g.lu[lane + p * LD];
+      g.lu[lane + p * LD] = g.lu[lane + bj * LD];
+      g.lu[lane + bj * LD] = t;
     }
-    gen_sync();
+    gsync<G>();
     if (p < k - 1) {
-      double piv = G.lu[p + p * LD];
-      if (lane > p && lane < k) G.lu[lane + p * LD] /= piv;
-      gen_sync();
+      double piv = g.lu[p + p * LD];
+      if (lane > p && lane < k) g.lu[lane + p * LD] /= piv;
+      gsync<G>();
       const int mm = k - p - 1;
       for (int e = lane; e < mm * mm; e += HALF) {
         int i = p + 1 + e % mm, j = p + 1 + e / mm;
-        G.lu[i + j * LD] -= G.lu[i + p * LD] * G.lu[p + j * LD];
+        g.lu[i + j * LD] -= g.lu[i + p * LD] * g.lu[p + j * LD];
       }
-      gen_sync();
+      gsync<G>();
     }
   }
   if (lane == 0) {
-    for (int i = 0; i < k; i++) G.q[i] = i;
-    for (int p = 0; p < k; p++) { int t = G.q[p]; G.q[p] = G.q[G.colsT[p]]; G.q[G.colsT[p]] = t; }
+    for (int i = 0; i < k; i++) g.q[i] = i;
+    for (int p = 0; p < k; p++) { int t = g.q[p]; g.q[p] = g.q[g.colsT[p]]; g.q[g.colsT[p]] = t; }
   }
-  gen_sync();
+  gsync<G>();
   return info;
 }
 
-__device__ inline int lu_rank(const GenWS& G, const LUInfo& info, double thr) {
+template <class G>
+__device__ inline int lu_rank(const G& g, const LUInfo& info, double thr) {
+  constexpr int LD = G::LD;
   double pt = fabs(info.maxpivot) * thr;
   int r = 0;
-  for (int i = 0; i < info.nz; i++) r += fabs(G.lu[i + i * LD]) > pt;
+  for (int i = 0; i < info.nz; i++) r += fabs(g.lu[i + i * LD]) > pt;
   return r;
 }
 
 // column-oriented upper-triangular solve of vec[0..r) against U (ld LD), all lanes
+template <class G>
 __device__ void upper_solve_shared(const double* U, double* vec, int r, int lane) {
+  constexpr int LD = G::LD;
   for (int i = r - 1; i >= 0; i--) {
     double ci = vec[i];
     if (ci != 0) {
@@ -636,54 +673,58 @@ __device__ void upper_solve_shared(const double* U, double* vec, int r, int lane
       if (lane < i) vec[lane] -= xi * U[lane + i * LD];
       if (lane == i) vec[i] = xi;
     }
-    gen_sync();
+    gsync<G>();
   }
 }
 
-// FullPivLU::solve(-ntx0) -> G.y0
-__device__ void lu_solve(GenWS& G, const LUInfo& info, int k, int r, int lane) {
+// FullPivLU::solve(-ntx0) -> g.y0
+template <class G>
+__device__ void lu_solve(G& g, const LUInfo& info, int k, int r, int lane) {
+  constexpr int LD = G::LD;
   if (lane == 0) {
-    for (int i = 0; i < k; i++) G.c[i] = -G.ntx0[i];
-    for (int p = 0; p < k; p++) { double t = G.c[p]; G.c[p] = G.c[G.rowsT[p]]; G.c[G.rowsT[p]] = t; }
+    for (int i = 0; i < k; i++) g.c[i] = -g.ntx0[i];
+    for (int p = 0; p < k; p++) { double t = g.c[p]; g.c[p] = g.c[g.rowsT[p]]; g.c[g.rowsT[p]] = t; }
   }
-  if (lane < k) G.y0[lane] = 0.0;
-  gen_sync();
+  if (lane < k) g.y0[lane] = 0.0;
+  gsync<G>();
   if (r == 0) return;
   for (int j = 0; j < k; j++) {  // unit lower
-    double cj = G.c[j];
-    if (lane > j && lane < k) G.c[lane] -= cj * G.lu[lane + j * LD];
-    gen_sync();
+    double cj = g.c[j];
+    if (lane > j && lane < k) g.c[lane] -= cj * g.lu[lane + j * LD];
+    gsync<G>();
   }
-  upper_solve_shared(G.lu, G.c, r, lane);
-  if (lane < r) G.y0[G.q[lane]] = G.c[lane];
-  gen_sync();
+  upper_solve_shared<G>(g.lu, g.c, r, lane);
+  if (lane < r) g.y0[g.q[lane]] = g.c[lane];
+  gsync<G>();
 }
 
-// FullPivLU::kernel() -> G.Ny (k x dimker); uses G.qr as scratch; G.piv/rycol set
-__device__ void lu_kernel_image(GenWS& G, const LUInfo& info, int k, int r, double thr, int lane) {
+// FullPivLU::kernel() -> g.Ny (k x dimker); uses g.qr as scratch; g.piv/rycol set
+template <class G>
+__device__ void lu_kernel_image(G& g, const LUInfo& info, int k, int r, double thr, int lane) {
+  constexpr int LD = G::LD;
   if (lane == 0) {
     double pt = info.maxpivot * thr;
     int p = 0;
     for (int i = 0; i < info.nz; i++)
-      if (fabs(G.lu[i + i * LD]) > pt) G.piv[p++] = i;
-    for (int i = 0; i < r; i++) G.rycol[i] = G.q[G.piv[i]];  // image columns
+      if (fabs(g.lu[i + i * LD]) > pt) g.piv[p++] = i;
+    for (int i = 0; i < r; i++) g.rycol[i] = g.q[g.piv[i]];  // image columns
   }
-  gen_sync();
+  gsync<G>();
   const int dimker = k - r;
   if (dimker == 0) return;
-  double* mm = G.qr;  // r x k trapezoid
+  double* mm = g.qr;  // r x k trapezoid
   for (int e = lane; e < r * k; e += HALF) {
     int i = e % r, j = e / r;
-    mm[i + j * LD] = (j >= i) ? G.lu[G.piv[i] + j * LD] : 0.0;
+    mm[i + j * LD] = (j >= i) ? g.lu[g.piv[i] + j * LD] : 0.0;
   }
-  gen_sync();
+  gsync<G>();
   if (lane < r) {  // bring non-negligible pivots to the front (rows own a column swap each)
     for (int i = 0; i < r; i++) {
-      int pc = G.piv[i];
+      int pc = g.piv[i];
       if (pc != i) { double t = mm[lane + i * LD]; mm[lane + i * LD] = mm[lane + pc * LD]; mm[lane + pc * LD] = t; }
     }
   }
-  gen_sync();
+  gsync<G>();
   if (lane < dimker) {  // solve U11 X = U12, one right-hand column per lane
     double* col = &mm[(r + lane) * LD];
     for (int i = r - 1; i >= 0; i--) {
@@ -693,166 +734,185 @@ __device__ void lu_kernel_image(GenWS& G, const LUInfo& info, int k, int r, doub
       }
     }
   }
-  gen_sync();
+  gsync<G>();
   if (lane < r) {
     for (int i = r - 1; i >= 0; i--) {
-      int pc = G.piv[i];
+      int pc = g.piv[i];
       if (pc != i) { double t = mm[lane + i * LD]; mm[lane + i * LD] = mm[lane + pc * LD]; mm[lane + pc * LD] = t; }
     }
   }
-  gen_sync();
+  gsync<G>();
   for (int e = lane; e < k * dimker; e += HALF) {
     int i = e % k, kk = e / k;
-    int row = G.q[i];
+    int row = g.q[i];
     double v;
     if (i < r) v = -mm[i + (r + kk) * LD];
     else v = (i == r + kk) ? 1.0 : 0.0;
-    G.Ny[row + kk * LD] = v;
+    g.Ny[row + kk * LD] = v;
   }
-  gen_sync();
+  gsync<G>();
 }
 
-// Eigen 3.3 ColPivHouseholderQR on G.qr (k x k, copy of M); returns nonzero pivots
-__device__ int colpiv_qr(GenWS& G, int k, int lane) {
-  for (int e = lane; e < k * k; e += HALF) {
-    int i = e % k, j = e / k;
-    G.qr[i + j * LD] = G.M[i + j * LD];
+// entry (i, j) of m = [ntn1 Ny, ntn0 Ry] (ftsolver.cpp:222-226), evaluated where needed
+template <class G>
+__device__ inline double m_at(const G& g, int k, int dimker, int i, int j) {
+  constexpr int LD = G::LD;
+  double s = 0.0;
+  if (j < dimker) {
+    int b0 = (i / 3) * 3;
+    for (int kk = b0; kk < b0 + 3; kk++) s = s + ntn1_at(g, i, kk) * g.Ny[kk + j * LD];
+  } else {
+    int col = g.rycol[j - dimker];
+    for (int kk = 0; kk < k; kk++) s = s + g.ntn0[i + kk * LD] * g.ntn0[kk + col * LD];
   }
-  gen_sync();
+  return s;
+}
+
+// Eigen 3.3 ColPivHouseholderQR on g.qr (k x k, holding m); returns nonzero pivots
+template <class G>
+__device__ int colpiv_qr(G& g, int k, int lane) {
+  constexpr int LD = G::LD;
   if (lane < k) {
     double s = 0;
-    for (int i = 0; i < k; i++) s += G.qr[i + lane * LD] * G.qr[i + lane * LD];
-    G.nd[lane] = sqrt(s);
-    G.nu[lane] = G.nd[lane];
+    for (int i = 0; i < k; i++) s += g.qr[i + lane * LD] * g.qr[i + lane * LD];
+    g.nd[lane] = sqrt(s);
+    g.nu[lane] = g.nd[lane];
   }
-  gen_sync();
+  gsync<G>();
   double mx = 0;
-  for (int j = 0; j < k; j++) mx = fmax(mx, G.nu[j]);
+  for (int j = 0; j < k; j++) mx = fmax(mx, g.nu[j]);
   const double th = mx * DBL_EPSILON;
   const double threshold_helper = th * th / (double)k;
   const double ndt = sqrt(DBL_EPSILON);
   int np = k;
   for (int p = 0; p < k; p++) {
     int bi = p;
-    double bv = G.nu[p];
+    double bv = g.nu[p];
     for (int j = p + 1; j < k; j++)
-      if (G.nu[j] > bv) { bv = G.nu[j]; bi = j; }
+      if (g.nu[j] > bv) { bv = g.nu[j]; bi = j; }
     if (np == k && bv * bv < threshold_helper * (double)(k - p)) np = p;
-    gen_sync();
-    if (lane == 0) G.cperm[p] = bi;
+    gsync<G>();
+    if (lane == 0) g.cperm[p] = bi;
     if (bi != p) {
       if (lane < k) {
-        double t = G.qr[lane + p * LD];
-        G.qr[lane + p * LD] = G.qr[lane + bi * LD];
-        G.qr[lane + bi * LD] = t;
+        double t = g.qr[lane + p * LD];
+        g.qr[lane + p * LD] = g.qr[lane + bi * LD];
+        g.qr[lane + bi * LD] = t;
       }
       if (lane == 0) {
-        double t = G.nu[p]; G.nu[p] = G.nu[bi]; G.nu[bi] = t;
-        t = G.nd[p]; G.nd[p] = G.nd[bi]; G.nd[bi] = t;
+        double t = g.nu[p]; g.nu[p] = g.nu[bi]; g.nu[bi] = t;
+        t = g.nd[p]; g.nd[p] = g.nd[bi]; g.nd[bi] = t;
       }
     }
-    gen_sync();
+    gsync<G>();
     // makeHouseholderInPlace on column p, rows p..k-1
     const int len = k - p;
-    double c0 = G.qr[p + p * LD];
+    double c0 = g.qr[p + p * LD];
     double tail = 0;
-    for (int i = 1; i < len; i++) tail += G.qr[p + i + p * LD] * G.qr[p + i + p * LD];
+    for (int i = 1; i < len; i++) tail += g.qr[p + i + p * LD] * g.qr[p + i + p * LD];
     double tau, beta;
     if (len == 1 || tail <= DBL_MIN) {
       tau = 0;
       beta = c0;
-      if (lane >= 1 && lane < len) G.qr[p + lane + p * LD] = 0;
+      if (lane >= 1 && lane < len) g.qr[p + lane + p * LD] = 0;
     } else {
       beta = sqrt(c0 * c0 + tail);
       if (c0 >= 0) beta = -beta;
       double den = c0 - beta;
-      if (lane >= 1 && lane < len) G.qr[p + lane + p * LD] /= den;
+      if (lane >= 1 && lane < len) g.qr[p + lane + p * LD] /= den;
       tau = (beta - c0) / beta;
     }
-    gen_sync();
-    if (lane == 0) { G.qr[p + p * LD] = beta; G.hc[p] = tau; }
+    gsync<G>();
+    if (lane == 0) { g.qr[p + p * LD] = beta; g.hc[p] = tau; }
     // apply to columns p+1..k-1, then downdate their norms (one column per lane)
     const int j = lane;
     if (j > p && j < k) {
       if (len == 1) {
-        G.qr[p + j * LD] *= (1 - tau);
+        g.qr[p + j * LD] *= (1 - tau);
       } else if (tau != 0) {
         double tmp = 0;
-        for (int i = 1; i < len; i++) tmp += G.qr[p + i + p * LD] * G.qr[p + i + j * LD];
-        tmp += G.qr[p + j * LD];
-        G.qr[p + j * LD] -= tau * tmp;
-        for (int i = 1; i < len; i++) G.qr[p + i + j * LD] -= tau * G.qr[p + i + p * LD] * tmp;
+        for (int i = 1; i < len; i++) tmp += g.qr[p + i + p * LD] * g.qr[p + i + j * LD];
+        tmp += g.qr[p + j * LD];
+        g.qr[p + j * LD] -= tau * tmp;
+        for (int i = 1; i < len; i++) g.qr[p + i + j * LD] -= tau * g.qr[p + i + p * LD] * tmp;
       }
-      if (G.nu[j] != 0) {
-        double temp = fabs(G.qr[p + j * LD]) / G.nu[j];
+      if (g.nu[j] != 0) {
+        double temp = fabs(g.qr[p + j * LD]) / g.nu[j];
         temp = (1 + temp) * (1 - temp);
         temp = temp < 0 ? 0 : temp;
-        double ratio = G.nu[j] / G.nd[j];
+        double ratio = g.nu[j] / g.nd[j];
         double temp2 = temp * (ratio * ratio);
         if (temp2 <= ndt) {
           double s = 0;
-          for (int i = p + 1; i < k; i++) s += G.qr[i + j * LD] * G.qr[i + j * LD];
-          G.nd[j] = sqrt(s);
-          G.nu[j] = G.nd[j];
+          for (int i = p + 1; i < k; i++) s += g.qr[i + j * LD] * g.qr[i + j * LD];
+          g.nd[j] = sqrt(s);
+          g.nu[j] = g.nd[j];
         } else {
-          G.nu[j] *= sqrt(temp);
+          g.nu[j] *= sqrt(temp);
         }
       }
     }
-    gen_sync();
+    gsync<G>();
   }
   return np;
 }
 
-// QR solve M z = b (least squares, basic solution) -> G.z
-__device__ void qr_solve(GenWS& G, int k, int np, int lane) {
-  if (lane < k) { G.c[lane] = G.b[lane]; G.z[lane] = 0.0; }
-  gen_sync();
+// QR solve m z = b (least squares, basic solution) -> g.z
+template <class G>
+__device__ void qr_solve(G& g, int k, int np, int lane) {
+  constexpr int LD = G::LD;
+  if (lane < k) { g.c[lane] = g.b[lane]; g.z[lane] = 0.0; }
+  gsync<G>();
   if (np == 0) return;
   for (int p = 0; p < np; p++) {
     const int len = k - p;
-    const double tau = G.hc[p];
+    const double tau = g.hc[p];
     if (len == 1) {
-      if (lane == p) G.c[p] *= (1 - tau);
+      if (lane == p) g.c[p] *= (1 - tau);
     } else if (tau != 0) {
       double tmp = 0;
-      for (int i = 1; i < len; i++) tmp += G.qr[p + i + p * LD] * G.c[p + i];
-      tmp += G.c[p];
-      gen_sync();
-      if (lane == 0) G.c[p] -= tau * tmp;
-      if (lane >= 1 && lane < len) G.c[p + lane] -= tau * G.qr[p + lane + p * LD] * tmp;
+      for (int i = 1; i < len; i++) tmp += g.qr[p + i + p * LD] * g.c[p + i];
+      tmp += g.c[p];
+      gsync<G>();
+      if (lane == 0) g.c[p] -= tau * tmp;
+      if (lane >= 1 && lane < len) g.c[p + lane] -= tau * g.qr[p + lane + p * LD] * tmp;
     }
-    gen_sync();
+    gsync<G>();
   }
-  upper_solve_shared(G.qr, G.c, np, lane);
+  upper_solve_shared<G>(g.qr, g.c, np, lane);
   if (lane == 0) {
     int perm[HS_KMAX];
     for (int i = 0; i < k; i++) perm[i] = i;
-    for (int p = 0; p < k; p++) { int t = perm[p]; perm[p] = perm[G.cperm[p]]; perm[G.cperm[p]] = t; }
-    for (int i = 0; i < np; i++) G.z[perm[i]] = G.c[i];
+    for (int p = 0; p < k; p++) { int t = perm[p]; perm[p] = perm[g.cperm[p]]; perm[g.cperm[p]] = t; }
+    for (int i = 0; i < np; i++) g.z[perm[i]] = g.c[i];
   }
-  gen_sync();
+  gsync<G>();
 }
 
-// S3 general: adaptive-rank two-stage least squares (ftsolver.cpp:277-303) -> sv.y
-template <class SV>
-__device__ uint32_t contact_solve(SV& sv, GenWS& G, int k, int lane) {
+// S3 general: adaptive-rank two-stage least squares (ftsolver.cpp:277-303) -> sv.y.
+// The reference re-runs FullPivLU on the same zeroth-order Gram every pass; it
+// is factorized once here (identical factors), only the rank threshold moves.
+template <class SV, class G>
+__device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
+  constexpr int LD = G::LD;
   uint32_t flags = 0;
   if (k == 0) return HS_FLAG_NO_CONTACT;
+  const LUInfo info = fullpiv_lu(g, k, lane);
+  STAMP(10);
   int rank0 = k;
   int iters = 0;
   double rel_error = 0;
   do {
     iters++;
-    LUInfo info = fullpiv_lu(G, k, lane);
     double thr = DBL_EPSILON * (double)k;
-    int r = lu_rank(G, info, thr);
+    int r = lu_rank(g, info, thr);
     for (int guard = 0; guard < 2100 && r > rank0; guard++) {  // setThreshold doubling
       thr = 2 * thr;
-      r = lu_rank(G, info, thr);
+      r = lu_rank(g, info, thr);
     }
-    lu_solve(G, info, k, r, lane);
-    lu_kernel_image(G, info, k, r, thr, lane);
+    lu_solve(g, info, k, r, lane);
+    lu_kernel_image(g, info, k, r, thr, lane);
+    STAMP(11);
     if (r == k) flags |= HS_FLAG_FULL_RANK;
     rank0 = r;
     const int dimker = k - r;
@@ -860,52 +920,48 @@ __device__ uint32_t contact_solve(SV& sv, GenWS& G, int k, int lane) {
     if (lane < k) {
       int i = lane, b0 = (i / 3) * 3;
       double t = 0.0;
-      for (int kk = b0; kk < b0 + 3; kk++) t = t + ntn1_at(G, i, kk) * G.y0[kk];
-      G.b[i] = -(G.ntx1[i] + t);
+      for (int kk = b0; kk < b0 + 3; kk++) t = t + ntn1_at(g, i, kk) * g.y0[kk];
+      g.b[i] = -(g.ntx1[i] + t);
     }
-    // M = [ntn1 Ny, ntn0 Ry]
-    for (int e = lane; e < k * k; e += HALF) {
+    for (int e = lane; e < k * k; e += HALF) {  // m, built straight into the QR buffer
       int i = e % k, j = e / k;
-      double s = 0.0;
-      if (j < dimker) {
-        int b0 = (i / 3) * 3;
-        for (int kk = b0; kk < b0 + 3; kk++) s = s + ntn1_at(G, i, kk) * G.Ny[kk + j * LD];
-      } else {
-        int col = G.rycol[j - dimker];
-        for (int kk = 0; kk < k; kk++) s = s + G.ntn0[i + kk * LD] * G.ntn0[kk + col * LD];
-      }
-      G.M[i + j * LD] = s;
+      g.qr[i + j * LD] = m_at(g, k, dimker, i, j);
     }
-    gen_sync();
-    int np = colpiv_qr(G, k, lane);
-    qr_solve(G, k, np, lane);
-    // rel_error = |M z - b| / |b|
+    gsync<G>();
+    STAMP(12);
+    int np = colpiv_qr(g, k, lane);
+    STAMP(13);
+    qr_solve(g, k, np, lane);
+    STAMP(14);
+    // rel_error = |m z - b| / |b|
     if (lane < k) {
       double s = 0.0;
-      for (int j = 0; j < k; j++) s = s + G.M[lane + j * LD] * G.z[j];
-      G.c[lane] = s - G.b[lane];
+      for (int j = 0; j < k; j++) s = s + m_at(g, k, dimker, lane, j) * g.z[j];
+      g.c[lane] = s - g.b[lane];
     }
-    gen_sync();
+    gsync<G>();
     double rn = 0, bn = 0;
-    for (int i = 0; i < k; i++) { rn += G.c[i] * G.c[i]; bn += G.b[i] * G.b[i]; }
+    for (int i = 0; i < k; i++) { rn += g.c[i] * g.c[i]; bn += g.b[i] * g.b[i]; }
     rel_error = sqrt(rn) / sqrt(bn);
     rank0--;
     if (lane < k) {
       double s = 0.0;
-      for (int j = 0; j < dimker; j++) s = s + G.Ny[lane + j * LD] * G.z[j];
-      sv.y[lane] = G.y0[lane] + s;
+      for (int j = 0; j < dimker; j++) s = s + g.Ny[lane + j * LD] * g.z[j];
+      sv.y[lane] = g.y0[lane] + s;
     }
-    gen_sync();
+    gsync<G>();
     if (rel_error > 1e-6 && rank0 <= 0) { flags |= HS_FLAG_LOOP_EXHAUST; break; }
   } while (rel_error > 1e-6 && iters <= HS_KMAX + 1);
   if (iters > 1) flags |= HS_FLAG_RANK_RETRY;
   return flags;
 }
 
-template <class SV>
-__device__ __attribute__((always_inline)) inline uint32_t general_solve(const hs_topo* T, SV* sv, GenWS* G, int k, int lane) {
-  build_grams(T, *sv, *G, k, lane);
-  return contact_solve(*sv, *G, k, lane);
+template <class W, class SV, class G>
+__device__ __attribute__((always_inline)) inline uint32_t general_solve(const hs_topo* T, SV& sv, G& g, const W& w,
+                                                                        int k, int lane) {
+  build_grams(T, sv, g, w, k, lane);
+  STAMP(9);
+  return contact_solve(sv, g, k, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -966,6 +1022,104 @@ __device__ inline void cross_rows(const double* d, double v[3][3]) {
   v[2][0] = -d[1]; v[2][1] = d[0];  v[2][2] = 0;
 }
 
+// nc >= 3 with a singular D_c (straight, IK-clamped leg) or Schur complement:
+// augmented system K = D + rho A^T A, w = -K^-1 (g~ + A^T lam),
+// (A K^-1 A^T) lam = a - A K^-1 g~ (oracle aug_solve, same operation order; the
+// half-wave right-looking Cholesky subtracts in the oracle's left-looking order).
+// False when the minimizer is not unique (a pivot under the guard).
+template <class SV>
+__device__ bool aug_solve(FastL& fl, SV& sv, const double* a, int nc, int lane) {
+  AugL& ag = fl.ag;
+  const int k = 3 * nc;
+  auto Aat = [&](int r, int i) { return fl.A[i / 3][r * 3 + i % 3]; };  // A (6 x k)
+  double md = 0, ma = 0;
+  for (int c = 0; c < nc; c++)
+    for (int i = 0; i < 3; i++) {
+      md = fmax(md, fl.D[c][4 * i]);
+      double s = 0;
+      for (int r = 0; r < 6; r++) s += Aat(r, 3 * c + i) * Aat(r, 3 * c + i);
+      ma = fmax(ma, s);
+    }
+  const double rho = (md > 0 && ma > 0) ? md / ma : 1.0;
+  for (int e = lane; e < k * k; e += HALF) {
+    const int i = e / k, j = e % k;
+    double s = 0;
+    for (int r = 0; r < 6; r++) s += Aat(r, i) * Aat(r, j);
+    ag.K[i * k + j] = ((i / 3 == j / 3) ? fl.D[i / 3][3 * (i % 3) + j % 3] : 0.0) + rho * s;
+  }
+  for (int e = lane; e < k * 7; e += HALF) {
+    const int i = e / 7, q = e % 7;
+    double v;
+    if (q < 6) {
+      v = Aat(q, i);
+    } else {
+      double s = 0;
+      for (int r = 0; r < 6; r++) s += Aat(r, i) * a[r];
+      v = fl.g[i / 3][i % 3] + rho * s;
+    }
+    ag.X[i * 7 + q] = v;
+  }
+  wave_sync();
+  double mx = 0;
+  for (int i = 0; i < k; i++) mx = fmax(mx, ag.K[i * k + i]);
+  for (int j = 0; j < k; j++) {
+    const double s = ag.K[j * k + j];
+    if (!(s > kFastPivotGuard * mx)) return false;  // wave-uniform
+    const double l = sqrt(s);
+    if (lane == 0) ag.K[j * k + j] = l;
+    for (int i = j + 1 + lane; i < k; i += HALF) ag.K[i * k + j] = ag.K[i * k + j] / l;
+    wave_sync();
+    const int m = k - 1 - j;
+    for (int e = lane; e < m * m; e += HALF) {
+      const int i = j + 1 + e / m, c2 = j + 1 + e % m;
+      if (c2 <= i) ag.K[i * k + c2] -= ag.K[i * k + j] * ag.K[c2 * k + j];
+    }
+    wave_sync();
+  }
+  if (lane < 7) {  // K X = [A^T | g~], one right-hand column per lane
+    const int q = lane;
+    for (int i = 0; i < k; i++) {
+      double s = ag.X[i * 7 + q];
+      for (int m = 0; m < i; m++) s -= ag.K[i * k + m] * ag.X[m * 7 + q];
+      ag.X[i * 7 + q] = s / ag.K[i * k + i];
+    }
+    for (int i = k - 1; i >= 0; i--) {
+      double s = ag.X[i * 7 + q];
+      for (int m = i + 1; m < k; m++) s -= ag.K[m * k + i] * ag.X[m * 7 + q];
+      ag.X[i * 7 + q] = s / ag.K[i * k + i];
+    }
+  }
+  wave_sync();
+  for (int e = lane; e < 42; e += HALF) {
+    const int r = e / 7, q = e % 7;
+    double s = 0;
+    for (int i = 0; i < k; i++) s += Aat(r, i) * ag.X[i * 7 + q];
+    if (q < 6) ag.St[6 * r + q] = s;
+    else ag.lam[r] = a[r] - s;
+  }
+  wave_sync();
+  if (lane == 0) {
+    double St[36], lam[6];
+    for (int i = 0; i < 36; i++) St[i] = ag.St[i];
+    for (int i = 0; i < 6; i++) lam[i] = ag.lam[i];
+    int ok = chol_n<6>(St, kFastPivotGuard);
+    if (ok) {
+      chol_solve_n<6>(St, lam);
+      for (int i = 0; i < 6; i++) ag.lam[i] = lam[i];
+    }
+    ag.ok = ok;
+  }
+  wave_sync();
+  if (!ag.ok) return false;
+  for (int i = lane; i < k; i += HALF) {
+    double s = ag.X[i * 7 + 6];
+    for (int r = 0; r < 6; r++) s += ag.X[i * 7 + r] * ag.lam[r];
+    sv.y[i] = -s;
+  }
+  wave_sync();
+  return true;
+}
+
 template <class W, class SV>
 __device__ bool fast_solve(const hs_topo* T, SV& sv, FastL& fl, const W& w, int nc, int lane) {
   const int n = T->n;
@@ -1023,21 +1177,21 @@ __device__ bool fast_solve(const hs_topo* T, SV& sv, FastL& fl, const W& w, int 
           for (int q = 0; q < 6; q++) {
             double s = 0;
             for (int j = 0; j < 3; j++) s += E[r * 3 + j] * Ac[q * 3 + j];
-            fl.S[c][6 * r + q] = s;
+            fl.sc.S[c][6 * r + q] = s;
           }
           double s = 0;
           for (int j = 0; j < 3; j++) s += E[r * 3 + j] * g[j];
-          fl.h[c][r] = s;
+          fl.sc.h[c][r] = s;
         }
-        for (int i = 0; i < 9; i++) fl.Dinv[c][i] = Dinv[i];
+        for (int i = 0; i < 9; i++) fl.sc.Dinv[c][i] = Dinv[i];
       }
     }
     fl.ok[c] = ok;
   }
   wave_sync();
-  for (int c = 0; c < nc; c++)
-    if (!fl.ok[c]) return false;
   const double a[6] = {sv.x[0], sv.x[1], sv.x[2], sv.x[3 * n], sv.x[3 * n + 1], sv.x[3 * n + 2]};
+  for (int c = 0; c < nc; c++)
+    if (!fl.ok[c]) return aug_solve(fl, sv, a, nc, lane);  // only nc >= 3 factors D_c
   int ok = 1;
   if (nc == 1) {  // unique least-squares solution (A^T A) w = -A^T a
     if (lane == 0) {
@@ -1104,31 +1258,32 @@ __device__ bool fast_solve(const hs_topo* T, SV& sv, FastL& fl, const W& w, int 
       for (int i = 0; i < 36; i++) Sm[i] = 0;
       for (int i = 0; i < 6; i++) h[i] = 0;
       for (int c = 0; c < nc; c++) {
-        for (int i = 0; i < 36; i++) Sm[i] += fl.S[c][i];
-        for (int i = 0; i < 6; i++) h[i] += fl.h[c][i];
+        for (int i = 0; i < 36; i++) Sm[i] += fl.sc.S[c][i];
+        for (int i = 0; i < 6; i++) h[i] += fl.sc.h[c][i];
       }
       double lam[6];
       for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
       ok = chol_n<6>(Sm, kFastPivotGuard);
       if (ok) {
         chol_solve_n<6>(Sm, lam);
-        for (int r = 0; r < 6; r++) fl.lam[r] = lam[r];
+        for (int r = 0; r < 6; r++) fl.sc.lam[r] = lam[r];
       }
       fl.ok[0] = ok;
     }
     wave_sync();
-    if (fl.ok[0] && lane < nc) {
+    if (!fl.ok[0]) return aug_solve(fl, sv, a, nc, lane);
+    if (lane < nc) {
       const int c = lane;
       const double* Ac = fl.A[c];
       double t[3];
       for (int i = 0; i < 3; i++) {
         double s = fl.g[c][i];
-        for (int r = 0; r < 6; r++) s += Ac[r * 3 + i] * fl.lam[r];
+        for (int r = 0; r < 6; r++) s += Ac[r * 3 + i] * fl.sc.lam[r];
         t[i] = s;
       }
       for (int i = 0; i < 3; i++) {
         double s = 0;
-        for (int j = 0; j < 3; j++) s += fl.Dinv[c][3 * i + j] * t[j];
+        for (int j = 0; j < 3; j++) s += fl.sc.Dinv[c][3 * i + j] * t[j];
         sv.y[3 * c + i] = -s;
       }
     }
@@ -1149,7 +1304,8 @@ __device__ inline uint64_t best_key(double cot, int64_t id) {
 // ---------------------------------------------------------------------------
 template <class W, class SV>
 __device__ void step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st, SV& sv,
-                     FastL& fl, WorkL& wk, const W& w, GenWS* G, int b, bool live, int h, double& work, int lane) {
+                     FastL& fl, GenLDS& gl, WorkL& wk, const W& w, GenWS* G, int b, bool live, int h,
+                     double& work, int lane) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
   STAMP(3);
   dynamics(T, st, sv, w, lane);
@@ -1167,15 +1323,10 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const hs::launch_ma
   if (fast_solve(T, sv, fl, w, nc, lane)) {
     if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
     if (nc == 1) flags |= HS_FLAG_FULL_RANK;
+  } else if (k <= GenLDS::LD) {
+    flags = general_solve(T, sv, gl, w, k, lane) | HS_FLAG_GENERAL;
   } else {
-    for (int e = lane; e < 3 * n; e += HALF) {
-      G->jpos[e / 3][e % 3] = w.jpos(0, e / 3)[e % 3];
-      G->jz[e / 3][e % 3] = w.jz(0, e / 3)[e % 3];
-    }
-    if (lane < 3 * nf) G->fpos[lane / 3][lane % 3] = w.fpos(0, lane / 3)[lane % 3];
-    if (lane < 3) G->pos0[lane] = w.pos(0, 0)[lane];
-    gen_sync();
-    flags = general_solve(T, &sv, G, k, lane) | HS_FLAG_GENERAL;
+    flags = general_solve(T, sv, *G, w, k, lane) | HS_FLAG_GENERAL;
   }
   STAMP(7);
 
@@ -1291,7 +1442,7 @@ __global__ __launch_bounds__(WAVE, HS_MIN_WAVES) void hs_rollout_kernel(const hs
     wave_sync();
   }
   STAMP(2);
-  step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.wk, OneWin<NM>{&sm.d}, G, b, live, mp.h_row, work, lane);
+  step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.gl, sm.d.wk, OneWin<NM>{&sm.d}, G, b, live, mp.h_row, work, lane);
   if (lane == 0 && live) {
     double cot = work / (T->total_mass * g.step_length);
     if (a.work_cot) {

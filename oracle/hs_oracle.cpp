@@ -1437,6 +1437,64 @@ inline void cross_rows(const double* d, double v[3][3]) {
   v[2][0] = -d[1]; v[2][1] = d[0];  v[2][2] = 0;
 }
 
+// nc >= 3 when a block D_c is singular (a straight, IK-clamped leg: no joint
+// torque resists a force along it) or the per-contact Schur complement is. The
+// equality-constrained minimizer is still unique when D is positive definite on
+// null(A), and then K = D + rho A^T A is positive definite and
+//   w = -K^-1 (g~ + A^T lam),  (A K^-1 A^T) lam = a - A K^-1 g~,  g~ = g + rho A^T a
+// gives it independently of rho (rho balances the two terms' scales). A pivot
+// under the guard means the minimizer is not unique: the Eigen-style path decides.
+bool aug_solve(int nc, const std::vector<double>& A, const std::vector<double>& D, const std::vector<double>& g,
+               const double* a, std::vector<double>& y) {
+  const int k = 3 * nc;
+  auto Aat = [&](int r, int i) { return A[18 * (i / 3) + r * 3 + i % 3]; };  // A (6 x k)
+  double md = 0, ma = 0;
+  for (int c = 0; c < nc; c++)
+    for (int i = 0; i < 3; i++) {
+      md = std::max(md, D[9 * c + 4 * i]);
+      double s = 0;
+      for (int r = 0; r < 6; r++) s += Aat(r, 3 * c + i) * Aat(r, 3 * c + i);
+      ma = std::max(ma, s);
+    }
+  const double rho = (md > 0 && ma > 0) ? md / ma : 1.0;
+  std::vector<double> K(k * k), X(k * 7);
+  for (int i = 0; i < k; i++) {
+    for (int j = 0; j < k; j++) {
+      double s = 0;
+      for (int r = 0; r < 6; r++) s += Aat(r, i) * Aat(r, j);
+      K[i * k + j] = ((i / 3 == j / 3) ? D[9 * (i / 3) + 3 * (i % 3) + j % 3] : 0.0) + rho * s;
+    }
+    double s = 0;
+    for (int r = 0; r < 6; r++) s += Aat(r, i) * a[r];
+    X[i * 7 + 6] = g[i] + rho * s;
+    for (int q = 0; q < 6; q++) X[i * 7 + q] = Aat(q, i);
+  }
+  if (!chol(K.data(), k, kFastPivotGuard)) return false;
+  std::vector<double> col(k);
+  for (int q = 0; q < 7; q++) {
+    for (int i = 0; i < k; i++) col[i] = X[i * 7 + q];
+    chol_solve(K.data(), k, col.data());
+    for (int i = 0; i < k; i++) X[i * 7 + q] = col[i];
+  }
+  double St[36], lam[6];
+  for (int r = 0; r < 6; r++) {
+    for (int q = 0; q < 7; q++) {
+      double s = 0;
+      for (int i = 0; i < k; i++) s += Aat(r, i) * X[i * 7 + q];
+      if (q < 6) St[6 * r + q] = s;
+      else lam[r] = a[r] - s;
+    }
+  }
+  if (!chol(St, 6, kFastPivotGuard)) return false;
+  chol_solve(St, 6, lam);
+  for (int i = 0; i < k; i++) {
+    double s = X[i * 7 + 6];
+    for (int r = 0; r < 6; r++) s += X[i * 7 + r] * lam[r];
+    y[i] = -s;
+  }
+  return true;
+}
+
 bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<double>& x, std::vector<double>& y) {
   const int n = m->n;
   std::vector<int> cf;  // contact -> foot index
@@ -1523,7 +1581,7 @@ bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<d
   for (int c = 0; c < nc; c++) {
     double L[9];
     for (int i = 0; i < 9; i++) L[i] = D[9 * c + i];
-    if (!chol(L, 3, kFastPivotGuard)) return false;
+    if (!chol(L, 3, kFastPivotGuard)) return aug_solve(nc, A, D, g, a, y);
     for (int j = 0; j < 3; j++) {  // Dinv columns
       double e[3] = {0, 0, 0};
       e[j] = 1;
@@ -1551,7 +1609,7 @@ bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<d
   }
   double lam[6];
   for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
-  if (!chol(S, 6, kFastPivotGuard)) return false;
+  if (!chol(S, 6, kFastPivotGuard)) return aug_solve(nc, A, D, g, a, y);
   chol_solve(S, 6, lam);
   for (int c = 0; c < nc; c++) {
     const double* Ac = &A[18 * c];

@@ -201,6 +201,24 @@ def test_full_size_properties(gpu, hmodels):
         assert (np.abs(torso[good]).max(axis=1) < 1e-9 * scale[good]).all()
 
 
+def test_straight_leg_steps_use_augmented_closed_form(gpu, hmodels, oracle_mod, omodels):
+    """IK-clamped steps (singular D_c) go through the kernel's augmented-system tier, not the
+    Eigen-style path, and match the oracle's fast and tree modes."""
+    from hslabs_amd import synth
+    from test_oracle import DEGENERATE_MYANT
+
+    arr = synth.gen_params(4096, "myant")[list(DEGENERATE_MYANT)]
+    g = gpu.run_host(hmodels["myant"], arr, n_t=20, horizon=20)
+    assert not (g["flags"] & 64).any()
+    assert ((g["flags"] & 16) != 0).sum() >= 10
+    for b, r in enumerate(arr):
+        og = record_to_oracle_gait(oracle_mod, r)
+        for basis in (oracle_mod.BASIS_FAST, oracle_mod.BASIS_TREE):
+            ro = oracle_mod.rollout(omodels["myant"], og, 20, basis=basis)
+            assert np.abs(g["tau"][b] - ro["tau"]).max() < TAU_TOL * max(1, np.abs(ro["tau"]).max())
+            assert np.abs(g["cf"][b] - ro["cf"]).max() < CF_TOL * max(1, np.abs(ro["cf"]).max())
+
+
 def test_edge_cases(gpu, hmodels):
     from hslabs_amd import PgsConfigParams
 

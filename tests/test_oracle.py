@@ -229,3 +229,29 @@ def test_closed_form_synthetic(oracle_mod, omodels, name, curved):
     err = np.abs(rt["tau"] - rf["tau"]).max(axis=2) / np.maximum(1, np.abs(rt["tau"]).max(axis=2))
     assert err.max() < 1e-10
     assert ((rf["flags"] & oracle_mod.FLAG_GENERAL) != 0).mean() < 0.01
+
+
+# myant rollouts of gen_params(4096, "myant") whose IK-clamped (straight) legs make a
+# first-order Gram block D_c singular: the per-contact Schur solve declines them
+DEGENERATE_MYANT = (497, 737, 844, 1084)
+
+
+def test_augmented_closed_form_on_straight_legs(oracle_mod, omodels):
+    """Steps with a singular D_c: the augmented-system tier (K = D + rho A^T A) reproduces the
+    Eigen-style two-stage LS (tree and orthonormal bases) -- the minimizer is unique there."""
+    from hslabs_amd import synth
+    from conftest import record_to_oracle_gait
+
+    arr = synth.gen_params(4096, "myant")[list(DEGENERATE_MYANT)]
+    m = omodels["myant"]
+    n_aug = 0
+    for r in arr:
+        g = record_to_oracle_gait(oracle_mod, r)
+        rf = oracle_mod.rollout(m, g, 20, basis=oracle_mod.BASIS_FAST)
+        assert not (rf["flags"] & oracle_mod.FLAG_GENERAL).any()
+        n_aug += int(((rf["flags"] & 16) != 0).sum())
+        for basis in (oracle_mod.BASIS_TREE, oracle_mod.BASIS_ORTHO):
+            rt = oracle_mod.rollout(m, g, 20, basis=basis)
+            assert np.abs(rt["tau"] - rf["tau"]).max() < 1e-10 * max(1.0, np.abs(rt["tau"]).max())
+            assert np.abs(rt["cf"] - rf["cf"]).max() < 1e-10 * max(1.0, np.abs(rt["cf"]).max())
+    assert n_aug >= 10  # the clamped steps are really exercised

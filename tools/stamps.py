@@ -17,6 +17,9 @@ from hslabs_amd import build as B  # noqa: E402
 LIB = os.path.join(B.OUT_DIR, "libhslabs_stamps.so")
 PHASES = [("setup", 0, 1), ("kin(5 samples)", 1, 2), ("dynamics", 3, 4), ("particular", 4, 5),
           ("contact list", 5, 6), ("contact solve", 6, 7), ("outputs", 7, 8), ("TOTAL", 0, 8)]
+# general path (waves where it ran): grams, LU, LU solve + kernel, m, QR, QR solve
+GENERAL = [("g:grams", 6, 9), ("g:LU", 9, 10), ("g:solve+kernel", 10, 11), ("g:m", 11, 12), ("g:QR", 12, 13),
+           ("g:QR solve", 13, 14), ("g:rest", 14, 7)]
 
 
 def build():
@@ -41,15 +44,17 @@ def main():
     model = os.environ.get("MODEL", "hexapod")
     m = H.KinematicModel(os.path.join(ROOT, "models", f"{model}.xml"))
     params = synth.gen_params(n, model)
-    H.run_host(m, params, n_t=20, k0=0, horizon=1, want=("tau",))  # warm
+    k0 = int(os.environ.get("K0", "0"))
+    H.run_host(m, params, n_t=20, k0=k0, horizon=1, want=("tau",))  # warm
     L.hs_debug_clear_stamps()
-    H.run_host(m, params, n_t=20, k0=0, horizon=1, want=("tau",))
+    H.run_host(m, params, n_t=20, k0=k0, horizon=1, want=("tau",))
     st = np.zeros((4096, 16), dtype=np.uint64)
     L.hs_debug_read_stamps(st.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), 4096)
     st = st[:min((n + 1) // 2, 4096)].astype(np.int64)  # one row per wavefront (two rollouts)
-    for name, a, b in PHASES:
-        d = st[:, b] - st[:, a]
-        print(f"{name:22s} mean {d.mean():10.0f}  p50 {np.median(d):10.0f}  p90 {np.percentile(d, 90):10.0f}")
+    gen = st[:, 9] != 0
+    for name, a, b in PHASES + (GENERAL if gen.any() else []):
+        d = (st[gen] if name.startswith("g:") else st)[:, b] - (st[gen] if name.startswith("g:") else st)[:, a]
+        print(f"{name:22s} mean {d.mean():10.0f}  p50 {np.median(d):10.0f}  p90 {np.percentile(d, 90):10.0f}  max {d.max():10.0f}")
 
 
 if __name__ == "__main__":
