@@ -211,6 +211,17 @@ class DeviceBatch:
     def run(self, stream=None, best: bool = True, accumulate: bool = False) -> None:
         self._launch(self._args(stream, best, accumulate), 1, None)
 
+    def run_forces(self, tau_in, stream=None) -> None:
+        """Contact forces of all feet given motor torques (hs_run_forces,
+        forcetorquesolver::solve_forces): tau_in is a device tensor [B][H][nmj]; writes
+        self.cf (and q / flags if allocated)."""
+        t = tau_in.to(dtype=self.torch.float64, device=self.device).contiguous()
+        assert t.shape == (self.B, self.H, self.model.nmj)
+        a = self._args(stream, False, False)
+        a.tau = a.x = a.work_cot = None
+        capi.check(capi.load().hs_run_forces(self.model.handle, ctypes.byref(a), t.data_ptr()), "hs_run_forces")
+        self._tau_in = t  # keep alive until the stream has consumed it
+
     def run_steps(self, n_calls: int, stream=None, best: bool = False, accumulate: bool = True,
                   events=None) -> None:
         """n_calls launches marching k0 through the cycle (hs_run_steps); the launch loop is

@@ -179,6 +179,20 @@ int hs_run_steps(hs_model_t m, const hs_run_args* a, int32_t n_calls, void* cons
   return launch_steps(d, *a, ws, hs::single_model_map(m->host, a->n_rollouts), n_calls, kernel_events);
 }
 
+int hs_run_forces(hs_model_t m, const hs_run_args* a, const double* tau_in) {
+  int rc = check_args(m, a);
+  if (rc != HS_OK) return rc;
+  if (a->n_rollouts > 0 && !tau_in) return fail(HS_E_ARG, "tau_in is null");
+  if (a->n_rollouts == 0) return HS_OK;
+  const hs_topo* d = nullptr;
+  void* ws = nullptr;
+  rc = device_state(m, a->n_rollouts + 1, &d, &ws);
+  if (rc != HS_OK) return rc;
+  hs::launch_map mp = hs::single_model_map(m->host, a->n_rollouts);
+  mp.tau_in = tau_in;
+  return launch_steps(d, *a, ws, mp, 1, nullptr);
+}
+
 int hs_mixed_create(const hs_model_t* models, int32_t n_models, const int32_t* model_index, int32_t n_rollouts,
                     hs_mixed_t* out) {
   if (!models || !out || (n_rollouts > 0 && !model_index)) return fail(HS_E_ARG, "null argument");

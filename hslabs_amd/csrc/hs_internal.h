@@ -21,6 +21,7 @@ struct launch_map {
   int32_t n_waves;
   int32_t max_parts;             // LDS layout class (largest model)
   int32_t h_row;                 // output row of this launch's step within the horizon
+  const double* tau_in;          // forces-given-torques mode: motor torques [B][H][st_tau] (else null)
   int32_t st_tau, st_cf, st_q, st_x;  // output row strides (mixed: maxima over the models)
 };
 

@@ -32,6 +32,7 @@
 
 #include <cfloat>
 #include <cstdint>
+#include <type_traits>
 
 #include "hs_internal.h"
 #include "hs_math.h"
@@ -107,13 +108,20 @@ struct CentreL {  // fields read after D
   int unreach[HS_LMAX];
 };
 
-template <int NM>
+struct ForceL {  // solve_forces: W = I + G G^T, later the normal matrix; L^-1 [C | d]
+  double W[(6 + HS_KMAX) * (6 + HS_KMAX)];
+  double Ct[(6 + HS_KMAX) * (HS_KMAX + 1)];
+  double y[HS_KMAX];
+};
+
+template <int NM, bool FORCES>
 struct OneStore {
   union {
     StencilL<NM> sten;
     FastL fl;  // written only after D has consumed the stencil
     GenLDS gl;  // general path, k <= 12 (fast solve declined)
     WorkL wk;
+    typename std::conditional<FORCES, ForceL, WorkL>::type fr;  // forces-given-torques mode
   };
   CentreL<NM> c;
 };
@@ -134,9 +142,9 @@ struct SolveL {
   int cfoot[HS_LMAX];
 };
 
-template <int NM>
+template <int NM, bool FORCES>
 struct Smem {
-  OneStore<NM> d;
+  OneStore<NM, FORCES> d;
   SetupL st;
   SolveL<NM> sv;
 };
@@ -177,9 +185,9 @@ __device__ inline A34 node_pj(const hs_topo* T, int v) { return load34(T->node[v
 // ---------------------------------------------------------------------------
 // Sample views. k = offset from the step's centre sample (-2..2).
 // ---------------------------------------------------------------------------
-template <int NM>
+template <int NM, bool FORCES>
 struct OneWin {
-  OneStore<NM>* d;
+  OneStore<NM, FORCES>* d;
   __device__ bool want_pos(int k) const { return (k & 1) == 0; }
   __device__ bool want_ust(int k) const { return (k & 1) == 0; }
   __device__ bool want_rot(int k) const { return (k & 1) != 0; }
@@ -1022,6 +1030,30 @@ __device__ inline void cross_rows(const double* d, double v[3][3]) {
   v[2][0] = -d[1]; v[2][1] = d[0];  v[2][2] = 0;
 }
 
+// In-place Cholesky of a k x k SPD matrix (row-major, lower triangle used) by
+// the half-wave, right-looking: element (i, j) gets its products subtracted in
+// increasing order, exactly like the oracle's left-looking chol(). False (wave-
+// uniform) when a pivot falls to guard * (max original diagonal) or below.
+__device__ bool chol_half(double* K, int k, double guard, int lane) {
+  double mx = 0;
+  for (int i = 0; i < k; i++) mx = fmax(mx, K[i * k + i]);
+  for (int j = 0; j < k; j++) {
+    const double s = K[j * k + j];
+    if (!(s > guard * mx)) return false;
+    const double l = sqrt(s);
+    if (lane == 0) K[j * k + j] = l;
+    for (int i = j + 1 + lane; i < k; i += HALF) K[i * k + j] = K[i * k + j] / l;
+    wave_sync();
+    const int m = k - 1 - j;
+    for (int e = lane; e < m * m; e += HALF) {
+      const int i = j + 1 + e / m, c2 = j + 1 + e % m;
+      if (c2 <= i) K[i * k + c2] -= K[i * k + j] * K[c2 * k + j];
+    }
+    wave_sync();
+  }
+  return true;
+}
+
 // nc >= 3 with a singular D_c (straight, IK-clamped leg) or Schur complement:
 // augmented system K = D + rho A^T A, w = -K^-1 (g~ + A^T lam),
 // (A K^-1 A^T) lam = a - A K^-1 g~ (oracle aug_solve, same operation order; the
@@ -1060,22 +1092,7 @@ __device__ bool aug_solve(FastL& fl, SV& sv, const double* a, int nc, int lane) 
     ag.X[i * 7 + q] = v;
   }
   wave_sync();
-  double mx = 0;
-  for (int i = 0; i < k; i++) mx = fmax(mx, ag.K[i * k + i]);
-  for (int j = 0; j < k; j++) {
-    const double s = ag.K[j * k + j];
-    if (!(s > kFastPivotGuard * mx)) return false;  // wave-uniform
-    const double l = sqrt(s);
-    if (lane == 0) ag.K[j * k + j] = l;
-    for (int i = j + 1 + lane; i < k; i += HALF) ag.K[i * k + j] = ag.K[i * k + j] / l;
-    wave_sync();
-    const int m = k - 1 - j;
-    for (int e = lane; e < m * m; e += HALF) {
-      const int i = j + 1 + e / m, c2 = j + 1 + e % m;
-      if (c2 <= i) ag.K[i * k + c2] -= ag.K[i * k + j] * ag.K[c2 * k + j];
-    }
-    wave_sync();
-  }
+  if (!chol_half(ag.K, k, kFastPivotGuard, lane)) return false;
   if (lane < 7) {  // K X = [A^T | g~], one right-hand column per lane
     const int q = lane;
     for (int i = 0; i < k; i++) {
@@ -1403,11 +1420,192 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const hs::launch_ma
   STAMP(8);
 }
 
-template <int NM>
+// ---------------------------------------------------------------------------
+// Contact forces given motor torques: forcetorquesolver::solve_forces
+// (ftsolver.cpp:331-378; oracle solve_forces). Least squares over the tree
+// rows, the torso rows (torso force/torque forced to zero) and the torque rows
+// jz_h . x_h = z_h, unknowns = non-root joint wrenches + forces of ALL feet.
+// The tree rows' coefficient block is unit triangular, so eliminating the
+// joint wrenches exactly leaves (Woodbury)
+//   y = argmin (C y - d)^T (I + G G^T)^-1 (C y - d)
+// over m = 6 + nmj rows: G = (torso, torque) rows composed with the tree
+// inverse -- T_i = -[[I, 0], [[p_i - p_0]x, I]] for the torso, (u_hi, jz_h) with
+// u_hi = (jpos_h - pos_i) x jz_h on the subtree of hinge h -- C = [I; [fpos -
+// p_0]x] and jz_h . [(jpos_h - fpos)x] (the tree basis seen by those rows),
+// d = (torso part of x_part, z - jz . x_part). Rank-deficient normal matrix
+// (a straight leg): HS_FLAG_GENERAL, Tikhonov 1e-12 of its largest diagonal.
+// ---------------------------------------------------------------------------
+__device__ inline bool in_subtree(const hs_topo* T, int i, int h) {
+  for (int a = i; a >= 0; a = T->node[a].parent)
+    if (a == h) return true;
+  return false;
+}
+
+__device__ inline void cross3(const double* a, const double* b, double* c) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+template <class W, class SV>
+__device__ uint32_t forces_solve(const hs_topo* T, const SV& sv, ForceL& fr, const W& w, const double* z, int lane) {
+  const int n = T->n, nj = T->nmj, nf = T->nf, m = 6 + nj, nq = 3 * nf, ld = nq + 1;
+  const double* P0 = w.pos(0, 0);
+  for (int e = lane; e < m * m; e += HALF) {  // I + G G^T, lower triangle
+    const int r = e / m, c = e % m;
+    if (c > r) continue;
+    double s = 0.0;
+    if (r < 6) {
+      for (int i = 1; i < n; i++) {
+        const double* Pi = w.pos(0, i);
+        double ri[3], Sr[3] = {0, 0, 0}, Sc[3] = {0, 0, 0};
+        for (int t = 0; t < 3; t++) ri[t] = Pi[t] - P0[t];
+        // T_i row a = -(e_a, 0) for a < 3, -([r_i]x row a-3, e_{a-3}) for a >= 3
+        if (r >= 3) for (int t = 0; t < 3; t++) Sr[t] = cross_e(ri, t, r - 3);
+        if (c >= 3) for (int t = 0; t < 3; t++) Sc[t] = cross_e(ri, t, c - 3);
+        double v;
+        if (r < 3 && c < 3) v = (r == c) ? 1.0 : 0.0;
+        else if (c < 3) v = Sr[c];
+        else v = Sr[0] * Sc[0] + Sr[1] * Sc[1] + Sr[2] * Sc[2] + ((r == c) ? 1.0 : 0.0);
+        s += v;
+      }
+    } else {
+      const int h = T->hinge_ids[r - 6];
+      const double* Jh = w.jpos(0, h);
+      const double* Zh = w.jz(0, h);
+      const int h2 = (c >= 6) ? T->hinge_ids[c - 6] : -1;
+      for (int i = 1; i < n; i++) {
+        if (!in_subtree(T, i, h) || (h2 >= 0 && !in_subtree(T, i, h2))) continue;
+        const double* Pi = w.pos(0, i);
+        double a3[3], u[3];
+        for (int t = 0; t < 3; t++) a3[t] = Jh[t] - Pi[t];
+        cross3(a3, Zh, u);
+        if (c < 6) {  // T_i row c . (u, jz_h)
+          if (c < 3) {
+            s += -u[c];
+          } else {
+            double ri[3], ru[3];
+            for (int t = 0; t < 3; t++) ri[t] = Pi[t] - P0[t];
+            cross3(ri, u, ru);
+            s += -(ru[c - 3] + Zh[c - 3]);
+          }
+        } else {
+          const double* J2 = w.jpos(0, h2);
+          const double* Z2 = w.jz(0, h2);
+          double b3[3], u2[3];
+          for (int t = 0; t < 3; t++) b3[t] = J2[t] - Pi[t];
+          cross3(b3, Z2, u2);
+          s += u[0] * u2[0] + u[1] * u2[1] + u[2] * u2[2] + (Zh[0] * Z2[0] + Zh[1] * Z2[1] + Zh[2] * Z2[2]);
+        }
+      }
+    }
+    fr.W[r * m + c] = ((r == c) ? 1.0 : 0.0) + s;
+  }
+  for (int e = lane; e < m * ld; e += HALF) {  // [C | d]
+    const int r = e / ld, q = e % ld;
+    double v = 0.0;
+    if (q < nq) {
+      const int fi = q / 3, jj = q % 3;
+      const double* fp = w.fpos(0, fi);
+      if (r < 3) {
+        v = (r == jj) ? 1.0 : 0.0;
+      } else if (r < 6) {
+        double d[3];
+        for (int t = 0; t < 3; t++) d[t] = fp[t] - P0[t];
+        v = cross_e(d, jj, r - 3);
+      } else {
+        const int h = T->hinge_ids[r - 6];
+        if (in_subtree(T, T->footis[fi], h)) {
+          const double* Jh = w.jpos(0, h);
+          const double* Zh = w.jz(0, h);
+          double d[3];
+          for (int t = 0; t < 3; t++) d[t] = Jh[t] - fp[t];
+          for (int t = 0; t < 3; t++) v += Zh[t] * cross_e(d, jj, t);
+        }
+      }
+    } else if (r < 3) {
+      v = sv.x[r];
+    } else if (r < 6) {
+      v = sv.x[3 * n + r - 3];
+    } else {
+      const int h = T->hinge_ids[r - 6];
+      const double* Zh = w.jz(0, h);
+      double t = 0;
+      for (int j = 0; j < 3; j++) t += Zh[j] * sv.x[3 * n + 3 * h + j];
+      v = z[r - 6] - t;
+    }
+    fr.Ct[r * ld + q] = v;
+  }
+  wave_sync();
+  chol_half(fr.W, m, 0.0, lane);  // I + G G^T: eigenvalues >= 1
+  if (lane < ld) {                // L^-1 [C | d], one column per lane
+    for (int i = 0; i < m; i++) {
+      double s = fr.Ct[i * ld + lane];
+      for (int t = 0; t < i; t++) s -= fr.W[i * m + t] * fr.Ct[t * ld + lane];
+      fr.Ct[i * ld + lane] = s / fr.W[i * m + i];
+    }
+  }
+  wave_sync();
+  uint32_t flags = 0;
+  for (int pass = 0; pass < 2; pass++) {  // normal equations; second pass regularized
+    double eps = 0;
+    if (pass == 1) {
+      for (int p = 0; p < nq; p++) {
+        double s = 0;
+        for (int i = 0; i < m; i++) s += fr.Ct[i * ld + p] * fr.Ct[i * ld + p];
+        eps = fmax(eps, s);
+      }
+      eps *= 1e-12;
+    }
+    for (int e = lane; e < nq * ld; e += HALF) {
+      const int p = e / ld, q = e % ld;
+      if (q < nq && q > p) continue;
+      double s = 0;
+      for (int i = 0; i < m; i++) s += fr.Ct[i * ld + p] * fr.Ct[i * ld + q];
+      if (q < nq) fr.W[p * nq + q] = s + ((p == q) ? eps : 0.0);
+      else fr.y[p] = s;
+    }
+    wave_sync();
+    if (chol_half(fr.W, nq, pass == 0 ? kFastPivotGuard : 0.0, lane)) break;
+    flags = HS_FLAG_GENERAL;  // least squares not unique
+  }
+  if (lane == 0) {
+    for (int i = 0; i < nq; i++) {
+      double s = fr.y[i];
+      for (int k = 0; k < i; k++) s -= fr.W[i * nq + k] * fr.y[k];
+      fr.y[i] = s / fr.W[i * nq + i];
+    }
+    for (int i = nq - 1; i >= 0; i--) {
+      double s = fr.y[i];
+      for (int k = i + 1; k < nq; k++) s -= fr.W[k * nq + i] * fr.y[k];
+      fr.y[i] = s / fr.W[i * nq + i];
+    }
+  }
+  wave_sync();
+  return flags;
+}
+
+template <class W, class SV>
+__device__ void forces_step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st,
+                            SV& sv, ForceL& fr, const W& w, int b, bool live, int h, int lane) {
+  const int nf = T->nf, cfg = T->cfg, nl = T->n_limbs, nq = 3 * nf;
+  dynamics(T, st, sv, w, lane);
+  particular(T, sv, w, lane);
+  const size_t row = (size_t)b * a.horizon + h;
+  const double* z = mp.tau_in + (live ? row : 0) * mp.st_tau;
+  uint32_t flags = forces_solve(T, sv, fr, w, z, lane);
+  if (half_ballot(lane < nq && fr.y[lane] != fr.y[lane])) flags |= HS_FLAG_NAN;
+  if (half_ballot(lane < nl && w.unreach(0, lane))) flags |= HS_FLAG_UNREACH;
+  if (live && a.cf && lane < mp.st_cf) a.cf[row * mp.st_cf + lane] = (lane < nq) ? fr.y[lane] : 0.0;
+  if (live && a.q && lane < mp.st_q) a.q[row * mp.st_q + lane] = (lane < cfg) ? w.q(0)[lane] : 0.0;
+  if (live && a.flags && lane == 0) a.flags[row] = flags;
+}
+
+template <int NM, bool FORCES>
 __global__ __launch_bounds__(WAVE, HS_MIN_WAVES) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
                                                                                  hs_run_args a, GenWS* __restrict__ gws,
                                                                                  hs::launch_map mp) {
-  __shared__ Smem<NM> smem[2];
+  __shared__ Smem<NM, FORCES> smem[2];
   const int sub = threadIdx.x / HALF;  // rollout slot within the wave
   const int lane = threadIdx.x % HALF; // lane within the rollout
   // one model per wavefront: the topology pointer stays wave-uniform (scalar loads)
@@ -1424,7 +1622,7 @@ __global__ __launch_bounds__(WAVE, HS_MIN_WAVES) void hs_rollout_kernel(const hs
     bb = live ? b : a.n_rollouts - 1;
   }
   GenWS* G = gws + (live ? b : a.n_rollouts);
-  Smem<NM>& sm = smem[sub];
+  Smem<NM, FORCES>& sm = smem[sub];
   double work = (live && a.accumulate && a.work_cot) ? a.work_cot[2 * (size_t)b] : 0.0;
   const hs_gait_params g = a.params[bb];
   const int nl = T->n_limbs;
@@ -1438,11 +1636,17 @@ __global__ __launch_bounds__(WAVE, HS_MIN_WAVES) void hs_rollout_kernel(const hs
   const int i = a.k0 + 2;  // centre sample of this launch's step
   {
     const int sl = lane / nl, L = lane % nl;
-    if (sl < NS) kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM>{&sm.d}, sl - 2);
+    if (sl < NS) kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2);
     wave_sync();
   }
   STAMP(2);
-  step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.gl, sm.d.wk, OneWin<NM>{&sm.d}, G, b, live, mp.h_row, work, lane);
+  if constexpr (FORCES) {
+    forces_step(T, a, mp, sm.st, sm.sv, sm.d.fr, OneWin<NM, FORCES>{&sm.d}, b, live, mp.h_row, lane);
+    return;
+  } else {
+    step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.gl, sm.d.wk, OneWin<NM, FORCES>{&sm.d}, G, b, live, mp.h_row, work,
+         lane);
+  }
   if (lane == 0 && live) {
     double cot = work / (T->total_mass * g.step_length);
     if (a.work_cot) {
@@ -1484,7 +1688,10 @@ launch_map single_model_map(const hs_topo& t, int32_t n_rollouts) {
 
 template <int NM>
 void launch_nm(const hs_topo* d_topo, const hs_run_args& a, GenWS* ws, const launch_map& mp, hipStream_t st) {
-  hipLaunchKernelGGL((hs_rollout_kernel<NM>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
+  if (mp.tau_in)
+    hipLaunchKernelGGL((hs_rollout_kernel<NM, true>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
+  else
+    hipLaunchKernelGGL((hs_rollout_kernel<NM, false>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
 }
 
 int launch_rollouts(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp) {

@@ -131,6 +131,17 @@ int hs_run(hs_model_t model, const hs_run_args* args);
  * and after each launch (per-launch kernel timing on the launch stream). */
 int hs_run_steps(hs_model_t model, const hs_run_args* args, int32_t n_calls, void* const* kernel_events);
 
+/* Contact forces given motor torques: forcetorquesolver::solve_forces via
+ * periodic::solve_contforces_given_torques (ftsolver.cpp:331-378,
+ * periodic.cpp:368-374) for steps k0 .. k0+H-1 of every rollout. tau_in is a
+ * DEVICE array [B][H][nmj]; args->cf receives the least-squares forces of ALL
+ * feet (airborne ones included, contact_feet_flag = false), torso force and
+ * torque forced to zero; args->q and args->flags as in hs_run (HS_FLAG_GENERAL
+ * = the least squares is rank deficient, e.g. a straight leg; then the
+ * Tikhonov-regularized solution is returned). tau, x, work_cot and best_key are
+ * not written. */
+int hs_run_forces(hs_model_t model, const hs_run_args* args, const double* tau_in);
+
 /* Mixed-topology batches (BASELINE configs[4], e.g. myant + hexapod interleaved):
  * rollout b runs models[model_index[b]]. The reference runs one kinematicmodel
  * per periodic object (periodic.cpp:34-58); a plan batches several in one

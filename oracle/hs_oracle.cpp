@@ -1628,6 +1628,87 @@ bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<d
   return true;
 }
 
+// forcetorquesolver::solve_forces (ftsolver.cpp:331-378): contact forces of ALL feet
+// (set_forcetorque_system_contacts with contact_feet_flag = false, dynrec.cpp:313-325)
+// realising the motor torques z, torso force/torque columns zeroed, least squares
+// over [B0 Bc_all; jz-rows] [x; y] = [f; z] (add_torque_constraints_to_B, 359-378).
+// SparseQR's basic solution leaves the zero torso columns at 0 and is the unique
+// LS solution of the remaining columns when they have full rank; here a dense
+// Householder QR of those columns. Rank deficiency (a straight leg's torques
+// cannot fix its foot force) returns false and the Tikhonov-regularized
+// (1e-12 * max diag) normal-equations solution.
+bool solve_forces(const hso_model* m, const DynRec& d, const double* z, std::vector<double>& y) {
+  const int n = m->n, nf = m->nf, nmj = m->nmj;
+  Mat B0;
+  std::vector<double> f;
+  build_B0_f(m, d, B0, f);
+  const int rows = 6 * n + nmj, cols = 6 * n - 6 + 3 * nf;
+  std::vector<int> keep;  // B0 columns without the torso force / torque
+  for (int c = 0; c < 6 * n; c++)
+    if (!(c < 3 || (c >= 3 * n && c < 3 * n + 3))) keep.push_back(c);
+  Mat A(rows, cols);
+  for (int j = 0; j < (int)keep.size(); j++)
+    for (int i = 0; i < 6 * n; i++) A(i, j) = B0(i, keep[j]);
+  const int y0 = (int)keep.size();
+  for (int fi = 0; fi < nf; fi++) {  // all feet
+    int i = m->footis[fi];
+    for (int j = 0; j < 3; j++) A(3 * i + j, y0 + 3 * fi + j) = 1;
+    Vec r = d.fpos[fi];
+    r.subtract(d.pos[i]);
+    int kk = 3 * (n + i), k1 = y0 + 3 * fi;
+    for (int l = 0; l < 3; l++) {
+      int dk[3];
+      for (int l1 = 0; l1 < 3; l1++) dk[l1] = (l + l1) % 3;
+      A(kk + dk[0], k1 + dk[1]) = -r.v[dk[2]];
+      A(kk + dk[1], k1 + dk[0]) = r.v[dk[2]];
+    }
+  }
+  std::vector<double> b(f);
+  b.resize(rows);
+  for (int jj = 0; jj < nmj; jj++) {  // torque constraint rows
+    int h = m->hinge_ids[jj];
+    for (int j = 0; j < 3; j++) {
+      int col = -1;
+      for (int q = 0; q < (int)keep.size(); q++)
+        if (keep[q] == 3 * n + 3 * h + j) col = q;
+      A(6 * n + jj, col) = d.jzaxis[h].v[j];
+    }
+    b[6 * n + jj] = z[jj];
+  }
+  HQR qr;
+  qr.compute(A);
+  double rmax = 0;
+  for (int i = 0; i < cols; i++) rmax = std::max(rmax, fabs(qr.qr(i, i)));
+  bool full = true;
+  for (int i = 0; i < cols; i++) full = full && fabs(qr.qr(i, i)) > 1e-10 * rmax;
+  std::vector<double> u;
+  if (full) {
+    u = qr.solve(b);
+  } else {
+    Mat N(cols, cols);
+    std::vector<double> r(cols, 0.0);
+    double dmax = 0;
+    for (int i = 0; i < cols; i++) {
+      for (int j = 0; j < cols; j++) {
+        double s = 0;
+        for (int t = 0; t < rows; t++) s += A(t, i) * A(t, j);
+        N(i, j) = s;
+      }
+      for (int t = 0; t < rows; t++) r[i] += A(t, i) * b[t];
+      dmax = std::max(dmax, N(i, i));
+    }
+    for (int i = 0; i < cols; i++) N(i, i) += 1e-12 * dmax;
+    std::vector<double> nn(cols * cols);
+    for (int i = 0; i < cols; i++)
+      for (int j = 0; j < cols; j++) nn[i * cols + j] = N(i, j);
+    chol(nn.data(), cols, 0.0);
+    chol_solve(nn.data(), cols, r.data());
+    u = r;
+  }
+  y.assign(u.begin() + y0, u.begin() + y0 + 3 * nf);
+  return full;
+}
+
 // forcetorquesolver::solve_forcetorques, ftsolver.cpp:78-102
 void solve_forcetorques(const hso_model* m, const DynRec& d, int basis, FTOut& out) {
   int n = m->n;
@@ -1830,6 +1911,51 @@ int run_rollout(const hso_model* m0, const hso_gait* g, int n_t, int k0, int H, 
   return 0;
 }
 
+// periodic::solve_contforces_given_torques (periodic.cpp:368-374) over steps
+// k0 .. k0+H-1 of one rollout; tau_in [H][nmj] -> cf [H][3 nf]
+int run_forces(const hso_model* m0, const hso_gait* g, int n_t, int k0, int H, int ignore_reach,
+               const double* tau_in, double* cf, uint32_t* flags) {
+  hso_model mm = *m0;
+  hso_model* m = &mm;
+  tl_ignore_reach = ignore_reach != 0;
+  PGS pgs;
+  setup_pergen(m, pgs, g);
+  int n = m->n, cfg = m->cfg, nf = m->nf, nmj = m->nmj;
+  int nsamp = k0 + H + 4;
+  double dt = pgs.pergen.period / n_t;
+  std::vector<double> traj((size_t)nsamp * cfg);
+  std::vector<char> unreach(nsamp, 0);
+  std::vector<double> rec(cfg);
+  double t = 0;
+  for (int i = 0; i < nsamp; i++) {
+    tl_unreach = false;
+    pgs.set_rec(rec.data(), t);
+    if (!set_jvalues_with_lik(m, rec.data())) return -10;
+    unreach[i] = tl_unreach;
+    for (int j = 0; j < cfg; j++) traj[(size_t)i * cfg + j] = jv(m, j);
+    t += dt;
+  }
+  std::vector<DynRec> dr(nsamp);
+  for (int i = k0; i < nsamp; i++) {
+    dr[i].init(n, nf);
+    for (int j = 0; j < cfg; j++) jv(m, j) = traj[(size_t)i * cfg + j];
+    recompute_modelnodes(m);
+    dynrec_initialize(m, dr[i], m->rcap);
+  }
+  for (int i = k0 + 1; i <= nsamp - 2; i++) compute_ders(m, dr[i], 0, dr[i - 1], dr[i + 1], dt);
+  for (int i = k0 + 2; i <= nsamp - 3; i++) compute_ders(m, dr[i], 1, dr[i - 1], dr[i + 1], dt);
+  for (int h = 0; h < H; h++) {
+    int i = k0 + h + 2;
+    std::vector<double> y;
+    uint32_t fl = solve_forces(m, dr[i], tau_in + (size_t)h * nmj, y) ? 0u : HSO_FLAG_GENERAL;
+    if (unreach[i]) fl |= HSO_FLAG_UNREACH;
+    for (double v : y) if (std::isnan(v)) fl |= HSO_FLAG_NAN;
+    if (cf) std::copy(y.begin(), y.end(), cf + (size_t)h * 3 * nf);
+    if (flags) flags[h] = fl;
+  }
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1844,6 +1970,12 @@ int hso_rollout(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, i
                 double* q, double* tau, double* cf, double* x, uint32_t* flags, double* work_cot, double* diag) {
   if (!m || !g || n_t <= 0 || k0 < 0 || H <= 0) return -1;
   return run_rollout(m, g, n_t, k0, H, basis, ignore_reach, q, tau, cf, x, flags, work_cot, diag);
+}
+
+int hso_forces(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, int ignore_reach, const double* tau_in,
+               double* cf, uint32_t* flags) {
+  if (!m || !g || !tau_in || n_t <= 0 || k0 < 0 || H <= 0) return -1;
+  return run_forces(m, g, n_t, k0, H, ignore_reach, tau_in, cf, flags);
 }
 
 int hso_batch(const hso_model* m, const hso_gait* params, int B, int n_t, int k0, int H, int basis,

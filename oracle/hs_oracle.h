@@ -78,6 +78,11 @@ int hso_rollout(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, i
 /* Batched CPU baseline: B rollouts (params[B]), same k0/H for all, tree basis,
  * n_threads std::threads over rollouts. Outputs tau[B][H][nmj], cf[B][H][3nf],
  * work_cot[B][2]. Returns 0 on success. */
+/* forcetorquesolver::solve_forces via periodic::solve_contforces_given_torques
+ * (ftsolver.cpp:331-378, periodic.cpp:368-374): tau_in [H][nmj] -> cf [H][3 nf]
+ * for ALL feet; flags HSO_FLAG_GENERAL when the least squares is rank deficient. */
+int hso_forces(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, int ignore_reach, const double* tau_in,
+               double* cf, uint32_t* flags);
 int hso_batch(const hso_model* m, const hso_gait* params, int B, int n_t, int k0, int H,
               int basis, int ignore_reach, int n_threads, double* tau, double* cf,
               double* work_cot, uint32_t* flags);

@@ -142,6 +142,8 @@ def lib():
         L.hso_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, dp,
                                 ctypes.POINTER(ctypes.c_uint32)]
+        L.hso_forces.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, dp, dp, ctypes.POINTER(ctypes.c_uint32)]
         L.hso_lik_roundtrip.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]
         L.hso_lik_roundtrip.restype = ctypes.c_double
         L.hso_euler_roundtrip.argtypes = [dp, dp]
@@ -210,6 +212,20 @@ def rollout(model: Model, gait: GaitParams, n_t: int = 20, k0: int = 0, H: int |
     if rc != 0:
         raise RuntimeError(f"oracle rollout failed rc={rc}")
     return dict(q=q, tau=tau, cf=cf, x=x, flags=flags, work=wc[0], cot=wc[1], diag=diag)
+
+
+def forces(model: Model, gait: GaitParams, tau_in, n_t: int = 20, k0: int = 0, ignore_reach: bool = True) -> dict:
+    """Contact forces of all feet given motor torques tau_in [H][nmj] (ftsolver.cpp:331-378)."""
+    tau_in = np.ascontiguousarray(tau_in, dtype=np.float64)
+    H = tau_in.shape[0]
+    cf = np.zeros((H, 3 * model.nf))
+    flags = np.zeros(H, dtype=np.uint32)
+    g = gait.to_c()
+    rc = lib().hso_forces(model.handle, ctypes.byref(g), n_t, k0, H, int(ignore_reach), _ptr(tau_in), _ptr(cf),
+                          flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    if rc != 0:
+        raise RuntimeError(f"oracle forces failed rc={rc}")
+    return dict(cf=cf, flags=flags)
 
 
 def batch(model: Model, gaits: list, n_t: int, k0: int, H: int, basis: int = BASIS_TREE,

@@ -294,3 +294,52 @@ def test_mixed_batch_matches_oracle(gpu, hmodels, oracle_mod, omodels):
                                basis=oracle_mod.BASIS_FAST)
         nmj = hmodels[name].nmj
         assert np.abs(tau[b, :, :nmj] - r["tau"]).max() < 1e-6 * max(1, np.abs(r["tau"]).max())
+
+
+@pytest.mark.parametrize("name", ["hexapod", "spider", "myant"])
+def test_forces_given_torques_match_oracle(gpu, hmodels, oracle_mod, omodels, name):
+    """hs_run_forces (solve_forces, ftsolver.cpp:331-378): the kernel's reduced weighted least
+    squares equals the oracle's dense Householder LS, for torques inconsistent with the motion."""
+    import torch
+
+    from hslabs_amd import synth
+
+    m = hmodels[name]
+    params = synth.gen_params(12, name, id0=4321)
+    full = gpu.DeviceBatch(m, params, n_t=20, horizon=20, outputs=("tau", "cf"))
+    full.run(best=False)
+    tau = full.tau + 0.25 * torch.cos(torch.arange(20, device=full.tau.device)[None, :, None]
+                                      + torch.arange(m.nmj, device=full.tau.device)[None, None, :])
+    fb = gpu.DeviceBatch(m, params, n_t=20, horizon=20, outputs=("cf", "flags"))
+    fb.run_forces(tau)
+    torch.cuda.synchronize()
+    cf, flags, tz = fb.cf.cpu().numpy(), fb.flags.cpu().numpy(), tau.cpu().numpy()
+    for b, r in enumerate(params):
+        fo = oracle_mod.forces(omodels[name], record_to_oracle_gait(oracle_mod, r), tz[b], 20)
+        ok = (fo["flags"] & 64) == 0
+        assert ((flags[b] & 64) == 0)[ok].all()
+        scale = max(1.0, np.abs(fo["cf"]).max())
+        assert np.abs(cf[b][ok] - fo["cf"][ok]).max() < 1e-9 * scale
+
+
+def test_forces_round_trip(gpu, hmodels):
+    """modelplayer::test_dynamics (playerexperim.cpp:95-121) on the GPU at configs[1] size:
+    forces recovered from the kernel's own torques equal its contact forces where >= 3 feet
+    are down (torso actuation zero)."""
+    import torch
+
+    from hslabs_amd import synth
+
+    m = hmodels["hexapod"]
+    params = synth.gen_params(4096, "hexapod")
+    b = gpu.DeviceBatch(m, params, n_t=20, k0=5, horizon=1, outputs=("tau", "cf"))
+    b.run(best=False)
+    f = gpu.DeviceBatch(m, params, n_t=20, k0=5, horizon=1, outputs=("cf", "flags"))
+    f.run_forces(b.tau)
+    torch.cuda.synchronize()
+    cf, cf2 = b.cf.cpu().numpy()[:, 0], f.cf.cpu().numpy()[:, 0]
+    nc = (np.abs(cf.reshape(-1, 6, 3)).max(axis=2) > 0).sum(axis=1)
+    sel = nc >= 3
+    assert sel.mean() > 0.5
+    scale = np.maximum(1, np.abs(cf).max(axis=1))
+    assert (np.abs(cf2 - cf).max(axis=1)[sel] < 1e-9 * scale[sel]).all()

@@ -255,3 +255,56 @@ def test_augmented_closed_form_on_straight_legs(oracle_mod, omodels):
             assert np.abs(rt["tau"] - rf["tau"]).max() < 1e-10 * max(1.0, np.abs(rt["tau"]).max())
             assert np.abs(rt["cf"] - rf["cf"]).max() < 1e-10 * max(1.0, np.abs(rt["cf"]).max())
     assert n_aug >= 10  # the clamped steps are really exercised
+
+
+# --- solve_forces (ftsolver.cpp:331-378): contact forces given motor torques --------------------
+def dense_forces(d, n, z):
+    """Independent numpy statement of solve_forces: B0 + all-feet contact columns + jz torque rows,
+    torso columns dropped, np.linalg.lstsq."""
+    nf = len(d["footis"])
+    d2 = dict(d)
+    d2["contacts"] = np.ones(nf, np.int32)  # contact_feet_flag = false: all feet
+    B0, f, Bc = build_system(d2, n)
+    nmj = len(d["hinge_ids"])
+    Tr = np.zeros((nmj, 6 * n))
+    for jj, h in enumerate(d["hinge_ids"]):
+        Tr[jj, 3 * n + 3 * h:3 * n + 3 * h + 3] = d["jz"][h]
+    Bf = np.block([[B0, Bc], [Tr, np.zeros((nmj, 3 * nf))]])
+    keep = [c for c in range(Bf.shape[1]) if not (c < 3 or 3 * n <= c < 3 * n + 3)]
+    sol = np.linalg.lstsq(Bf[:, keep], np.concatenate([f, z]), rcond=None)[0]
+    return sol[-3 * nf:]
+
+
+@pytest.mark.parametrize("sid", PGS_IDS)
+def test_solve_forces_round_trip(oracle_mod, omodels, sid):
+    """modelplayer::test_dynamics (playerexperim.cpp:95-121): the contact forces solve_forces
+    recovers from solve_forcetorques' motor torques equal its contact forces wherever the
+    torso actuation vanished (>= 3 feet down)."""
+    g = pgs(oracle_mod, sid)
+    m = model_for(oracle_mod, omodels, g)
+    r = oracle_mod.rollout(m, g, 20, basis=oracle_mod.BASIS_FAST)
+    fo = oracle_mod.forces(m, g, r["tau"], 20)
+    nc = (np.abs(r["cf"].reshape(20, -1, 3)).max(axis=2) > 0).sum(axis=1)
+    sel = nc >= 3
+    assert sel.any()
+    scale = max(1.0, np.abs(r["cf"]).max())
+    assert np.abs(fo["cf"][sel] - r["cf"][sel]).max() < 1e-10 * scale
+    assert not (fo["flags"] & oracle_mod.FLAG_GENERAL).any()
+
+
+@pytest.mark.parametrize("name", ["hexapod", "spider", "myant"])
+def test_solve_forces_matches_independent_lstsq(oracle_mod, omodels, name):
+    """Arbitrary torques (inconsistent with the trajectory): the oracle's Householder LS equals
+    numpy's lstsq of the same system."""
+    from hslabs_amd import synth
+    from conftest import record_to_oracle_gait
+
+    m = omodels[name]
+    for r in synth.gen_params(3, name, id0=321):
+        g = record_to_oracle_gait(oracle_mod, r)
+        ro = oracle_mod.rollout(m, g, 20, basis=oracle_mod.BASIS_FAST)
+        z = ro["tau"] + 0.25 * np.cos(np.arange(20)[:, None] + np.arange(m.nmj)[None, :])
+        fo = oracle_mod.forces(m, g, z, 20)
+        for step in (0, 6, 15):
+            ref = dense_forces(oracle_mod.dynrec_dump(m, g, 20, step), m.n, z[step])
+            assert np.abs(fo["cf"][step] - ref).max() < 1e-10 * max(1.0, np.abs(ref).max())
