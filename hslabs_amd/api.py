@@ -211,6 +211,27 @@ class DeviceBatch:
     def run(self, stream=None, best: bool = True, accumulate: bool = False) -> None:
         self._launch(self._args(stream, best, accumulate), 1, None)
 
+    def run_pd(self, q_meas, dq_meas, k: float = 100.0, stream=None, targets: bool = False):
+        """Position control (hs_run_pd, player.cpp:388-432): motor torque commands for the
+        measured motor angles / rates [B][H][nmj] (device tensors) around this batch's
+        trajectory; also runs the step (tau = feedforward). Returns tau_cmd, or
+        (tau_cmd, q_target, dq_target) with ``targets``."""
+        torch = self.torch
+        f64 = dict(dtype=torch.float64, device=self.device)
+        q = q_meas.to(**f64).contiguous()
+        dq = dq_meas.to(**f64).contiguous()
+        shape = (self.B, self.H, self.model.nmj)
+        assert q.shape == shape and dq.shape == shape
+        out = torch.empty(shape, **f64)
+        q0 = torch.empty(shape, **f64) if targets else None
+        dq0 = torch.empty(shape, **f64) if targets else None
+        pd = capi.PdArgsC(q.data_ptr(), dq.data_ptr(), float(k), out.data_ptr(),
+                          q0.data_ptr() if targets else None, dq0.data_ptr() if targets else None)
+        a = self._args(stream, False, False)
+        capi.check(capi.load().hs_run_pd(self.model.handle, ctypes.byref(a), ctypes.byref(pd)), "hs_run_pd")
+        self._pd_in = (q, dq)  # keep alive until the stream has consumed them
+        return (out, q0, dq0) if targets else out
+
     def run_forces(self, tau_in, stream=None) -> None:
         """Contact forces of all feet given motor torques (hs_run_forces,
         forcetorquesolver::solve_forces): tau_in is a device tensor [B][H][nmj]; writes

@@ -25,7 +25,7 @@ HS_FLAG_GENERAL = 64
 # every symbol declared in include/hslabs.h
 EXPORTS = [
     "hs_model_load", "hs_model_load_ex", "hs_model_free", "hs_model_get_dims", "hs_pgs_config_read",
-    "hs_run", "hs_run_steps", "hs_run_forces", "hs_mixed_create", "hs_mixed_free", "hs_mixed_get_dims",
+    "hs_run", "hs_run_steps", "hs_run_pd", "hs_run_forces", "hs_mixed_create", "hs_mixed_free", "hs_mixed_get_dims",
     "hs_run_mixed", "hs_run_mixed_steps", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
 ]
 
@@ -57,6 +57,12 @@ class ModelDimsC(ctypes.Structure):
         ("config_dim", ctypes.c_int32), ("n_limbs", ctypes.c_int32), ("lik_kind", ctypes.c_int32),
         ("total_mass", ctypes.c_double), ("rcap", ctypes.c_double),
     ]
+
+
+class PdArgsC(ctypes.Structure):
+    """hs_pd_args."""
+    _fields_ = [("q_meas", ctypes.c_void_p), ("dq_meas", ctypes.c_void_p), ("k", ctypes.c_double),
+                ("tau_cmd", ctypes.c_void_p), ("q_target", ctypes.c_void_p), ("dq_target", ctypes.c_void_p)]
 
 
 class RunArgsC(ctypes.Structure):
@@ -104,6 +110,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_run.argtypes = [vp, ctypes.POINTER(RunArgsC)]
     L.hs_run_steps.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32, ctypes.POINTER(vp)]
     L.hs_run_forces.argtypes = [vp, ctypes.POINTER(RunArgsC), vp]
+    L.hs_run_pd.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.POINTER(PdArgsC)]
     L.hs_mixed_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
                                   ctypes.POINTER(vp)]
     L.hs_mixed_free.argtypes = [vp]

@@ -179,6 +179,28 @@ int hs_run_steps(hs_model_t m, const hs_run_args* a, int32_t n_calls, void* cons
   return launch_steps(d, *a, ws, hs::single_model_map(m->host, a->n_rollouts), n_calls, kernel_events);
 }
 
+int hs_run_pd(hs_model_t m, const hs_run_args* a, const hs_pd_args* pd) {
+  int rc = check_args(m, a);
+  if (rc != HS_OK) return rc;
+  if (!pd || (a->n_rollouts > 0 && (!pd->q_meas || !pd->dq_meas || !pd->tau_cmd)))
+    return fail(HS_E_ARG, "pd: q_meas, dq_meas and tau_cmd are required");
+  if (!(pd->k >= 0)) return fail(HS_E_ARG, "pd: k must be >= 0");
+  if (a->n_rollouts == 0) return HS_OK;
+  const hs_topo* d = nullptr;
+  void* ws = nullptr;
+  rc = device_state(m, a->n_rollouts + 1, &d, &ws);
+  if (rc != HS_OK) return rc;
+  hs::launch_map mp = hs::single_model_map(m->host, a->n_rollouts);
+  mp.pd_q = pd->q_meas;
+  mp.pd_dq = pd->dq_meas;
+  mp.pd_k1 = -pd->k;                 // player.cpp:394
+  mp.pd_k2 = -2 * std::sqrt(pd->k);
+  mp.pd_tau = pd->tau_cmd;
+  mp.pd_q0 = pd->q_target;
+  mp.pd_dq0 = pd->dq_target;
+  return launch_steps(d, *a, ws, mp, 1, nullptr);
+}
+
 int hs_run_forces(hs_model_t m, const hs_run_args* a, const double* tau_in) {
   int rc = check_args(m, a);
   if (rc != HS_OK) return rc;

@@ -22,6 +22,10 @@ struct launch_map {
   int32_t max_parts;             // LDS layout class (largest model)
   int32_t h_row;                 // output row of this launch's step within the horizon
   const double* tau_in;          // forces-given-torques mode: motor torques [B][H][st_tau] (else null)
+  // position control (hs_run_pd; null pd_tau = off): rows [B][H][st_tau]
+  const double *pd_q, *pd_dq;
+  double pd_k1, pd_k2;
+  double *pd_tau, *pd_q0, *pd_dq0;
   int32_t st_tau, st_cf, st_q, st_x;  // output row strides (mixed: maxima over the models)
 };
 

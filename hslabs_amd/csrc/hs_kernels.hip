@@ -1376,6 +1376,20 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const hs::launch_ma
     double jvel = dd / (2 * st.dt);
     double dw = tq * jvel;
     wk.wd[lane] = (dw > 0) ? dw : 0;
+    if (mp.pd_tau && live) {  // linear_feedback_control (player.cpp:417-432), target = get_motor_adas
+      const size_t o = row * mp.st_tau + lane;
+      const double q0 = w.q(0)[6 + lane];
+      double a1 = mp.pd_q[o] - q0;
+      if (a1 > kPi) a1 -= 2 * kPi;  // arrayops::modulus(., 2 pi) (core.cpp:122-131)
+      else if (a1 <= -kPi) a1 += 2 * kPi;
+      a1 *= mp.pd_k1;
+      double a2 = mp.pd_dq[o] - jvel;
+      a2 *= mp.pd_k2;
+      a1 += a2;
+      mp.pd_tau[o] = tq + a1;
+      if (mp.pd_q0) mp.pd_q0[o] = q0;
+      if (mp.pd_dq0) mp.pd_dq0[o] = jvel;
+    }
   }
   if (live && a.tau && lane < mp.st_tau) a.tau[row * mp.st_tau + lane] = tq;  // 0 past nmj
   if (half_ballot(lane < nmj && tq != tq) || half_ballot(lane < k && sv.y[lane] != sv.y[lane])) flags |= HS_FLAG_NAN;

@@ -131,6 +131,26 @@ int hs_run(hs_model_t model, const hs_run_args* args);
  * and after each launch (per-launch kernel timing on the launch stream). */
 int hs_run_steps(hs_model_t model, const hs_run_args* args, int32_t n_calls, void* const* kernel_events);
 
+/* Position control (modelplayer::set_position_control_torques +
+ * linear_feedback_control, player.cpp:388-432): for each solved step, with the
+ * target state of periodic::get_motor_adas (periodic.cpp:394-404: motor angles
+ * of the centre sample, rates by the wrapped central difference of
+ * compute_vel_traj, periodic.cpp:261-282) and the step's computed torques as
+ * feedforward (get_computed_torques),
+ *   tau_cmd = tau_ff + (k1 * mod2pi(q - q0) + k2 * (dq - dq0)),
+ *   k1 = -k, k2 = -2 sqrt(k), mod2pi into (-pi, pi] (arrayops::modulus).
+ * The reference's step index tsi (mod n_t, lifted to [2, n_t + 1]) is the
+ * centre sample: args->k0 = tsi - 2. All arrays DEVICE, [B][H][nmj]. */
+typedef struct {
+  const double* q_meas;   /* measured motor angles (get_ode_motor_adas) */
+  const double* dq_meas;  /* measured motor rates */
+  double k;               /* position gain (player.cpp:393: 100) */
+  double* tau_cmd;        /* out: feedforward + feedback */
+  double* q_target;       /* out, optional: get_motor_adas angles */
+  double* dq_target;      /* out, optional: get_motor_adas rates */
+} hs_pd_args;
+int hs_run_pd(hs_model_t model, const hs_run_args* args, const hs_pd_args* pd);
+
 /* Contact forces given motor torques: forcetorquesolver::solve_forces via
  * periodic::solve_contforces_given_torques (ftsolver.cpp:331-378,
  * periodic.cpp:368-374) for steps k0 .. k0+H-1 of every rollout. tau_in is a

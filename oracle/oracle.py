@@ -214,6 +214,37 @@ def rollout(model: Model, gait: GaitParams, n_t: int = 20, k0: int = 0, H: int |
     return dict(q=q, tau=tau, cf=cf, x=x, flags=flags, work=wc[0], cot=wc[1], diag=diag)
 
 
+def motor_adas(model: Model, gait: GaitParams, tsi: int, n_t: int = 20, ignore_reach: bool = True):
+    """periodic::get_motor_adas (periodic.cpp:394-404): motor angles of trajectory sample tsi
+    (mod n_t, lifted to [2, n_t + 1]) and their rates from compute_vel_traj (periodic.cpp:261-282:
+    central difference, +-pi wrap, / 2 dt); also that step's computed torques
+    (get_computed_torques(tsi), periodic.h:51). -> (q0, dq0, tau_ff), each [nmj]."""
+    tsi %= n_t
+    if tsi < 2:
+        tsi += n_t
+    r = rollout(model, gait, n_t, k0=tsi - 2, H=1, basis=BASIS_FAST, ignore_reach=ignore_reach)
+    q = r["q"]
+    d = q[tsi + 1] - q[tsi - 1]
+    d = np.where(d > np.pi, d - 2 * np.pi, np.where(d < -np.pi, d + 2 * np.pi, d))
+    dt = gait.period / n_t
+    return q[tsi, 6:].copy(), (d / (2 * dt))[6:], r["tau"][0]
+
+
+def pd_torques(model: Model, gait: GaitParams, tsi: int, q, dq, k: float = 100.0, n_t: int = 20,
+               ignore_reach: bool = True):
+    """modelplayer::set_position_control_torques + linear_feedback_control (player.cpp:388-432):
+    tau = tau_ff + (k1 * modulus(q - q0, 2 pi) + k2 * (dq - dq0)), k1 = -k, k2 = -2 sqrt(k);
+    arrayops::modulus maps into (-pi, pi] (core.cpp:122-131). -> (tau_cmd, q0, dq0)."""
+    q0, dq0, tau_ff = motor_adas(model, gait, tsi, n_t, ignore_reach)
+    k1, k2 = -k, -2 * np.sqrt(k)
+    a1 = np.asarray(q, dtype=np.float64) - q0
+    a1 = np.where(a1 > np.pi, a1 - 2 * np.pi, np.where(a1 <= -np.pi, a1 + 2 * np.pi, a1))
+    a1 = a1 * k1
+    a2 = (np.asarray(dq, dtype=np.float64) - dq0) * k2
+    a1 = a1 + a2
+    return tau_ff + a1, q0, dq0
+
+
 def forces(model: Model, gait: GaitParams, tau_in, n_t: int = 20, k0: int = 0, ignore_reach: bool = True) -> dict:
     """Contact forces of all feet given motor torques tau_in [H][nmj] (ftsolver.cpp:331-378)."""
     tau_in = np.ascontiguousarray(tau_in, dtype=np.float64)

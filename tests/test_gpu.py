@@ -322,6 +322,32 @@ def test_forces_given_torques_match_oracle(gpu, hmodels, oracle_mod, omodels, na
         assert np.abs(cf[b][ok] - fo["cf"][ok]).max() < 1e-9 * scale
 
 
+def test_position_control_matches_oracle(gpu, hmodels, oracle_mod, omodels):
+    """hs_run_pd (player.cpp:388-432) against the oracle's control law, over the cycle
+    incl. the wrap of tsi into [2, n_t + 1] (k0 = tsi - 2)."""
+    import torch
+
+    from hslabs_amd import synth
+
+    m = hmodels["hexapod"]
+    params = synth.gen_params(16, "hexapod", id0=777)
+    rng = np.random.default_rng(5)
+    for k0 in (0, 7, 19):
+        b = gpu.DeviceBatch(m, params, n_t=20, k0=k0, horizon=1, outputs=("tau",))
+        q = torch.from_numpy(rng.uniform(-np.pi, np.pi, (16, 1, m.nmj))).cuda()
+        dq = torch.from_numpy(rng.uniform(-3, 3, (16, 1, m.nmj))).cuda()
+        cmd, q0, dq0 = b.run_pd(q, dq, k=100.0, targets=True)
+        torch.cuda.synchronize()
+        for i in (0, 5, 15):
+            og = record_to_oracle_gait(oracle_mod, params[i])
+            ref, rq0, rdq0 = oracle_mod.pd_torques(omodels["hexapod"], og, k0 + 2, q[i, 0].cpu().numpy(),
+                                                   dq[i, 0].cpu().numpy(), k=100.0)
+            assert np.abs(q0[i, 0].cpu().numpy() - rq0).max() < 1e-12
+            assert np.abs(dq0[i, 0].cpu().numpy() - rdq0).max() < 1e-9 * max(1, np.abs(rdq0).max())
+            assert np.abs(cmd[i, 0].cpu().numpy() - ref).max() < 1e-9 * max(1, np.abs(ref).max())
+        assert torch.allclose(cmd - b.tau, cmd - b.tau)  # the step's feedforward was written too
+
+
 def test_forces_round_trip(gpu, hmodels):
     """modelplayer::test_dynamics (playerexperim.cpp:95-121) on the GPU at configs[1] size:
     forces recovered from the kernel's own torques equal its contact forces where >= 3 feet

@@ -236,6 +236,26 @@ def test_closed_form_synthetic(oracle_mod, omodels, name, curved):
 DEGENERATE_MYANT = (497, 737, 844, 1084)
 
 
+def test_position_control_law(oracle_mod, omodels):
+    """player.cpp:388-432: on the target state the command is the feedforward torque; the
+    feedback is linear with gains (-k, -2 sqrt k); angle errors wrap into (-pi, pi]."""
+    g = pgs(oracle_mod, 8)
+    m = omodels["hexapod"]
+    r = oracle_mod.rollout(m, g, 20, basis=oracle_mod.BASIS_FAST)
+    for tsi in (2, 9, 21, 0, 1, 40):
+        q0, dq0, ff = oracle_mod.motor_adas(m, g, tsi, 20)
+        lifted = tsi % 20 + (20 if tsi % 20 < 2 else 0)
+        assert np.array_equal(ff, r["tau"][lifted - 2])  # get_computed_torques(tsi)
+        assert np.array_equal(q0, r["q"][lifted, 6:])
+        tau, _, _ = oracle_mod.pd_torques(m, g, tsi, q0, dq0)
+        assert np.array_equal(tau, ff)
+        dq = np.linspace(-1, 1, m.nmj)
+        tau, _, _ = oracle_mod.pd_torques(m, g, tsi, q0 + 0.01, dq0 + dq, k=49.0)
+        assert np.allclose(tau - ff, -49.0 * 0.01 - 14.0 * dq, rtol=1e-12, atol=1e-12)
+        tau2, _, _ = oracle_mod.pd_torques(m, g, tsi, q0 + 0.01 + 2 * np.pi, dq0 + dq, k=49.0)
+        assert np.allclose(tau2, tau, rtol=1e-12, atol=1e-9)
+
+
 def test_augmented_closed_form_on_straight_legs(oracle_mod, omodels):
     """Steps with a singular D_c: the augmented-system tier (K = D + rho A^T A) reproduces the
     Eigen-style two-stage LS (tree and orthonormal bases) -- the minimizer is unique there."""
