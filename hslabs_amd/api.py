@@ -176,6 +176,7 @@ class DeviceBatch:
         f64 = dict(dtype=torch.float64, device=dev)
         B, H = self.B, self.H
         self.q = torch.empty((B, H, dims.config_dim), **f64) if "q" in outputs else None
+        self.dq = torch.empty((B, H, dims.config_dim), **f64) if "dq" in outputs else None
         self.tau = torch.empty((B, H, dims.nmj), **f64) if "tau" in outputs else None
         self.cf = torch.empty((B, H, 3 * dims.nfeet), **f64) if "cf" in outputs else None
         self.x = torch.empty((B, H, 6 * dims.n_parts), **f64) if "x" in outputs else None
@@ -198,7 +199,7 @@ class DeviceBatch:
 
         a.params = ptr(self.params)
         a.q, a.tau, a.cf, a.x = ptr(self.q), ptr(self.tau), ptr(self.cf), ptr(self.x)
-        a.flags, a.work_cot = ptr(self.flags), ptr(self.work_cot)
+        a.flags, a.work_cot, a.dq = ptr(self.flags), ptr(self.work_cot), ptr(self.dq)
         a.best_key = ptr(self.best_key) if best else None
         a.rollout_id_base = self.rollout_id_base
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
@@ -302,6 +303,27 @@ class MixedBatch(DeviceBatch):
             self.plan = None
 
 
+def complete_traj(model: KinematicModel, params, n_t: int = 20, ignore_reach: bool = True) -> np.ndarray:
+    """periodic::get_complete_traj (periodic.cpp:406-426) for a batch (hs_complete_traj):
+    [B][n_t][2 * config_dim + nmj] = (configuration, rates, computed torques) per tsi."""
+    arr = params_array(params)
+    B = len(arr)
+    rec = np.zeros((B, n_t, 2 * model.config_dim + model.nmj))
+    L = capi.load()
+    rc = L.hs_complete_traj(model.handle, arr.ctypes.data_as(ctypes.POINTER(capi.GaitParamsC)), B, n_t,
+                            int(ignore_reach), rec.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    capi.check(rc, "hs_complete_traj")
+    return rec
+
+
+def save_2d_array(path: str, rec, append: bool = False) -> None:
+    """save_2d_array (core.cpp:46-61) through hs_traj_save: the traj.txt format."""
+    a = np.ascontiguousarray(np.asarray(rec, dtype=np.float64).reshape(-1, np.shape(rec)[-1]))
+    rc = capi.load().hs_traj_save(path.encode(), a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), a.shape[0],
+                                  a.shape[1], int(append))
+    capi.check(rc, "hs_traj_save")
+
+
 def decode_best_key(key: int):
     """-> (cot as float32, global rollout id)"""
     L = capi.load()
@@ -373,3 +395,20 @@ class ModelPlayer:
         sw = self.sweep_params(pgs, param_name, val0, val1, n_val)
         r = run_host(self.model, [p for _, p in sw], n_t=n_t, k0=0, horizon=n_t, want=("work_cot",))
         return [(v, float(r["work_cot"][i, 1])) for i, (v, _) in enumerate(sw)]
+
+    def record_per_traj(self, pgs: PgsConfigParams, n_t: int, path: str = "traj.txt") -> np.ndarray:
+        """modelplayer::record_per_traj (player.cpp:617-629): the complete trajectory records of
+        one cycle written to traj.txt (n_t rows of 2 * config_dim + nmj)."""
+        rec = complete_traj(self.model, [pgs], n_t)[0]
+        save_2d_array(path, rec, append=False)
+        return rec
+
+    def record_per_traj_sweep(self, pgs: PgsConfigParams, n_t: int, param_name: str, val0: float, val1: float,
+                              n_val: int, path: str = "traj.txt") -> np.ndarray:
+        """modelplayer::record_per_traj_sweep (player.cpp:631-653): every sweep value's cycle,
+        appended one after another; all values in one batched launch."""
+        sw = self.sweep_params(pgs, param_name, val0, val1, n_val)
+        rec = complete_traj(self.model, [p for _, p in sw], n_t)
+        for i in range(len(sw)):
+            save_2d_array(path, rec[i], append=i > 0)
+        return rec

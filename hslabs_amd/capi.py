@@ -11,7 +11,7 @@ import os
 
 from . import build as _build
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 HS_OK = 0
 HS_FLAG_RANK_RETRY = 1
@@ -25,7 +25,8 @@ HS_FLAG_GENERAL = 64
 # every symbol declared in include/hslabs.h
 EXPORTS = [
     "hs_model_load", "hs_model_load_ex", "hs_model_free", "hs_model_get_dims", "hs_pgs_config_read",
-    "hs_run", "hs_run_steps", "hs_run_pd", "hs_run_forces", "hs_mixed_create", "hs_mixed_free", "hs_mixed_get_dims",
+    "hs_run", "hs_run_steps", "hs_run_pd", "hs_run_forces", "hs_mixed_create", "hs_mixed_free",
+    "hs_mixed_get_dims", "hs_complete_traj", "hs_traj_save",
     "hs_run_mixed", "hs_run_mixed_steps", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
 ]
 
@@ -72,7 +73,7 @@ class RunArgsC(ctypes.Structure):
         ("params", ctypes.c_void_p), ("q", ctypes.c_void_p), ("tau", ctypes.c_void_p),
         ("cf", ctypes.c_void_p), ("x", ctypes.c_void_p), ("flags", ctypes.c_void_p),
         ("work_cot", ctypes.c_void_p), ("best_key", ctypes.c_void_p),
-        ("rollout_id_base", ctypes.c_int64), ("stream", ctypes.c_void_p),
+        ("rollout_id_base", ctypes.c_int64), ("stream", ctypes.c_void_p), ("dq", ctypes.c_void_p),
     ]
 
 
@@ -111,6 +112,10 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_run_steps.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32, ctypes.POINTER(vp)]
     L.hs_run_forces.argtypes = [vp, ctypes.POINTER(RunArgsC), vp]
     L.hs_run_pd.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.POINTER(PdArgsC)]
+    L.hs_complete_traj.argtypes = [vp, ctypes.POINTER(GaitParamsC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                   ctypes.POINTER(ctypes.c_double)]
+    L.hs_traj_save.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_int32,
+                               ctypes.c_int32]
     L.hs_mixed_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
                                   ctypes.POINTER(vp)]
     L.hs_mixed_free.argtypes = [vp]

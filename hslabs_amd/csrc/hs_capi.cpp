@@ -5,8 +5,10 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <fstream>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "hs_internal.h"
 
@@ -318,6 +320,75 @@ int hs_run_mixed_steps(hs_mixed_t p, const hs_run_args* a, int32_t n_calls, void
   mp.st_q = p->st_q;
   mp.st_x = p->st_x;
   return launch_steps(nullptr, *a, p->ws, mp, n_calls, kernel_events);
+}
+
+int hs_complete_traj(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n_t, int32_t ignore_reach,
+                     double* rec) {
+  if (!m || (B > 0 && (!params || !rec))) return fail(HS_E_ARG, "null argument");
+  if (B <= 0 || n_t < 2) return fail(HS_E_ARG, "empty batch or n_t < 2");
+  const hs_topo& t = m->host;
+  const size_t rows = (size_t)B * n_t, cfg = (size_t)t.cfg, nmj = (size_t)t.nmj;
+  hs_gait_params* dp = nullptr;
+  double *dq = nullptr, *ddq = nullptr, *dtau = nullptr;
+  hipError_t e = hipMalloc(&dp, (size_t)B * sizeof(hs_gait_params));
+  if (e == hipSuccess) e = hipMalloc(&dq, rows * cfg * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&ddq, rows * cfg * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&dtau, rows * nmj * sizeof(double));
+  if (e == hipSuccess) e = hipMemcpy(dp, params, (size_t)B * sizeof(hs_gait_params), hipMemcpyHostToDevice);
+  int rc = HS_OK;
+  if (e != hipSuccess) {
+    rc = hip_fail(e, "alloc/copy");
+  } else {
+    hs_run_args a;
+    memset(&a, 0, sizeof(a));
+    a.n_rollouts = B;
+    a.horizon = n_t;  // compute_torques_over_period: steps i = 2 .. n_t + 1
+    a.n_t = n_t;
+    a.ignore_reach = ignore_reach;
+    a.params = dp;
+    a.q = dq;
+    a.dq = ddq;
+    a.tau = dtau;
+    rc = hs_run(m, &a);
+    std::vector<double> q(rows * cfg), v(rows * cfg), tau(rows * nmj);
+    if (rc == HS_OK) e = hipDeviceSynchronize();
+    if (rc == HS_OK && e == hipSuccess) e = hipMemcpy(q.data(), dq, q.size() * sizeof(double), hipMemcpyDeviceToHost);
+    if (rc == HS_OK && e == hipSuccess) e = hipMemcpy(v.data(), ddq, v.size() * sizeof(double), hipMemcpyDeviceToHost);
+    if (rc == HS_OK && e == hipSuccess)
+      e = hipMemcpy(tau.data(), dtau, tau.size() * sizeof(double), hipMemcpyDeviceToHost);
+    if (rc == HS_OK && e != hipSuccess) rc = hip_fail(e, "run/copy back");
+    if (rc == HS_OK) {
+      const size_t len = 2 * cfg + nmj;
+      for (int32_t b = 0; b < B; b++)
+        for (int32_t tsi = 0; tsi < n_t; tsi++) {  // get_complete_traj_rec: tsi < 2 -> tsi + n_t
+          const int32_t i = (tsi < 2) ? tsi + n_t : tsi;
+          const size_t src = (size_t)b * n_t + (size_t)(i - 2);
+          double* r = rec + ((size_t)b * n_t + tsi) * len;
+          std::copy(&q[src * cfg], &q[src * cfg] + cfg, r);
+          std::copy(&v[src * cfg], &v[src * cfg] + cfg, r + cfg);
+          std::copy(&tau[src * nmj], &tau[src * nmj] + nmj, r + 2 * cfg);
+        }
+    }
+  }
+  (void)hipFree(dp);
+  (void)hipFree(dq);
+  (void)hipFree(ddq);
+  (void)hipFree(dtau);
+  return rc;
+}
+
+int hs_traj_save(const char* path, const double* rec, int32_t n_rows, int32_t rec_len, int32_t append) {
+  if (!path || (n_rows > 0 && !rec) || n_rows < 0 || rec_len < 0) return fail(HS_E_ARG, "bad argument");
+  std::ofstream file(path, append ? std::ios_base::app : std::ios_base::out);
+  if (!file) return fail(HS_E_IO, std::string("cannot open ") + path);
+  for (int32_t i = 0; i < n_rows; i++) {
+    for (int32_t j = 0; j < rec_len; j++) {
+      if (j) file << " ";
+      file << rec[(size_t)i * rec_len + j];
+    }
+    file << std::endl;
+  }
+  return file ? HS_OK : fail(HS_E_IO, std::string("write failed: ") + path);
 }
 
 int hs_run_host(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n_t, int32_t k0, int32_t H,

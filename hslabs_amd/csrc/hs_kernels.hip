@@ -1425,6 +1425,16 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const hs::launch_ma
     for (int rI = 6 * n + lane; rI < mp.st_x; rI += HALF) a.x[row * mp.st_x + rI] = 0.0;
   }
   if (live && a.q && lane < mp.st_q) a.q[row * mp.st_q + lane] = (lane < cfg) ? w.q(0)[lane] : 0.0;
+  if (live && a.dq && lane < mp.st_q) {  // compute_vel_traj (periodic.cpp:261-282)
+    double v = 0.0;
+    if (lane < cfg) {
+      double d = w.q(1)[lane] - w.q(-1)[lane];
+      if (d > kPi) d -= 2 * kPi;
+      else if (d < -kPi) d += 2 * kPi;
+      v = d / (2 * st.dt);
+    }
+    a.dq[row * mp.st_q + lane] = v;
+  }
   if (live && a.flags && lane == 0) a.flags[row] = flags;
   wave_sync();
   double work_dt = 0;  // summed in joint order like work_over_period

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 1
+#define HSLABS_ABI_VERSION 2
 
 enum {
   HS_OK = 0,
@@ -118,6 +118,8 @@ typedef struct {
   uint64_t* best_key;     /* scalar; atomically min-reduced (cot key, see hs_best_key_decode) */
   int64_t rollout_id_base;/* global id of rollout 0 (shard offset) */
   void* stream;           /* hipStream_t */
+  double* dq;             /* [B][H][config_dim]: rates at each solved sample (compute_vel_traj,
+                             periodic.cpp:261-282: wrapped central difference / 2 dt) */
 } hs_run_args;
 
 int hs_run(hs_model_t model, const hs_run_args* args);
@@ -187,6 +189,19 @@ int hs_run_mixed_steps(hs_mixed_t plan, const hs_run_args* args, int32_t n_calls
 int hs_run_host(hs_model_t model, const hs_gait_params* params, int32_t n_rollouts, int32_t n_t,
                 int32_t k0, int32_t horizon, int32_t ignore_reach, double* q, double* tau, double* cf,
                 double* x, uint32_t* flags, double* work_cot);
+
+/* periodic::get_complete_traj (periodic.cpp:406-426) for a batch of rollouts
+ * (synchronous, host buffers): rec[b][tsi] for tsi = 0 .. n_t-1 (tsi < 2 read
+ * at tsi + n_t, like get_complete_traj_rec) = [configuration (config_dim),
+ * rates (config_dim), computed torques (nmj)] -- the records
+ * modelplayer::record_per_traj writes to traj.txt (player.cpp:619-629).
+ * rec holds n_rollouts * n_t * (2 * config_dim + nmj) doubles. */
+int hs_complete_traj(hs_model_t model, const hs_gait_params* params, int32_t n_rollouts, int32_t n_t,
+                     int32_t ignore_reach, double* rec);
+
+/* save_2d_array (core.cpp:46-61): n_rows rows of rec_len doubles, space
+ * separated, default ostream formatting, appended when append != 0. */
+int hs_traj_save(const char* path, const double* rec, int32_t n_rows, int32_t rec_len, int32_t append);
 
 /* Best-rollout key: (order-preserving bits of (float)cot) << 32 | (uint32)rollout id.
  * NaN COT maps to the largest key. Initial value for a reduction: UINT64_MAX. */

@@ -191,3 +191,16 @@ def test_mixed_synthetic_batch_layout(product):
     a = synth.gen_params(64, "myant", id0=10)
     h = synth.gen_params(64, "hexapod", id0=10)
     assert (p[idx == 0] == a[idx == 0]).all() and (p[idx == 1] == h[idx == 1]).all()
+
+
+def test_traj_save_format(product, tmp_path):
+    """save_2d_array (core.cpp:46-61): space-separated rows, default ostream formatting
+    (6 significant digits, %g), append mode for sweeps."""
+    rec = np.array([[0.1, -2.5e-7, 123456789.0, 0.0], [-0.0, 1.0 / 3.0, 1e-5, 42.0]])
+    path = str(tmp_path / "traj.txt")
+    product.save_2d_array(path, rec)
+    product.save_2d_array(path, rec[:1], append=True)
+    lines = open(path).read().splitlines()
+    want = [" ".join("%g" % v for v in row) for row in rec] + [" ".join("%g" % v for v in rec[0])]
+    assert lines == want
+    assert lines[0] == "0.1 -2.5e-07 1.23457e+08 0"

@@ -348,6 +348,30 @@ def test_position_control_matches_oracle(gpu, hmodels, oracle_mod, omodels):
         assert torch.allclose(cmd - b.tau, cmd - b.tau)  # the step's feedforward was written too
 
 
+@pytest.mark.parametrize("sid", [8, 9, 24])
+def test_complete_traj_matches_oracle(gpu, hmodels, oracle_mod, omodels, sid, tmp_path):
+    """periodic::get_complete_traj (periodic.cpp:406-426) / record_per_traj's traj.txt:
+    rows tsi = 0 .. n_t-1 (tsi < 2 read at tsi + n_t) of (q, compute_vel_traj rates, torques)."""
+    p = gpu.read_pgs_config(PGS_CONFIG, sid)
+    name = p.fname.replace(".xml", "")
+    m = hmodels[name]
+    rec = gpu.complete_traj(m, [p], 20)[0]
+    r = oracle_mod.rollout(omodels[name], to_oracle_gait(oracle_mod, p), 20, basis=oracle_mod.BASIS_FAST)
+    cfg, nmj, dt = m.config_dim, m.nmj, p.period / 20
+    for tsi in range(20):
+        i = tsi + 20 if tsi < 2 else tsi
+        d = r["q"][i + 1] - r["q"][i - 1]
+        d = np.where(d > np.pi, d - 2 * np.pi, np.where(d < -np.pi, d + 2 * np.pi, d))
+        assert wrapdiff(rec[tsi, :cfg], r["q"][i]).max() < 1e-12
+        assert np.abs(rec[tsi, cfg:2 * cfg] - d / (2 * dt)).max() < 1e-9
+        assert np.abs(rec[tsi, 2 * cfg:] - r["tau"][i - 2]).max() < TAU_TOL * max(1, np.abs(r["tau"]).max())
+    path = str(tmp_path / "traj.txt")
+    out = gpu.ModelPlayer(m).record_per_traj(p, 20, path)
+    rows = open(path).read().splitlines()
+    assert len(rows) == 20 and len(rows[0].split()) == 2 * cfg + nmj
+    np.testing.assert_allclose(np.loadtxt(path), out, rtol=1e-5, atol=1e-5)  # 6 significant digits
+
+
 def test_forces_round_trip(gpu, hmodels):
     """modelplayer::test_dynamics (playerexperim.cpp:95-121) on the GPU at configs[1] size:
     forces recovered from the kernel's own torques equal its contact forces where >= 3 feet
