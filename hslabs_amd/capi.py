@@ -26,7 +26,7 @@ HS_FLAG_GENERAL = 64
 EXPORTS = [
     "hs_model_load", "hs_model_load_ex", "hs_model_free", "hs_model_get_dims", "hs_pgs_config_read",
     "hs_run", "hs_run_steps", "hs_run_pd", "hs_run_forces", "hs_mixed_create", "hs_mixed_free",
-    "hs_mixed_get_dims", "hs_complete_traj", "hs_traj_save",
+    "hs_mixed_get_dims", "hs_complete_traj", "hs_traj_save", "hs_run_forces_host",
     "hs_run_mixed", "hs_run_mixed_steps", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
 ]
 
@@ -111,6 +111,9 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_run.argtypes = [vp, ctypes.POINTER(RunArgsC)]
     L.hs_run_steps.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32, ctypes.POINTER(vp)]
     L.hs_run_forces.argtypes = [vp, ctypes.POINTER(RunArgsC), vp]
+    L.hs_run_forces_host.argtypes = [vp, ctypes.POINTER(GaitParamsC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                     ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
     L.hs_run_pd.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.POINTER(PdArgsC)]
     L.hs_complete_traj.argtypes = [vp, ctypes.POINTER(GaitParamsC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                    ctypes.POINTER(ctypes.c_double)]

@@ -377,6 +377,49 @@ int hs_complete_traj(hs_model_t m, const hs_gait_params* params, int32_t B, int3
   return rc;
 }
 
+int hs_run_forces_host(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n_t, int32_t k0, int32_t H,
+                       int32_t ignore_reach, const double* tau_in, double* cf, uint32_t* flags) {
+  if (!m || (B > 0 && (!params || !tau_in))) return fail(HS_E_ARG, "null argument");
+  if (B <= 0 || H <= 0) return fail(HS_E_ARG, "empty batch");
+  const hs_topo& t = m->host;
+  const size_t rows = (size_t)B * H, nmj = (size_t)t.nmj, ncf = 3 * (size_t)t.nf;
+  hs_gait_params* dp = nullptr;
+  double *dtau = nullptr, *dcf = nullptr;
+  uint32_t* dfl = nullptr;
+  hipError_t e = hipMalloc(&dp, (size_t)B * sizeof(hs_gait_params));
+  if (e == hipSuccess) e = hipMalloc(&dtau, rows * nmj * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&dcf, rows * ncf * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&dfl, rows * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemcpy(dp, params, (size_t)B * sizeof(hs_gait_params), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dtau, tau_in, rows * nmj * sizeof(double), hipMemcpyHostToDevice);
+  int rc = HS_OK;
+  if (e != hipSuccess) {
+    rc = hip_fail(e, "alloc/copy");
+  } else {
+    hs_run_args a;
+    memset(&a, 0, sizeof(a));
+    a.n_rollouts = B;
+    a.horizon = H;
+    a.k0 = k0;
+    a.n_t = n_t;
+    a.ignore_reach = ignore_reach;
+    a.params = dp;
+    a.cf = dcf;
+    a.flags = dfl;
+    rc = hs_run_forces(m, &a, dtau);
+    if (rc == HS_OK) e = hipDeviceSynchronize();
+    if (rc == HS_OK && e == hipSuccess && cf) e = hipMemcpy(cf, dcf, rows * ncf * sizeof(double), hipMemcpyDeviceToHost);
+    if (rc == HS_OK && e == hipSuccess && flags)
+      e = hipMemcpy(flags, dfl, rows * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (rc == HS_OK && e != hipSuccess) rc = hip_fail(e, "run/copy back");
+  }
+  (void)hipFree(dp);
+  (void)hipFree(dtau);
+  (void)hipFree(dcf);
+  (void)hipFree(dfl);
+  return rc;
+}
+
 int hs_traj_save(const char* path, const double* rec, int32_t n_rows, int32_t rec_len, int32_t append) {
   if (!path || (n_rows > 0 && !rec) || n_rows < 0 || rec_len < 0) return fail(HS_E_ARG, "bad argument");
   std::ofstream file(path, append ? std::ios_base::app : std::ios_base::out);

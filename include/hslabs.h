@@ -163,6 +163,9 @@ int hs_run_pd(hs_model_t model, const hs_run_args* args, const hs_pd_args* pd);
  * Tikhonov-regularized solution is returned). tau, x, work_cot and best_key are
  * not written. */
 int hs_run_forces(hs_model_t model, const hs_run_args* args, const double* tau_in);
+/* Host-buffer, synchronous form: tau_in [B][H][nmj] -> cf [B][H][3*nfeet], flags [B][H] (may be NULL). */
+int hs_run_forces_host(hs_model_t model, const hs_gait_params* params, int32_t n_rollouts, int32_t n_t, int32_t k0,
+                       int32_t horizon, int32_t ignore_reach, const double* tau_in, double* cf, uint32_t* flags);
 
 /* Mixed-topology batches (BASELINE configs[4], e.g. myant + hexapod interleaved):
  * rollout b runs models[model_index[b]]. The reference runs one kinematicmodel

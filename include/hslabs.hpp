@@ -8,8 +8,12 @@
 //   periodic::record_trajectory / compute_dynrecs / compute_dynrec_ders /
 //            switch_torso_penalty / compute_torques_over_period /
 //            get_computed_torques / work_over_period / get_total_mass /
-//            get_contforce_stat / get_motor_torques                        (periodic.h:27-87)
-//   modelplayer::make_pergensu / measure_cot / measure_cot_sweep           (player.cpp:147-321)
+//            get_contforce_stat / get_motor_torques /
+//            solve_contforces_given_torques / get_complete_traj /
+//            get_motor_adas                                                (periodic.h:27-87)
+//   modelplayer::make_pergensu / measure_cot / measure_cot_sweep /
+//            record_per_traj / test_dynamics                               (player.cpp:147-321,
+//                                                                           617-629; playerexperim.cpp:95-121)
 //   new_2d_array / delete_2d_array / save_2d_array                         (core.h:11-14)
 //
 // Differences from the reference: errors throw hslabs::error instead of
@@ -144,11 +148,12 @@ class periodic {
   bool force_pen_ = true, torque_pen_ = true;
   std::vector<double> tau_, cf_, x_, wc_;
   std::vector<uint32_t> flags_;
+  std::vector<double> rec_;  // get_complete_traj records
   double min_cfz_ = 1e10, max_mu_ = -1e10;
 
  public:
   explicit periodic(const kinematicmodel* model) : model_(model) {}
-  void record_trajectory(const pergensetup* pgs, int n_t) { pgs_ = pgs; n_t_ = n_t; tau_.clear(); }
+  void record_trajectory(const pergensetup* pgs, int n_t) { pgs_ = pgs; n_t_ = n_t; tau_.clear(); rec_.clear(); }
   void compute_dynrecs() {}
   void compute_dynrec_ders() {}
   void switch_torso_penalty(bool force, bool torque) {
@@ -194,6 +199,36 @@ class periodic {
   }
   uint32_t get_flags(int i) const { return flags_[((i - 2) % n_t_ + n_t_) % n_t_]; }
   void get_contforce_stat(double* stat) const { stat[0] = min_cfz_; stat[1] = max_mu_; }
+  // periodic.cpp:368-374 (forcetorquesolver::solve_forces): forces of all feet for step i
+  void solve_contforces_given_torques(int i, double* contforces, const double* torques) const {
+    if (!pgs_) throw error(HS_E_ARG, "record_trajectory first");
+    hs_gait_params g = pgs_->params().to_c();
+    int k0 = ((i - 2) % n_t_ + n_t_) % n_t_;
+    check(hs_run_forces_host(model_->handle(), &g, 1, n_t_, k0, 1, 1, torques, contforces, nullptr),
+          "solve_contforces_given_torques");
+  }
+  // periodic.cpp:406-426: n_t records of (q, dq, torques) = 2 config_dim + nmj
+  void get_complete_traj(double** complete_traj) {
+    if (!pgs_) throw error(HS_E_ARG, "record_trajectory first");
+    const int len = 2 * model_->get_config_dim() + model_->number_of_motor_joints();
+    if (rec_.empty()) {
+      hs_gait_params g = pgs_->params().to_c();
+      rec_.assign((size_t)n_t_ * len, 0);
+      check(hs_complete_traj(model_->handle(), &g, 1, n_t_, 1, rec_.data()), "get_complete_traj");
+    }
+    for (int i = 0; i < n_t_; i++) std::copy(&rec_[(size_t)i * len], &rec_[(size_t)i * len] + len, complete_traj[i]);
+  }
+  // periodic.cpp:394-404: motor angles and rates of trajectory sample tsi
+  void get_motor_adas(int tsi, double* as, double* das) {
+    const int cfg = model_->get_config_dim(), len = 2 * cfg + model_->number_of_motor_joints();
+    std::vector<double*> rows((size_t)n_t_);
+    std::vector<double> buf((size_t)n_t_ * len);
+    for (int i = 0; i < n_t_; i++) rows[i] = &buf[(size_t)i * len];
+    get_complete_traj(rows.data());
+    const double* r = rows[((tsi % n_t_) + n_t_) % n_t_];  // records are indexed by tsi mod n_t
+    std::copy(r + 6, r + cfg, as);
+    std::copy(r + cfg + 6, r + 2 * cfg, das);
+  }
   // periodic.cpp:285-307
   double work_over_period() {
     if (tau_.empty()) compute_torques_over_period();
@@ -269,6 +304,34 @@ class modelplayer {
       if (print) std::cout << "val = " << vals[i] << " COT = " << wc[2 * i + 1] << std::endl;
     }
     return out;
+  }
+  // player.cpp:617-629: one cycle's complete trajectory records to traj.txt
+  void record_per_traj(const pergensetup* pgs, int n_t, const std::string& fname = "traj.txt") {
+    const int len = 2 * model_.get_config_dim() + model_.number_of_motor_joints();
+    double** traj = new_2d_array(n_t, len);
+    periodic per(&model_);
+    per.record_trajectory(pgs, n_t);
+    per.get_complete_traj(traj);
+    save_2d_array(traj, n_t, len, fname, false);
+    delete_2d_array(traj, n_t);
+  }
+  // playerexperim.cpp:95-121: contact forces recovered from the computed torques; returns the
+  // distance s the reference prints
+  double test_dynamics(const pergensetup* pgs, int n_t = 20, int tsi = 2) {
+    periodic per(&model_);
+    per.record_trajectory(pgs, n_t);
+    per.compute_torques_over_period();
+    const int nf = per.get_nfeet();
+    std::vector<double> cf1(3 * nf);
+    per.solve_contforces_given_torques(tsi, cf1.data(), per.get_computed_torques(tsi));
+    const double* cf = per.get_contact_forces(tsi);
+    double s = 0;
+    for (int i = 0; i < 3 * nf; i++) {
+      double d = cf[i] - cf1[i];
+      s += d * d;
+    }
+    std::cout << "s = " << std::sqrt(s) << std::endl;
+    return std::sqrt(s);
   }
 };
 

@@ -26,6 +26,12 @@ int main(int argc, char** argv) {
   std::printf("work = %.12f\n", work);
   const double* tau = per.get_computed_torques(2);
   std::printf("tau[2][0] = %.12f\n", tau[0]);
+  double as[18], das[18];
+  per.get_motor_adas(2, as, das);
+  std::printf("adas[2][0] = %.12f %.12f\n", as[0], das[0]);
+  double s = player0.test_dynamics(pgs);                      // playerexperim.cpp:95-121
+  player0.record_per_traj(pgs, 20, argc > 2 ? argv[2] : "traj.txt");  // player.cpp:617-629
+  if (!(s < 1e-9)) return 3;
   try {
     player0.measure_cot_sweep(pgs, 20, "curvature", 0, 1, 2, false);
     return 2;

@@ -33,7 +33,13 @@ def test_shim_compiles_and_links(product, tmp_path):
 @pytest.mark.gpu
 def test_shim_runs_reference_shaped_main(product, tmp_path):
     exe = compile_prog(product, tmp_path / "cot_sweep")
-    out = subprocess.run([str(exe), MODELS], check=True, capture_output=True, text=True, timeout=300).stdout
+    traj = tmp_path / "traj.txt"
+    out = subprocess.run([str(exe), MODELS, str(traj)], check=True, capture_output=True, text=True,
+                         timeout=300).stdout
+    s = float([ln for ln in out.splitlines() if ln.startswith("s = ")][0].split("=")[1])
+    assert s < 1e-9  # test_dynamics: forces from the computed torques == computed forces
+    rec = np.loadtxt(traj)
+    assert rec.shape == (20, 2 * 24 + 18)
     lines = out.splitlines()
     cot = float(lines[0].split("=")[1])
     p = product.read_pgs_config(PGS_CONFIG, 8)
