@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--model", default="hexapod", choices=["hexapod", "spider", "myant"])
     ap.add_argument("--n_t", type=int, default=20)
     ap.add_argument("--curved", action="store_true")
+    ap.add_argument("--fp32", action="store_true",
+                    help="single-precision kernels (HS_PREC_F32), e.g. BASELINE configs[2]: --model spider "
+                         "--rollouts 16384 --horizon 32 --fp32")
     ap.add_argument("--mixed", action="store_true",
                     help="BASELINE configs[4]: myant.xml + hexapod.xml 50/50, interleaved, one launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -115,25 +118,35 @@ def main():
     B, Hh, n_t = args.rollouts, args.horizon, args.n_t
     id0 = rank * B
     outs = ("tau", "cf", "work_cot", "flags")
+    dtype = torch.float32 if args.fp32 else torch.float64
+    prec = "fp32" if args.fp32 else "fp64"
+    width = 0.5 if args.fp32 else 1.0  # fp32 halves the output and parameter bytes
     if args.mixed:
         model_names = list(synth.MIXED_MODELS)
         models = [H.KinematicModel(os.path.join(ROOT, "models", f"{n}.xml")) for n in model_names]
         params, midx = synth.gen_mixed(B, id0=id0, curved=args.curved)
         batch = H.MixedBatch(models, midx, params, n_t=n_t, k0=0, horizon=Hh, outputs=outs, device=dev,
-                             rollout_id_base=id0)
+                             rollout_id_base=id0, dtype=dtype)
         out_bytes = float(np.mean([OUT_BYTES_PER_STEP[model_names[k]] for k in midx]))
-        workload = f"myant.xml+hexapod.xml 50/50 interleaved B={B}/GPU H={Hh} n_t={n_t} fp64 (BASELINE configs[4])"
-        traffic_key = f"mixed B={B} H={Hh}"
+        workload = (f"myant.xml+hexapod.xml 50/50 interleaved B={B}/GPU H={Hh} n_t={n_t} {prec} "
+                    f"(BASELINE configs[4])")
+        traffic_key = f"mixed B={B} H={Hh} {prec}"
     else:
         model_names = [args.model]
         model = H.KinematicModel(os.path.join(ROOT, "models", f"{args.model}.xml"))
         params = synth.gen_params(B, args.model, id0=id0, curved=args.curved)
         batch = H.DeviceBatch(model, params, n_t=n_t, k0=0, horizon=Hh, outputs=outs, device=dev,
-                              rollout_id_base=id0)
+                              rollout_id_base=id0, dtype=dtype)
         out_bytes = OUT_BYTES_PER_STEP[args.model]
-        cfg = "configs[1]" if args.model == "hexapod" and Hh == 1 else "custom"
-        workload = f"{args.model}.xml B={B}/GPU H={Hh} n_t={n_t} fp64 (BASELINE {cfg})"
-        traffic_key = f"{args.model} B={B} H={Hh}"
+        if args.model == "hexapod" and Hh == 1 and not args.fp32:
+            cfg = "configs[1]"
+        elif args.model == "spider" and Hh == 32 and args.fp32:
+            cfg = "configs[2]"
+        else:
+            cfg = "custom"
+        workload = f"{args.model}.xml B={B}/GPU H={Hh} n_t={n_t} {prec} (BASELINE {cfg})"
+        traffic_key = f"{args.model} B={B} H={Hh}" + (" fp32" if args.fp32 else "")
+    out_bytes *= width
     stream = torch.cuda.current_stream(dev)
 
     # warmup (untimed): the same native launch loop as the timed region
@@ -180,7 +193,7 @@ def main():
         steps_total = B * Hh * args.steps * world
         value = steps_total / elapsed
         ms_per_step = 1e3 * elapsed / args.steps
-        alg_bytes = B * Hh * (out_bytes + PARAM_BYTES / Hh)
+        alg_bytes = B * Hh * (out_bytes + width * PARAM_BYTES / Hh)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
         tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -194,7 +207,8 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32" if args.fp32 else "f64",
             "data": "synthetic (splitmix64 gait parameters around pgs id 8; SURVEY.md 8d)",
             "config": {"workload": workload,
                        "rollouts_per_gpu": B, "horizon": Hh, "n_t": n_t,

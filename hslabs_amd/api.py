@@ -157,14 +157,16 @@ class DeviceBatch:
 
     def __init__(self, model: KinematicModel, params, n_t: int = 20, k0: int = 0, horizon: int = 1,
                  ignore_reach: bool = True, outputs=("tau", "cf", "work_cot", "flags"), device=None,
-                 rollout_id_base: int = 0):
+                 rollout_id_base: int = 0, dtype=None):
         import torch
 
         self.torch = torch
         self.model = model
-        self._alloc(model, params, n_t, k0, horizon, ignore_reach, outputs, device, rollout_id_base)
+        self._alloc(model, params, n_t, k0, horizon, ignore_reach, outputs, device, rollout_id_base, dtype)
 
-    def _alloc(self, dims, params, n_t, k0, horizon, ignore_reach, outputs, device, rollout_id_base):
+    def _alloc(self, dims, params, n_t, k0, horizon, ignore_reach, outputs, device, rollout_id_base, dtype=None):
+        """dtype: torch.float64 (default) or torch.float32 (HS_PREC_F32: single-precision
+        arithmetic and outputs, BASELINE configs[2])."""
         torch = self.torch
         arr = params_array(params)
         self.B, self.H, self.n_t, self.k0 = len(arr), horizon, n_t, k0
@@ -172,8 +174,11 @@ class DeviceBatch:
         self.rollout_id_base = rollout_id_base
         dev = device or torch.device("cuda", torch.cuda.current_device())
         self.device = dev
+        self.dtype = dtype or torch.float64
+        assert self.dtype in (torch.float64, torch.float32)
+        self.precision = capi.HS_PREC_F32 if self.dtype == torch.float32 else capi.HS_PREC_F64
         self.params = torch.from_numpy(arr.view(np.uint8).copy()).to(dev)
-        f64 = dict(dtype=torch.float64, device=dev)
+        f64 = dict(dtype=self.dtype, device=dev)
         B, H = self.B, self.H
         self.q = torch.empty((B, H, dims.config_dim), **f64) if "q" in outputs else None
         self.dq = torch.empty((B, H, dims.config_dim), **f64) if "dq" in outputs else None
@@ -202,6 +207,7 @@ class DeviceBatch:
         a.flags, a.work_cot, a.dq = ptr(self.flags), ptr(self.work_cot), ptr(self.dq)
         a.best_key = ptr(self.best_key) if best else None
         a.rollout_id_base = self.rollout_id_base
+        a.precision = self.precision
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         a.stream = st.cuda_stream
         return a
@@ -218,7 +224,7 @@ class DeviceBatch:
         trajectory; also runs the step (tau = feedforward). Returns tau_cmd, or
         (tau_cmd, q_target, dq_target) with ``targets``."""
         torch = self.torch
-        f64 = dict(dtype=torch.float64, device=self.device)
+        f64 = dict(dtype=self.dtype, device=self.device)
         q = q_meas.to(**f64).contiguous()
         dq = dq_meas.to(**f64).contiguous()
         shape = (self.B, self.H, self.model.nmj)
@@ -237,7 +243,7 @@ class DeviceBatch:
         """Contact forces of all feet given motor torques (hs_run_forces,
         forcetorquesolver::solve_forces): tau_in is a device tensor [B][H][nmj]; writes
         self.cf (and q / flags if allocated)."""
-        t = tau_in.to(dtype=self.torch.float64, device=self.device).contiguous()
+        t = tau_in.to(dtype=self.dtype, device=self.device).contiguous()
         assert t.shape == (self.B, self.H, self.model.nmj)
         a = self._args(stream, False, False)
         a.tau = a.x = a.work_cot = None
@@ -268,7 +274,7 @@ class MixedBatch(DeviceBatch):
 
     def __init__(self, models, model_index, params, n_t: int = 20, k0: int = 0, horizon: int = 1,
                  ignore_reach: bool = True, outputs=("tau", "cf", "work_cot", "flags"), device=None,
-                 rollout_id_base: int = 0):
+                 rollout_id_base: int = 0, dtype=None):
         import torch
 
         self.torch = torch
@@ -288,7 +294,7 @@ class MixedBatch(DeviceBatch):
         self.dims = d
         self.model = self.models[0]
         assert len(params_array(params)) == len(self.model_index)
-        self._alloc(d, params, n_t, k0, horizon, ignore_reach, outputs, device, rollout_id_base)
+        self._alloc(d, params, n_t, k0, horizon, ignore_reach, outputs, device, rollout_id_base, dtype)
 
     def _launch(self, a, n_calls, ev):
         capi.check(capi.load().hs_run_mixed_steps(self.plan, ctypes.byref(a), n_calls, ev), "hs_run_mixed_steps")

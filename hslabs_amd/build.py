@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT_DIR, "libhslabs.so")
-SOURCES = ["hs_kernels.hip", "hs_capi.cpp", "hs_model.cpp"]
+SOURCES = ["hs_kernels.hip", "hs_kernels_f32.hip", "hs_capi.cpp", "hs_model.cpp"]
 HEADERS = ["hs_topo.h", "hs_math.h", "hs_internal.h", os.path.join("..", "..", "include", "hslabs.h")]
 ARCH = os.environ.get("HSLABS_ARCH", "gfx950")
 

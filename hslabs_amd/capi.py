@@ -11,7 +11,7 @@ import os
 
 from . import build as _build
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 HS_OK = 0
 HS_FLAG_RANK_RETRY = 1
@@ -21,6 +21,8 @@ HS_FLAG_NAN = 8
 HS_FLAG_UNREACH = 16
 HS_FLAG_NO_CONTACT = 32
 HS_FLAG_GENERAL = 64
+HS_PREC_F64 = 0
+HS_PREC_F32 = 1
 
 # every symbol declared in include/hslabs.h
 EXPORTS = [
@@ -74,6 +76,7 @@ class RunArgsC(ctypes.Structure):
         ("cf", ctypes.c_void_p), ("x", ctypes.c_void_p), ("flags", ctypes.c_void_p),
         ("work_cot", ctypes.c_void_p), ("best_key", ctypes.c_void_p),
         ("rollout_id_base", ctypes.c_int64), ("stream", ctypes.c_void_p), ("dq", ctypes.c_void_p),
+        ("precision", ctypes.c_int32),
     ]
 
 
@@ -93,7 +96,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    path = os.environ.get("HSLABS_LIB", _build.LIB)  # tuning-variant override (build.build_variant)
+    path = os.environ.get("HSLABS_LIB") or _build.LIB  # tuning-variant override (build.build_variant)
     if not os.path.exists(path):
         if not build_if_missing:
             raise HSError(f"libhslabs.so not built ({path}); run `python -m hslabs_amd.build`")

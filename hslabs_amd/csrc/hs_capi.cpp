@@ -46,7 +46,7 @@ int device_state(hs_model_t m, int n_rollouts, const hs_topo** topo, void** ws) 
   }
   if (m->ws_rollouts[dev] < (size_t)n_rollouts) {
     void* w = nullptr;
-    e = hipMalloc(&w, (size_t)n_rollouts * hs::general_workspace_bytes());
+    e = hipMalloc(&w, (size_t)n_rollouts * hs::general_workspace_bytes());  // fp64 slot >= fp32 slot
     if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
     if (m->ws[dev]) m->retired.emplace_back(dev, m->ws[dev]);
     m->ws[dev] = w;
@@ -67,7 +67,7 @@ int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::lau
     hipError_t e = hipSuccess;
     if (kernel_events) e = hipEventRecord((hipEvent_t)kernel_events[2 * i], st);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
-    int le = hs::launch_rollouts(d, c, ws, mp);
+    int le = (a.precision == HS_PREC_F32) ? hs::launch_rollouts_f32(d, c, ws, mp) : hs::launch_rollouts(d, c, ws, mp);
     if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
     if (kernel_events) e = hipEventRecord((hipEvent_t)kernel_events[2 * i + 1], st);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
@@ -88,6 +88,7 @@ int check_args(const hs_model_s* m, const hs_run_args* a) {
   if (a->n_rollouts < 0) return fail(HS_E_ARG, "n_rollouts < 0");
   if (a->horizon < 1) return fail(HS_E_ARG, "horizon must be >= 1");
   if (a->k0 < 0) return fail(HS_E_ARG, "k0 must be >= 0");
+  if (a->precision != HS_PREC_F64 && a->precision != HS_PREC_F32) return fail(HS_E_ARG, "unknown precision");
   if (a->n_t < 1) return fail(HS_E_ARG, "n_t must be >= 1");
   if (a->n_rollouts > 0 && !a->params) return fail(HS_E_ARG, "params is null");
   if (a->n_rollouts > (1 << 30)) return fail(HS_E_ARG, "too many rollouts");
@@ -95,6 +96,21 @@ int check_args(const hs_model_s* m, const hs_run_args* a) {
 }
 
 }  // namespace
+
+namespace hs {
+
+launch_map single_model_map(const hs_topo& t, int32_t n_rollouts) {
+  launch_map mp{};
+  mp.n_waves = (n_rollouts + 1) / 2;  // two rollouts per wavefront
+  mp.max_parts = t.n;
+  mp.st_tau = t.nmj;
+  mp.st_cf = 3 * t.nf;
+  mp.st_q = t.cfg;
+  mp.st_x = 6 * t.n;
+  return mp;
+}
+
+}  // namespace hs
 
 struct hs_mixed_s {
   int dev = 0;

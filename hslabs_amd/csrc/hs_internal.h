@@ -34,6 +34,9 @@ struct launch_map {
 // extra slot serves idle half-waves). Returns a hipError_t value.
 size_t general_workspace_bytes();
 int launch_rollouts(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
+// single precision build of the same kernels (hs_kernels_f32.hip): outputs are float
+size_t general_workspace_bytes_f32();
+int launch_rollouts_f32(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
 launch_map single_model_map(const hs_topo& t, int32_t n_rollouts);
 
 }  // namespace hs

@@ -4,26 +4,38 @@
 // from an explicit 0 and adds the translation last, which is the rounding of
 // the reference's 4x4 affine::mult (matrix.cpp:78-97) with its exact (0,0,0,1)
 // bottom row. The file is compiled with -ffp-contract=off so a*b+c is never
-// fused: device results round like the reference's x86-64 -O2 build.
+// fused: device results round like the reference's x86-64 -O2 build. `real`
+// is double, or float for the fp32 build (hs_kernels_f32.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include "hs_topo.h"
 
-namespace hsd {
+#ifndef HS_REAL
+#define HS_REAL double
+#endif
 
-constexpr double kPi = 3.14159265358979323846;  // M_PI
+namespace hsd {
+// one instantiation per precision (hs_kernels.hip: double, hs_kernels_f32.hip: float)
+#if HS_REAL_IS_FLOAT
+inline namespace f32 {
+#else
+inline namespace f64 {
+#endif
+
+using real = HS_REAL;
+constexpr real kPi = (real)3.14159265358979323846;  // M_PI
 
 struct A34 {
-  double m[12];
-  __device__ double operator()(int r, int c) const { return m[c * 3 + r]; }
-  __device__ double& at(int r, int c) { return m[c * 3 + r]; }
+  real m[12];
+  __device__ real operator()(int r, int c) const { return m[c * 3 + r]; }
+  __device__ real& at(int r, int c) { return m[c * 3 + r]; }
 };
 
 __device__ inline A34 load34(const hs_aff34& s) {
   A34 a;
 #pragma unroll
-  for (int i = 0; i < 12; i++) a.m[i] = s.m[i];
+  for (int i = 0; i < 12; i++) a.m[i] = (real)s.m[i];
   return a;
 }
 
@@ -34,7 +46,7 @@ __device__ inline A34 mul(const A34& A, const A34& B) {
   for (int c = 0; c < 4; c++)
 #pragma unroll
     for (int r = 0; r < 3; r++) {
-      double s = 0.0;
+      real s = real(0);
       s = s + A(r, 0) * B(0, c);
       s = s + A(r, 1) * B(1, c);
       s = s + A(r, 2) * B(2, c);
@@ -45,10 +57,10 @@ __device__ inline A34 mul(const A34& A, const A34& B) {
 }
 
 // u = A * (v, 1) (matrix.cpp:149-164)
-__device__ inline void mulp(const A34& A, const double* v, double* u) {
+__device__ inline void mulp(const A34& A, const real* v, real* u) {
 #pragma unroll
   for (int r = 0; r < 3; r++) {
-    double s = 0.0;
+    real s = real(0);
     s = s + A(r, 0) * v[0];
     s = s + A(r, 1) * v[1];
     s = s + A(r, 2) * v[2];
@@ -60,26 +72,26 @@ __device__ inline void mulp(const A34& A, const double* v, double* u) {
 // affine::invert_rigidbody (matrix.cpp:182-193)
 __device__ inline A34 invert(const A34& A) {
   A34 I;
-  double t[3] = {-A(0, 3), -A(1, 3), -A(2, 3)};
+  real t[3] = {-A(0, 3), -A(1, 3), -A(2, 3)};
 #pragma unroll
   for (int r = 0; r < 3; r++)
 #pragma unroll
     for (int c = 0; c < 3; c++) I.at(r, c) = A(c, r);
 #pragma unroll
   for (int r = 0; r < 3; r++) {
-    double s = 0.0;
+    real s = real(0);
     s = s + I(r, 0) * t[0];
     s = s + I(r, 1) * t[1];
     s = s + I(r, 2) * t[2];
-    I.at(r, 3) = 0.0 + s;
+    I.at(r, 3) = real(0) + s;
   }
   return I;
 }
 
 // ODE dRFromEulerAngles transposed into affine layout (model.cpp:45, visualization.cpp:62-69)
-__device__ inline A34 from_euler(const double* pos, double phi, double theta, double psi) {
-  double sphi = sin(phi), cphi = cos(phi), sth = sin(theta), cth = cos(theta);
-  double spsi = sin(psi), cpsi = cos(psi);
+__device__ inline A34 from_euler(const real* pos, real phi, real theta, real psi) {
+  real sphi = sin(phi), cphi = cos(phi), sth = sin(theta), cth = cos(theta);
+  real spsi = sin(psi), cpsi = cos(psi);
   A34 A;
   // column c of the affine = row c of the ODE matrix
   A.at(0, 0) = cpsi * cth;
@@ -98,20 +110,20 @@ __device__ inline A34 from_euler(const double* pos, double phi, double theta, do
 }
 
 // free joint transformation: set_rotation then translate (model.cpp:37-49)
-__device__ inline A34 free_joint(const double* q6) {
+__device__ inline A34 free_joint(const real* q6) {
   A34 A = from_euler(q6, q6[3], q6[4], q6[5]);
 #pragma unroll
-  for (int r = 0; r < 3; r++) A.at(r, 3) = 0.0 + q6[r];
+  for (int r = 0; r < 3; r++) A.at(r, 3) = real(0) + q6[r];
   return A;
 }
 
 // hinge transformation Rz(q) (model.cpp:50-57)
-__device__ inline A34 hinge_joint(double q) {
-  double c = cos(q), s = sin(q);
+__device__ inline A34 hinge_joint(real q) {
+  real c = cos(q), s = sin(q);
   A34 A;
 #pragma unroll
-  for (int i = 0; i < 12; i++) A.m[i] = 0.0;
-  A.at(2, 2) = 1.0;
+  for (int i = 0; i < 12; i++) A.m[i] = real(0);
+  A.at(2, 2) = real(1);
   A.at(0, 0) = c;
   A.at(0, 1) = -1 * s;
   A.at(1, 1) = c;
@@ -120,17 +132,17 @@ __device__ inline A34 hinge_joint(double q) {
 }
 
 // euler_angles_from_affine (visualization.cpp:81-101)
-__device__ inline void euler_from(const A34& A, double* ang) {
-  double r11 = A(0, 0), r21 = A(1, 0), r31 = A(2, 0), r32 = A(2, 1), r33 = A(2, 2);
-  double th1 = -asin(r31);
-  double ct1 = cos(th1);
+__device__ inline void euler_from(const A34& A, real* ang) {
+  real r11 = A(0, 0), r21 = A(1, 0), r31 = A(2, 0), r32 = A(2, 1), r33 = A(2, 2);
+  real th1 = -asin(r31);
+  real ct1 = cos(th1);
   ang[0] = atan2(r32 / ct1, r33 / ct1);
   ang[1] = th1;
   ang[2] = atan2(r21 / ct1, r11 / ct1);
 }
 
 // mod_twopi (visualization.cpp:73-79); bounded loops
-__device__ inline void mod_twopi(double& a) {
+__device__ inline void mod_twopi(real& a) {
   if (a < -kPi) {
     for (int i = 0; i < 64 && a < -kPi; i++) a += 2 * kPi;
   } else if (a > kPi) {
@@ -138,8 +150,8 @@ __device__ inline void mod_twopi(double& a) {
   }
 }
 
-__device__ inline double norm3(const double* v) {
-  double s = 0.0;
+__device__ inline real norm3(const real* v) {
+  real s = real(0);
   s = s + v[0] * v[0];
   s = s + v[1] * v[1];
   s = s + v[2] * v[2];
@@ -147,24 +159,24 @@ __device__ inline double norm3(const double* v) {
 }
 
 // limb_solver_yxx (lik.cpp:151-184) and limb_solver_zxx (lik.cpp:189-223), bend = true
-__device__ inline void limb_ik(int kind, const double* ls, int ysign, const double* p, double* ja, bool ignore_reach,
+__device__ inline void limb_ik(int kind, const real* ls, int ysign, const real* p, real* ja, bool ignore_reach,
                                bool& unreach, bool& fail) {
-  double l0 = ls[0], l1 = ls[1], l2 = ls[2];
+  real l0 = ls[0], l1 = ls[1], l2 = ls[2];
   int s0 = ysign;
   int s1 = 1;
-  double d[3];
+  real d[3];
   if (kind == HS_LIK_YXX) {
-    double z0 = s0 * l0;
-    d[0] = p[0] - 0.0; d[1] = p[1] - 0.0; d[2] = p[2] - z0;
+    real z0 = s0 * l0;
+    d[0] = p[0] - real(0); d[1] = p[1] - real(0); d[2] = p[2] - z0;
   } else {
-    d[0] = p[0] + 0.0; d[1] = p[1] + 0.0; d[2] = p[2] + l0;
+    d[0] = p[0] + real(0); d[1] = p[1] + real(0); d[2] = p[2] + l0;
   }
-  double l = norm3(d);
+  real l = norm3(d);
   if (l1 + l2 - l < 0) {
     if (ignore_reach) { l = l1 + l2; unreach = true; }
     else { fail = true; }
   }
-  double c, theta, phi = atan2(p[0], p[1]);
+  real c, theta, phi = atan2(p[0], p[1]);
   if (kind == HS_LIK_YXX) {
     c = (p[2] - s0 * l0) / l;
     theta = acos(c) + (1 - s0) * kPi / 2;
@@ -174,9 +186,9 @@ __device__ inline void limb_ik(int kind, const double* ls, int ysign, const doub
   }
   mod_twopi(phi);
   mod_twopi(theta);
-  double ll = l * l;
-  double del = l2 * l2 - l1 * l1;
-  double beta, gamma;
+  real ll = l * l;
+  real del = l2 * l2 - l1 * l1;
+  real beta, gamma;
   if (kind == HS_LIK_YXX) {
     beta = s1 * s0 * acos((ll - del) / (2 * l1 * l));
     gamma = s1 * s0 * acos((ll + del) / (2 * l2 * l));
@@ -189,4 +201,5 @@ __device__ inline void limb_ik(int kind, const double* ls, int ysign, const doub
   ja[2] = -(beta + gamma);
 }
 
+}  // inline namespace
 }  // namespace hsd

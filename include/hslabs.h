@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 2
+#define HSLABS_ABI_VERSION 3
 
 enum {
   HS_OK = 0,
@@ -120,7 +120,14 @@ typedef struct {
   void* stream;           /* hipStream_t */
   double* dq;             /* [B][H][config_dim]: rates at each solved sample (compute_vel_traj,
                              periodic.cpp:261-282: wrapped central difference / 2 dt) */
+  int32_t precision;      /* HS_PREC_F64 (0) or HS_PREC_F32 (1, BASELINE configs[2]): with F32 the
+                             arithmetic is single precision and every floating-point array of the
+                             call (q, dq, tau, cf, x, work_cot; hs_pd_args; hs_run_forces' tau_in)
+                             holds float (the pointer types stay double*). params stay double. */
 } hs_run_args;
+
+#define HS_PREC_F64 0
+#define HS_PREC_F32 1
 
 int hs_run(hs_model_t model, const hs_run_args* args);
 

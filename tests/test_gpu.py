@@ -372,6 +372,69 @@ def test_complete_traj_matches_oracle(gpu, hmodels, oracle_mod, omodels, sid, tm
     np.testing.assert_allclose(np.loadtxt(path), out, rtol=1e-5, atol=1e-5)  # 6 significant digits
 
 
+FP32_TOL = 1e-3  # stated single-precision bound: |tau_f32 - tau_f64| <= 1e-3 max(1, |tau|) per step
+
+
+def contact_sets(cf, nf):
+    return np.abs(cf.reshape(*cf.shape[:-1], nf, 3)).max(axis=-1) > 0
+
+
+@pytest.mark.parametrize("name", ["hexapod", "spider", "myant"])
+def test_fp32_matches_fp64(gpu, hmodels, name):
+    """HS_PREC_F32 (BASELINE configs[2] precision) against the fp64 kernel (== oracle to 1e-12)
+    on synthetic straight and curved gaits: within FP32_TOL wherever both precisions chose the
+    same contact set; a contact decision (foot height within rounding of rcap + 1e-4) may flip
+    on a handful of steps."""
+    import torch
+
+    from hslabs_amd import synth
+
+    m = hmodels[name]
+    for curved in (False, True):
+        p = synth.gen_params(512, name, id0=2024, curved=curved)
+        out = {}
+        for dt in (torch.float64, torch.float32):
+            b = gpu.DeviceBatch(m, p, n_t=20, horizon=20, outputs=("tau", "cf", "flags", "work_cot"), dtype=dt)
+            b.run(best=False)
+            torch.cuda.synchronize()
+            assert b.tau.dtype == dt
+            out[dt] = (b.tau.double().cpu().numpy(), b.cf.double().cpu().numpy(), b.flags.cpu().numpy())
+        t64, c64, f64 = out[torch.float64]
+        t32, c32, f32 = out[torch.float32]
+        same = (contact_sets(c64, m.nfeet) == contact_sets(c32, m.nfeet)).all(axis=-1)
+        assert same.mean() > 0.995
+        err = np.abs(t32 - t64).max(axis=-1) / np.maximum(1, np.abs(t64).max(axis=-1))
+        assert err[same].max() < FP32_TOL
+        assert not (f32 & 8).any() and np.isfinite(t32).all()
+
+
+def test_fp32_configs2_size(gpu, hmodels):
+    """BASELINE configs[2]: spider, 16384 rollouts x horizon 32, fp32 -- finite, no NaN or
+    general-path steps, and the first rollouts agree with fp64 within FP32_TOL."""
+    import torch
+
+    from hslabs_amd import synth
+
+    m = hmodels["spider"]
+    p = synth.gen_params(16384, "spider")
+    b = gpu.DeviceBatch(m, p, n_t=20, horizon=32, outputs=("tau", "cf", "flags", "work_cot"),
+                        dtype=torch.float32)
+    b.work_cot.zero_()
+    b.run_steps(2, best=False, accumulate=True)  # 64 steps, k0 marching through the cycle
+    torch.cuda.synchronize()
+    flags = b.flags.cpu().numpy()
+    assert not (flags & (8 | 64)).any()
+    assert torch.isfinite(b.tau).all() and torch.isfinite(b.work_cot).all()
+    ref = gpu.DeviceBatch(m, p[:64], n_t=20, k0=12, horizon=32, outputs=("tau", "cf"))
+    ref.run(best=False)
+    torch.cuda.synchronize()
+    t64, c64 = ref.tau.cpu().numpy(), ref.cf.cpu().numpy()
+    t32, c32 = b.tau[:64].double().cpu().numpy(), b.cf[:64].double().cpu().numpy()  # 2nd call: k0 = 32 % 20
+    same = (contact_sets(c64, m.nfeet) == contact_sets(c32, m.nfeet)).all(axis=-1)
+    err = np.abs(t32 - t64).max(axis=-1) / np.maximum(1, np.abs(t64).max(axis=-1))
+    assert same.mean() > 0.99 and err[same].max() < FP32_TOL
+
+
 def test_forces_round_trip(gpu, hmodels):
     """modelplayer::test_dynamics (playerexperim.cpp:95-121) on the GPU at configs[1] size:
     forces recovered from the kernel's own torques equal its contact forces where >= 3 feet
