@@ -136,6 +136,7 @@ struct SetupL {
   real pos0[HS_LMAX][3];  // default foot positions, pergen order
   real ts[HS_LMAX], xs[HS_LMAX];
   real t_step, max_radius, v, dt;
+  SC3 tsc;  // sin / cos of the configured torso angles (every sample of a straight gait)
 };
 
 template <int NM>
@@ -252,7 +253,9 @@ __device__ void gait_setup(const hs_topo* T, const GaitR& g, int n_t, SetupL& st
     const int L = lane;
     real q6[6] = {g.torso_pos[0], g.torso_pos[1], g.torso_pos[2],
                     g.torso_angles[0], g.torso_angles[1], g.torso_angles[2]};
-    A34 A0 = mul(mul(node_joint_parent(T, 0), free_joint(q6)), node_pj(T, 0));  // orient_torso
+    const SC3 tsc = sincos3(q6[3], q6[4], q6[5]);
+    if (L == 0) st.tsc = tsc;
+    A34 A0 = mul(mul(node_joint_parent(T, 0), free_joint_sc(q6, tsc)), node_pj(T, 0));  // orient_torso
     A34 A = A0;
     for (int k = 1; k < T->limb_chain_len[L]; k++) A = mul(A, node_pj(T, T->limb_chain[L][k]));
     int c = T->limb_child[L];
@@ -315,8 +318,13 @@ __device__ void gait_setup(const hs_topo* T, const GaitR& g, int n_t, SetupL& st
 // ---------------------------------------------------------------------------
 // K: one (sample, limb) pair per lane
 // ---------------------------------------------------------------------------
-__device__ inline real stepx(real t) { return (1 - cos(kPi * t)) / 2; }
-__device__ inline real stepz(real t) { real a = sin(kPi * t); return a * a; }
+// pergen.cpp:143-153 step profiles: stepx(t) = (1 - cos(pi t)) / 2, stepz(t) = sin(pi t)^2, from one sincos
+__device__ inline void step_profiles(real t, real& sx, real& sz) {
+  real s, c;
+  sincos(kPi * t, &s, &c);
+  sx = (1 - c) / 2;
+  sz = s * s;
+}
 
 template <class W>
 __device__ void node_features(const hs_topo* T, int v, const A34& A, const A34* J, const W& w, int k) {
@@ -373,9 +381,11 @@ __device__ void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, i
     o0[0] += tv;
   } else {
     real rc = real(1) / g.curvature;
-    real tp[3] = {rc * sin(psi), rc * (1 - cos(psi)), 0};
-    A34 At = from_euler(tp, real(0), real(0), psi);
-    A34 A0 = from_euler(o0, o1[0], o1[1], o1[2]);
+    real sp, cp;
+    sincos(psi, &sp, &cp);
+    real tp[3] = {rc * sp, rc * (1 - cp), 0};
+    A34 At = from_euler_sc(tp, SC3{real(0), real(1), real(0), real(1), sp, cp});  // sin 0 = 0, cos 0 = 1
+    A34 A0 = from_euler_sc(o0, st.tsc);
     A34 A1 = mul(At, A0);
     o0[0] = A1(0, 3); o0[1] = A1(1, 3); o0[2] = A1(2, 3);
     euler_from(A1, o1);
@@ -391,9 +401,11 @@ __device__ void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, i
     if (t_frac < t_lift) stepf = 0;
     else if (t_frac < t_lift + st.t_step) stepf = (t_frac - t_lift) / st.t_step;
     else stepf = 1;
-    real dx = (t_int + st.xs[j] + stepx(stepf)) * g.step_length;
+    real sx, sz;
+    step_profiles(stepf, sx, sz);
+    real dx = (t_int + st.xs[j] + sx) * g.step_length;
     real dy = 0;
-    real dz = stepz(stepf) * g.step_height;
+    real dz = sz * g.step_height;
     if (g.curvature != 0) {  // turn_position (pergen.cpp:160-183)
       int s = (g.curvature > 0) ? 1 : -1;
       real x0 = st.pos0[j][0], y0 = st.pos0[j][1];
@@ -404,8 +416,10 @@ __device__ void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, i
       real beta = -s * dx / st.max_radius;
       real gamma = alpha - beta / 2;
       real sb = 2 * sin(beta / 2);
-      dx = r * sin(gamma) * sb;
-      dy += -r * cos(gamma) * sb;
+      real sg, cg;
+      sincos(gamma, &sg, &cg);
+      dx = r * sg * sb;
+      dy += -r * cg * sb;
     }
     target[0] = dx + st.pos0[j][0];
     target[1] = dy + st.pos0[j][1];
@@ -413,7 +427,8 @@ __device__ void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, i
   }
   // set_jvalues_with_lik: torso + body chain FK, then limb IK (model.cpp:354-359, lik.cpp:89-99)
   real q6[6] = {o0[0], o0[1], o0[2], o1[0], o1[1], o1[2]};
-  A34 A0 = mul(mul(node_joint_parent(T, 0), free_joint(q6)), node_pj(T, 0));
+  const A34 F = turned ? free_joint(q6) : free_joint_sc(q6, st.tsc);  // straight gait: torso angles fixed
+  A34 A0 = mul(mul(node_joint_parent(T, 0), F), node_pj(T, 0));
   const bool wq = w.want_q(k);
   if (L == 0) {
     if (wq) for (int i = 0; i < 6; i++) w.q(k)[i] = q6[i];

@@ -88,10 +88,27 @@ __device__ inline A34 invert(const A34& A) {
   return I;
 }
 
+// sines / cosines of three Euler angles (one shared range reduction per angle:
+// sincos is bitwise identical to sin and cos, tools/sincos_check.hip)
+struct SC3 {
+  real sphi, cphi, sth, cth, spsi, cpsi;
+};
+
+#if HS_REAL_IS_FLOAT
+__device__ inline void sincos(float x, float* s, float* c) { sincosf(x, s, c); }
+#endif
+
+__device__ inline SC3 sincos3(real phi, real theta, real psi) {
+  SC3 t;
+  sincos(phi, &t.sphi, &t.cphi);
+  sincos(theta, &t.sth, &t.cth);
+  sincos(psi, &t.spsi, &t.cpsi);
+  return t;
+}
+
 // ODE dRFromEulerAngles transposed into affine layout (model.cpp:45, visualization.cpp:62-69)
-__device__ inline A34 from_euler(const real* pos, real phi, real theta, real psi) {
-  real sphi = sin(phi), cphi = cos(phi), sth = sin(theta), cth = cos(theta);
-  real spsi = sin(psi), cpsi = cos(psi);
+__device__ inline A34 from_euler_sc(const real* pos, const SC3& t) {
+  const real sphi = t.sphi, cphi = t.cphi, sth = t.sth, cth = t.cth, spsi = t.spsi, cpsi = t.cpsi;
   A34 A;
   // column c of the affine = row c of the ODE matrix
   A.at(0, 0) = cpsi * cth;
@@ -109,17 +126,24 @@ __device__ inline A34 from_euler(const real* pos, real phi, real theta, real psi
   return A;
 }
 
-// free joint transformation: set_rotation then translate (model.cpp:37-49)
-__device__ inline A34 free_joint(const real* q6) {
-  A34 A = from_euler(q6, q6[3], q6[4], q6[5]);
+__device__ inline A34 from_euler(const real* pos, real phi, real theta, real psi) {
+  return from_euler_sc(pos, sincos3(phi, theta, psi));
+}
+
+// free joint transformation: set_rotation then translate (model.cpp:37-49); t = sincos3 of q6[3..5]
+__device__ inline A34 free_joint_sc(const real* q6, const SC3& t) {
+  A34 A = from_euler_sc(q6, t);
 #pragma unroll
   for (int r = 0; r < 3; r++) A.at(r, 3) = real(0) + q6[r];
   return A;
 }
 
+__device__ inline A34 free_joint(const real* q6) { return free_joint_sc(q6, sincos3(q6[3], q6[4], q6[5])); }
+
 // hinge transformation Rz(q) (model.cpp:50-57)
 __device__ inline A34 hinge_joint(real q) {
-  real c = cos(q), s = sin(q);
+  real c, s;
+  sincos(q, &s, &c);
   A34 A;
 #pragma unroll
   for (int i = 0; i < 12; i++) A.m[i] = real(0);
