@@ -118,7 +118,7 @@ struct hs_mixed_s {
   std::vector<hs_model_t> models;
   hs_model_dims max_dims;
   int32_t st_tau = 0, st_cf = 0, st_q = 0, st_x = 0;
-  const hs_topo** d_topos = nullptr;
+  hs_topo* d_topos = nullptr;  // the models' topologies, contiguous (wave_model indexes it)
   int32_t* d_wave_model = nullptr;
   int32_t* d_wave_rollouts = nullptr;
   void* ws = nullptr;
@@ -247,19 +247,15 @@ int hs_mixed_create(const hs_model_t* models, int32_t n_models, const int32_t* m
   hs_mixed_s* p = new hs_mixed_s;
   p->n_rollouts = n_rollouts;
   p->models.assign(models, models + n_models);
-  std::vector<const hs_topo*> topos;
+  std::vector<hs_topo> topos;
   std::vector<int32_t> wave_model, wave_rollouts;
   hs_model_dims& md = p->max_dims;
   memset(&md, 0, sizeof(md));
   int32_t max_cf = 0, max_x = 0;
   for (int k = 0; k < n_models; k++) {
     if (!models[k]) { delete p; return fail(HS_E_ARG, "null model"); }
-    const hs_topo* d = nullptr;
-    void* ws = nullptr;
-    int rc = device_state(models[k], 1, &d, &ws);
-    if (rc != HS_OK) { delete p; return rc; }
-    topos.push_back(d);
     const hs_topo& t = models[k]->host;
+    topos.push_back(t);
     if (t.n > md.n_parts) {
       hs_model_get_dims(models[k], &md);  // the model with the most parts, maxima patched below
     }
@@ -281,7 +277,7 @@ int hs_mixed_create(const hs_model_t* models, int32_t n_models, const int32_t* m
   p->st_x = max_x;
   p->n_waves = (int32_t)wave_model.size();
   hipError_t e = hipGetDevice(&p->dev);
-  size_t nt = topos.size() * sizeof(hs_topo*), nw = wave_model.size() * sizeof(int32_t);
+  size_t nt = topos.size() * sizeof(hs_topo), nw = wave_model.size() * sizeof(int32_t);
   if (e == hipSuccess) e = hipMalloc(&p->d_topos, nt);
   if (e == hipSuccess && nw) e = hipMalloc(&p->d_wave_model, nw);
   if (e == hipSuccess && nw) e = hipMalloc(&p->d_wave_rollouts, 2 * nw);
@@ -326,7 +322,6 @@ int hs_run_mixed_steps(hs_mixed_t p, const hs_run_args* a, int32_t n_calls, void
   if (dev != p->dev) return fail(HS_E_DEVICE, "plan was created on another device");
   if (a->n_rollouts == 0 || n_calls == 0) return HS_OK;
   hs::launch_map mp{};
-  mp.topos = p->d_topos;
   mp.wave_model = p->d_wave_model;
   mp.wave_rollouts = p->d_wave_rollouts;
   mp.n_waves = p->n_waves;
@@ -335,7 +330,7 @@ int hs_run_mixed_steps(hs_mixed_t p, const hs_run_args* a, int32_t n_calls, void
   mp.st_cf = p->st_cf;
   mp.st_q = p->st_q;
   mp.st_x = p->st_x;
-  return launch_steps(nullptr, *a, p->ws, mp, n_calls, kernel_events);
+  return launch_steps(p->d_topos, *a, p->ws, mp, n_calls, kernel_events);
 }
 
 int hs_complete_traj(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n_t, int32_t ignore_reach,

@@ -15,8 +15,8 @@ int read_pgs_config(const char* path, int setup_id, hs_gait_params* out, std::st
 
 // Which rollouts a launch's wavefronts run and where their output rows go.
 struct launch_map {
-  const hs_topo* const* topos;   // mixed batches: device array of per-model topologies (null: one model)
-  const int32_t* wave_model;     // mixed: model of each wavefront
+  const int32_t* wave_model;     // mixed: model of each wavefront, an index into the launch's
+                                 // contiguous topology array (null: one model)
   const int32_t* wave_rollouts;  // mixed: [2 * n_waves] rollout ids, -1 = idle half
   int32_t n_waves;
   int32_t max_parts;             // LDS layout class (largest model)

@@ -182,13 +182,19 @@ __device__ inline void gsync() {
 
 #ifdef HS_STAMPS
 // diagnostic build only: per-phase shader-clock stamps of the first 4096 rollouts
-__device__ unsigned long long g_stamps[4096][16];
+// (slots 16, 17: the constant 100 MHz clock at wave entry and exit, comparable across CUs)
+__device__ unsigned long long g_stamps[4096][18];
 #define STAMP(slot)                                                                                    \
   do {                                                                                                 \
     if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][slot] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+#define RSTAMP(slot)                                                                                       \
+  do {                                                                                                     \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
 #define STAMP(slot) do {} while (0)
+#define RSTAMP(slot) do {} while (0)
 #endif
 
 // ballot over the 32 lanes of this rollout (bit l = sub-lane l)
@@ -247,7 +253,7 @@ __device__ inline GaitR load_gait(const hs_gait_params& p) {
 // ---------------------------------------------------------------------------
 // S: gait setup, lanes L < n_limbs (pergen.cpp:453-507, 30-51, 143-153)
 // ---------------------------------------------------------------------------
-__device__ void gait_setup(const hs_topo* T, const GaitR& g, int n_t, SetupL& st, int lane) {
+__device__ __attribute__((always_inline)) inline void gait_setup(const hs_topo* T, const GaitR& g, int n_t, SetupL& st, int lane) {
   const int nl = T->n_limbs;
   if (lane < nl) {
     const int L = lane;
@@ -327,7 +333,7 @@ __device__ inline void step_profiles(real t, real& sx, real& sz) {
 }
 
 template <class W>
-__device__ void node_features(const hs_topo* T, int v, const A34& A, const A34* J, const W& w, int k) {
+__device__ __attribute__((always_inline)) inline void node_features(const hs_topo* T, int v, const A34& A, const A34* J, const W& w, int k) {
   const hs_node& nd = T->node[v];
   if (w.want_pos(k)) {
     real com[3] = {(real)nd.com[0], (real)nd.com[1], (real)nd.com[2]}, p[3];
@@ -362,7 +368,7 @@ __device__ void node_features(const hs_topo* T, int v, const A34& A, const A34* 
 }
 
 template <class W>
-__device__ void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, int isample, int L,
+__device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, int isample, int L,
                            bool ignore_reach, const W& w, int k) {
   real t = 0;  // t accumulates dt (periodic.cpp:171-181)
   for (int i = 0; i < isample; i++) t += st.dt;
@@ -466,7 +472,7 @@ __device__ void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, i
 // D: finite differences at the centre sample, lane = part (dynrec.cpp:175-224)
 // ---------------------------------------------------------------------------
 template <class W, class SV>
-__device__ void dynamics(const hs_topo* T, const SetupL& st, SV& sv, const W& w, int lane) {
+__device__ __attribute__((always_inline)) inline void dynamics(const hs_topo* T, const SetupL& st, SV& sv, const W& w, int lane) {
   const int n = T->n;
   if (lane < n) {
     const int i = lane;
@@ -521,17 +527,24 @@ __device__ void dynamics(const hs_topo* T, const SetupL& st, SV& sv, const W& w,
 // S1: tree back-substitution B0 x = f, level by level (deepest first)
 // ---------------------------------------------------------------------------
 template <class W, class SV>
-__device__ void particular(const hs_topo* T, SV& sv, const W& w, int lane) {
+__device__ __attribute__((always_inline)) inline void particular(const hs_topo* T, SV& sv, const W& w, int lane) {
   const int n = T->n;
+  // this lane's node links, loaded once (independent loads, not one L2 round trip per level)
+  const hs_node& nd = T->node[lane < n ? lane : 0];
+  const int depth = lane < n ? nd.depth : -1, parent = nd.parent, nk = nd.nkids;
+  int kids[HS_CMAX];
+#pragma unroll
+  for (int kk = 0; kk < HS_CMAX; kk++) kids[kk] = nd.kids[kk];
   for (int level = T->max_depth; level >= 0; level--) {
-    if (lane < n && T->node[lane].depth == level) {
+    if (depth == level) {
       const int i = lane;
-      const hs_node& nd = T->node[i];
       const real* Pi = w.pos(0, i);
       real F[3], Tq[3];
       for (int j = 0; j < 3; j++) { F[j] = sv.f[3 * i + j]; Tq[j] = sv.f[3 * (n + i) + j]; }
-      for (int kk = 0; kk < nd.nkids; kk++) {
-        int c = nd.kids[kk];
+#pragma unroll
+      for (int kk = 0; kk < HS_CMAX; kk++) {
+        if (kk >= nk) break;
+        const int c = kids[kk];
         const real* Jc = w.jpos(0, c);
         for (int j = 0; j < 3; j++) F[j] += sv.x[3 * c + j];
         real r[3];
@@ -543,7 +556,7 @@ __device__ void particular(const hs_topo* T, SV& sv, const W& w, int lane) {
         for (int j = 0; j < 3; j++) Tq[j] += sv.x[3 * (n + c) + j];
       }
       for (int j = 0; j < 3; j++) sv.x[3 * i + j] = F[j];
-      if (nd.parent >= 0) {
+      if (parent >= 0) {
         const real* Ji = w.jpos(0, i);
         real r[3];
         for (int j = 0; j < 3; j++) r[j] = Ji[j] - Pi[j];
@@ -1093,7 +1106,7 @@ __device__ inline void cross_rows(const real* d, real v[3][3]) {
 // the half-wave, right-looking: element (i, j) gets its products subtracted in
 // increasing order, exactly like the oracle's left-looking chol(). False (wave-
 // uniform) when a pivot falls to guard * (max original diagonal) or below.
-__device__ bool chol_half(real* K, int k, real guard, int lane) {
+__device__ __attribute__((always_inline)) inline bool chol_half(real* K, int k, real guard, int lane) {
   real mx = 0;
   for (int i = 0; i < k; i++) mx = fmax(mx, K[i * k + i]);
   for (int j = 0; j < k; j++) {
@@ -1119,7 +1132,7 @@ __device__ bool chol_half(real* K, int k, real guard, int lane) {
 // half-wave right-looking Cholesky subtracts in the oracle's left-looking order).
 // False when the minimizer is not unique (a pivot under the guard).
 template <class SV>
-__device__ bool aug_solve(FastL& fl, SV& sv, const real* a, int nc, int lane) {
+__device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, SV& sv, const real* a, int nc, int lane) {
   AugL& ag = fl.ag;
   const int k = 3 * nc;
   auto Aat = [&](int r, int i) { return fl.A[i / 3][r * 3 + i % 3]; };  // A (6 x k)
@@ -1197,7 +1210,7 @@ __device__ bool aug_solve(FastL& fl, SV& sv, const real* a, int nc, int lane) {
 }
 
 template <class W, class SV>
-__device__ bool fast_solve(const hs_topo* T, SV& sv, FastL& fl, const W& w, int nc, int lane) {
+__device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* T, SV& sv, FastL& fl, const W& w, int nc, int lane) {
   const int n = T->n;
   if (nc == 0) return true;
   const real* P0 = w.pos(0, 0);
@@ -1379,7 +1392,7 @@ __device__ inline uint64_t best_key(real cot, int64_t id) {
 // One control-loop step at centre sample i (row = b * H + h of the outputs)
 // ---------------------------------------------------------------------------
 template <class W, class SV>
-__device__ void step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st, SV& sv,
+__device__ __attribute__((always_inline)) inline void step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st, SV& sv,
                      FastL& fl, GenLDS& gl, WorkL& wk, const W& w, GenWS* G, int b, bool live, int h,
                      real& work, int lane) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
@@ -1501,6 +1514,7 @@ __device__ void step(const hs_topo* T, const hs_run_args& a, const hs::launch_ma
   work_dt *= st.dt;
   work += work_dt;
   STAMP(8);
+  RSTAMP(17);
 }
 
 // ---------------------------------------------------------------------------
@@ -1531,7 +1545,7 @@ __device__ inline void cross3(const real* a, const real* b, real* c) {
 }
 
 template <class W, class SV>
-__device__ uint32_t forces_solve(const hs_topo* T, const SV& sv, ForceL& fr, const W& w, const real* z, int lane) {
+__device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_topo* T, const SV& sv, ForceL& fr, const W& w, const real* z, int lane) {
   const int n = T->n, nj = T->nmj, nf = T->nf, m = 6 + nj, nq = 3 * nf, ld = nq + 1;
   const real* P0 = w.pos(0, 0);
   for (int e = lane; e < m * m; e += HALF) {  // I + G G^T, lower triangle
@@ -1669,7 +1683,7 @@ __device__ uint32_t forces_solve(const hs_topo* T, const SV& sv, ForceL& fr, con
 }
 
 template <class W, class SV>
-__device__ void forces_step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st,
+__device__ __attribute__((always_inline)) inline void forces_step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st,
                             SV& sv, ForceL& fr, const W& w, int b, bool live, int h, int lane) {
   const int nf = T->nf, cfg = T->cfg, nl = T->n_limbs, nq = 3 * nf;
   dynamics(T, st, sv, w, lane);
@@ -1689,10 +1703,13 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
                                                                                  hs_run_args a, GenWS* __restrict__ gws,
                                                                                  hs::launch_map mp) {
   __shared__ Smem<NM, FORCES> smem[2];
+  RSTAMP(16);
+  STAMP(15);
   const int sub = threadIdx.x / HALF;  // rollout slot within the wave
   const int lane = threadIdx.x % HALF; // lane within the rollout
   // one model per wavefront: the topology pointer stays wave-uniform (scalar loads)
-  const hs_topo* __restrict__ T = mp.topos ? mp.topos[mp.wave_model[blockIdx.x]] : T0;
+  // (indexing the kernel argument keeps T a known-global pointer: global_load, not flat_load)
+  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[blockIdx.x] : T0;
   int b, bb;
   bool live;  // an idle half (odd group) computes a copy of its neighbour and stores nothing
   if (mp.wave_rollouts) {
@@ -1745,11 +1762,11 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
 #if defined(HS_STAMPS) && !HS_REAL_IS_FLOAT
 extern "C" int hs_debug_read_stamps(unsigned long long* out, int n_rows) {
   if (n_rows > 4096) n_rows = 4096;
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16 * n_rows, 0,
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 18 * n_rows, 0,
                                   hipMemcpyDeviceToHost);
 }
 extern "C" int hs_debug_clear_stamps() {
-  static unsigned long long zero[4096][16];
+  static unsigned long long zero[4096][18];
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
 }
 #endif

@@ -48,14 +48,24 @@ def main():
     H.run_host(m, params, n_t=20, k0=k0, horizon=1, want=("tau",))  # warm
     L.hs_debug_clear_stamps()
     H.run_host(m, params, n_t=20, k0=k0, horizon=1, want=("tau",))
-    st = np.zeros((4096, 16), dtype=np.uint64)
+    st = np.zeros((4096, 18), dtype=np.uint64)
     L.hs_debug_read_stamps(st.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), 4096)
     st = st[:min((n + 1) // 2, 4096)].astype(np.int64)  # one row per wavefront (two rollouts)
     gen = st[:, 9] != 0
     for name, a, b in PHASES + (GENERAL if gen.any() else []):
         d = (st[gen] if name.startswith("g:") else st)[:, b] - (st[gen] if name.startswith("g:") else st)[:, a]
         print(f"{name:22s} mean {d.mean():10.0f}  p50 {np.median(d):10.0f}  p90 {np.percentile(d, 90):10.0f}  max {d.max():10.0f}")
-
+    # launch shape on the 100 MHz clock (slots 16, 17), relative to the first wave's entry, in us
+    t0 = st[:, 16].min()
+    d = st[:, 0] - st[:, 15]
+    print(f"{'entry->setup (cyc)':22s} mean {d.mean():10.0f}  p50 {np.median(d):10.0f}  p90 {np.percentile(d, 90):10.0f}  max {d.max():10.0f}")
+    for name, col in (("wave start (us)", 16), ("wave end (us)", 17)):
+        d = (st[:, col] - t0) / 100.0
+        print(f"{name:22s} mean {d.mean():10.2f}  p50 {np.median(d):10.2f}  p90 {np.percentile(d, 90):10.2f}  max {d.max():10.2f}")
+    d = (st[:, 17] - st[:, 16]) / 100.0
+    print(f"{'wave life (us)':22s} mean {d.mean():10.2f}  p50 {np.median(d):10.2f}  p90 {np.percentile(d, 90):10.2f}  max {d.max():10.2f}")
+    hist = np.histogram((st[:, 16] - t0) / 100.0, bins=10)
+    print("start histogram:", list(hist[0]), "edges(us):", [round(e, 1) for e in hist[1]])
 
 if __name__ == "__main__":
     main()
