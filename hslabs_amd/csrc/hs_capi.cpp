@@ -26,11 +26,53 @@ int hip_fail(hipError_t e, const char* what) {
   return HS_E_DEVICE;
 }
 
+void free_on_device(int dev, void* p) {
+  int cur = 0;
+  if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(dev) == hipSuccess) {
+    (void)hipFree(p);
+    (void)hipSetDevice(cur);
+  }
+}
+
+}  // namespace
+
+int ws_pool::get(void* stream, size_t n, void** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  for (slot& s : live) {
+    if (s.dev != dev || s.stream != stream) continue;
+    if (s.n < n) {
+      void* w = nullptr;
+      e = hipMalloc(&w, n * hs::general_workspace_bytes());  // fp64 slot >= fp32 slot
+      if (e != hipSuccess) return (int)e;
+      retired.emplace_back(dev, s.ptr);
+      s.ptr = w;
+      s.n = n;
+    }
+    *out = s.ptr;
+    return 0;
+  }
+  void* w = nullptr;
+  e = hipMalloc(&w, n * hs::general_workspace_bytes());
+  if (e != hipSuccess) return (int)e;
+  live.push_back({dev, stream, w, n});
+  *out = w;
+  return 0;
+}
+
+void ws_pool::release() {
+  for (slot& s : live) free_on_device(s.dev, s.ptr);
+  for (auto& r : retired) free_on_device(r.first, r.second);
+  live.clear();
+  retired.clear();
+}
+
+namespace {
+
 // Device copy of the topology for the current device (created once per device)
-// and a fallback workspace for at least n_rollouts rollouts. An outgrown
-// workspace is retired, not freed: kernels queued on other streams may still
-// use it; hs_model_free releases it.
-int device_state(hs_model_t m, int n_rollouts, const hs_topo** topo, void** ws) {
+// and the rollout workspace of (device, stream) for at least n_rollouts rollouts.
+int device_state(hs_model_t m, int n_rollouts, void* stream, const hs_topo** topo, void** ws) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
@@ -44,16 +86,9 @@ int device_state(hs_model_t m, int n_rollouts, const hs_topo** topo, void** ws) 
     if (e != hipSuccess) { (void)hipFree(d); return hip_fail(e, "hipMemcpy(topo)"); }
     m->dev[dev] = d;
   }
-  if (m->ws_rollouts[dev] < (size_t)n_rollouts) {
-    void* w = nullptr;
-    e = hipMalloc(&w, (size_t)n_rollouts * hs::general_workspace_bytes());  // fp64 slot >= fp32 slot
-    if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
-    if (m->ws[dev]) m->retired.emplace_back(dev, m->ws[dev]);
-    m->ws[dev] = w;
-    m->ws_rollouts[dev] = (size_t)n_rollouts;
-  }
+  e = (hipError_t)m->ws.get(stream, (size_t)n_rollouts, ws);
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
   *topo = m->dev[dev];
-  *ws = m->ws[dev];
   return HS_OK;
 }
 
@@ -62,12 +97,16 @@ int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::lau
                  void* const* kernel_events) {
   hs_run_args c = a;
   hipStream_t st = (hipStream_t)a.stream;
+  // one gait setup per rollout per call: the first launch stores it, later launches load it
+  const bool several = (int64_t)n_calls * a.horizon > 1;
   for (int32_t i = 0; i < n_calls; i++) {
     c.k0 = (int32_t)(((int64_t)a.k0 + (int64_t)i * a.horizon) % a.n_t);
+    hs::launch_map mi = mp;
+    mi.setup_io = !several ? hs::SETUP_COMPUTE : (i == 0 ? hs::SETUP_STORE : hs::SETUP_LOAD);
     hipError_t e = hipSuccess;
     if (kernel_events) e = hipEventRecord((hipEvent_t)kernel_events[2 * i], st);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
-    int le = (a.precision == HS_PREC_F32) ? hs::launch_rollouts_f32(d, c, ws, mp) : hs::launch_rollouts(d, c, ws, mp);
+    int le = (a.precision == HS_PREC_F32) ? hs::launch_rollouts_f32(d, c, ws, mi) : hs::launch_rollouts(d, c, ws, mi);
     if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
     if (kernel_events) e = hipEventRecord((hipEvent_t)kernel_events[2 * i + 1], st);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
@@ -75,13 +114,6 @@ int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::lau
   return HS_OK;
 }
 
-void free_on_device(int dev, void* p) {
-  int cur = 0;
-  if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(dev) == hipSuccess) {
-    (void)hipFree(p);
-    (void)hipSetDevice(cur);
-  }
-}
 
 int check_args(const hs_model_s* m, const hs_run_args* a) {
   if (!m || !a) return fail(HS_E_ARG, "null model or args");
@@ -121,7 +153,8 @@ struct hs_mixed_s {
   hs_topo* d_topos = nullptr;  // the models' topologies, contiguous (wave_model indexes it)
   int32_t* d_wave_model = nullptr;
   int32_t* d_wave_rollouts = nullptr;
-  void* ws = nullptr;
+  ws_pool ws;
+  std::mutex mu;
 };
 
 extern "C" {
@@ -134,8 +167,6 @@ int hs_model_load_ex(const char* xml_path, int lik_variant, hs_model_t* out) {
   if (!xml_path || !out) return fail(HS_E_ARG, "null argument");
   hs_model_s* m = new hs_model_s;
   memset(m->dev, 0, sizeof(m->dev));
-  memset(m->ws, 0, sizeof(m->ws));
-  memset(m->ws_rollouts, 0, sizeof(m->ws_rollouts));
   std::string err;
   int rc = hs::load_model_file(xml_path, lik_variant, &m->host, err);
   if (rc != HS_OK) {
@@ -150,11 +181,9 @@ int hs_model_load(const char* xml_path, hs_model_t* out) { return hs_model_load_
 
 void hs_model_free(hs_model_t m) {
   if (!m) return;
-  for (int d = 0; d < HS_MAX_DEVICES; d++) {
+  for (int d = 0; d < HS_MAX_DEVICES; d++)
     if (m->dev[d]) free_on_device(d, m->dev[d]);
-    if (m->ws[d]) free_on_device(d, m->ws[d]);
-  }
-  for (auto& r : m->retired) free_on_device(r.first, r.second);
+  m->ws.release();
   delete m;
 }
 
@@ -192,7 +221,7 @@ int hs_run_steps(hs_model_t m, const hs_run_args* a, int32_t n_calls, void* cons
   if (a->n_rollouts == 0 || n_calls == 0) return HS_OK;
   const hs_topo* d = nullptr;
   void* ws = nullptr;
-  rc = device_state(m, a->n_rollouts + 1, &d, &ws);  // + the idle half-wave of an odd batch
+  rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);  // + the idle half-wave of an odd batch
   if (rc != HS_OK) return rc;
   return launch_steps(d, *a, ws, hs::single_model_map(m->host, a->n_rollouts), n_calls, kernel_events);
 }
@@ -206,7 +235,7 @@ int hs_run_pd(hs_model_t m, const hs_run_args* a, const hs_pd_args* pd) {
   if (a->n_rollouts == 0) return HS_OK;
   const hs_topo* d = nullptr;
   void* ws = nullptr;
-  rc = device_state(m, a->n_rollouts + 1, &d, &ws);
+  rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);
   if (rc != HS_OK) return rc;
   hs::launch_map mp = hs::single_model_map(m->host, a->n_rollouts);
   mp.pd_q = pd->q_meas;
@@ -226,7 +255,7 @@ int hs_run_forces(hs_model_t m, const hs_run_args* a, const double* tau_in) {
   if (a->n_rollouts == 0) return HS_OK;
   const hs_topo* d = nullptr;
   void* ws = nullptr;
-  rc = device_state(m, a->n_rollouts + 1, &d, &ws);
+  rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);
   if (rc != HS_OK) return rc;
   hs::launch_map mp = hs::single_model_map(m->host, a->n_rollouts);
   mp.tau_in = tau_in;
@@ -284,7 +313,6 @@ int hs_mixed_create(const hs_model_t* models, int32_t n_models, const int32_t* m
   if (e == hipSuccess) e = hipMemcpy(p->d_topos, topos.data(), nt, hipMemcpyHostToDevice);
   if (e == hipSuccess && nw) e = hipMemcpy(p->d_wave_model, wave_model.data(), nw, hipMemcpyHostToDevice);
   if (e == hipSuccess && nw) e = hipMemcpy(p->d_wave_rollouts, wave_rollouts.data(), 2 * nw, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMalloc(&p->ws, ((size_t)n_rollouts + 1) * hs::general_workspace_bytes());
   if (e != hipSuccess) {
     hs_mixed_free(p);
     return hip_fail(e, "mixed plan upload");
@@ -298,7 +326,7 @@ void hs_mixed_free(hs_mixed_t p) {
   if (p->d_topos) free_on_device(p->dev, p->d_topos);
   if (p->d_wave_model) free_on_device(p->dev, p->d_wave_model);
   if (p->d_wave_rollouts) free_on_device(p->dev, p->d_wave_rollouts);
-  if (p->ws) free_on_device(p->dev, p->ws);
+  p->ws.release();
   delete p;
 }
 
@@ -330,7 +358,13 @@ int hs_run_mixed_steps(hs_mixed_t p, const hs_run_args* a, int32_t n_calls, void
   mp.st_cf = p->st_cf;
   mp.st_q = p->st_q;
   mp.st_x = p->st_x;
-  return launch_steps(p->d_topos, *a, p->ws, mp, n_calls, kernel_events);
+  void* ws = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(p->mu);
+    e = (hipError_t)p->ws.get(a->stream, (size_t)p->n_rollouts + 1, &ws);
+  }
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
+  return launch_steps(p->d_topos, *a, ws, mp, n_calls, kernel_events);
 }
 
 int hs_complete_traj(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n_t, int32_t ignore_reach,

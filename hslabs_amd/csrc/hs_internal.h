@@ -13,6 +13,10 @@ namespace hs {
 int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& err);
 int read_pgs_config(const char* path, int setup_id, hs_gait_params* out, std::string& xml, std::string& err);
 
+// Gait setup (pergensetup::setup_pergen, once per rollout in the reference) across the
+// launches of one call: the first launch computes and stores it per rollout, the rest load it.
+enum { SETUP_COMPUTE = 0, SETUP_STORE = 1, SETUP_LOAD = 2 };
+
 // Which rollouts a launch's wavefronts run and where their output rows go.
 struct launch_map {
   const int32_t* wave_model;     // mixed: model of each wavefront, an index into the launch's
@@ -21,6 +25,7 @@ struct launch_map {
   int32_t n_waves;
   int32_t max_parts;             // LDS layout class (largest model)
   int32_t h_row;                 // output row of this launch's step within the horizon
+  int32_t setup_io;              // SETUP_*: gait setup computed here, also stored, or loaded
   const double* tau_in;          // forces-given-torques mode: motor torques [B][H][st_tau] (else null)
   // position control (hs_run_pd; null pd_tau = off): rows [B][H][st_tau]
   const double *pd_q, *pd_dq;
@@ -43,11 +48,26 @@ launch_map single_model_map(const hs_topo& t, int32_t n_rollouts);
 
 constexpr int HS_MAX_DEVICES = 64;
 
+// Per-rollout device workspaces (general-path scratch + the setup cache), one per
+// (device, stream): launches on one stream run in order, so a call's launches may pass
+// the setup cache from one to the next, and calls on different streams never share one.
+struct ws_pool {
+  struct slot {
+    int dev;
+    void* stream;
+    void* ptr;
+    size_t n;
+  };
+  std::vector<slot> live;
+  std::vector<std::pair<int, void*>> retired;  // outgrown: kernels still queued may use them
+  // workspace of >= n rollouts for (current device, stream); returns a hipError_t value
+  int get(void* stream, size_t n, void** out);
+  void release();
+};
+
 struct hs_model_s {
   hs_topo host;
   hs_topo* dev[HS_MAX_DEVICES];  // per-device topology copy, created lazily
-  void* ws[HS_MAX_DEVICES];      // per-device fallback workspace
-  size_t ws_rollouts[HS_MAX_DEVICES];
-  std::vector<std::pair<int, void*>> retired;  // outgrown workspaces (in-flight kernels may use them)
+  ws_pool ws;
   std::mutex mu;
 };

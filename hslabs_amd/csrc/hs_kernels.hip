@@ -1698,9 +1698,17 @@ __device__ __attribute__((always_inline)) inline void forces_step(const hs_topo*
   if (live && a.flags && lane == 0) a.flags[row] = flags;
 }
 
+// Global per-rollout workspace: the general path's scratch and the gait-setup cache that
+// carries SetupL from the first launch of a call to the later ones (hs::SETUP_*).
+struct RolloutWS {
+  GenWS gen;
+  SetupL st;
+};
+static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
+
 template <int NM, bool FORCES>
 __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_F32 : HS_MIN_WAVES) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
-                                                                                 hs_run_args a, GenWS* __restrict__ gws,
+                                                                                 hs_run_args a, RolloutWS* __restrict__ rws,
                                                                                  hs::launch_map mp) {
   __shared__ Smem<NM, FORCES> smem[2];
   RSTAMP(16);
@@ -1721,7 +1729,7 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
     live = b < a.n_rollouts;
     bb = live ? b : a.n_rollouts - 1;
   }
-  GenWS* G = gws + (live ? b : a.n_rollouts);
+  GenWS* G = &rws[live ? b : a.n_rollouts].gen;
   Smem<NM, FORCES>& sm = smem[sub];
   real work = (live && a.accumulate && a.work_cot) ? outp(a.work_cot)[2 * (size_t)b] : real(0);
   const GaitR g = load_gait(a.params[bb]);
@@ -1729,7 +1737,19 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
   const bool ignore_reach = a.ignore_reach != 0;
 
   STAMP(0);
-  gait_setup(T, g, a.n_t, sm.st, lane);
+  {
+    constexpr int NW = sizeof(SetupL) / sizeof(real);
+    real* cache = reinterpret_cast<real*>(&rws[bb].st);  // the idle half reads its neighbour's
+    real* lds = reinterpret_cast<real*>(&sm.st);
+    if (mp.setup_io == hs::SETUP_LOAD) {
+      for (int e = lane; e < NW; e += HALF) lds[e] = cache[e];
+      wave_sync();
+    } else {
+      gait_setup(T, g, a.n_t, sm.st, lane);
+      if (mp.setup_io == hs::SETUP_STORE && live)
+        for (int e = lane; e < NW; e += HALF) cache[e] = lds[e];
+    }
+  }
   STAMP(1);
 
   // K: the five-sample window, lane = (sample, limb)
@@ -1774,13 +1794,13 @@ extern "C" int hs_debug_clear_stamps() {
 namespace hs {
 
 #if HS_REAL_IS_FLOAT
-size_t general_workspace_bytes_f32() { return sizeof(GenWS); }
+size_t general_workspace_bytes_f32() { return sizeof(RolloutWS); }
 #else
-size_t general_workspace_bytes() { return sizeof(GenWS); }
+size_t general_workspace_bytes() { return sizeof(RolloutWS); }
 #endif
 
 template <int NM>
-void launch_nm(const hs_topo* d_topo, const hs_run_args& a, GenWS* ws, const launch_map& mp, hipStream_t st) {
+void launch_nm(const hs_topo* d_topo, const hs_run_args& a, RolloutWS* ws, const launch_map& mp, hipStream_t st) {
   if (mp.tau_in)
     hipLaunchKernelGGL((hs_rollout_kernel<NM, true>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
   else
@@ -1794,7 +1814,7 @@ int launch_rollouts(const hs_topo* d_topo, const hs_run_args& a, void* workspace
 #endif
   if (a.n_rollouts <= 0 || mp.n_waves <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
-  GenWS* ws = (GenWS*)workspace;
+  RolloutWS* ws = (RolloutWS*)workspace;
   // one launch per step of the horizon: step h writes output row h, work accumulates in
   // step order (periodic.cpp:291-304), the best key is taken after the last step
   for (int h = 0; h < a.horizon; h++) {
@@ -1804,6 +1824,7 @@ int launch_rollouts(const hs_topo* d_topo, const hs_run_args& a, void* workspace
     ah.accumulate = (h == 0) ? a.accumulate : 1;
     if (h + 1 < a.horizon) ah.best_key = nullptr;
     mh.h_row = h;
+    if (h > 0 && mp.setup_io != SETUP_COMPUTE) mh.setup_io = SETUP_LOAD;
     // smallest LDS layout that holds the (largest) model's parts: myant 17, spider 19, hexapod 22
     if (mp.max_parts <= 18) launch_nm<18>(d_topo, ah, ws, mh, st);
     else if (mp.max_parts <= 22) launch_nm<22>(d_topo, ah, ws, mh, st);

@@ -153,6 +153,36 @@ def test_run_steps_matches_launch_loop(gpu, hmodels):
     assert all(ev[2 * i].elapsed_time(ev[2 * i + 1]) > 0 for i in range(27))
 
 
+def test_setup_cache_is_per_call_and_per_stream(gpu, hmodels):
+    """The gait setup stored by a call's first launch (and loaded by its later ones) never
+    reaches another call: interleaved calls with other gait parameters, on one stream and on
+    two streams, give the bits of independent runs."""
+    import torch
+
+    from hslabs_amd import synth
+
+    m = hmodels["hexapod"]
+    pa, pb = synth.gen_params(96, "hexapod", id0=11), synth.gen_params(96, "hexapod", id0=12, curved=True)
+    ref_a = gpu.run_host(m, pa, n_t=20, k0=3, horizon=4)
+    ref_b = gpu.run_host(m, pb, n_t=20, k0=3, horizon=4)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for sa, sb in [(s1, s1), (s1, s2)]:
+        a = gpu.DeviceBatch(m, pa, n_t=20, k0=3, horizon=2)
+        b = gpu.DeviceBatch(m, pb, n_t=20, k0=3, horizon=2)
+        torch.cuda.synchronize()
+        ta, tb = [], []
+        for _ in range(2):  # a, b, a, b: each call's second launch loads that call's setup
+            a.run(stream=sa, best=False)
+            b.run(stream=sb, best=False)
+            sa.synchronize()
+            sb.synchronize()
+            ta.append(a.tau.cpu().numpy().copy())
+            tb.append(b.tau.cpu().numpy().copy())
+            a.k0, b.k0 = 5, 5
+        assert np.array_equal(np.concatenate(ta, axis=1), ref_a["tau"])
+        assert np.array_equal(np.concatenate(tb, axis=1), ref_b["tau"])
+
+
 def test_device_batch_best_key(gpu, hmodels):
     import torch
 

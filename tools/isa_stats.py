@@ -16,7 +16,7 @@ SRC = os.path.join(ROOT, "hslabs_amd", "csrc")
 def stats(src, defines=()):
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "k.s")
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast",
                         f"-I{SRC}", f"-I{os.path.join(ROOT, 'include')}", *[f"-D{d}" for d in defines],
                         "--cuda-device-only", "-S", src, "-o", out], check=True, stderr=subprocess.DEVNULL)
         text = open(out).read()

@@ -45,9 +45,12 @@ def main():
     m = H.KinematicModel(os.path.join(ROOT, "models", f"{model}.xml"))
     params = synth.gen_params(n, model)
     k0 = int(os.environ.get("K0", "0"))
-    H.run_host(m, params, n_t=20, k0=k0, horizon=1, want=("tau",))  # warm
+    # horizon 2 (default): the stamps kept are the second launch's, which loads the gait setup
+    # stored by the first (the steady state of hs_run_steps); HZ=1 stamps a computing launch
+    hz = int(os.environ.get("HZ", "2"))
+    H.run_host(m, params, n_t=20, k0=k0, horizon=hz, want=("tau",))  # warm
     L.hs_debug_clear_stamps()
-    H.run_host(m, params, n_t=20, k0=k0, horizon=1, want=("tau",))
+    H.run_host(m, params, n_t=20, k0=k0, horizon=hz, want=("tau",))
     st = np.zeros((4096, 18), dtype=np.uint64)
     L.hs_debug_read_stamps(st.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), 4096)
     st = st[:min((n + 1) // 2, 4096)].astype(np.int64)  # one row per wavefront (two rollouts)
