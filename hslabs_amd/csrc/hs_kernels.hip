@@ -63,11 +63,12 @@ static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a
 
 struct SchurL {  // per-contact Schur complement (all D_c invertible)
   real Dinv[HS_LMAX][9], S[HS_LMAX][36], h[HS_LMAX][6];
+  real Ssum[42];  // sum over contacts of [S_c | h_c] (lane per entry)
   real lam[6];
 };
 
 struct AugL {  // augmented system K = D + rho A^T A (a singular D_c)
-  real K[HS_KMAX * HS_KMAX], X[HS_KMAX * 7], St[36], lam[6];
+  real K[HS_KMAX * HS_KMAX], X[HS_KMAX * 7], St[36], lam[6], rdiag[HS_KMAX];
   int ok;
 };
 
@@ -183,7 +184,7 @@ __device__ inline void gsync() {
 #ifdef HS_STAMPS
 // diagnostic build only: per-phase shader-clock stamps of the first 4096 rollouts
 // (slots 16, 17: the constant 100 MHz clock at wave entry and exit, comparable across CUs)
-__device__ unsigned long long g_stamps[4096][18];
+__device__ unsigned long long g_stamps[4096][24];
 #define STAMP(slot)                                                                                    \
   do {                                                                                                 \
     if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][slot] = __builtin_amdgcn_s_memtime(); \
@@ -1065,14 +1066,14 @@ __device__ inline bool chol_n(real* a, real guard) {  // row-major, in place
 #pragma unroll
     for (int k = 0; k < j; k++) s -= a[j * N + k] * a[j * N + k];
     if (!(s > guard * mx)) return false;
-    real l = sqrt(s);
+    const real l = sqrt(s), rl = real(1) / l;  // one division per pivot (oracle chol)
     a[j * N + j] = l;
 #pragma unroll
     for (int i = j + 1; i < N; i++) {
       real t = a[i * N + j];
 #pragma unroll
       for (int k = 0; k < j; k++) t -= a[i * N + k] * a[j * N + k];
-      a[i * N + j] = t / l;
+      a[i * N + j] = t * rl;
     }
   }
   return true;
@@ -1080,19 +1081,22 @@ __device__ inline bool chol_n(real* a, real guard) {  // row-major, in place
 
 template <int N>
 __device__ inline void chol_solve_n(const real* L, real* b) {
+  real rl[N];  // 1 / L_ii (bitwise the reciprocals chol_n formed)
+#pragma unroll
+  for (int i = 0; i < N; i++) rl[i] = real(1) / L[i * N + i];
 #pragma unroll
   for (int i = 0; i < N; i++) {
     real s = b[i];
 #pragma unroll
     for (int k = 0; k < i; k++) s -= L[i * N + k] * b[k];
-    b[i] = s / L[i * N + i];
+    b[i] = s * rl[i];
   }
 #pragma unroll
   for (int i = N - 1; i >= 0; i--) {
     real s = b[i];
 #pragma unroll
     for (int k = i + 1; k < N; k++) s -= L[k * N + i] * b[k];
-    b[i] = s / L[i * N + i];
+    b[i] = s * rl[i];
   }
 }
 
@@ -1106,15 +1110,20 @@ __device__ inline void cross_rows(const real* d, real v[3][3]) {
 // the half-wave, right-looking: element (i, j) gets its products subtracted in
 // increasing order, exactly like the oracle's left-looking chol(). False (wave-
 // uniform) when a pivot falls to guard * (max original diagonal) or below.
-__device__ __attribute__((always_inline)) inline bool chol_half(real* K, int k, real guard, int lane) {
+// rdiag (optional) receives 1 / L_jj.
+__device__ __attribute__((always_inline)) inline bool chol_half(real* K, int k, real guard, int lane,
+                                                                 real* rdiag = nullptr) {
   real mx = 0;
   for (int i = 0; i < k; i++) mx = fmax(mx, K[i * k + i]);
   for (int j = 0; j < k; j++) {
     const real s = K[j * k + j];
     if (!(s > guard * mx)) return false;
-    const real l = sqrt(s);
-    if (lane == 0) K[j * k + j] = l;
-    for (int i = j + 1 + lane; i < k; i += HALF) K[i * k + j] = K[i * k + j] / l;
+    const real l = sqrt(s), rl = real(1) / l;
+    if (lane == 0) {
+      K[j * k + j] = l;
+      if (rdiag) rdiag[j] = rl;
+    }
+    for (int i = j + 1 + lane; i < k; i += HALF) K[i * k + j] = K[i * k + j] * rl;
     wave_sync();
     const int m = k - 1 - j;
     for (int e = lane; e < m * m; e += HALF) {
@@ -1164,18 +1173,19 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, SV& s
     ag.X[i * 7 + q] = v;
   }
   wave_sync();
-  if (!chol_half(ag.K, k, kFastPivotGuard, lane)) return false;
+  if (!chol_half(ag.K, k, kFastPivotGuard, lane, ag.rdiag)) return false;
+  wave_sync();
   if (lane < 7) {  // K X = [A^T | g~], one right-hand column per lane
     const int q = lane;
     for (int i = 0; i < k; i++) {
       real s = ag.X[i * 7 + q];
       for (int m = 0; m < i; m++) s -= ag.K[i * k + m] * ag.X[m * 7 + q];
-      ag.X[i * 7 + q] = s / ag.K[i * k + i];
+      ag.X[i * 7 + q] = s * ag.rdiag[i];
     }
     for (int i = k - 1; i >= 0; i--) {
       real s = ag.X[i * 7 + q];
       for (int m = i + 1; m < k; m++) s -= ag.K[m * k + i] * ag.X[m * 7 + q];
-      ag.X[i * 7 + q] = s / ag.K[i * k + i];
+      ag.X[i * 7 + q] = s * ag.rdiag[i];
     }
   }
   wave_sync();
@@ -1225,7 +1235,14 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       for (int j = 0; j < 3; j++) { Ac[r * 3 + j] = (r == j) ? real(-1) : real(0); Ac[(3 + r) * 3 + j] = v[r][j]; }
     for (int i = 0; i < 18; i++) fl.A[c][i] = Ac[i];
     real D[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-    for (int p = T->footis[fi]; p >= 0 && T->node[p].parent >= 0; p = T->node[p].parent) {
+    const int nch = T->foot_chain_len[fi];
+    int chain[HS_CHAIN_MAX];  // independent loads instead of a parent-pointer chase
+#pragma unroll
+    for (int m = 0; m < HS_CHAIN_MAX; m++) chain[m] = T->foot_chain[fi][m];
+#pragma unroll
+    for (int m = 0; m < HS_CHAIN_MAX; m++) {
+      if (m >= nch) break;
+      const int p = chain[m];
       const real* Jp = w.jpos(0, p);
       const real* Jz = w.jz(0, p);
       real da[3], va[3][3];
@@ -1278,6 +1295,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
     fl.ok[c] = ok;
   }
   wave_sync();
+  STAMP(18);
   const real a[6] = {sv.x[0], sv.x[1], sv.x[2], sv.x[3 * n], sv.x[3 * n + 1], sv.x[3 * n + 2]};
   for (int c = 0; c < nc; c++)
     if (!fl.ok[c]) return aug_solve(fl, sv, a, nc, lane);  // only nc >= 3 factors D_c
@@ -1342,14 +1360,16 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       fl.ok[0] = ok;
     }
   } else {  // Schur complement of the 6 zeroth-order constraints
+    for (int e = lane; e < 42; e += HALF) {  // entry sums in contact order (lane per entry)
+      real s = 0;
+      for (int c = 0; c < nc; c++) s += (e < 36) ? fl.sc.S[c][e] : fl.sc.h[c][e - 36];
+      fl.sc.Ssum[e] = s;
+    }
+    wave_sync();
     if (lane == 0) {
       real Sm[36], h[6];
-      for (int i = 0; i < 36; i++) Sm[i] = 0;
-      for (int i = 0; i < 6; i++) h[i] = 0;
-      for (int c = 0; c < nc; c++) {
-        for (int i = 0; i < 36; i++) Sm[i] += fl.sc.S[c][i];
-        for (int i = 0; i < 6; i++) h[i] += fl.sc.h[c][i];
-      }
+      for (int i = 0; i < 36; i++) Sm[i] = fl.sc.Ssum[i];
+      for (int i = 0; i < 6; i++) h[i] = fl.sc.Ssum[36 + i];
       real lam[6];
       for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
       ok = chol_n<6>(Sm, kFastPivotGuard);
@@ -1360,6 +1380,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       fl.ok[0] = ok;
     }
     wave_sync();
+    STAMP(19);
     if (!fl.ok[0]) return aug_solve(fl, sv, a, nc, lane);
     if (lane < nc) {
       const int c = lane;
@@ -1425,7 +1446,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   real tq = real(0);
   if (lane < nmj) {
     int h_id = T->hinge_ids[lane];
-    int fi = T->node[h_id].limb_below;
+    int fi = T->hinge_foot[lane];
     int cc = -1;
     for (int c = 0; c < nc; c++) if (sv.cfoot[c] == fi) cc = c;
     const real* Jp = w.jpos(0, h_id);
@@ -1782,11 +1803,11 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
 #if defined(HS_STAMPS) && !HS_REAL_IS_FLOAT
 extern "C" int hs_debug_read_stamps(unsigned long long* out, int n_rows) {
   if (n_rows > 4096) n_rows = 4096;
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 18 * n_rows, 0,
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 24 * n_rows, 0,
                                   hipMemcpyDeviceToHost);
 }
 extern "C" int hs_debug_clear_stamps() {
-  static unsigned long long zero[4096][18];
+  static unsigned long long zero[4096][24];
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
 }
 #endif

@@ -387,6 +387,15 @@ int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& 
       }
     }
   if (nf != nl) { err = "foot count"; return HS_E_TOPOLOGY; }
+  for (int fi = 0; fi < nf; fi++) {
+    int m = 0;
+    for (int a = t->footis[fi]; a >= 0 && t->node[a].parent >= 0; a = t->node[a].parent) {
+      if (m == HS_CHAIN_MAX) { err = "limb chain too long"; return HS_E_TOPOLOGY; }
+      t->foot_chain[fi][m++] = a;
+    }
+    t->foot_chain_len[fi] = m;
+  }
+  for (int j = 0; j < nh; j++) t->hinge_foot[j] = t->node[t->hinge_ids[j]].limb_below;
   return HS_OK;
 }
 

@@ -12,6 +12,7 @@
 #define HS_LMAX 6   // limbs / feet
 #define HS_KMAX 18  // 3 * contacts
 #define HS_CMAX 6   // children per node
+#define HS_CHAIN_MAX 6  // ancestors of a foot below the root (hexapod 4)
 
 enum { HS_J_NONE = -1, HS_J_FREE = 0, HS_J_HINGE = 1 };
 enum { HS_LIK_YXX = 0, HS_LIK_ZXX = 1 };
@@ -51,5 +52,9 @@ struct hs_topo {
   int32_t limb_pergen[HS_LMAX];  // likpergen_map (pergen.cpp:243-262)
   int32_t limb_chain_len[HS_LMAX];      // nodes from root to limb parent (inclusive)
   int32_t limb_chain[HS_LMAX][HS_NMAX]; // root ... limb parent
+  // index tables that turn pointer chases into independent loads:
+  int32_t foot_chain_len[HS_LMAX];      // ancestors of foot fi with a parent (foot part first)
+  int32_t foot_chain[HS_LMAX][HS_NMAX];
+  int32_t hinge_foot[HS_NMAX];          // node[hinge_ids[j]].limb_below by motor index j
   hs_node node[HS_NMAX];
 };

@@ -1407,12 +1407,12 @@ bool chol(double* a, int n, double guard) {
     double s = a[j * n + j];
     for (int k = 0; k < j; k++) s -= a[j * n + k] * a[j * n + k];
     if (!(s > guard * mx)) return false;
-    double l = sqrt(s);
+    double l = sqrt(s), rl = 1.0 / l;  // one division per pivot, as the kernel
     a[j * n + j] = l;
     for (int i = j + 1; i < n; i++) {
       double t = a[i * n + j];
       for (int k = 0; k < j; k++) t -= a[i * n + k] * a[j * n + k];
-      a[i * n + j] = t / l;
+      a[i * n + j] = t * rl;
     }
   }
   return true;
@@ -1421,12 +1421,12 @@ void chol_solve(const double* L, int n, double* b) {
   for (int i = 0; i < n; i++) {
     double s = b[i];
     for (int k = 0; k < i; k++) s -= L[i * n + k] * b[k];
-    b[i] = s / L[i * n + i];
+    b[i] = s * (1.0 / L[i * n + i]);
   }
   for (int i = n - 1; i >= 0; i--) {
     double s = b[i];
     for (int k = i + 1; k < n; k++) s -= L[k * n + i] * b[k];
-    b[i] = s / L[i * n + i];
+    b[i] = s * (1.0 / L[i * n + i]);
   }
 }
 

@@ -51,10 +51,15 @@ def main():
     H.run_host(m, params, n_t=20, k0=k0, horizon=hz, want=("tau",))  # warm
     L.hs_debug_clear_stamps()
     H.run_host(m, params, n_t=20, k0=k0, horizon=hz, want=("tau",))
-    st = np.zeros((4096, 18), dtype=np.uint64)
+    st = np.zeros((4096, 24), dtype=np.uint64)
     L.hs_debug_read_stamps(st.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), 4096)
     st = st[:min((n + 1) // 2, 4096)].astype(np.int64)  # one row per wavefront (two rollouts)
     gen = st[:, 9] != 0
+    sch = (st[:, 18] != 0) & (st[:, 19] != 0) & ~gen  # Schur tier: contact blocks | 6x6 solve | back-sub
+    if sch.any():
+        for name, x, y in (("s:blocks", 6, 18), ("s:schur 6x6", 18, 19), ("s:backsub", 19, 7)):
+            d = st[sch, y] - st[sch, x]
+            print(f"{name:22s} mean {d.mean():10.0f}  p50 {np.median(d):10.0f}  p90 {np.percentile(d, 90):10.0f}  max {d.max():10.0f}  (n={sch.sum()})")
     for name, a, b in PHASES + (GENERAL if gen.any() else []):
         d = (st[gen] if name.startswith("g:") else st)[:, b] - (st[gen] if name.startswith("g:") else st)[:, a]
         print(f"{name:22s} mean {d.mean():10.0f}  p50 {np.median(d):10.0f}  p90 {np.percentile(d, 90):10.0f}  max {d.max():10.0f}")
