@@ -267,6 +267,101 @@ class DeviceBatch:
         self._launch(a, n_calls, ev)
 
 
+class SimBatch:
+    """Closed-loop simulation of a batch of robots (hs_sim_reset / hs_sim_step).
+
+    modelplayer::setup_per_controller (player.cpp:370-382) for every rollout:
+    the controller tables come from hs_run over one cycle sampled at
+    n_t = int(T / play_dt + .5) (k0 = 0, H = n_t: trajectory, compute_vel_traj
+    rates, computed torques), the initial state is the configuration of
+    trajectory sample tsi0 with zero velocities (init_play_config); then each
+    ``step(n)`` runs n times modelplayer::simulate_ode with position control
+    (player.cpp:325-339) in one launch. n_t must be the same for the whole batch
+    (group rollouts by period otherwise). All state lives in HBM as torch tensors.
+    """
+
+    def __init__(self, model: KinematicModel, params, dt: float = 0.01, tsi0: int = 2, device=None,
+                 ignore_reach: bool = True, **sim_overrides):
+        import torch
+
+        self.torch = torch
+        self.model = model
+        arr = params_array(params)
+        n_ts = {int(float(T) / dt + .5) for T in arr["period"]}
+        if len(n_ts) != 1:
+            raise ValueError(f"rollouts need one table length n_t = int(T / dt + .5); got {sorted(n_ts)}")
+        self.n_t = n_ts.pop()
+        if self.n_t < 2:
+            raise ValueError("period shorter than two simulation steps")
+        self.B = len(arr)
+        self.params = SimBatch.default_params()
+        self.params.dt = dt
+        for k, v in sim_overrides.items():
+            if not hasattr(self.params, k):
+                raise TypeError(f"unknown simulation parameter {k}")
+            setattr(self.params, k, v)
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        self.tables = DeviceBatch(model, arr, n_t=self.n_t, k0=0, horizon=self.n_t, ignore_reach=ignore_reach,
+                                  outputs=("q", "dq", "tau"), device=dev)
+        self.tables.run(best=False)
+        self.body = torch.empty((self.B, model.n_parts, capi.SIM_BODY_STRIDE), dtype=torch.float64, device=dev)
+        self.seed = torch.zeros(self.B, dtype=torch.int32, device=dev)
+        self.tsi = torch.full((self.B,), int(tsi0), dtype=torch.int32, device=dev)
+        self.reset(tsi0)
+
+    @staticmethod
+    def default_params() -> "capi.SimParamsC":
+        p = capi.SimParamsC()
+        capi.load().hs_sim_default_params(ctypes.byref(p))
+        return p
+
+    def table_row(self, tsi: int) -> int:
+        """hs_run output row holding trajectory sample tsi (get_motor_adas lifts tsi < 2 by n_t)."""
+        return (tsi % self.n_t + self.n_t - 2) % self.n_t
+
+    def reset(self, tsi0: int = 2, stream=None) -> None:
+        """init_play_config (player.cpp:351-356): bodies at trajectory sample tsi0, at rest."""
+        torch = self.torch
+        config = self.tables.q[:, self.table_row(tsi0), :].contiguous()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        capi.check(capi.load().hs_sim_reset(self.model.handle, self.B, config.data_ptr(), config.shape[1],
+                                            self.body.data_ptr(), st.cuda_stream), "hs_sim_reset")
+        self._config = config
+        self.seed.zero_()
+        self.tsi.fill_(int(tsi0))
+
+    def step(self, n_steps: int = 1, stream=None, outputs=("tau_cmd", "q_meas", "torso", "n_contacts",
+                                                           "normal_force")) -> dict:
+        """n_steps of simulate_ode for every rollout (one launch). Returns the requested
+        per-step outputs as device tensors [B][n_steps][...]."""
+        torch = self.torch
+        B, nmj = self.B, self.model.nmj
+        f64 = dict(dtype=torch.float64, device=self.device)
+        out = {}
+        if "tau_cmd" in outputs:
+            out["tau_cmd"] = torch.empty((B, n_steps, nmj), **f64)
+        if "q_meas" in outputs:
+            out["q_meas"] = torch.empty((B, n_steps, nmj), **f64)
+        if "torso" in outputs:
+            out["torso"] = torch.empty((B, n_steps, 3), **f64)
+        if "n_contacts" in outputs:
+            out["n_contacts"] = torch.empty((B, n_steps), dtype=torch.int32, device=self.device)
+        if "normal_force" in outputs:
+            out["normal_force"] = torch.empty((B, n_steps), **f64)
+        a = capi.SimArgsC()
+        a.n_rollouts, a.n_steps, a.n_t = B, n_steps, self.n_t
+        a.params = self.params
+        a.body, a.seed, a.tsi = self.body.data_ptr(), self.seed.data_ptr(), self.tsi.data_ptr()
+        a.q_tab, a.dq_tab, a.tau_tab = self.tables.q.data_ptr(), self.tables.dq.data_ptr(), self.tables.tau.data_ptr()
+        for k in ("tau_cmd", "q_meas", "torso", "n_contacts", "normal_force"):
+            setattr(a, k, out[k].data_ptr() if k in out else None)
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        a.stream = st.cuda_stream
+        capi.check(capi.load().hs_sim_step(self.model.handle, ctypes.byref(a)), "hs_sim_step")
+        return out
+
+
 class MixedBatch(DeviceBatch):
     """Mixed-topology batch (BASELINE configs[4]): rollout b runs models[model_index[b]]
     through one hs_mixed plan. Output rows use the maxima over the models

@@ -6,6 +6,11 @@ the reference's x86-64 ``g++ -O2`` build, which has no FMA). That is 12 % fewer
 cycles per step on gfx950 (the kernel is VALU-issue bound) and moves per-joint
 torques by <= 2.3e-12 against the unfused CPU restatement on every pgs setup
 (profiles/r01_parity_report.txt); host code (x86-64 baseline) is unaffected.
+The closed-loop simulation (hs_sim.hip) is the exception, built with
+-ffp-contract=off: its contact test (depth >= 0) is decided within rounding for
+stance feet, so it keeps the oracle's unfused rounding (clang ignores
+`#pragma clang fp contract` under -ffp-contract=fast, hence a per-file flag).
+Sources compile to objects in parallel, then link.
 """
 from __future__ import annotations
 
@@ -13,14 +18,16 @@ import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT_DIR, "libhslabs.so")
-SOURCES = ["hs_kernels.hip", "hs_kernels_f32.hip", "hs_capi.cpp", "hs_model.cpp"]
-HEADERS = ["hs_topo.h", "hs_math.h", "hs_internal.h", os.path.join("..", "..", "include", "hslabs.h")]
+SOURCES = ["hs_kernels.hip", "hs_kernels_f32.hip", "hs_sim.hip", "hs_capi.cpp", "hs_model.cpp"]
+HEADERS = ["hs_topo.h", "hs_simtopo.h", "hs_ode.h", "hs_math.h", "hs_internal.h", os.path.join("..", "..", "include", "hslabs.h")]
 ARCH = os.environ.get("HSLABS_ARCH", "gfx950")
+CONTRACT = {"hs_sim.hip": "off"}  # per-source FMA contraction (default: fast)
 
 
 def _hipcc() -> str:
@@ -40,12 +47,27 @@ def _stale() -> bool:
 
 def _compile(out: str, defines=(), verbose: bool = False, flags=()) -> str:
     os.makedirs(OUT_DIR, exist_ok=True)
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=fast", "-Wall", "-Wno-unused-function", *flags, *[f"-D{d}" for d in defines],
-           *[os.path.join(SRC, s) for s in SOURCES], "-o", out + ".tmp"]
+    tag = os.path.splitext(os.path.basename(out))[0]
+
+    def obj(src):
+        o = os.path.join(OUT_DIR, f"{tag}.{src}.o")
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
+               f"-ffp-contract={CONTRACT.get(src, 'fast')}", "-Wall", "-Wno-unused-function", *flags,
+               *[f"-D{d}" for d in defines], os.path.join(SRC, src), "-o", o]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        return o
+
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(obj, SOURCES))
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
+    for o in objs:
+        os.remove(o)
     os.replace(out + ".tmp", out)
     return out
 

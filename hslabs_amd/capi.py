@@ -11,7 +11,7 @@ import os
 
 from . import build as _build
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 HS_OK = 0
 HS_FLAG_RANK_RETRY = 1
@@ -30,7 +30,9 @@ EXPORTS = [
     "hs_run", "hs_run_steps", "hs_run_pd", "hs_run_forces", "hs_mixed_create", "hs_mixed_free",
     "hs_mixed_get_dims", "hs_complete_traj", "hs_traj_save", "hs_run_forces_host",
     "hs_run_mixed", "hs_run_mixed_steps", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
+    "hs_sim_default_params", "hs_sim_reset", "hs_sim_step",
 ]
+SIM_BODY_STRIDE = 13
 
 
 class GaitParamsC(ctypes.Structure):
@@ -78,6 +80,21 @@ class RunArgsC(ctypes.Structure):
         ("rollout_id_base", ctypes.c_int64), ("stream", ctypes.c_void_p), ("dq", ctypes.c_void_p),
         ("precision", ctypes.c_int32),
     ]
+
+
+class SimParamsC(ctypes.Structure):
+    """hs_sim_params."""
+    _fields_ = [(f, ctypes.c_double) for f in ("dt", "k", "sor_w", "erp", "cfm", "gravity", "bounce", "bounce_vel",
+                                               "soft_cfm", "mu")] + [("iterations", ctypes.c_int32),
+                                                                     ("reserved", ctypes.c_int32)]
+
+
+class SimArgsC(ctypes.Structure):
+    """hs_sim_args."""
+    _fields_ = [("n_rollouts", ctypes.c_int32), ("n_steps", ctypes.c_int32), ("n_t", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("params", SimParamsC)] + \
+               [(f, ctypes.c_void_p) for f in ("body", "seed", "tsi", "q_tab", "dq_tab", "tau_tab", "tau_cmd", "q_meas",
+                                               "torso", "n_contacts", "normal_force", "stream")]
 
 
 class HSError(RuntimeError):
@@ -135,6 +152,10 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_best_key_encode.restype = ctypes.c_uint64
     L.hs_best_key_decode.argtypes = [ctypes.c_uint64, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64)]
     L.hs_best_key_decode.restype = None
+    L.hs_sim_default_params.argtypes = [ctypes.POINTER(SimParamsC)]
+    L.hs_sim_default_params.restype = None
+    L.hs_sim_reset.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int32, vp, vp]
+    L.hs_sim_step.argtypes = [vp, ctypes.POINTER(SimArgsC)]
     L.hs_last_error.argtypes = []
     L.hs_last_error.restype = ctypes.c_char_p
     L.hs_abi_version.argtypes = []

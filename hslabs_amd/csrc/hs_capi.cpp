@@ -86,9 +86,31 @@ int device_state(hs_model_t m, int n_rollouts, void* stream, const hs_topo** top
     if (e != hipSuccess) { (void)hipFree(d); return hip_fail(e, "hipMemcpy(topo)"); }
     m->dev[dev] = d;
   }
-  e = (hipError_t)m->ws.get(stream, (size_t)n_rollouts, ws);
-  if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
+  if (ws) {  // null: topology only
+    e = (hipError_t)m->ws.get(stream, (size_t)n_rollouts, ws);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
+  }
   *topo = m->dev[dev];
+  return HS_OK;
+}
+
+// Device copies of the topology and the ODE world description for the current device.
+int sim_device_state(hs_model_t m, const hs_topo** topo, const hs_simtopo** sim) {
+  int rc = device_state(m, 0, nullptr, topo, nullptr);
+  if (rc != HS_OK) return rc;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  std::lock_guard<std::mutex> lk(m->mu);
+  if (!m->sim_dev[dev]) {
+    hs_simtopo* d = nullptr;
+    e = hipMalloc(&d, sizeof(hs_simtopo));
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(simtopo)");
+    e = hipMemcpy(d, &m->sim, sizeof(hs_simtopo), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { (void)hipFree(d); return hip_fail(e, "hipMemcpy(simtopo)"); }
+    m->sim_dev[dev] = d;
+  }
+  *sim = m->sim_dev[dev];
   return HS_OK;
 }
 
@@ -167,8 +189,9 @@ int hs_model_load_ex(const char* xml_path, int lik_variant, hs_model_t* out) {
   if (!xml_path || !out) return fail(HS_E_ARG, "null argument");
   hs_model_s* m = new hs_model_s;
   memset(m->dev, 0, sizeof(m->dev));
+  memset(m->sim_dev, 0, sizeof(m->sim_dev));
   std::string err;
-  int rc = hs::load_model_file(xml_path, lik_variant, &m->host, err);
+  int rc = hs::load_model_file(xml_path, lik_variant, &m->host, err, &m->sim);
   if (rc != HS_OK) {
     delete m;
     return fail(rc, err);
@@ -181,8 +204,10 @@ int hs_model_load(const char* xml_path, hs_model_t* out) { return hs_model_load_
 
 void hs_model_free(hs_model_t m) {
   if (!m) return;
-  for (int d = 0; d < HS_MAX_DEVICES; d++)
+  for (int d = 0; d < HS_MAX_DEVICES; d++) {
     if (m->dev[d]) free_on_device(d, m->dev[d]);
+    if (m->sim_dev[d]) free_on_device(d, m->sim_dev[d]);
+  }
   m->ws.release();
   delete m;
 }
@@ -558,6 +583,71 @@ void hs_best_key_decode(uint64_t key, float* cot, int64_t* id) {
   if (ord == 0xFFFFFFFFu) c = NAN;
   if (cot) *cot = c;
   if (id) *id = (int64_t)(uint32_t)key;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// closed-loop simulation (hs_sim.hip)
+// ---------------------------------------------------------------------------
+extern "C" {
+
+void hs_sim_default_params(hs_sim_params* p) {
+  if (!p) return;
+  memset(p, 0, sizeof(*p));
+  p->dt = 0.01;          // modelplayer::play_dt (player.cpp:23)
+  p->k = 100;            // set_position_control_torques (player.cpp:393)
+  p->sor_w = 1.3;        // ODE dWorldSetQuickStepW default
+  p->erp = 0.8;          // visualization.cpp:146
+  p->cfm = 1e-10;        // ODE global CFM default (double precision); visualization.cpp:147 leaves it
+  p->gravity = 1;        // visualization.cpp:144
+  p->bounce = 0.5;       // nearCallback (visualization.cpp:310-320)
+  p->bounce_vel = 0.1;
+  p->soft_cfm = 0.001;
+  p->mu = INFINITY;      // dInfinity
+  p->iterations = 20;    // ODE dWorldSetQuickStepNumIterations default
+}
+
+int hs_sim_reset(hs_model_t m, int32_t n_rollouts, const double* config, int32_t config_stride, double* body,
+                 void* stream) {
+  if (!m) return fail(HS_E_ARG, "null model");
+  if (n_rollouts < 0 || n_rollouts > (1 << 30)) return fail(HS_E_ARG, "bad n_rollouts");
+  if (n_rollouts == 0) return HS_OK;
+  if (!config || !body) return fail(HS_E_ARG, "null config or body");
+  if (config_stride < m->host.cfg) return fail(HS_E_ARG, "config_stride < config_dim");
+  const hs_topo* d = nullptr;
+  const hs_simtopo* ds = nullptr;
+  int rc = sim_device_state(m, &d, &ds);
+  if (rc != HS_OK) return rc;
+  int e = hs::launch_sim_reset(d, ds, n_rollouts, config, config_stride, body, stream);
+  if (e != 0) return hip_fail((hipError_t)e, "hs_sim_reset launch");
+  return HS_OK;
+}
+
+int hs_sim_step(hs_model_t m, const hs_sim_args* a) {
+  if (!m || !a) return fail(HS_E_ARG, "null model or args");
+  if (a->n_rollouts < 0 || a->n_rollouts > (1 << 30)) return fail(HS_E_ARG, "bad n_rollouts");
+  if (a->n_steps < 0) return fail(HS_E_ARG, "n_steps < 0");
+  if (a->n_rollouts == 0 || a->n_steps == 0) return HS_OK;
+  if (!a->body || !a->seed || !a->tsi) return fail(HS_E_ARG, "body, seed and tsi are required");
+  const hs_sim_params& P = a->params;
+  if (!(P.dt > 0)) return fail(HS_E_ARG, "dt must be > 0");
+  if (P.iterations < 0) return fail(HS_E_ARG, "iterations < 0");
+  if (!(P.mu > 0)) return fail(HS_E_ARG, "mu must be > 0 (the reference uses dInfinity: 3 rows per contact)");
+  if (P.k > 0) {
+    if (a->n_t < 1) return fail(HS_E_ARG, "n_t must be >= 1 with position control");
+    if (!a->q_tab || !a->dq_tab || !a->tau_tab) return fail(HS_E_ARG, "controller tables are required when k > 0");
+  }
+  if (m->sim.m_max > 9 * HS_NMAX) return fail(HS_E_TOPOLOGY, "too many constraint rows for the simulation kernel");
+  const hs_topo* d = nullptr;
+  const hs_simtopo* ds = nullptr;
+  int rc = sim_device_state(m, &d, &ds);
+  if (rc != HS_OK) return rc;
+  hs_sim_args c = *a;
+  if (c.n_t < 1) c.n_t = 1;
+  int e = hs::launch_sim_steps(d, ds, m->sim, c);
+  if (e != 0) return hip_fail((hipError_t)e, "hs_sim_step launch");
+  return HS_OK;
 }
 
 }  // extern "C"

@@ -6,11 +6,12 @@
 #include <vector>
 
 #include "../../include/hslabs.h"
+#include "hs_simtopo.h"
 #include "hs_topo.h"
 
 namespace hs {
 
-int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& err);
+int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& err, hs_simtopo* sim = nullptr);
 int read_pgs_config(const char* path, int setup_id, hs_gait_params* out, std::string& xml, std::string& err);
 
 // Gait setup (pergensetup::setup_pergen, once per rollout in the reference) across the
@@ -44,6 +45,12 @@ size_t general_workspace_bytes_f32();
 int launch_rollouts_f32(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
 launch_map single_model_map(const hs_topo& t, int32_t n_rollouts);
 
+// closed-loop simulation kernels (hs_sim.hip); return hipError_t values
+int launch_sim_reset(const hs_topo* d_topo, const hs_simtopo* d_sim, int32_t n_rollouts, const double* config,
+                     int32_t config_stride, double* body, void* stream);
+int launch_sim_steps(const hs_topo* d_topo, const hs_simtopo* d_sim, const hs_simtopo& host_sim,
+                     const hs_sim_args& a);
+
 }  // namespace hs
 
 constexpr int HS_MAX_DEVICES = 64;
@@ -68,6 +75,8 @@ struct ws_pool {
 struct hs_model_s {
   hs_topo host;
   hs_topo* dev[HS_MAX_DEVICES];  // per-device topology copy, created lazily
+  hs_simtopo sim;                // ODE world of the model (closed-loop simulation)
+  hs_simtopo* sim_dev[HS_MAX_DEVICES];
   ws_pool ws;
   std::mutex mu;
 };

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "hs_internal.h"
+#include "hs_ode.h"
 
 namespace hs {
 
@@ -167,6 +168,9 @@ struct Build {
   hs_topo* t;
   std::vector<M4> Apj, JAp;
   std::vector<double> rcap;
+  std::vector<M4> geomA;          // odepart::A_body_geom
+  std::vector<int> gtype;         // HS_GEOM_*
+  std::vector<double> gr, glen;   // radius, cylinder length
   std::vector<int> jtype, parent;
   std::vector<std::vector<int>> kids;
   int cfg = 0, nhinge = 0;
@@ -181,6 +185,9 @@ struct Build {
     Apj.push_back(M4::translation(pos));
     JAp.push_back(M4::unity());
     rcap.push_back(0);
+    gtype.push_back(HS_GEOM_NONE);
+    gr.push_back(0);
+    glen.push_back(0);
     jtype.push_back(HS_J_NONE);
     parent.push_back(par);
     kids.emplace_back();
@@ -202,6 +209,8 @@ struct Build {
         double gp[3] = {0, 0, 0};
         parse_vals(d->attr(g, "pos"), gp, 3);
         geom = M4::translation(gp);
+        gtype[id] = HS_GEOM_SPHERE;
+        parse_vals(d->attr(g, "size"), &gr[id], 1);
       } else if (type == "capsule" || type == "cylinder") {
         double r = 0, ft[6] = {0, 0, 0, 0, 0, 0};
         parse_vals(d->attr(g, "size"), &r, 1);
@@ -215,8 +224,14 @@ struct Build {
         for (int i = 0; i < 3; i++) geom.a[12 + i] = mid[i];
         for (int i = 0; i < 3; i++) cap[i] = ft[i + 3];
         if (type == "capsule") rcap[id] = r;
+        gtype[id] = (type == "capsule") ? HS_GEOM_CAPSULE : HS_GEOM_CYLINDER;
+        gr[id] = r;
+        double l2 = 0;  // extvec::norm of fromto[3:] - fromto[:3] (visualization.cpp:495-499)
+        for (int i = 0; i < 3; i++) l2 += dir[i] * dir[i];
+        glen[id] = sqrt(l2);
       }
     }
+    geomA.push_back(geom);
     for (int i = 0; i < 3; i++) { nd.com[i] = geom.a[12 + i]; nd.cap[i] = cap[i]; }
     int j = d->child(e, "joint");
     if (j >= 0) {
@@ -268,9 +283,131 @@ struct Build {
   }
 };
 
+// The ODE world of the model (hs_simtopo.h): bodies oriented at the loaded configuration
+// (all joint values 0), joints created in preorder, the static island order.
+void build_sim(const Build& b, const hs_topo& t, hs_simtopo* s) {
+  memset(s, 0, sizeof(*s));
+  const int n = t.n;
+  s->n = n;
+  s->nmj = t.nmj;
+  // A_ground at joint values 0 (model.cpp:183-201; E(0) is the identity, so A * E is exact)
+  std::vector<M4> Ag(n), JAg(n);
+  for (int i = 0; i < n; i++) {
+    M4 A = (b.parent[i] < 0) ? M4::unity() : Ag[b.parent[i]];
+    if (b.jtype[i] != HS_J_NONE) {
+      JAg[i] = A * b.JAp[i];
+      Ag[i] = JAg[i] * b.Apj[i];
+    } else {
+      Ag[i] = A * b.Apj[i];
+    }
+  }
+  // orient_odebodys (model.cpp:295-305): pose of A_ground * A_body_geom, dBodySetRotation
+  std::vector<double> pos(3 * n), q(4 * n), R(12 * n);
+  for (int i = 0; i < n; i++) {
+    M4 A = Ag[i] * b.geomA[i];
+    double Rin[12];
+    for (int r = 0; r < 3; r++) {
+      for (int c = 0; c < 3; c++) Rin[r * 4 + c] = A.a[c * 4 + r];
+      Rin[r * 4 + 3] = 0;
+      pos[3 * i + r] = A.a[12 + r];
+    }
+    hsode::q_from_R(&q[4 * i], Rin);
+    hsode::normalize4(&q[4 * i]);
+    hsode::q_to_R(&q[4 * i], &R[12 * i]);
+    s->gtype[i] = b.gtype[i];
+    s->gr[i] = b.gr[i];
+    s->glen[i] = b.glen[i];
+    s->body_geom[i] = b.geomA[i].to34();
+    s->mass[i] = 1.0;  // dBodyCreate: dMassSetParameters(1, 0,0,0, 1,1,1, 0,0,0)
+    for (int k = 0; k < 3; k++) s->inertia[i][4 * k] = s->inv_inertia[i][4 * k] = 1.0;
+    if (b.gtype[i] == HS_GEOM_SPHERE || b.gtype[i] == HS_GEOM_CAPSULE) s->n_coll++;
+  }
+  // kinematicmodel::set_ode_joints (model.cpp:375-400); per-body joint lists newest first
+  std::vector<std::vector<int>> blist(n);
+  int nj = 0, rows = 0;
+  for (int p = 0; p < n; p++) {
+    if (b.parent[p] < 0 || b.jtype[p] == HS_J_FREE) continue;
+    hs_simjoint& J = s->joint[nj];
+    J.motor = -1;
+    if (b.jtype[p] == HS_J_HINGE) {  // odepart::make_hinge_joint (visualization.cpp:583-603)
+      J.type = HS_SJ_HINGE;
+      J.b1 = p;
+      J.b2 = b.parent[p];
+      double anc[3], ax[3], d1[3], d2[3];
+      for (int i = 0; i < 3; i++) { anc[i] = JAg[p].a[12 + i]; ax[i] = JAg[p].a[8 + i]; }
+      for (int i = 0; i < 3; i++) { d1[i] = anc[i] - pos[3 * J.b1 + i]; d2[i] = anc[i] - pos[3 * J.b2 + i]; }
+      hsode::mul1_331(J.anchor1, &R[12 * J.b1], d1);  // setAnchors
+      hsode::mul1_331(J.anchor2, &R[12 * J.b2], d2);
+      hsode::normalize3(ax);  // setAxes
+      hsode::mul1_331(J.axis1, &R[12 * J.b1], ax);
+      hsode::mul1_331(J.axis2, &R[12 * J.b2], ax);
+      hsode::qmul1(J.qrel, &q[4 * J.b1], &q[4 * J.b2]);
+      J.motor = t.node[p].hinge;
+      s->motor_joint[J.motor] = nj;
+      rows += 5;
+    } else {  // odepart::make_fixed_joint (visualization.cpp:572-579) + dJointSetFixed
+      J.type = HS_SJ_FIXED;
+      J.b1 = b.parent[p];
+      J.b2 = p;
+      hsode::qmul1(J.qrel, &q[4 * J.b1], &q[4 * J.b2]);
+      double ofs[3];
+      for (int i = 0; i < 3; i++) ofs[i] = pos[3 * J.b1 + i] - pos[3 * J.b2 + i];
+      hsode::mul1_331(J.offset, &R[12 * J.b1], ofs);
+      rows += 6;
+    }
+    blist[J.b1].insert(blist[J.b1].begin(), nj);  // addJointReferencesToBodies
+    blist[J.b2].insert(blist[J.b2].begin(), nj);
+    nj++;
+  }
+  s->nj = nj;
+  s->m_max = rows + 3 * s->n_coll;
+  // dxProcessIslands from the newest body (world body list is newest first); contacts attach to
+  // the environment, so the visitation order is static
+  std::vector<char> btag(n, 0), jtag(nj, 0);
+  std::vector<int> stack;
+  int nv = 0, ns = 0;
+  for (int bb = n - 1; bb >= 0; bb--) {
+    if (btag[bb]) continue;
+    btag[bb] = 1;
+    stack.push_back(bb);
+    while (!stack.empty()) {
+      int v = stack.back();
+      stack.pop_back();
+      s->jseq_start[nv] = ns;
+      s->border[nv++] = v;
+      for (int jid : blist[v]) {
+        if (jtag[jid]) continue;
+        jtag[jid] = 1;
+        s->jseq[ns++] = jid;
+        const hs_simjoint& J = s->joint[jid];
+        int other = (J.b1 == v) ? J.b2 : J.b1;
+        if (other >= 0 && !btag[other]) { btag[other] = 1; stack.push_back(other); }
+      }
+    }
+  }
+  s->jseq_start[nv] = ns;
+  // dRand jump-ahead tables (misc.cpp: seed' = 1664525 seed + 1013904223 mod 2^32)
+  s->lcg_a[0] = 1;
+  s->lcg_c[0] = 0;
+  for (int i = 1; i < HS_SIM_LCG; i++) {
+    s->lcg_a[i] = s->lcg_a[i - 1] * 1664525u;
+    s->lcg_c[i] = s->lcg_c[i - 1] * 1664525u + 1013904223u;
+  }
+  // dJointAddHingeTorque terms per body in motor order
+  for (int j = 0; j < t.nmj; j++) {
+    const hs_simjoint& J = s->joint[s->motor_joint[j]];
+    for (int k = 0; k < 2; k++) {
+      int bd = k == 0 ? J.b1 : J.b2;
+      int c = s->tq_n[bd]++;
+      s->tq_motor[bd][c] = j;
+      s->tq_sign[bd][c] = k == 0 ? 1 : -1;
+    }
+  }
+}
+
 }  // namespace
 
-int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& err) {
+int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& err, hs_simtopo* sim) {
   std::ifstream f(path);
   if (!f) { err = std::string("cannot open ") + path; return HS_E_IO; }
   std::stringstream ss;
@@ -396,6 +533,17 @@ int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& 
     t->foot_chain_len[fi] = m;
   }
   for (int j = 0; j < nh; j++) t->hinge_foot[j] = t->node[t->hinge_ids[j]].limb_below;
+  if (sim) {
+    for (int i = 0; i < n; i++) {
+      int nt = 0;
+      for (int j = 0; j < t->nmj; j++) {
+        int p = t->hinge_ids[j];
+        if (p == i || b.parent[p] == i) nt++;
+      }
+      if (nt > HS_SIM_TQMAX) { err = "too many hinges on one body for the simulation tables"; return HS_E_TOPOLOGY; }
+    }
+    build_sim(b, *t, sim);
+  }
   return HS_OK;
 }
 

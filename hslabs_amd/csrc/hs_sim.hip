@@ -1,0 +1,736 @@
+// hs_sim.hip -- the reference's closed-loop simulation step on gfx950: position
+// control -> motor torques -> plane collisions -> ODE QuickStep (projected
+// Gauss-Seidel / SOR-LCP), for a batch of independent robots.
+//
+// One rollout per wavefront (a 64-thread workgroup); the whole ODE world of the
+// rollout lives in LDS for all n_steps steps of a launch (bodies, the constraint
+// rows, the SOR state), so HBM sees only the controller tables and the outputs.
+// Per step:
+//   P  lane = motor: hinge angle / rate (dJointGetHingeAngle/Rate), PD torque
+//      (player.cpp:388-432);
+//   B  lane = body: dJointAddHingeTorque sums in motor order, collision with the
+//      z = 0 plane (dCollideCapsulePlane / dCollideSpherePlane), world inverse
+//      inertia, gyroscopic torque, gravity, v/h + M^-1 f;
+//   R  lane = joint (hinges, fixed joints, then this step's contacts): getInfo2
+//      rows at the offsets of ODE's island order (dxProcessIslands);
+//   A  lane = row: rhs = c/h - J (v/h + M^-1 f), CFM/h, Ad = w / (J M^-1 J^T + cfm);
+//   G  SOR_LCP sweeps. The row order is ODE's: identity, reshuffled by dRandInt
+//      every 8 sweeps. Gauss-Seidel is sequential, but consecutive rows that touch
+//      disjoint bodies commute exactly (each reads and writes only its bodies'
+//      constraint accelerations fc), so after each reshuffle the order is cut into
+//      maximal runs of body-disjoint rows and a run is solved by one lane per row:
+//      the sequential semantics (and ODE's per-row operation order) are kept;
+//   U  lane = body: velocity update and dxStepBody.
+// M^-1 J^T (ODE's iMJ) is recomputed from J where it is used instead of stored,
+// which halves the row storage: LDS per hexapod rollout ~ 33 KB.
+//
+// Every formula follows oracle/hs_oracle_sim.cpp (the CPU restatement, test
+// infrastructure) in the same operation order, and this file is compiled
+// with -ffp-contract=off (hslabs_amd/build.py) like the oracle and the
+// reference's x86-64 build: a contact exists when a capsule end's depth is
+// >= 0, and a stance foot planned at z = rcap sits within rounding of that
+// threshold, so a fused multiply-add would flip contact sets against the CPU
+// restatement. The remaining differences are the device atan2 (hinge angle)
+// versus glibc.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hs_internal.h"
+#include "hs_math.h"
+#include "hs_ode.h"
+
+namespace {
+
+using namespace hsode;
+constexpr int WAVE = 64;
+
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+enum { ROW_BILATERAL = 0, ROW_NORMAL = 1, ROW_FRICTION = 2 };
+
+// Diagnostic build (-DHS_SIM_STAMPS, tools/sim_stamps.py): shader-clock cycles per phase,
+// summed over the steps of a launch, per wavefront.
+#ifdef HS_SIM_STAMPS
+__device__ unsigned long long g_sim_stamps[4096][12];
+#define SIM_ACC(slot)                                                                 \
+  do {                                                                                \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                     \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_sim_stamps[blockIdx.x][slot] += now_ - t_last; \
+    t_last = now_;                                                                    \
+  } while (0)
+#else
+#define SIM_ACC(slot) do {} while (0)
+#endif
+
+template <int NM, int MM>
+struct SimL {
+  // bodies (part ids index everything; ODE's island numbering does not change any arithmetic)
+  double pos[NM][3], q[NM][4], R[NM][12], lvel[NM][3], avel[NM][3], facc[NM][3], tacc[NM][3];
+  double invI[NM][12];
+  double invm[NM];         // 1 / mass, kept on chip: the SOR rows read it for every update
+  double tmp1[NM][6], fc[NM][6];
+  double cpos[NM][3], cdepth[NM];
+  double tau[NM];
+  // constraint rows
+  double J[MM][12];        // Jacobian rows; scaled by Ad before the sweeps (SOR_LCP "scale J and b by Ad")
+  double iM[MM][12];       // M^-1 J^T rows (compute_invM_JT), from the unscaled J
+  double rhs[MM];          // c, then rhs, then rhs * Ad
+  double cfm[MM];          // cfm, then cfm / h, then Ad * cfm
+  double Ad[MM];
+  double lambda[MM];
+  int8_t rb1[MM], rb2[MM], rtype[MM];
+  int16_t order[MM];       // row at each sweep position
+  int16_t swp[MM];         // Fisher-Yates swap targets of a reshuffle
+  uint32_t mask[MM];       // body bit mask of the row at each position
+  int32_t run_se[MM];      // runs of body-disjoint rows: start | length << 16
+  int16_t joff[HS_SIM_JMAX], coff[NM];
+  int8_t contact[NM];
+  int32_t m, nc, nruns;
+  uint32_t seed;
+};
+
+// hinge.cpp getHingeAngle (body1 = part, body2 = parent; no dJOINT_REVERSE)
+template <class L>
+__device__ inline double hinge_angle(const L& s, const hs_simjoint& J) {
+  double qq[4], qr[4];
+  qmul1(qq, s.q[J.b1], s.q[J.b2]);
+  qmul2(qr, qq, J.qrel);
+  double cost2 = qr[0];
+  double sint2 = sqrt(qr[1] * qr[1] + qr[2] * qr[2] + qr[3] * qr[3]);
+  double theta = (dot3(qr + 1, J.axis1) >= 0) ? (2 * atan2(sint2, cost2)) : (2 * atan2(sint2, -cost2));
+  if (theta > M_PI) theta -= 2 * M_PI;
+  return -theta;
+}
+
+template <class L>
+__device__ inline void set_ball(L& s, const hs_simjoint& J, double k, int r0) {
+  double a1[3], a2[3];
+  mul0_331(a1, s.R[J.b1], J.anchor1);
+  mul0_331(a2, s.R[J.b2], J.anchor2);
+  double (*Jr)[12] = &s.J[r0];
+  // J1l = I, J1a = -[a1]x, J2l = -I, J2a = [a2]x
+  const double rows[3][12] = {
+      {1, 0, 0, 0, a1[2], -a1[1], -1, 0, 0, 0, -a2[2], a2[1]},
+      {0, 1, 0, -a1[2], 0, a1[0], 0, -1, 0, a2[2], 0, -a2[0]},
+      {0, 0, 1, a1[1], -a1[0], 0, 0, 0, -1, -a2[1], a2[0], 0}};
+  for (int r = 0; r < 3; r++) {
+    for (int j = 0; j < 12; j++) Jr[r][j] = rows[r][j];
+    s.rhs[r0 + r] = k * (a2[r] + s.pos[J.b2][r] - a1[r] - s.pos[J.b1][r]);
+  }
+}
+
+template <class L>
+__device__ inline void hinge_rows(L& s, const hs_simjoint& J, double fps, double erp, double cfm, int r0) {
+  const double k = fps * erp;
+  set_ball(s, J, k, r0);
+  double ax1[3], p[3], qv[3], ax2[3], b[3];
+  mul0_331(ax1, s.R[J.b1], J.axis1);
+  plane_space(ax1, p, qv);
+  mul0_331(ax2, s.R[J.b2], J.axis2);
+  cross3(b, ax1, ax2);
+  for (int j = 0; j < 3; j++) {
+    s.J[r0 + 3][j] = 0; s.J[r0 + 3][3 + j] = p[j]; s.J[r0 + 3][6 + j] = 0; s.J[r0 + 3][9 + j] = -p[j];
+    s.J[r0 + 4][j] = 0; s.J[r0 + 4][3 + j] = qv[j]; s.J[r0 + 4][6 + j] = 0; s.J[r0 + 4][9 + j] = -qv[j];
+  }
+  s.rhs[r0 + 3] = k * dot3(b, p);
+  s.rhs[r0 + 4] = k * dot3(b, qv);
+  for (int r = 0; r < 5; r++) {
+    s.cfm[r0 + r] = cfm;
+    s.rtype[r0 + r] = ROW_BILATERAL;
+    s.rb1[r0 + r] = (int8_t)J.b1;
+    s.rb2[r0 + r] = (int8_t)J.b2;
+  }
+}
+
+template <class L>
+__device__ inline void fixed_rows(L& s, const hs_simjoint& J, double fps, double erp, double cfm, int r0) {
+  const double k = fps * erp;
+  // three linear rows: J1l = I, J1a = [ofs]x, J2l = -I
+  double ofs[3];
+  mul0_331(ofs, s.R[J.b1], J.offset);
+  const double rows[3][12] = {
+      {1, 0, 0, 0, -ofs[2], ofs[1], -1, 0, 0, 0, 0, 0},
+      {0, 1, 0, ofs[2], 0, -ofs[0], 0, -1, 0, 0, 0, 0},
+      {0, 0, 1, -ofs[1], ofs[0], 0, 0, 0, -1, 0, 0, 0}};
+  for (int r = 0; r < 3; r++) {
+    for (int j = 0; j < 12; j++) s.J[r0 + r][j] = rows[r][j];
+    s.rhs[r0 + r] = k * (s.pos[J.b2][r] - s.pos[J.b1][r] + ofs[r]);
+  }
+  // setFixedOrientation: rows 3..5, J1a = I, J2a = -I
+  double qq[4], qerr[4], e[3];
+  qmul1(qq, s.q[J.b1], s.q[J.b2]);
+  qmul2(qerr, qq, J.qrel);
+  if (qerr[0] < 0) { qerr[1] = -qerr[1]; qerr[2] = -qerr[2]; qerr[3] = -qerr[3]; }
+  mul0_331(e, s.R[J.b1], qerr + 1);
+  for (int r = 0; r < 3; r++) {
+    for (int j = 0; j < 12; j++) s.J[r0 + 3 + r][j] = 0;
+    s.J[r0 + 3 + r][3 + r] = 1;
+    s.J[r0 + 3 + r][9 + r] = -1;
+    s.rhs[r0 + 3 + r] = 2 * k * e[r];
+  }
+  for (int r = 0; r < 6; r++) {
+    s.cfm[r0 + r] = cfm;
+    s.rtype[r0 + r] = ROW_BILATERAL;
+    s.rb1[r0 + r] = (int8_t)J.b1;
+    s.rb2[r0 + r] = (int8_t)J.b2;
+  }
+}
+
+// contact.cpp getInfo2: body1 = the geom's body, body2 = the environment, normal (0,0,1)
+template <class L>
+__device__ inline void contact_rows(L& s, int b, const hs_sim_params& P, double fps, int r0) {
+  const double normal[3] = {0, 0, 1};
+  double c1[3];
+  for (int i = 0; i < 3; i++) c1[i] = s.cpos[b][i] - s.pos[b][i];
+  double jn[3], t1[3], t2[3], j1[3], j2[3];
+  cross3(jn, c1, normal);
+  plane_space(normal, t1, t2);
+  cross3(j1, c1, t1);
+  cross3(j2, c1, t2);
+  for (int j = 0; j < 3; j++) {
+    s.J[r0][j] = normal[j]; s.J[r0][3 + j] = jn[j];
+    s.J[r0 + 1][j] = t1[j]; s.J[r0 + 1][3 + j] = j1[j];
+    s.J[r0 + 2][j] = t2[j]; s.J[r0 + 2][3 + j] = j2[j];
+  }
+  for (int r = 0; r < 3; r++)
+    for (int j = 6; j < 12; j++) s.J[r0 + r][j] = 0;
+  const double k = fps * P.erp;
+  double depth = s.cdepth[b];
+  if (depth < 0) depth = 0;
+  double c = k * depth;
+  double outgoing = dot3(normal, s.lvel[b]) + dot3(jn, s.avel[b]);
+  if (P.bounce_vel >= 0 && (-outgoing) > P.bounce_vel) {
+    double newc = -P.bounce * outgoing;
+    if (newc > c) c = newc;
+  }
+  s.rhs[r0] = c;
+  s.rhs[r0 + 1] = 0;
+  s.rhs[r0 + 2] = 0;
+  s.cfm[r0] = P.soft_cfm;
+  s.cfm[r0 + 1] = P.cfm;
+  s.cfm[r0 + 2] = P.cfm;
+  s.rtype[r0] = ROW_NORMAL;
+  s.rtype[r0 + 1] = ROW_FRICTION;
+  s.rtype[r0 + 2] = ROW_FRICTION;
+  for (int r = 0; r < 3; r++) {
+    s.rb1[r0 + r] = (int8_t)b;
+    s.rb2[r0 + r] = -1;
+  }
+}
+
+// iMJ block of one body: linear invMass * J, angular invI * J (compute_invM_JT)
+template <class L>
+__device__ inline void imj_block(const L& s, const hs_simtopo& T, int b, const double* Jb, double* out) {
+  const double k1 = s.invm[b];
+  for (int j = 0; j < 3; j++) out[j] = k1 * Jb[j];
+  mul0_331(out + 3, s.invI[b], Jb + 3);
+}
+
+__device__ inline double swap_pair(double v) {  // value of the other lane of the pair (DPP quad_perm 1,0,3,2)
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// What one lane of a row's lane pair needs of the row: its body block of the scaled J and of
+// iMJ (half 0: body1 columns 0..5, half 1: body2 columns 6..11); the even lane also the row's
+// scalars. Nothing here changes during the sweeps, so it is loaded one run ahead of use.
+struct RowData {
+  double Js[6], iM[6], rhs, adcfm;
+  int body, b2, rt;
+};
+
+template <class L>
+__device__ inline RowData load_row(const L& s, int row, int half) {
+  RowData r;
+  const int rr = row < 0 ? 0 : row;
+  const int b1 = s.rb1[rr], b2 = s.rb2[rr];
+  r.body = row < 0 ? -1 : (half ? b2 : b1);
+  r.b2 = b2;
+  r.rt = s.rtype[rr];
+  const int c0 = half * 6;
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    r.Js[j] = s.J[rr][c0 + j];
+    r.iM[j] = s.iM[rr][c0 + j];
+  }
+  r.rhs = s.rhs[rr];
+  r.adcfm = s.cfm[rr];
+  return r;
+}
+
+// One SOR row update (SOR_LCP inner loop) on a lane pair, in ODE's operation order:
+// delta = (b - lambda Ad) - sum_body1 - sum_body2, each sum f0 J0 + f1 J1 + ... left to right;
+// the two sums are computed by the two lanes and exchanged.
+template <class L>
+__device__ inline void sor_pair(L& s, const RowData& r, int row, int half, double mu) {
+  const bool act = row >= 0 && r.body >= 0;
+  const double* f = s.fc[act ? r.body : 0];
+  const double f0 = f[0], f1 = f[1], f2 = f[2], f3 = f[3], f4 = f[4], f5 = f[5];
+  const double lam = s.lambda[row < 0 ? 0 : row];
+  double sum = f0 * r.Js[0] + f1 * r.Js[1] + f2 * r.Js[2] + f3 * r.Js[3] + f4 * r.Js[4] + f5 * r.Js[5];
+  if (!act) sum = 0;
+  const double other = swap_pair(sum);  // the body2 sum, on the even lane
+  double delta = r.rhs - lam * r.adcfm;
+  delta -= sum;
+  if (r.b2 >= 0) delta -= other;
+  const double lo = (r.rt == ROW_BILATERAL) ? -INFINITY : (r.rt == ROW_NORMAL ? 0.0 : -mu);
+  const double hi = (r.rt == ROW_BILATERAL) ? INFINITY : mu;
+  const double nl = lam + delta;
+  double newl;
+  if (nl < lo) {
+    delta = lo - lam;
+    newl = lo;
+  } else if (nl > hi) {
+    delta = hi - lam;
+    newl = hi;
+  } else {
+    newl = nl;
+  }
+  if (row >= 0 && half == 0) s.lambda[row] = newl;
+  const double d2 = swap_pair(delta);
+  if (half) delta = d2;
+  if (act) {
+    double* g = s.fc[r.body];
+    g[0] = f0 + delta * r.iM[0];
+    g[1] = f1 + delta * r.iM[1];
+    g[2] = f2 + delta * r.iM[2];
+    g[3] = f3 + delta * r.iM[3];
+    g[4] = f4 + delta * r.iM[4];
+    g[5] = f5 + delta * r.iM[5];
+  }
+}
+
+template <class L>
+__device__ inline int run_row(const L& s, int se, int pair) {  // row of a lane pair in a run, -1 = idle
+  return pair < (se >> 16) ? s.order[(se & 0xFFFF) + pair] : -1;
+}
+
+template <int NM, int MM>
+__global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restrict__ T0,
+                                                         const hs_simtopo* __restrict__ S, hs_sim_args a) {
+  __shared__ SimL<NM, MM> s;
+  const int lane = threadIdx.x;
+  const int b = blockIdx.x;
+  if (b >= a.n_rollouts) return;
+  const hs_simtopo& T = *S;
+  const int n = T.n, nmj = T.nmj, nj = T.nj, cfg = T0->cfg;
+  const hs_sim_params& P = a.params;
+  const double h = P.dt, h1 = 1.0 / h;
+#ifdef HS_SIM_STAMPS
+  unsigned long long t_last = __builtin_amdgcn_s_memtime();
+#endif
+  double* gbody = a.body + (size_t)b * n * HS_SIM_BODY;
+  // load the world
+  for (int e = lane; e < n * HS_SIM_BODY; e += WAVE) {
+    const int p = e / HS_SIM_BODY, c = e % HS_SIM_BODY;
+    const double v = gbody[e];
+    if (c < 3) s.pos[p][c] = v;
+    else if (c < 7) s.q[p][c - 3] = v;
+    else if (c < 10) s.lvel[p][c - 7] = v;
+    else s.avel[p][c - 10] = v;
+  }
+  if (lane == 0) s.seed = a.seed[b];
+  int tsi = a.tsi[b];
+  wave_sync();
+  if (lane < n) {
+    q_to_R(s.q[lane], s.R[lane]);
+    s.invm[lane] = 1.0 / T.mass[lane];
+  }
+  wave_sync();
+
+  SIM_ACC(0);
+  for (int step = 0; step < a.n_steps; step++) {
+    const size_t orow = (size_t)b * a.n_steps + step;
+    // ---- P: position control (set_position_control_torques, player.cpp:388-409)
+    if (lane < nmj) {
+      const hs_simjoint& J = T.joint[T.motor_joint[lane]];
+      const double qm = hinge_angle(s, J);
+      double tq = 0;
+      if (P.k > 0) {
+        double ax[3];
+        mul0_331(ax, s.R[J.b1], J.axis1);
+        const double rate = dot3(ax, s.avel[J.b1]) - dot3(ax, s.avel[J.b2]);
+        const int t = tsi % a.n_t;
+        const int hrow = (t + a.n_t - 2) % a.n_t;
+        const size_t tb = (size_t)b * a.n_t + hrow;
+        double a1 = qm - a.q_tab[tb * cfg + 6 + lane];
+        double a2 = rate - a.dq_tab[tb * cfg + 6 + lane];
+        if (a1 > M_PI) a1 -= 2 * M_PI;  // arrayops::modulus (core.cpp:122-131)
+        else if (a1 <= -M_PI) a1 += 2 * M_PI;
+        a1 *= -P.k;
+        a2 *= -2 * sqrt(P.k);
+        a1 += a2;
+        tq = a.tau_tab[tb * nmj + lane] + a1;
+      }
+      s.tau[lane] = tq;
+      if (a.q_meas) a.q_meas[orow * nmj + lane] = qm;
+      if (a.tau_cmd) a.tau_cmd[orow * nmj + lane] = tq;
+    }
+    wave_sync();
+    SIM_ACC(1);
+    // ---- B: per body accumulators, collision, inertia, v/h + M^-1 f
+    if (lane < n) {
+      const int p = lane;
+      double tq[3] = {0, 0, 0};
+      if (P.k > 0) {
+        for (int c = 0; c < T.tq_n[p]; c++) {  // dJointAddHingeTorque in motor order
+          const int j = T.tq_motor[p][c];
+          const hs_simjoint& J = T.joint[T.motor_joint[j]];
+          double ax[3];
+          mul0_331(ax, s.R[J.b1], J.axis1);
+          for (int i = 0; i < 3; i++) ax[i] *= s.tau[j];
+          if (T.tq_sign[p][c] > 0)
+            for (int i = 0; i < 3; i++) tq[i] += ax[i];
+          else
+            for (int i = 0; i < 3; i++) tq[i] += -ax[i];
+        }
+      }
+      // collision with the plane (0,0,1,0)
+      bool hit = false;
+      const double* R = s.R[p];
+      if (T.gtype[p] == HS_GEOM_CAPSULE) {
+        const double sign = (R[10] > 0) ? -1.0 : 1.0;  // dCalcVectorDot3_14(plane normal, R + 2)
+        double pp[3];
+        pp[0] = s.pos[p][0] + R[2] * T.glen[p] * 0.5 * sign;
+        pp[1] = s.pos[p][1] + R[6] * T.glen[p] * 0.5 * sign;
+        pp[2] = s.pos[p][2] + R[10] * T.glen[p] * 0.5 * sign;
+        const double depth = 0 - (pp[0] * 0.0 + pp[1] * 0.0 + pp[2] * 1.0) + T.gr[p];
+        if (depth >= 0) {
+          hit = true;
+          s.cpos[p][0] = pp[0] - 0.0 * T.gr[p];
+          s.cpos[p][1] = pp[1] - 0.0 * T.gr[p];
+          s.cpos[p][2] = pp[2] - 1.0 * T.gr[p];
+          s.cdepth[p] = depth;
+        }
+      } else if (T.gtype[p] == HS_GEOM_SPHERE) {
+        const double depth = 0 - (s.pos[p][0] * 0.0 + s.pos[p][1] * 0.0 + s.pos[p][2] * 1.0) + T.gr[p];
+        if (depth >= 0) {
+          hit = true;
+          s.cpos[p][0] = s.pos[p][0] - 0.0 * T.gr[p];
+          s.cpos[p][1] = s.pos[p][1] - 0.0 * T.gr[p];
+          s.cpos[p][2] = s.pos[p][2] - 1.0 * T.gr[p];
+          s.cdepth[p] = depth;
+        }
+      }
+      s.contact[p] = hit ? 1 : 0;
+      // world inverse inertia R invI_b R^T, gyroscopic torque, gravity (dxQuickStepper)
+      double Ib[12], iIb[12], tmp[12], I[12];
+      for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) { Ib[r * 4 + c] = T.inertia[p][r * 3 + c]; iIb[r * 4 + c] = T.inv_inertia[p][r * 3 + c]; }
+        Ib[r * 4 + 3] = iIb[r * 4 + 3] = 0;
+      }
+      for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) tmp[r * 4 + c] = dot3(iIb + r * 4, R + c * 4);
+      for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) s.invI[p][r * 4 + c] = dot3_14(R + r * 4, tmp + c);
+        s.invI[p][r * 4 + 3] = 0;
+      }
+      for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) tmp[r * 4 + c] = dot3(Ib + r * 4, R + c * 4);
+      for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) I[r * 4 + c] = dot3_14(R + r * 4, tmp + c);
+      double t3[3];
+      const double* w = s.avel[p];
+      mul0_331(t3, I, w);
+      tq[0] -= w[1] * t3[2] - w[2] * t3[1];
+      tq[1] -= w[2] * t3[0] - w[0] * t3[2];
+      tq[2] -= w[0] * t3[1] - w[1] * t3[0];
+      double fa[3] = {0, 0, 0};
+      if (P.gravity != 0) fa[2] += T.mass[p] * (-P.gravity);
+      const double im = s.invm[p];
+      for (int i = 0; i < 3; i++) {
+        s.facc[p][i] = fa[i];
+        s.tacc[p][i] = tq[i];
+        s.tmp1[p][i] = fa[i] * im + s.lvel[p][i] * h1;
+      }
+      double it[3];
+      mul0_331(it, s.invI[p], tq);
+      for (int i = 0; i < 3; i++) s.tmp1[p][3 + i] = it[i] + w[i] * h1;
+      for (int i = 0; i < 6; i++) s.fc[p][i] = 0;
+    }
+    wave_sync();
+    SIM_ACC(2);
+    // ---- row offsets in island order (dxProcessIslands: per visited body, its contact
+    // first -- the newest joint in its list -- then the static joints first reached from it)
+    if (lane == 0) {
+      int off = 0, nc = 0;
+      for (int v = 0; v < n; v++) {
+        const int bv = T.border[v];
+        if (s.contact[bv]) { s.coff[bv] = (int16_t)off; off += (P.mu > 0) ? 3 : 1; nc++; }
+        for (int k = T.jseq_start[v]; k < T.jseq_start[v + 1]; k++) {
+          const int jid = T.jseq[k];
+          s.joff[jid] = (int16_t)off;
+          off += (T.joint[jid].type == HS_SJ_HINGE) ? 5 : 6;
+        }
+      }
+      s.m = off;
+      s.nc = nc;
+    }
+    wave_sync();
+    SIM_ACC(3);
+    const int m = s.m;
+    // ---- R: getInfo2 of every joint
+    if (lane < nj) {
+      const hs_simjoint& J = T.joint[lane];
+      if (J.type == HS_SJ_HINGE) hinge_rows(s, J, h1, P.erp, P.cfm, s.joff[lane]);
+      else fixed_rows(s, J, h1, P.erp, P.cfm, s.joff[lane]);
+    } else if (lane < nj + n) {
+      const int p = lane - nj;
+      if (s.contact[p]) contact_rows(s, p, P, h1, s.coff[p]);
+    }
+    wave_sync();
+    SIM_ACC(4);
+    // ---- A: rhs, CFM / h, Ad (SOR_LCP prologue)
+    for (int i = lane; i < m; i += WAVE) {
+      const int b1 = s.rb1[i], b2 = s.rb2[i];
+      double Jr[12];
+      for (int j = 0; j < 12; j++) Jr[j] = s.J[i][j];
+      double sum = 0;
+      for (int j = 0; j < 6; j++) sum += Jr[j] * s.tmp1[b1][j];
+      if (b2 >= 0)
+        for (int j = 0; j < 6; j++) sum += Jr[6 + j] * s.tmp1[b2][j];
+      const double rhs = s.rhs[i] * h1 - sum;
+      const double cfm = s.cfm[i] * h1;
+      double iM[6], dsum = 0;
+      imj_block(s, T, b1, Jr, iM);
+      for (int j = 0; j < 6; j++) dsum += iM[j] * Jr[j];
+      if (b2 >= 0) {
+        imj_block(s, T, b2, Jr + 6, iM);
+        for (int j = 0; j < 6; j++) dsum += iM[j] * Jr[6 + j];
+      }
+      const double ad = P.sor_w / (dsum + cfm);
+      imj_block(s, T, b1, Jr, s.iM[i]);
+      if (b2 >= 0) imj_block(s, T, b2, Jr + 6, s.iM[i] + 6);
+      else
+        for (int j = 6; j < 12; j++) s.iM[i][j] = 0;
+      for (int j = 0; j < 12; j++) s.J[i][j] *= ad;
+      s.Ad[i] = ad;
+      s.rhs[i] = rhs * ad;
+      s.cfm[i] = ad * cfm;
+      s.lambda[i] = 0;
+    }
+    wave_sync();
+    SIM_ACC(5);
+    // ---- G: SOR sweeps
+    {
+      const int pair = lane >> 1, half = lane & 1;
+      for (int i = lane; i < m; i += WAVE) s.order[i] = (int16_t)i;  // findex all -1: identity order
+      uint32_t seed = __builtin_amdgcn_readfirstlane(s.seed);
+      for (int it0 = 0; it0 < P.iterations; it0 += 8) {
+        // RANDOMLY_REORDER_CONSTRAINTS: Fisher-Yates with dRandInt. The draws are independent given
+        // the jump-ahead tables (all lanes); the swaps are a chain (lane 0).
+        for (int i = lane + 1; i < m; i += WAVE) {
+          uint32_t sd = T.lcg_a[i] * seed + T.lcg_c[i];
+          s.swp[i] = (int16_t)rand_int_from(sd, i + 1);
+        }
+        if (m > 1) seed = T.lcg_a[m - 1] * seed + T.lcg_c[m - 1];
+        wave_sync();
+        if (lane == 0) {
+          for (int i = 1; i < m; i++) {
+            const int sw = s.swp[i];
+            const int16_t t = s.order[i];
+            s.order[i] = s.order[sw];
+            s.order[sw] = t;
+          }
+        }
+        wave_sync();
+        for (int p = lane; p < m; p += WAVE) {
+          const int row = s.order[p];
+          s.mask[p] = (1u << s.rb1[row]) | (s.rb2[row] >= 0 ? (1u << s.rb2[row]) : 0u);
+        }
+        wave_sync();
+        if (lane == 0) {  // maximal runs of body-disjoint rows
+          int nb = 0, start = 0;
+          uint32_t used = 0;
+          for (int p = 0; p < m; p++) {
+            const uint32_t mk = s.mask[p];
+            if (used & mk) {
+              s.run_se[nb++] = start | ((p - start) << 16);
+              start = p;
+              used = 0;
+            }
+            used |= mk;
+          }
+          s.run_se[nb++] = start | ((m - start) << 16);
+          s.nruns = nb;
+        }
+        wave_sync();
+        SIM_ACC(6);
+        // sweeps it0 .. it0+7 over the same runs, software-pipelined: while run t is solved, the
+        // row data of run t+1, the rows of run t+2 and the bounds of run t+3 are loaded
+        const int nb = __builtin_amdgcn_readfirstlane(s.nruns);
+        const int total = min(8, P.iterations - it0) * nb;
+        int k2 = (2 % nb), k3 = (3 % nb);
+        int se2 = __builtin_amdgcn_readfirstlane(s.run_se[k2]);
+        int row0 = run_row(s, __builtin_amdgcn_readfirstlane(s.run_se[0]), pair);
+        int row1 = run_row(s, __builtin_amdgcn_readfirstlane(s.run_se[1 % nb]), pair);
+        RowData d0 = load_row(s, row0, half);
+        for (int t = 0; t < total; t++) {
+          const RowData d1 = load_row(s, row1, half);
+          const int row2 = run_row(s, se2, pair);
+          const int se3 = __builtin_amdgcn_readfirstlane(s.run_se[k3]);
+          sor_pair(s, d0, row0, half, P.mu);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+          d0 = d1;
+          row0 = row1;
+          row1 = row2;
+          se2 = se3;
+          k3 = (k3 + 1 == nb) ? 0 : k3 + 1;
+        }
+        wave_sync();
+        SIM_ACC(7);
+#ifdef HS_SIM_STAMPS
+        if (lane == 0 && blockIdx.x < 4096) g_sim_stamps[blockIdx.x][9] += nb;
+#endif
+      }
+      if (lane == 0) s.seed = seed;
+    }
+    // ---- U: velocities (constraint part, then external forces) and dxStepBody
+    if (lane < n) {
+      const int p = lane;
+      for (int j = 0; j < 3; j++) s.lvel[p][j] += h * s.fc[p][j];
+      for (int j = 0; j < 3; j++) s.avel[p][j] += h * s.fc[p][3 + j];
+      const double hm = h * s.invm[p];
+      double ta[3];
+      for (int j = 0; j < 3; j++) {
+        s.lvel[p][j] += hm * s.facc[p][j];
+        ta[j] = s.tacc[p][j] * h;
+      }
+      double t3[3];
+      mul0_331(t3, s.invI[p], ta);
+      for (int j = 0; j < 3; j++) s.avel[p][j] += t3[j];
+      for (int j = 0; j < 3; j++) s.pos[p][j] += h * s.lvel[p][j];
+      const double* w = s.avel[p];
+      double* qv = s.q[p];
+      double dq[4];
+      dq[0] = 0.5 * (-w[0] * qv[1] - w[1] * qv[2] - w[2] * qv[3]);
+      dq[1] = 0.5 * (w[0] * qv[0] + w[1] * qv[3] - w[2] * qv[2]);
+      dq[2] = 0.5 * (-w[0] * qv[3] + w[1] * qv[0] + w[2] * qv[1]);
+      dq[3] = 0.5 * (w[0] * qv[2] - w[1] * qv[1] + w[2] * qv[0]);
+      for (int j = 0; j < 4; j++) qv[j] += h * dq[j];
+      normalize4(qv);
+      q_to_R(qv, s.R[p]);
+    }
+    if (lane == 0) {
+      if (a.n_contacts) a.n_contacts[orow] = s.nc;
+      if (a.normal_force) {
+        double fsum = 0;
+        for (int v = 0; v < n; v++) {
+          const int bv = T.border[v];
+          if (s.contact[bv]) fsum += s.lambda[s.coff[bv]];
+        }
+        a.normal_force[orow] = fsum;
+      }
+    }
+    wave_sync();
+    if (a.torso && lane < 3) a.torso[orow * 3 + lane] = s.pos[0][lane];
+    tsi++;
+    SIM_ACC(8);
+#ifdef HS_SIM_STAMPS
+    if (lane == 0 && blockIdx.x < 4096) g_sim_stamps[blockIdx.x][10] += m;
+#endif
+  }
+  // store the world
+  for (int e = lane; e < n * HS_SIM_BODY; e += WAVE) {
+    const int p = e / HS_SIM_BODY, c = e % HS_SIM_BODY;
+    double v;
+    if (c < 3) v = s.pos[p][c];
+    else if (c < 7) v = s.q[p][c - 3];
+    else if (c < 10) v = s.lvel[p][c - 7];
+    else v = s.avel[p][c - 10];
+    gbody[e] = v;
+  }
+  if (lane == 0) {
+    a.seed[b] = s.seed;
+    a.tsi[b] = tsi;
+  }
+}
+
+// init_play_config + orient_odebodys: lane = part, A_ground by walking the chain from the root
+// (each product in the reference's order: J_A_ground = A_parent J_A_parent, then * E(q) * A_pj_body)
+__global__ __launch_bounds__(WAVE) void hs_sim_reset_kernel(const hs_topo* __restrict__ T, const hs_simtopo* __restrict__ S,
+                                                             int32_t n_rollouts, const double* __restrict__ config,
+                                                             int32_t stride, double* __restrict__ body) {
+  using namespace hsd;
+  const int b = blockIdx.x, p = threadIdx.x;
+  if (b >= n_rollouts || p >= T->n) return;
+  const double* cf = config + (size_t)b * stride;
+  int chain[HS_NMAX], len = 0;
+  for (int a = p; a >= 0; a = T->node[a].parent) chain[len++] = a;
+  A34 A;
+  for (int i = 0; i < 12; i++) A.m[i] = (i % 4 == 0) ? 1.0 : 0.0;  // unity (columns 0..2 of I, zero translation)
+  for (int k = len - 1; k >= 0; k--) {
+    const hs_node& nd = T->node[chain[k]];
+    if (nd.jtype == HS_J_FREE) {
+      A34 JA = mul(A, load34(nd.J_A_parent));
+      A = mul(mul(JA, free_joint(cf)), load34(nd.A_pj_body));
+    } else if (nd.jtype == HS_J_HINGE) {
+      A34 JA = mul(A, load34(nd.J_A_parent));
+      A = mul(mul(JA, hinge_joint(cf[6 + nd.hinge])), load34(nd.A_pj_body));
+    } else {
+      A = mul(A, load34(nd.A_pj_body));
+    }
+  }
+  A34 G = mul(A, load34(S->body_geom[p]));
+  double Rin[12], q[4], R[12];
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) Rin[r * 4 + c] = G(r, c);
+    Rin[r * 4 + 3] = 0;
+  }
+  q_from_R(q, Rin);
+  normalize4(q);
+  double* o = body + ((size_t)b * T->n + p) * HS_SIM_BODY;
+  for (int i = 0; i < 3; i++) o[i] = G(i, 3);
+  for (int i = 0; i < 4; i++) o[3 + i] = q[i];
+  for (int i = 7; i < 13; i++) o[i] = 0;
+  (void)R;
+}
+
+}  // namespace
+
+#ifdef HS_SIM_STAMPS
+extern "C" int hs_debug_read_sim_stamps(unsigned long long* out, int n_rows) {
+  if (n_rows > 4096) n_rows = 4096;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sim_stamps), sizeof(unsigned long long) * 12 * n_rows, 0,
+                                  hipMemcpyDeviceToHost);
+}
+extern "C" int hs_debug_clear_sim_stamps() {
+  static unsigned long long zero[4096][12];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_sim_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+#endif
+
+namespace hs {
+
+int launch_sim_reset(const hs_topo* d_topo, const hs_simtopo* d_sim, int32_t n_rollouts, const double* config,
+                     int32_t config_stride, double* body, void* stream) {
+  if (n_rollouts <= 0) return 0;
+  hipLaunchKernelGGL(hs_sim_reset_kernel, dim3(n_rollouts), dim3(WAVE), 0, (hipStream_t)stream, d_topo, d_sim,
+                     n_rollouts, config, config_stride, body);
+  return (int)hipGetLastError();
+}
+
+int launch_sim_steps(const hs_topo* d_topo, const hs_simtopo* d_sim, const hs_simtopo& hs, const hs_sim_args& a) {
+  if (a.n_rollouts <= 0 || a.n_steps <= 0) return 0;
+  hipStream_t st = (hipStream_t)a.stream;
+  // smallest LDS layout holding the model: parts and rows (6 per fixed, 5 per hinge, 3 per contact)
+  if (hs.n <= 18 && hs.m_max <= 144)
+    hipLaunchKernelGGL((hs_sim_kernel<18, 144>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
+  else if (hs.n <= 22 && hs.m_max <= 176)
+    hipLaunchKernelGGL((hs_sim_kernel<22, 176>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
+  else if (hs.n <= HS_NMAX && hs.m_max <= 9 * HS_NMAX)
+    hipLaunchKernelGGL((hs_sim_kernel<HS_NMAX, 9 * HS_NMAX>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+}  // namespace hs

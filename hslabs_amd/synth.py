@@ -85,3 +85,12 @@ def gen_mixed(n: int, id0: int = 0, curved: bool = False, seed: int = SEED):
     other = gen_params(n, MIXED_MODELS[1], id0, curved, seed)
     out[idx == 1] = other[idx == 1]
     return out, idx
+
+
+def gen_sim_params(n: int, model: str = "hexapod", id0: int = 0, period: float = 3.0, seed: int = SEED) -> np.ndarray:
+    """Closed-loop simulation batches: gen_params with one period for the whole batch, so every
+    rollout's controller table has the same length n_t = int(T / play_dt + .5)
+    (setup_per_controller, player.cpp:370-382; pgs id 8 has T = 3 -> n_t = 300 at play_dt = .01)."""
+    arr = gen_params(n, model, id0, False, seed)
+    arr["period"] = period
+    return arr

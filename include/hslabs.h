@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 3
+#define HSLABS_ABI_VERSION 4
 
 enum {
   HS_OK = 0,
@@ -217,6 +217,79 @@ int hs_traj_save(const char* path, const double* rec, int32_t n_rows, int32_t re
  * NaN COT maps to the largest key. Initial value for a reduction: UINT64_MAX. */
 uint64_t hs_best_key_encode(double cot, int64_t rollout_id);
 void hs_best_key_decode(uint64_t key, float* cot, int64_t* rollout_id);
+
+/*
+ * Closed-loop simulation: modelplayer::simulate_ode with position control
+ * (player.cpp:325-339) for a batch of independent robots, each in its own ODE
+ * world as the reference sets it up (visualization.cpp:140-150: gravity 1,
+ * ERP .8, a z = 0 plane; one body per part with ODE's default mass, hinge and
+ * fixed joints from kinematicmodel::set_ode_joints, model.cpp:375-400). One
+ * step is
+ *   set_position_control_torques (player.cpp:388-432): targets and
+ *     feedforward torques of the controller tables at tsi, measured hinge
+ *     angles / rates (dJointGetHingeAngle/Rate), k1 = -k, k2 = -2 sqrt(k);
+ *   dJointAddHingeTorque for every motor (visualization.cpp:350-356);
+ *   dSpaceCollide + nearCallback (visualization.cpp:296-326): one contact per
+ *     capsule / sphere touching the plane, Bounce|SoftCFM, mu = inf;
+ *   dWorldQuickStep (visualization.cpp:333-337): the projected Gauss-Seidel
+ *     (SOR-LCP) constraint solve, `iterations` sweeps with ODE's random
+ *     reordering every 8 sweeps, then the semi-implicit body update;
+ *   tsi += 1 (play_t += play_dt).
+ * The ODE formulas are restated from ODE 0.13 (the reference links an
+ * unpinned -lode); see DESIGN.md.
+ */
+#define HS_SIM_BODY_STRIDE 13 /* per part: pos[3], quaternion (w,x,y,z)[4], lvel[3], avel[3] */
+
+typedef struct {
+  double dt;          /* play_dt (player.cpp:23: 0.01) */
+  double k;           /* position gain (player.cpp:393: 100); <= 0: no position control */
+  double sor_w;       /* dWorldSetQuickStepW (ODE default 1.3) */
+  double erp;         /* dWorldSetERP (visualization.cpp:146: 0.8) */
+  double cfm;         /* global CFM (ODE double-precision default 1e-10) */
+  double gravity;     /* visualization.cpp:144: 1 */
+  double bounce;      /* nearCallback surface (visualization.cpp:310-320): .5 */
+  double bounce_vel;  /* .1 */
+  double soft_cfm;    /* .001 */
+  double mu;          /* dInfinity */
+  int32_t iterations; /* dWorldSetQuickStepNumIterations (ODE default 20) */
+  int32_t reserved;
+} hs_sim_params;
+
+/* The reference's values (above). */
+void hs_sim_default_params(hs_sim_params* p);
+
+/* init_play_config (player.cpp:351-356) + orient_odebodys (model.cpp:295-305):
+ * body states of B configurations (joint values, config [B][config_stride],
+ * DEVICE), zero velocities. body: DEVICE [B][n_parts][HS_SIM_BODY_STRIDE]. */
+int hs_sim_reset(hs_model_t model, int32_t n_rollouts, const double* config, int32_t config_stride, double* body,
+                 void* stream);
+
+typedef struct {
+  int32_t n_rollouts;
+  int32_t n_steps;         /* simulation steps of this call (one launch runs them all) */
+  int32_t n_t;             /* controller table rows (setup_per_controller: int(T / play_dt + .5)) */
+  int32_t reserved;
+  hs_sim_params params;
+  /* per-rollout state, DEVICE, read and advanced */
+  double* body;            /* [B][n_parts][HS_SIM_BODY_STRIDE] */
+  uint32_t* seed;          /* [B] ODE dRand state (dRandInt reshuffles of the SOR rows) */
+  int32_t* tsi;            /* [B] play step index, int(play_t / play_dt + .5) */
+  /* controller tables, DEVICE: exactly what hs_run writes with k0 = 0, H = n_t (row h = trajectory
+     sample h + 2; get_motor_adas / get_computed_torques of tsi read row (tsi mod n_t + n_t - 2) mod n_t) */
+  const double* q_tab;     /* [B][n_t][config_dim] (hs_run_args.q) */
+  const double* dq_tab;    /* [B][n_t][config_dim] (hs_run_args.dq) */
+  const double* tau_tab;   /* [B][n_t][nmj] (hs_run_args.tau) */
+  /* optional per-step outputs, DEVICE (NULL to skip) */
+  double* tau_cmd;         /* [B][n_steps][nmj] motor torques applied */
+  double* q_meas;          /* [B][n_steps][nmj] hinge angles at the start of the step */
+  double* torso;           /* [B][n_steps][3] root body position after the step */
+  int32_t* n_contacts;     /* [B][n_steps] */
+  double* normal_force;    /* [B][n_steps] sum of the contact normal constraint forces */
+  void* stream;            /* hipStream_t */
+} hs_sim_args;
+
+/* n_steps closed-loop steps of every rollout, one launch (state stays on chip between steps). */
+int hs_sim_step(hs_model_t model, const hs_sim_args* args);
 
 const char* hs_last_error(void);
 int hs_abi_version(void);

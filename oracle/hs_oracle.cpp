@@ -304,6 +304,8 @@ struct Node {
   Aff A_body_geom;
   Vec capsule_to_pos;
   double rcap = 0;
+  int gtype = 0;          // dGeomGetClass of the part's geom: 0 none, 1 sphere, 2 capsule, 3 cylinder
+  double gr = 0, glen = 0;  // radius, cylinder length (dCreateSphere / dCreateCapsule, visualization.cpp:459,486)
   std::string name;
 };
 
@@ -397,6 +399,9 @@ void make_ccylinder(Node& nd, const XNode* g, bool capped) {
   nd.capsule_to_pos.set(fromto + 3);
   affine_from_posrot(nd.A_body_geom, pos, rot);
   if (capped) nd.rcap = r;
+  nd.gtype = capped ? 2 : 3;
+  nd.gr = r;
+  nd.glen = r2.norm();
 }
 
 // kinematicmodel::mnode_from_xnode, model.cpp:246-260 (+ make_odepart 264-271, make_joint 272-289)
@@ -423,6 +428,8 @@ int mnode_from_xnode(hso_model* m, const XNode* x, const Aff& A, int parent) {
         if (const char* s = g->attr("size")) str_to_vals(s, &r, 1);
         if (const char* s = g->attr("pos")) str_to_vals(s, gp, 3);
         nd.A_body_geom.set_translation(gp);
+        nd.gtype = 1;
+        nd.gr = r;
       } else if (type == "capsule") {
         make_ccylinder(nd, g, true);
       } else if (type == "cylinder") {
@@ -2193,3 +2200,6 @@ int hso_residuals(const hso_model* m0, const hso_gait* g, int n_t, int step, int
 }
 
 }  // extern "C"
+
+// closed-loop simulation restatement (same translation unit: uses the model code above)
+#include "hs_oracle_sim.cpp"

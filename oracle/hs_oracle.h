@@ -106,6 +106,23 @@ int hso_dynrec_dump(const hso_model* m, const hso_gait* g, int n_t, int step, do
                     double* jz, double* mom_rate, double* amr, double* fpos, int32_t* contacts,
                     int32_t* parents, int32_t* footis, int32_t* hinge_ids);
 
+/* ---- closed-loop simulation (hs_oracle_sim.cpp): modelplayer::simulate_ode with position
+ * control on a restated ODE 0.13 dWorldQuickStep (player.cpp:325-339, visualization.cpp:296-337).
+ * Body state rows: pos[3], quaternion (w,x,y,z)[4], lvel[3], avel[3] per part (preorder). */
+/* init_play_config (player.cpp:351-356): configuration -> body states (zero velocities) */
+int hso_sim_reset(const hso_model* m, const double* config, double* body);
+/* dJointGetHingeAngle / Rate of every motor for a body state */
+int hso_sim_hinges(const hso_model* m, const double* body, double* q, double* dq);
+/* n_steps simulation steps of one rollout. p10 = dt, k, sor_w, erp, cfm, gravity, bounce,
+ * bounce_vel, soft_cfm, mu. Tables as hs_run writes them with k0 = 0, H = n_t:
+ * q_tab/dq_tab [n_t][config_dim], tau_tab [n_t][nmj] (row h = trajectory sample h + 2).
+ * seed: dRand state, tsi: play step index; both advanced. Outputs per step (may be NULL):
+ * tau_cmd/q_meas [n_steps][nmj], torso [n_steps][3], n_contacts [n_steps], normal_force [n_steps]. */
+int hso_sim_run(const hso_model* m, const double* p10, int iterations, int n_t, const double* q_tab,
+                const double* dq_tab, const double* tau_tab, double* body, uint32_t* seed, int32_t* tsi,
+                int n_steps, double* tau_cmd, double* q_meas, double* torso, int32_t* n_contacts,
+                double* normal_force);
+
 #ifdef __cplusplus
 }
 #endif

@@ -155,6 +155,11 @@ def lib():
         ip = ctypes.POINTER(ctypes.c_int32)
         L.hso_dynrec_dump.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int,
                                       dp, dp, dp, dp, dp, dp, ip, ip, ip, ip]
+        up = ctypes.POINTER(ctypes.c_uint32)
+        L.hso_sim_reset.argtypes = [ctypes.c_void_p, dp, dp]
+        L.hso_sim_hinges.argtypes = [ctypes.c_void_p, dp, dp, dp]
+        L.hso_sim_run.argtypes = [ctypes.c_void_p, dp, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, up, ip,
+                                  ctypes.c_int, dp, dp, dp, ip, dp]
         _lib = L
     return _lib
 
@@ -321,4 +326,81 @@ def dynrec_dump(model: Model, gait: GaitParams, n_t: int, step: int) -> dict:
     if k < 0:
         raise RuntimeError("dynrec_dump failed")
     out["k"] = k
+    return out
+
+
+# ---------------------------------------------------------------------------
+# closed-loop simulation (hs_oracle_sim.cpp): simulate_ode with position control on a
+# restated ODE 0.13 QuickStep (player.cpp:325-339, visualization.cpp:140-150, 296-337)
+# ---------------------------------------------------------------------------
+SIM_BODY = 13  # pos[3], quaternion[4], lvel[3], avel[3]
+
+
+@dataclass
+class SimParams:
+    dt: float = 0.01           # modelplayer::play_dt (player.cpp:23)
+    k: float = 100.0           # set_position_control_torques (player.cpp:393)
+    sor_w: float = 1.3         # ODE default dWorldSetQuickStepW
+    erp: float = 0.8           # dWorldSetERP (visualization.cpp:146)
+    cfm: float = 1e-10         # ODE dDOUBLE default global CFM (visualization.cpp:147 leaves it)
+    gravity: float = 1.0       # visualization.cpp:144
+    bounce: float = 0.5        # nearCallback surface (visualization.cpp:310-320)
+    bounce_vel: float = 0.1
+    soft_cfm: float = 0.001
+    mu: float = float("inf")
+    iterations: int = 20       # ODE default dWorldSetQuickStepNumIterations
+
+    def p10(self) -> np.ndarray:
+        return np.array([self.dt, self.k, self.sor_w, self.erp, self.cfm, self.gravity, self.bounce,
+                         self.bounce_vel, self.soft_cfm, self.mu], dtype=np.float64)
+
+
+def sim_reset(model: Model, config) -> np.ndarray:
+    """init_play_config (player.cpp:351-356): body states [n][13] of a configuration."""
+    c = np.ascontiguousarray(config, dtype=np.float64)
+    body = np.zeros((model.n, SIM_BODY))
+    lib().hso_sim_reset(model.handle, _ptr(c), _ptr(body))
+    return body
+
+
+def sim_hinges(model: Model, body):
+    b = np.ascontiguousarray(body, dtype=np.float64)
+    q = np.zeros(model.nmj)
+    dq = np.zeros(model.nmj)
+    lib().hso_sim_hinges(model.handle, _ptr(b), _ptr(q), _ptr(dq))
+    return q, dq
+
+
+def controller_tables(model: Model, gait: GaitParams, n_t: int, ignore_reach: bool = True):
+    """setup_per_controller tables (player.cpp:370-382) in hs_run's layout (k0 = 0, H = n_t):
+    q_tab/dq_tab [n_t][cfg] = trajectory sample h + 2 and its compute_vel_traj rates, tau_tab [n_t][nmj]."""
+    r = rollout(model, gait, n_t, k0=0, H=n_t, basis=BASIS_FAST, ignore_reach=ignore_reach)
+    q = r["q"]
+    d = q[3:n_t + 3] - q[1:n_t + 1]
+    d = np.where(d > np.pi, d - 2 * np.pi, np.where(d < -np.pi, d + 2 * np.pi, d))
+    dt = gait.period / n_t
+    return q[2:n_t + 2].copy(), d / (2 * dt), r["tau"].copy()
+
+
+def sim_run(model: Model, params: SimParams, n_t: int, q_tab, dq_tab, tau_tab, body, seed: int, tsi: int,
+            n_steps: int) -> dict:
+    """n_steps of modelplayer::simulate_ode for one rollout. Returns the new state and per-step outputs."""
+    body = np.array(body, dtype=np.float64, copy=True)
+    q_tab = np.ascontiguousarray(q_tab, dtype=np.float64)
+    dq_tab = np.ascontiguousarray(dq_tab, dtype=np.float64)
+    tau_tab = np.ascontiguousarray(tau_tab, dtype=np.float64)
+    sd = np.array([seed], dtype=np.uint32)
+    ts = np.array([tsi], dtype=np.int32)
+    out = dict(tau_cmd=np.zeros((n_steps, model.nmj)), q_meas=np.zeros((n_steps, model.nmj)),
+               torso=np.zeros((n_steps, 3)), n_contacts=np.zeros(n_steps, np.int32),
+               normal_force=np.zeros(n_steps))
+    p10 = params.p10()
+    ip = ctypes.POINTER(ctypes.c_int32)
+    rc = lib().hso_sim_run(model.handle, _ptr(p10), params.iterations, n_t, _ptr(q_tab), _ptr(dq_tab),
+                           _ptr(tau_tab), _ptr(body), sd.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                           ts.ctypes.data_as(ip), n_steps, _ptr(out["tau_cmd"]), _ptr(out["q_meas"]),
+                           _ptr(out["torso"]), out["n_contacts"].ctypes.data_as(ip), _ptr(out["normal_force"]))
+    if rc != 0:
+        raise RuntimeError(f"oracle sim_run failed rc={rc}")
+    out.update(body=body, seed=int(sd[0]), tsi=int(ts[0]))
     return out
