@@ -21,8 +21,9 @@
 //      maximal runs of body-disjoint rows and a run is solved by one lane per row:
 //      the sequential semantics (and ODE's per-row operation order) are kept;
 //   U  lane = body: velocity update and dxStepBody.
-// M^-1 J^T (ODE's iMJ) is recomputed from J where it is used instead of stored,
-// which halves the row storage: LDS per hexapod rollout ~ 33 KB.
+// M^-1 J^T (ODE's iMJ) and the Ad-scaled J are recomputed from J where they are
+// used (same single roundings as ODE's stored copies), which keeps the row storage
+// at one J: LDS per hexapod rollout ~ 35 KB, 4 rollouts per CU.
 //
 // Every formula follows oracle/hs_oracle_sim.cpp (the CPU restatement, test
 // infrastructure) in the same operation order, and this file is compiled
@@ -70,24 +71,25 @@ __device__ unsigned long long g_sim_stamps[4096][12];
 template <int NM, int MM>
 struct SimL {
   // bodies (part ids index everything; ODE's island numbering does not change any arithmetic)
-  double pos[NM][3], q[NM][4], R[NM][12], lvel[NM][3], avel[NM][3], facc[NM][3], tacc[NM][3];
+  double pos[NM][3], q[NM][4], R[NM][12], lvel[NM][3], avel[NM][3], tacc[NM][3];
   double invI[NM][12];
   double invm[NM];         // 1 / mass, kept on chip: the SOR rows read it for every update
-  double tmp1[NM][6], fc[NM][6];
+  double fc[NM][6];        // v/h + M^-1 f while the rows are built (ODE's tmp1), then SOR's fc
   double cpos[NM][3], cdepth[NM];
   double tau[NM];
   // constraint rows
-  double J[MM][12];        // Jacobian rows; scaled by Ad before the sweeps (SOR_LCP "scale J and b by Ad")
-  double iM[MM][12];       // M^-1 J^T rows (compute_invM_JT), from the unscaled J
+  double J[MM][12];        // Jacobian rows (unscaled: the sweeps form J Ad and M^-1 J^T per use)
   double rhs[MM];          // c, then rhs, then rhs * Ad
   double cfm[MM];          // cfm, then cfm / h, then Ad * cfm
   double Ad[MM];
   double lambda[MM];
   int8_t rb1[MM], rb2[MM], rtype[MM];
-  int16_t order[MM];       // row at each sweep position
-  int16_t swp[MM];         // Fisher-Yates swap targets of a reshuffle
-  uint32_t mask[MM];       // body bit mask of the row at each position
-  int32_t run_se[MM];      // runs of body-disjoint rows: start | length << 16
+  int16_t order[MM];       // row at each sweep position (ODE's order)
+  int16_t sched[MM];       // rows grouped by level
+  int16_t lv[MM];          // level of each position
+  int32_t cnt[MM];         // rows per level
+  uint64_t bmask[NM][4];   // positions touching each body
+  int32_t run_se[MM];      // levels: start in sched | length << 16
   int16_t joff[HS_SIM_JMAX], coff[NM];
   int8_t contact[NM];
   int32_t m, nc, nruns;
@@ -254,61 +256,67 @@ __device__ inline RowData load_row(const L& s, int row, int half) {
   r.b2 = b2;
   r.rt = s.rtype[rr];
   const int c0 = half * 6;
+  const int bb = r.body < 0 ? 0 : r.body;
+  double Jb[6];
 #pragma unroll
-  for (int j = 0; j < 6; j++) {
-    r.Js[j] = s.J[rr][c0 + j];
-    r.iM[j] = s.iM[rr][c0 + j];
-  }
+  for (int j = 0; j < 6; j++) Jb[j] = s.J[rr][c0 + j];
+  const double ad = s.Ad[rr];
+#pragma unroll
+  for (int j = 0; j < 6; j++) r.Js[j] = Jb[j] * ad;  // SOR_LCP: J *= Ad
+  // compute_invM_JT: invMass J (linear), invI J (angular)
+  const double k1 = s.invm[bb];
+  for (int j = 0; j < 3; j++) r.iM[j] = k1 * Jb[j];
+  mul0_331(r.iM + 3, s.invI[bb], Jb + 3);
   r.rhs = s.rhs[rr];
   r.adcfm = s.cfm[rr];
   return r;
 }
 
-// One SOR row update (SOR_LCP inner loop) on a lane pair, in ODE's operation order:
+// One SOR row update (SOR_LCP inner loop) on a lane pair, in ODE's order of operations:
 // delta = (b - lambda Ad) - sum_body1 - sum_body2, each sum f0 J0 + f1 J1 + ... left to right;
-// the two sums are computed by the two lanes and exchanged.
+// the two sums are computed by the two lanes and exchanged. The multiply-adds of the sums and
+// of the fc update are fused here (explicit fma; the file is otherwise unfused), which moves
+// lambda by ulps against the unfused restatement and never decides a contact.
 template <class L>
 __device__ inline void sor_pair(L& s, const RowData& r, int row, int half, double mu) {
   const bool act = row >= 0 && r.body >= 0;
   const double* f = s.fc[act ? r.body : 0];
   const double f0 = f[0], f1 = f[1], f2 = f[2], f3 = f[3], f4 = f[4], f5 = f[5];
   const double lam = s.lambda[row < 0 ? 0 : row];
-  double sum = f0 * r.Js[0] + f1 * r.Js[1] + f2 * r.Js[2] + f3 * r.Js[3] + f4 * r.Js[4] + f5 * r.Js[5];
+  double sum = f0 * r.Js[0];
+  sum = fma(f1, r.Js[1], sum);
+  sum = fma(f2, r.Js[2], sum);
+  sum = fma(f3, r.Js[3], sum);
+  sum = fma(f4, r.Js[4], sum);
+  sum = fma(f5, r.Js[5], sum);
   if (!act) sum = 0;
   const double other = swap_pair(sum);  // the body2 sum, on the even lane
   double delta = r.rhs - lam * r.adcfm;
   delta -= sum;
-  if (r.b2 >= 0) delta -= other;
+  delta -= (r.b2 >= 0) ? other : 0.0;  // x - 0.0 == x
   const double lo = (r.rt == ROW_BILATERAL) ? -INFINITY : (r.rt == ROW_NORMAL ? 0.0 : -mu);
   const double hi = (r.rt == ROW_BILATERAL) ? INFINITY : mu;
   const double nl = lam + delta;
-  double newl;
-  if (nl < lo) {
-    delta = lo - lam;
-    newl = lo;
-  } else if (nl > hi) {
-    delta = hi - lam;
-    newl = hi;
-  } else {
-    newl = nl;
-  }
+  const bool below = nl < lo, above = !below && nl > hi;
+  const double newl = below ? lo : (above ? hi : nl);
+  delta = (below || above) ? newl - lam : delta;
   if (row >= 0 && half == 0) s.lambda[row] = newl;
   const double d2 = swap_pair(delta);
   if (half) delta = d2;
   if (act) {
     double* g = s.fc[r.body];
-    g[0] = f0 + delta * r.iM[0];
-    g[1] = f1 + delta * r.iM[1];
-    g[2] = f2 + delta * r.iM[2];
-    g[3] = f3 + delta * r.iM[3];
-    g[4] = f4 + delta * r.iM[4];
-    g[5] = f5 + delta * r.iM[5];
+    g[0] = fma(delta, r.iM[0], f0);
+    g[1] = fma(delta, r.iM[1], f1);
+    g[2] = fma(delta, r.iM[2], f2);
+    g[3] = fma(delta, r.iM[3], f3);
+    g[4] = fma(delta, r.iM[4], f4);
+    g[5] = fma(delta, r.iM[5], f5);
   }
 }
 
 template <class L>
-__device__ inline int run_row(const L& s, int se, int pair) {  // row of a lane pair in a run, -1 = idle
-  return pair < (se >> 16) ? s.order[(se & 0xFFFF) + pair] : -1;
+__device__ inline int run_row(const L& s, int se, int pair) {  // row of a lane pair in a level, -1 = idle
+  return pair < (se >> 16) ? s.sched[(se & 0xFFFF) + pair] : -1;
 }
 
 template <int NM, int MM>
@@ -445,14 +453,12 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
       if (P.gravity != 0) fa[2] += T.mass[p] * (-P.gravity);
       const double im = s.invm[p];
       for (int i = 0; i < 3; i++) {
-        s.facc[p][i] = fa[i];
         s.tacc[p][i] = tq[i];
-        s.tmp1[p][i] = fa[i] * im + s.lvel[p][i] * h1;
+        s.fc[p][i] = fa[i] * im + s.lvel[p][i] * h1;  // tmp1
       }
       double it[3];
       mul0_331(it, s.invI[p], tq);
-      for (int i = 0; i < 3; i++) s.tmp1[p][3 + i] = it[i] + w[i] * h1;
-      for (int i = 0; i < 6; i++) s.fc[p][i] = 0;
+      for (int i = 0; i < 3; i++) s.fc[p][3 + i] = it[i] + w[i] * h1;
     }
     wave_sync();
     SIM_ACC(2);
@@ -492,9 +498,9 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
       double Jr[12];
       for (int j = 0; j < 12; j++) Jr[j] = s.J[i][j];
       double sum = 0;
-      for (int j = 0; j < 6; j++) sum += Jr[j] * s.tmp1[b1][j];
+      for (int j = 0; j < 6; j++) sum += Jr[j] * s.fc[b1][j];  // fc holds tmp1 here
       if (b2 >= 0)
-        for (int j = 0; j < 6; j++) sum += Jr[6 + j] * s.tmp1[b2][j];
+        for (int j = 0; j < 6; j++) sum += Jr[6 + j] * s.fc[b2][j];
       const double rhs = s.rhs[i] * h1 - sum;
       const double cfm = s.cfm[i] * h1;
       double iM[6], dsum = 0;
@@ -505,16 +511,13 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
         for (int j = 0; j < 6; j++) dsum += iM[j] * Jr[6 + j];
       }
       const double ad = P.sor_w / (dsum + cfm);
-      imj_block(s, T, b1, Jr, s.iM[i]);
-      if (b2 >= 0) imj_block(s, T, b2, Jr + 6, s.iM[i] + 6);
-      else
-        for (int j = 6; j < 12; j++) s.iM[i][j] = 0;
-      for (int j = 0; j < 12; j++) s.J[i][j] *= ad;
       s.Ad[i] = ad;
       s.rhs[i] = rhs * ad;
       s.cfm[i] = ad * cfm;
       s.lambda[i] = 0;
     }
+    wave_sync();
+    for (int e = lane; e < n * 6; e += WAVE) s.fc[e / 6][e % 6] = 0;  // SOR_LCP: fc = 0 (no warm start)
     wave_sync();
     SIM_ACC(5);
     // ---- G: SOR sweeps
@@ -523,42 +526,132 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
       for (int i = lane; i < m; i += WAVE) s.order[i] = (int16_t)i;  // findex all -1: identity order
       uint32_t seed = __builtin_amdgcn_readfirstlane(s.seed);
       for (int it0 = 0; it0 < P.iterations; it0 += 8) {
-        // RANDOMLY_REORDER_CONSTRAINTS: Fisher-Yates with dRandInt. The draws are independent given
-        // the jump-ahead tables (all lanes); the swaps are a chain (lane 0).
-        for (int i = lane + 1; i < m; i += WAVE) {
-          uint32_t sd = T.lcg_a[i] * seed + T.lcg_c[i];
-          s.swp[i] = (int16_t)rand_int_from(sd, i + 1);
+        // RANDOMLY_REORDER_CONSTRAINTS: Fisher-Yates with dRandInt over the current order, i.e.
+        // order' = order o t_1 o ... o t_{m-1} with t_i the transposition (i, s_i). The draws s_i are
+        // independent given the jump-ahead tables; the composition is traced backwards from every
+        // position at once (lane-parallel), so no swap chain runs through LDS.
+        int swr[4], src[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int p = lane + 64 * k;
+          swr[k] = (p >= 1 && p < m) ? rand_int_from(T.lcg_a[p] * seed + T.lcg_c[p], p + 1) : 0;
+          src[k] = p;
         }
         if (m > 1) seed = T.lcg_a[m - 1] * seed + T.lcg_c[m - 1];
+#pragma unroll
+        for (int kk = 3; kk >= 0; kk--) {
+          for (int l = 63; l >= 0; l--) {
+            const int i = 64 * kk + l;
+            if (i >= m || i < 1) continue;
+            const int si = __builtin_amdgcn_readlane(swr[kk], l);
+#pragma unroll
+            for (int k = 0; k < 4; k++) src[k] = (src[k] == i) ? si : ((src[k] == si) ? i : src[k]);
+          }
+        }
+        int ordr[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) ordr[k] = (lane + 64 * k < m) ? s.order[src[k]] : 0;
         wave_sync();
-        if (lane == 0) {
-          for (int i = 1; i < m; i++) {
-            const int sw = s.swp[i];
-            const int16_t t = s.order[i];
-            s.order[i] = s.order[sw];
-            s.order[sw] = t;
+        // Dependency levels. Rows sharing a body must keep ODE's order; rows that share none
+        // commute exactly. level(p) = 1 + the level of the latest earlier position sharing a body
+        // with p, so one level is a set of body-disjoint rows whose earlier neighbours all sit in
+        // lower levels: solving the levels in turn, each in parallel, is Gauss-Seidel in ODE's order.
+        int pb1[4], pb2[4], pv1[4], pv2[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int p = lane + 64 * k;
+          if (p < m) s.order[p] = (int16_t)ordr[k];
+          pb1[k] = (p < m) ? s.rb1[ordr[k]] : -2;
+          pb2[k] = (p < m) ? s.rb2[ordr[k]] : -2;
+        }
+        // positions touching each body, as 4 x 64-bit masks
+        for (int bd = 0; bd < n; bd++) {
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const uint64_t bm = __ballot(pb1[k] == bd || pb2[k] == bd);
+            if (lane == 0) s.bmask[bd][k] = bm;
           }
         }
         wave_sync();
-        for (int p = lane; p < m; p += WAVE) {
-          const int row = s.order[p];
-          s.mask[p] = (1u << s.rb1[row]) | (s.rb2[row] >= 0 ? (1u << s.rb2[row]) : 0u);
-        }
-        wave_sync();
-        if (lane == 0) {  // maximal runs of body-disjoint rows
-          int nb = 0, start = 0;
-          uint32_t used = 0;
-          for (int p = 0; p < m; p++) {
-            const uint32_t mk = s.mask[p];
-            if (used & mk) {
-              s.run_se[nb++] = start | ((p - start) << 16);
-              start = p;
-              used = 0;
+        // latest earlier position touching the same body (-1: none)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          pv1[k] = pv2[k] = -1;
+          for (int e = 0; e < 2; e++) {
+            const int bd = e ? pb2[k] : pb1[k];
+            int pv = -1;
+            if (bd >= 0) {
+              const uint64_t below = (lane == 0) ? 0ull : (s.bmask[bd][k] & ((1ull << lane) - 1ull));
+              if (below) pv = 64 * k + 63 - __clzll(below);
+              else
+                for (int kk = k - 1; kk >= 0; kk--) {
+                  const uint64_t w = s.bmask[bd][kk];
+                  if (w) { pv = 64 * kk + 63 - __clzll(w); break; }
+                }
             }
-            used |= mk;
+            if (e) pv2[k] = pv; else pv1[k] = pv;
           }
-          s.run_se[nb++] = start | ((m - start) << 16);
-          s.nruns = nb;
+        }
+        // longest paths by relaxation (converges after the number of levels)
+#pragma unroll
+        for (int k = 0; k < 4; k++) if (lane + 64 * k < m) s.lv[lane + 64 * k] = 0;
+        wave_sync();
+        int lvr[4] = {0, 0, 0, 0};
+        for (;;) {
+          bool changed = false;
+          int nl[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const int a1 = pv1[k] >= 0 ? s.lv[pv1[k]] + 1 : 0;
+            const int a2 = pv2[k] >= 0 ? s.lv[pv2[k]] + 1 : 0;
+            nl[k] = a1 > a2 ? a1 : a2;
+            changed |= (lane + 64 * k < m) && nl[k] != lvr[k];
+          }
+          wave_sync();
+          if (!__any(changed)) break;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            lvr[k] = nl[k];
+            if (lane + 64 * k < m) s.lv[lane + 64 * k] = (int16_t)nl[k];
+          }
+          wave_sync();
+        }
+        int nlev = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (lane + 64 * k < m) nlev = max(nlev, lvr[k] + 1);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) nlev = max(nlev, __shfl_xor(nlev, off));
+        // level sizes and ranks (any order inside a level: its rows are body-disjoint)
+#pragma unroll
+        for (int k = 0; k < 4; k++) if (lane + 64 * k < m) s.cnt[lane + 64 * k] = 0;
+        wave_sync();
+        int rank[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) rank[k] = (lane + 64 * k < m) ? atomicAdd(&s.cnt[lvr[k]], 1) : 0;
+        wave_sync();
+        {
+          int base = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const int l = lane + 64 * k;
+            const int size = (l < nlev) ? s.cnt[l] : 0;
+            int incl = size;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+              const int up = __shfl_up(incl, off);
+              if (lane >= off) incl += up;
+            }
+            if (l < nlev) s.run_se[l] = (base + incl - size) | (size << 16);
+            base += __shfl(incl, 63);
+          }
+          wave_sync();
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const int p = lane + 64 * k;
+            if (p < m) s.sched[(s.run_se[lvr[k]] & 0xFFFF) + rank[k]] = (int16_t)ordr[k];
+          }
+          if (lane == 0) s.nruns = nlev;
         }
         wave_sync();
         SIM_ACC(6);
@@ -599,9 +692,11 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
       for (int j = 0; j < 3; j++) s.lvel[p][j] += h * s.fc[p][j];
       for (int j = 0; j < 3; j++) s.avel[p][j] += h * s.fc[p][3 + j];
       const double hm = h * s.invm[p];
+      double fa[3] = {0, 0, 0};  // facc: gravity only (the motors add torques)
+      if (P.gravity != 0) fa[2] += T.mass[p] * (-P.gravity);
       double ta[3];
       for (int j = 0; j < 3; j++) {
-        s.lvel[p][j] += hm * s.facc[p][j];
+        s.lvel[p][j] += hm * fa[j];
         ta[j] = s.tacc[p][j] * h;
       }
       double t3[3];
