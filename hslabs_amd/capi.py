@@ -113,6 +113,15 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process. torch ships its own libamdhip64 (SONAME libamdhip64.so.7) and
+    # its libraries NEED it by the unversioned name, so if libhslabs.so pulled /opt/rocm's copy in
+    # first, a later `import torch` would load a second runtime and libhslabs' runtime would then
+    # see no device (measured on the MI355X box). Importing torch first makes libhslabs bind to the
+    # runtime already in the process.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     path = os.environ.get("HSLABS_LIB") or _build.LIB  # tuning-variant override (build.build_variant)
     if not os.path.exists(path):
         if not build_if_missing:

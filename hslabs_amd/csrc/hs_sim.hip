@@ -57,7 +57,7 @@ enum { ROW_BILATERAL = 0, ROW_NORMAL = 1, ROW_FRICTION = 2 };
 // Diagnostic build (-DHS_SIM_STAMPS, tools/sim_stamps.py): shader-clock cycles per phase,
 // summed over the steps of a launch, per wavefront.
 #ifdef HS_SIM_STAMPS
-__device__ unsigned long long g_sim_stamps[4096][12];
+__device__ unsigned long long g_sim_stamps[4096][16];
 #define SIM_ACC(slot)                                                                 \
   do {                                                                                \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime();                     \
@@ -85,6 +85,7 @@ struct SimL {
   double lambda[MM];
   int8_t rb1[MM], rb2[MM], rtype[MM];
   int16_t order[MM];       // row at each sweep position (ODE's order)
+  int16_t swp[MM];         // Fisher-Yates swap targets s_i of a reshuffle
   int16_t sched[MM];       // rows grouped by level
   int16_t lv[MM];          // level of each position
   int32_t cnt[MM];         // rows per level
@@ -530,24 +531,25 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
         // order' = order o t_1 o ... o t_{m-1} with t_i the transposition (i, s_i). The draws s_i are
         // independent given the jump-ahead tables; the composition is traced backwards from every
         // position at once (lane-parallel), so no swap chain runs through LDS.
-        int swr[4], src[4];
+        const int nblk = (m + 63) >> 6;  // position blocks in use (uniform)
+        int src[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           const int p = lane + 64 * k;
-          swr[k] = (p >= 1 && p < m) ? rand_int_from(T.lcg_a[p] * seed + T.lcg_c[p], p + 1) : 0;
+          if (p >= 1 && p < m) s.swp[p] = (int16_t)rand_int_from(T.lcg_a[p] * seed + T.lcg_c[p], p + 1);
           src[k] = p;
         }
         if (m > 1) seed = T.lcg_a[m - 1] * seed + T.lcg_c[m - 1];
+        wave_sync();
+        // s_i are read as LDS broadcasts (VGPR operands: no v_readlane -> SGPR hazards)
+#pragma unroll 4
+        for (int i = m - 1; i >= 1; i--) {
+          const int si = s.swp[i];
 #pragma unroll
-        for (int kk = 3; kk >= 0; kk--) {
-          for (int l = 63; l >= 0; l--) {
-            const int i = 64 * kk + l;
-            if (i >= m || i < 1) continue;
-            const int si = __builtin_amdgcn_readlane(swr[kk], l);
-#pragma unroll
-            for (int k = 0; k < 4; k++) src[k] = (src[k] == i) ? si : ((src[k] == si) ? i : src[k]);
-          }
+          for (int k = 0; k < 4; k++)
+            if (k < nblk) src[k] = (src[k] == i) ? si : ((src[k] == si) ? i : src[k]);
         }
+        SIM_ACC(11);
         int ordr[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) ordr[k] = (lane + 64 * k < m) ? s.order[src[k]] : 0;
@@ -568,8 +570,8 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
         for (int bd = 0; bd < n; bd++) {
 #pragma unroll
           for (int k = 0; k < 4; k++) {
-            const uint64_t bm = __ballot(pb1[k] == bd || pb2[k] == bd);
-            if (lane == 0) s.bmask[bd][k] = bm;
+            const uint64_t bm = (k < nblk) ? __ballot(pb1[k] == bd || pb2[k] == bd) : 0ull;
+            if (lane == k) s.bmask[bd][k] = bm;
           }
         }
         wave_sync();
@@ -592,6 +594,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
             if (e) pv2[k] = pv; else pv1[k] = pv;
           }
         }
+        SIM_ACC(12);
         // longest paths by relaxation (converges after the number of levels)
 #pragma unroll
         for (int k = 0; k < 4; k++) if (lane + 64 * k < m) s.lv[lane + 64 * k] = 0;
@@ -602,20 +605,24 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
           int nl[4];
 #pragma unroll
           for (int k = 0; k < 4; k++) {
-            const int a1 = pv1[k] >= 0 ? s.lv[pv1[k]] + 1 : 0;
-            const int a2 = pv2[k] >= 0 ? s.lv[pv2[k]] + 1 : 0;
-            nl[k] = a1 > a2 ? a1 : a2;
-            changed |= (lane + 64 * k < m) && nl[k] != lvr[k];
+            nl[k] = 0;
+            if (k < nblk) {
+              const int a1 = pv1[k] >= 0 ? s.lv[pv1[k]] + 1 : 0;
+              const int a2 = pv2[k] >= 0 ? s.lv[pv2[k]] + 1 : 0;
+              nl[k] = a1 > a2 ? a1 : a2;
+              changed |= (lane + 64 * k < m) && nl[k] != lvr[k];
+            }
           }
           wave_sync();
           if (!__any(changed)) break;
 #pragma unroll
           for (int k = 0; k < 4; k++) {
             lvr[k] = nl[k];
-            if (lane + 64 * k < m) s.lv[lane + 64 * k] = (int16_t)nl[k];
+            if (k < nblk && lane + 64 * k < m) s.lv[lane + 64 * k] = (int16_t)nl[k];
           }
           wave_sync();
         }
+        SIM_ACC(13);
         int nlev = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++)
@@ -794,11 +801,11 @@ __global__ __launch_bounds__(WAVE) void hs_sim_reset_kernel(const hs_topo* __res
 #ifdef HS_SIM_STAMPS
 extern "C" int hs_debug_read_sim_stamps(unsigned long long* out, int n_rows) {
   if (n_rows > 4096) n_rows = 4096;
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sim_stamps), sizeof(unsigned long long) * 12 * n_rows, 0,
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sim_stamps), sizeof(unsigned long long) * 16 * n_rows, 0,
                                   hipMemcpyDeviceToHost);
 }
 extern "C" int hs_debug_clear_sim_stamps() {
-  static unsigned long long zero[4096][12];
+  static unsigned long long zero[4096][16];
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_sim_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
 }
 #endif

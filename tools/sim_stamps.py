@@ -42,7 +42,7 @@ def main():
     L.hs_debug_clear_sim_stamps()
     sb.step(steps, outputs=())
     torch.cuda.synchronize()
-    st = np.zeros((4096, 12), dtype=np.uint64)
+    st = np.zeros((4096, 16), dtype=np.uint64)
     L.hs_debug_read_sim_stamps(st.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), 4096)
     st = st[:min(n, 4096)].astype(np.float64)
     tot = st[:, :9].sum(axis=1) / steps
@@ -50,6 +50,10 @@ def main():
         d = st[:, i] / steps
         print(f"{name:20s} mean {d.mean():10.0f}  p50 {np.median(d):10.0f}  p90 {np.percentile(d, 90):10.0f}"
               f"  ({100 * d.mean() / tot.mean():5.1f} %)")
+    tot = tot + st[:, 11:14].sum(axis=1) / steps
+    for i, name in ((11, "  reshuffle: trace"), (12, "  reshuffle: prev"), (13, "  reshuffle: relax")):
+        d = st[:, i] / steps
+        print(f"{name:20s} mean {d.mean():10.0f}  ({100 * d.mean() / tot.mean():5.1f} %)")
     print(f"{'TOTAL / step':20s} mean {tot.mean():10.0f}")
     print(f"rows per step {st[:, 10].mean() / steps:.1f}, SOR runs per reshuffle {st[:, 9].mean() / steps:.1f}")
 
