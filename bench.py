@@ -14,6 +14,10 @@ all_reduce(MIN) of 8 bytes; that collective is inside the timed region.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 via
 torch.distributed.run (one process per GPU, RCCL).
+
+--sim benchmarks the closed-loop simulation instead (modelplayer::simulate_ode
+with position control on ODE's QuickStep, hs_sim_step): a step is one
+simulation step (play_dt) of every rollout; K steps run in one launch.
 """
 from __future__ import annotations
 
@@ -52,6 +56,8 @@ def parse():
                          "--rollouts 16384 --horizon 32 --fp32")
     ap.add_argument("--mixed", action="store_true",
                     help="BASELINE configs[4]: myant.xml + hexapod.xml 50/50, interleaved, one launch")
+    ap.add_argument("--sim", action="store_true",
+                    help="closed-loop simulation (PD control + ODE QuickStep, 20 SOR iterations) steps/s")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -96,6 +102,97 @@ def cpu_baseline(model_names, n_t, horizon, seconds, threads):
             "single_thread": round(single, 1)}
 
 
+SIM_METRIC = "closed-loop simulation steps/sec (position control + ODE QuickStep SOR-LCP, 20 iterations)"
+
+
+def sim_cpu_baseline(model, name, sb, seconds, threads):
+    """Oracle QuickStep restatement on a bounded sample of the same batch (same tables/states)."""
+    from oracle import oracle as O
+
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    om = O.Model(os.path.join(ROOT, "models", f"{name}.xml"))
+    nb = min(sb.B, 4 * threads)
+    qt = sb.tables.q[:nb].cpu().numpy().copy()
+    dqt = sb.tables.dq[:nb].cpu().numpy().copy()
+    tt = sb.tables.tau[:nb].cpu().numpy().copy()
+    body0 = sb.body[:nb].cpu().numpy().copy()
+    P = O.SimParams()
+
+    def timed(nthr, budget):
+        body = body0.copy()
+        seed = np.zeros(nb, np.uint32)
+        tsi = np.full(nb, 2, np.int32)
+        done, t0 = 0, time.perf_counter()
+        while True:
+            O.sim_batch(om, P, sb.n_t, qt, dqt, tt, body, seed, tsi, 10, nthr)
+            done += nb * 10
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return done / el, done, el
+
+    single, _, _ = timed(1, min(2.0, seconds / 4))
+    rate, done, el = timed(threads, seconds)
+    return {"value": round(rate, 1), "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"{done} simulation steps ({name}, {nb} rollouts of the batch, 10-step calls) in {el:.1f}s, "
+                      f"oracle ODE-QuickStep restatement, g++ -O2, std::thread x{threads}; "
+                      f"single-thread {single:.1f} steps/s",
+            "single_thread": round(single, 1)}
+
+
+def main_sim(args, torch, dist, world, rank, dev):
+    import hslabs_amd as H
+    from hslabs_amd import synth
+
+    B = args.rollouts
+    model = H.KinematicModel(os.path.join(ROOT, "models", f"{args.model}.xml"))
+    sb = H.SimBatch(model, synth.gen_sim_params(B, args.model, id0=rank * B), device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sb.step(args.warmup, stream=stream, outputs=())
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    sb.step(args.steps, stream=stream, outputs=())  # one launch, K steps (state stays in LDS)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed, ev0.elapsed_time(ev1)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+    finite = bool(torch.isfinite(sb.body).all().item())
+    if rank == 0:
+        nmj = model.nmj
+        # per rollout-step the kernel must read the controller row (q0, dq0, tau_ff: 3 nmj doubles);
+        # the body state (n x 13 doubles) crosses HBM once per launch in each direction
+        alg_bytes = B * (args.steps * 3 * nmj * 8 + 2 * model.n_parts * 13 * 8)
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        out = {
+            "metric": SIM_METRIC, "value": round(B * args.steps * world / elapsed, 1), "unit": "steps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (splitmix64 gait parameters around pgs id 8, period 3 -> n_t 300; SURVEY.md 8d)",
+            "config": {"workload": f"{args.model}.xml B={B}/GPU closed-loop simulation, play_dt .01, QuickStep 20 "
+                                   f"iterations, {args.steps} steps per launch (SURVEY.md 8f row 4)",
+                       "rollouts_per_gpu": B, "parallelism": f"rollout-sharded x{world}, no collective"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "hs_sim_kernel",
+                         "kernel_ms": round(kern_ms, 5), "alg_bytes_per_launch": alg_bytes},
+            "finite_state": finite,
+        }
+        out["cpu_baseline"] = None if (args.no_cpu or world > 1) else sim_cpu_baseline(
+            model, args.model, sb, args.cpu_seconds, args.cpu_threads)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     import torch
@@ -111,6 +208,8 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.sim:
+        return main_sim(args, torch, dist, world, rank, dev)
 
     import hslabs_amd as H
     from hslabs_amd import synth

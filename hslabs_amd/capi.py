@@ -30,7 +30,8 @@ EXPORTS = [
     "hs_run", "hs_run_steps", "hs_run_pd", "hs_run_forces", "hs_mixed_create", "hs_mixed_free",
     "hs_mixed_get_dims", "hs_complete_traj", "hs_traj_save", "hs_run_forces_host",
     "hs_run_mixed", "hs_run_mixed_steps", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
-    "hs_sim_default_params", "hs_sim_reset", "hs_sim_step",
+    "hs_sim_default_params", "hs_sim_reset", "hs_sim_step", "hs_sim_create", "hs_sim_advance", "hs_sim_get_state",
+    "hs_sim_free",
 ]
 SIM_BODY_STRIDE = 13
 
@@ -165,6 +166,12 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_sim_default_params.restype = None
     L.hs_sim_reset.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int32, vp, vp]
     L.hs_sim_step.argtypes = [vp, ctypes.POINTER(SimArgsC)]
+    L.hs_sim_create.argtypes = [vp, ctypes.POINTER(GaitParamsC), ctypes.c_int32, ctypes.POINTER(SimParamsC),
+                                ctypes.c_double, ctypes.POINTER(vp)]
+    L.hs_sim_advance.argtypes = [vp, ctypes.c_int32, dp, dp, dp, ctypes.POINTER(ctypes.c_int32), dp]
+    L.hs_sim_get_state.argtypes = [vp, dp, ctypes.POINTER(ctypes.c_int32)]
+    L.hs_sim_free.argtypes = [vp]
+    L.hs_sim_free.restype = None
     L.hs_last_error.argtypes = []
     L.hs_last_error.restype = ctypes.c_char_p
     L.hs_abi_version.argtypes = []

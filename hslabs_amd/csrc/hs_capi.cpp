@@ -650,4 +650,158 @@ int hs_sim_step(hs_model_t m, const hs_sim_args* a) {
   return HS_OK;
 }
 
+struct hs_sim_s {
+  hs_model_t model;
+  int dev;
+  hipStream_t stream;
+  int32_t B, n_t;
+  hs_sim_params params;
+  void *params_d, *q, *dq, *tau, *body, *seed, *tsi;
+  void* out[5];
+  size_t out_steps;
+};
+
+void hs_sim_free(hs_sim_t s) {
+  if (!s) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(s->dev);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  for (void* p : {s->params_d, s->q, s->dq, s->tau, s->body, s->seed, s->tsi}) (void)hipFree(p);
+  for (void* p : s->out) (void)hipFree(p);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  (void)hipSetDevice(cur);
+  delete s;
+}
+
+int hs_sim_create(hs_model_t m, const hs_gait_params* params, int32_t B, const hs_sim_params* sp, double t0,
+                  hs_sim_t* out) {
+  if (!m || !params || !out || B < 1) return fail(HS_E_ARG, "hs_sim_create: null argument or B < 1");
+  hs_sim_params P;
+  if (sp) P = *sp;
+  else hs_sim_default_params(&P);
+  if (!(P.dt > 0)) return fail(HS_E_ARG, "dt must be > 0");
+  const int n_t = (int)(params[0].period / P.dt + .5);  // setup_per_controller (player.cpp:376)
+  for (int b = 1; b < B; b++)
+    if ((int)(params[b].period / P.dt + .5) != n_t) return fail(HS_E_ARG, "rollouts need one n_t = int(T/dt+.5)");
+  if (n_t < 2) return fail(HS_E_ARG, "period shorter than two simulation steps");
+  hs_sim_s* s = new hs_sim_s();
+  s->model = m;
+  s->B = B;
+  s->n_t = n_t;
+  s->params = P;
+  const hs_topo& t = m->host;
+  hipError_t e = hipGetDevice(&s->dev);
+  if (e == hipSuccess) e = hipStreamCreate(&s->stream);
+  const size_t nb = (size_t)B;
+  auto alloc = [&](void** p, size_t bytes) {
+    if (e == hipSuccess) e = hipMalloc(p, bytes);
+  };
+  alloc(&s->params_d, nb * sizeof(hs_gait_params));
+  alloc(&s->q, nb * n_t * t.cfg * sizeof(double));
+  alloc(&s->dq, nb * n_t * t.cfg * sizeof(double));
+  alloc(&s->tau, nb * n_t * t.nmj * sizeof(double));
+  alloc(&s->body, nb * t.n * HS_SIM_BODY_STRIDE * sizeof(double));
+  alloc(&s->seed, nb * sizeof(uint32_t));
+  alloc(&s->tsi, nb * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemcpyAsync(s->params_d, params, nb * sizeof(hs_gait_params), hipMemcpyHostToDevice, s->stream);
+  if (e != hipSuccess) {
+    hs_sim_free(s);
+    return hip_fail(e, "hs_sim_create");
+  }
+  hs_run_args a;
+  memset(&a, 0, sizeof(a));
+  a.n_rollouts = B;
+  a.horizon = n_t;
+  a.k0 = 0;
+  a.n_t = n_t;
+  a.ignore_reach = 1;
+  a.params = (const hs_gait_params*)s->params_d;
+  a.q = (double*)s->q;
+  a.dq = (double*)s->dq;
+  a.tau = (double*)s->tau;
+  a.stream = s->stream;
+  int rc = hs_run(m, &a);
+  const int tsi0 = (int)(t0 / P.dt + .5);  // play_t = int(t0/play_dt+.5)*play_dt
+  const int h0 = ((tsi0 % n_t) + n_t - 2) % n_t;
+  if (rc == HS_OK)
+    rc = hs_sim_reset(m, B, (const double*)s->q + (size_t)h0 * t.cfg, n_t * t.cfg, (double*)s->body, s->stream);
+  std::vector<int32_t> tsi(nb, tsi0);
+  if (rc == HS_OK) {
+    e = hipMemsetAsync(s->seed, 0, nb * sizeof(uint32_t), s->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s->tsi, tsi.data(), nb * sizeof(int32_t), hipMemcpyHostToDevice, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    if (e != hipSuccess) rc = hip_fail(e, "hs_sim_create");
+  }
+  if (rc != HS_OK) {
+    std::string keep = g_err;
+    hs_sim_free(s);
+    g_err = keep;
+    return rc;
+  }
+  *out = s;
+  return HS_OK;
+}
+
+int hs_sim_advance(hs_sim_t s, int32_t n_steps, double* tau_cmd, double* q_meas, double* torso, int32_t* n_contacts,
+                   double* normal_force) {
+  if (!s || n_steps < 0) return fail(HS_E_ARG, "hs_sim_advance: bad argument");
+  if (n_steps == 0) return HS_OK;
+  const hs_topo& t = s->model->host;
+  const size_t rows = (size_t)s->B * n_steps;
+  const size_t bytes[5] = {rows * t.nmj * sizeof(double), rows * t.nmj * sizeof(double), rows * 3 * sizeof(double),
+                           rows * sizeof(int32_t), rows * sizeof(double)};
+  void* host[5] = {tau_cmd, q_meas, torso, n_contacts, normal_force};
+  hipError_t e = hipSetDevice(s->dev);
+  if (e == hipSuccess && (size_t)n_steps > s->out_steps) {
+    for (void*& p : s->out) {
+      (void)hipFree(p);
+      p = nullptr;
+    }
+    s->out_steps = 0;
+    for (int i = 0; i < 5 && e == hipSuccess; i++) e = hipMalloc(&s->out[i], bytes[i]);
+    if (e == hipSuccess) s->out_steps = (size_t)n_steps;
+  }
+  if (e != hipSuccess) return hip_fail(e, "hs_sim_advance");
+  hs_sim_args a;
+  memset(&a, 0, sizeof(a));
+  a.n_rollouts = s->B;
+  a.n_steps = n_steps;
+  a.n_t = s->n_t;
+  a.params = s->params;
+  a.body = (double*)s->body;
+  a.seed = (uint32_t*)s->seed;
+  a.tsi = (int32_t*)s->tsi;
+  a.q_tab = (const double*)s->q;
+  a.dq_tab = (const double*)s->dq;
+  a.tau_tab = (const double*)s->tau;
+  a.tau_cmd = tau_cmd ? (double*)s->out[0] : nullptr;
+  a.q_meas = q_meas ? (double*)s->out[1] : nullptr;
+  a.torso = torso ? (double*)s->out[2] : nullptr;
+  a.n_contacts = n_contacts ? (int32_t*)s->out[3] : nullptr;
+  a.normal_force = normal_force ? (double*)s->out[4] : nullptr;
+  a.stream = s->stream;
+  int rc = hs_sim_step(s->model, &a);
+  if (rc != HS_OK) return rc;
+  for (int i = 0; i < 5 && e == hipSuccess; i++)
+    if (host[i]) e = hipMemcpyAsync(host[i], s->out[i], bytes[i], hipMemcpyDeviceToHost, s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  if (e != hipSuccess) return hip_fail(e, "hs_sim_advance");
+  return HS_OK;
+}
+
+int hs_sim_get_state(hs_sim_t s, double* body, int32_t* tsi) {
+  if (!s) return fail(HS_E_ARG, "null sim");
+  const hs_topo& t = s->model->host;
+  hipError_t e = hipSetDevice(s->dev);
+  if (e == hipSuccess && body)
+    e = hipMemcpyAsync(body, s->body, (size_t)s->B * t.n * HS_SIM_BODY_STRIDE * sizeof(double), hipMemcpyDeviceToHost,
+                       s->stream);
+  if (e == hipSuccess && tsi)
+    e = hipMemcpyAsync(tsi, s->tsi, (size_t)s->B * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  if (e != hipSuccess) return hip_fail(e, "hs_sim_get_state");
+  return HS_OK;
+}
+
 }  // extern "C"

@@ -291,6 +291,22 @@ typedef struct {
 /* n_steps closed-loop steps of every rollout, one launch (state stays on chip between steps). */
 int hs_sim_step(hs_model_t model, const hs_sim_args* args);
 
+/* Host-side handle over the calls above, for callers without device memory of their own
+ * (the C++ shim's modelplayer): owns the device tables and state of B rollouts.
+ * hs_sim_create = modelplayer::setup_per_controller (player.cpp:370-382) for every rollout:
+ * n_t = int(period / params->dt + .5) controller rows from hs_run (same n_t for the whole
+ * batch, else HS_E_ARG), play_t = int(t0 / dt + .5) dt, bodies at that trajectory sample
+ * at rest (init_play_config). params is HOST memory; sim_params NULL = hs_sim_default_params. */
+typedef struct hs_sim_s* hs_sim_t;
+int hs_sim_create(hs_model_t model, const hs_gait_params* params, int32_t n_rollouts, const hs_sim_params* sim_params,
+                  double t0, hs_sim_t* out);
+/* n_steps of simulate_ode (synchronous); HOST outputs as in hs_sim_args, each may be NULL. */
+int hs_sim_advance(hs_sim_t sim, int32_t n_steps, double* tau_cmd, double* q_meas, double* torso, int32_t* n_contacts,
+                   double* normal_force);
+/* HOST copies of the state: body [B][n_parts][HS_SIM_BODY_STRIDE], tsi [B] (either may be NULL). */
+int hs_sim_get_state(hs_sim_t sim, double* body, int32_t* tsi);
+void hs_sim_free(hs_sim_t sim);
+
 const char* hs_last_error(void);
 int hs_abi_version(void);
 

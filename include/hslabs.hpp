@@ -14,6 +14,9 @@
 //   modelplayer::make_pergensu / measure_cot / measure_cot_sweep /
 //            record_per_traj / test_dynamics                               (player.cpp:147-321,
 //                                                                           617-629; playerexperim.cpp:95-121)
+//   modelplayer::setup_per_controller / simulate_ode / get_ode_motor_adas /
+//            torso position, fall_check                                    (player.cpp:325-382, 669-681;
+//                                                                           visualization.cpp:366-374)
 //   new_2d_array / delete_2d_array / save_2d_array                         (core.h:11-14)
 //
 // Differences from the reference: errors throw hslabs::error instead of
@@ -239,9 +242,67 @@ class periodic {
 class modelplayer {
   kinematicmodel model_;
   bool contact_force_flag_ = false;
+  hs_sim_t sim_ = nullptr;  // the ODE world of setup_per_controller (one rollout)
+  double play_t_ = 0, play_dt_ = 0.01;
+  std::vector<double> last_tau_, last_q_;
 
  public:
   modelplayer() {}
+  ~modelplayer() { unset_per_controller(); }
+  modelplayer(const modelplayer&) = delete;
+  modelplayer& operator=(const modelplayer&) = delete;
+  // player.cpp:370-382: controller tables over one cycle of n_t = int(T/play_dt+.5) samples, the
+  // world at the trajectory sample of t0, at rest; position control on (step_mode 6)
+  void setup_per_controller(const pergensetup* pgs, double t0) {
+    unset_per_controller();
+    hs_gait_params g = pgs->params().to_c();
+    hs_sim_params sp;
+    hs_sim_default_params(&sp);
+    sp.dt = play_dt_;
+    check(hs_sim_create(model_.handle(), &g, 1, &sp, t0, &sim_), "setup_per_controller");
+    play_t_ = int(t0 / play_dt_ + .5) * play_dt_;
+    last_tau_.assign(model_.number_of_motor_joints(), 0);
+    last_q_.assign(model_.number_of_motor_joints(), 0);
+  }
+  void unset_per_controller() {
+    if (sim_) hs_sim_free(sim_);
+    sim_ = nullptr;
+  }
+  // player.cpp:325-339 (position control): PD torques, dJointAddHingeTorque, collide, QuickStep
+  void simulate_ode(int n_steps = 1) {
+    if (!sim_) throw error(HS_E_ARG, "setup_per_controller first");
+    const int nmj = model_.number_of_motor_joints();
+    std::vector<double> tau((size_t)n_steps * nmj), q((size_t)n_steps * nmj);
+    check(hs_sim_advance(sim_, n_steps, tau.data(), q.data(), nullptr, nullptr, nullptr), "simulate_ode");
+    std::copy(tau.end() - nmj, tau.end(), last_tau_.begin());
+    std::copy(q.end() - nmj, q.end(), last_q_.begin());
+    play_t_ += n_steps * play_dt_;
+  }
+  double get_play_t() const { return play_t_; }
+  void set_play_dt(double dt) { play_dt_ = dt; }
+  // motor torques applied in the last step (set_ode_motor_torques) and the angles they saw
+  const double* get_last_motor_torques() const { return last_tau_.data(); }
+  const double* get_last_motor_angles() const { return last_q_.data(); }
+  // body state of part i: pos[3], quaternion[4], lvel[3], avel[3] (dBodyGetPosition etc.)
+  void get_ode_body(int part, double* state13) const {
+    if (!sim_) throw error(HS_E_ARG, "setup_per_controller first");
+    std::vector<double> b((size_t)model_.number_of_parts() * HS_SIM_BODY_STRIDE);
+    check(hs_sim_get_state(sim_, b.data(), nullptr), "get_ode_body");
+    std::copy(&b[(size_t)part * HS_SIM_BODY_STRIDE], &b[(size_t)part * HS_SIM_BODY_STRIDE] + HS_SIM_BODY_STRIDE,
+              state13);
+  }
+  // dBodyGetPosition(get_torso_odebody()) (player.cpp:664-674)
+  void get_torso_pos(double* pos) const {
+    double st[HS_SIM_BODY_STRIDE];
+    get_ode_body(0, st);
+    std::copy(st, st + 3, pos);
+  }
+  // player.cpp:669-681 without exit(1): true when the torso is below hc
+  bool fall_check(double hc) const {
+    double p[3];
+    get_torso_pos(p);
+    return p[2] < hc;
+  }
   kinematicmodel* get_model() { return &model_; }
   void set_flag(const std::string& name, bool v) {
     if (name == "contact_force") contact_force_flag_ = v;

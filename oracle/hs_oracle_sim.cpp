@@ -777,4 +777,23 @@ int hso_sim_run(const hso_model* m, const double* p10, int iterations, int n_t, 
   return 0;
 }
 
+/* B rollouts on n_threads std::threads (bench.py's cpu_baseline leg): tables [B][n_t][...],
+ * body [B][n][13], seed/tsi [B]; per-step outputs are not kept. */
+int hso_sim_batch(const hso_model* m, const double* p10, int iterations, int n_t, int B, const double* q_tab,
+                  const double* dq_tab, const double* tau_tab, double* body, uint32_t* seed, int32_t* tsi,
+                  int n_steps, int n_threads) {
+  const size_t cfg = m->cfg, nmj = m->nmj, nb = (size_t)m->n * SB;
+  std::vector<std::thread> th;
+  if (n_threads < 1) n_threads = 1;
+  for (int t = 0; t < n_threads; t++)
+    th.emplace_back([=]() {
+      for (int b = t; b < B; b += n_threads)
+        hso_sim_run(m, p10, iterations, n_t, q_tab + (size_t)b * n_t * cfg, dq_tab + (size_t)b * n_t * cfg,
+                    tau_tab + (size_t)b * n_t * nmj, body + (size_t)b * nb, seed + b, tsi + b, n_steps, nullptr,
+                    nullptr, nullptr, nullptr, nullptr);
+    });
+  for (auto& x : th) x.join();
+  return 0;
+}
+
 }  // extern "C"

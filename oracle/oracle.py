@@ -160,6 +160,8 @@ def lib():
         L.hso_sim_hinges.argtypes = [ctypes.c_void_p, dp, dp, dp]
         L.hso_sim_run.argtypes = [ctypes.c_void_p, dp, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, up, ip,
                                   ctypes.c_int, dp, dp, dp, ip, dp]
+        L.hso_sim_batch.argtypes = [ctypes.c_void_p, dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp,
+                                    up, ip, ctypes.c_int, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -404,3 +406,17 @@ def sim_run(model: Model, params: SimParams, n_t: int, q_tab, dq_tab, tau_tab, b
         raise RuntimeError(f"oracle sim_run failed rc={rc}")
     out.update(body=body, seed=int(sd[0]), tsi=int(ts[0]))
     return out
+
+
+def sim_batch(model: Model, params: SimParams, n_t: int, q_tab, dq_tab, tau_tab, body, seed, tsi, n_steps: int,
+              n_threads: int = 1) -> None:
+    """B rollouts of sim_run in place (body [B][n][13], seed/tsi [B] advanced), n_threads threads."""
+    B = body.shape[0]
+    for a in (q_tab, dq_tab, tau_tab, body):
+        assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    p10 = params.p10()
+    rc = lib().hso_sim_batch(model.handle, _ptr(p10), params.iterations, n_t, B, _ptr(q_tab), _ptr(dq_tab),
+                             _ptr(tau_tab), _ptr(body), seed.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                             tsi.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n_steps, n_threads)
+    if rc != 0:
+        raise RuntimeError(f"oracle sim_batch failed rc={rc}")

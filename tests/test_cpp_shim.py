@@ -9,10 +9,10 @@ import pytest
 from conftest import MODELS, PGS_CONFIG, ROOT
 
 
-def compile_prog(product, out):
+def compile_prog(product, out, src="cot_sweep.cpp"):
     libdir = os.path.dirname(product.capi.lib_path())
     cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
-           os.path.join(ROOT, "tests", "cpp", "cot_sweep.cpp"), "-L", libdir, "-lhslabs",
+           os.path.join(ROOT, "tests", "cpp", src), "-L", libdir, "-lhslabs",
            f"-Wl,-rpath,{libdir}", "-o", str(out)]
     subprocess.run(cmd, check=True)
     return out
@@ -21,6 +21,7 @@ def compile_prog(product, out):
 def test_shim_compiles_and_links(product, tmp_path):
     exe = compile_prog(product, tmp_path / "cot_sweep")
     assert os.path.exists(exe)
+    assert os.path.exists(compile_prog(product, tmp_path / "position_control", "position_control.cpp"))
     # the C header alone is valid C (no C++ or HIP types leak through the boundary)
     src = tmp_path / "c_only.c"
     src.write_text('#include "hslabs.h"\nint main(void){return hs_abi_version()==HSLABS_ABI_VERSION?0:1;}\n')
@@ -53,3 +54,25 @@ def test_shim_runs_reference_shaped_main(product, tmp_path):
     tau0 = float([ln for ln in lines if ln.startswith("tau[2][0]")][0].split("=")[1])
     assert tau0 == pytest.approx(ref["tau"][0, 0, 0], rel=1e-12)
     assert "error ok" in out
+
+
+@pytest.mark.gpu
+def test_shim_position_control_walks(product, tmp_path):
+    """setup_per_controller + 600 x simulate_ode through the shim: the hexapod of pgs id 8 walks two
+    step lengths (2 x 0.5); the run equals the Python binding's (oracle parity: tests/test_gpu_sim.py)."""
+    exe = compile_prog(product, tmp_path / "position_control", "position_control.cpp")
+    out = subprocess.run([str(exe), MODELS], check=True, capture_output=True, text=True, timeout=300).stdout
+    vals = {ln.split("=")[0].strip(): [float(v) for v in ln.split("=")[1].split()] for ln in out.splitlines()}
+    t0, t1 = np.array(vals["torso0"]), np.array(vals["torso1"])
+    assert vals["play_t"][0] == pytest.approx(6.0)
+    assert abs((t1[0] - t0[0]) - 1.0) < 0.2
+    assert vals["fallen"][0] == 0
+    # the same run through the Python binding (same kernels, same tables): identical to print precision
+    import torch
+
+    p = product.read_pgs_config(PGS_CONFIG, 8)
+    m = product.KinematicModel(os.path.join(MODELS, "hexapod.xml"))
+    sb = product.SimBatch(m, [p], tsi0=0)
+    out = sb.step(600, outputs=("torso",))
+    torch.cuda.synchronize()
+    assert np.abs(out["torso"][0, -1].cpu().numpy() - t1).max() < 2e-9
