@@ -78,7 +78,8 @@ struct SimL {
   double cpos[NM][3], cdepth[NM];
   double tau[NM];
   // constraint rows
-  double J[MM][12];        // Jacobian rows (unscaled: the sweeps form J Ad and M^-1 J^T per use)
+  double J[MM][9];         // Jacobian rows, unscaled, as J1l | J1a | J2a: every two-body row here has
+                           // J2l = -J1l (ball, fixed and hinge-axis rows), and contacts have no body2
   double rhs[MM];          // c, then rhs, then rhs * Ad
   double cfm[MM];          // cfm, then cfm / h, then Ad * cfm
   double Ad[MM];
@@ -111,18 +112,35 @@ __device__ inline double hinge_angle(const L& s, const hs_simjoint& J) {
 }
 
 template <class L>
+__device__ inline void put_row(L& s, int r, const double* j12) {
+#pragma unroll
+  for (int j = 0; j < 6; j++) s.J[r][j] = j12[j];
+#pragma unroll
+  for (int j = 0; j < 3; j++) s.J[r][6 + j] = j12[9 + j];
+}
+template <class L>
+__device__ inline void get_row(const L& s, int r, double* j12) {
+#pragma unroll
+  for (int j = 0; j < 6; j++) j12[j] = s.J[r][j];
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    j12[6 + j] = -j12[j];
+    j12[9 + j] = s.J[r][6 + j];
+  }
+}
+
+template <class L>
 __device__ inline void set_ball(L& s, const hs_simjoint& J, double k, int r0) {
   double a1[3], a2[3];
   mul0_331(a1, s.R[J.b1], J.anchor1);
   mul0_331(a2, s.R[J.b2], J.anchor2);
-  double (*Jr)[12] = &s.J[r0];
   // J1l = I, J1a = -[a1]x, J2l = -I, J2a = [a2]x
   const double rows[3][12] = {
       {1, 0, 0, 0, a1[2], -a1[1], -1, 0, 0, 0, -a2[2], a2[1]},
       {0, 1, 0, -a1[2], 0, a1[0], 0, -1, 0, a2[2], 0, -a2[0]},
       {0, 0, 1, a1[1], -a1[0], 0, 0, 0, -1, -a2[1], a2[0], 0}};
   for (int r = 0; r < 3; r++) {
-    for (int j = 0; j < 12; j++) Jr[r][j] = rows[r][j];
+    put_row(s, r0 + r, rows[r]);
     s.rhs[r0 + r] = k * (a2[r] + s.pos[J.b2][r] - a1[r] - s.pos[J.b1][r]);
   }
 }
@@ -136,10 +154,10 @@ __device__ inline void hinge_rows(L& s, const hs_simjoint& J, double fps, double
   plane_space(ax1, p, qv);
   mul0_331(ax2, s.R[J.b2], J.axis2);
   cross3(b, ax1, ax2);
-  for (int j = 0; j < 3; j++) {
-    s.J[r0 + 3][j] = 0; s.J[r0 + 3][3 + j] = p[j]; s.J[r0 + 3][6 + j] = 0; s.J[r0 + 3][9 + j] = -p[j];
-    s.J[r0 + 4][j] = 0; s.J[r0 + 4][3 + j] = qv[j]; s.J[r0 + 4][6 + j] = 0; s.J[r0 + 4][9 + j] = -qv[j];
-  }
+  const double r3[12] = {0, 0, 0, p[0], p[1], p[2], 0, 0, 0, -p[0], -p[1], -p[2]};
+  const double r4[12] = {0, 0, 0, qv[0], qv[1], qv[2], 0, 0, 0, -qv[0], -qv[1], -qv[2]};
+  put_row(s, r0 + 3, r3);
+  put_row(s, r0 + 4, r4);
   s.rhs[r0 + 3] = k * dot3(b, p);
   s.rhs[r0 + 4] = k * dot3(b, qv);
   for (int r = 0; r < 5; r++) {
@@ -161,7 +179,7 @@ __device__ inline void fixed_rows(L& s, const hs_simjoint& J, double fps, double
       {0, 1, 0, ofs[2], 0, -ofs[0], 0, -1, 0, 0, 0, 0},
       {0, 0, 1, -ofs[1], ofs[0], 0, 0, 0, -1, 0, 0, 0}};
   for (int r = 0; r < 3; r++) {
-    for (int j = 0; j < 12; j++) s.J[r0 + r][j] = rows[r][j];
+    put_row(s, r0 + r, rows[r]);
     s.rhs[r0 + r] = k * (s.pos[J.b2][r] - s.pos[J.b1][r] + ofs[r]);
   }
   // setFixedOrientation: rows 3..5, J1a = I, J2a = -I
@@ -171,9 +189,10 @@ __device__ inline void fixed_rows(L& s, const hs_simjoint& J, double fps, double
   if (qerr[0] < 0) { qerr[1] = -qerr[1]; qerr[2] = -qerr[2]; qerr[3] = -qerr[3]; }
   mul0_331(e, s.R[J.b1], qerr + 1);
   for (int r = 0; r < 3; r++) {
-    for (int j = 0; j < 12; j++) s.J[r0 + 3 + r][j] = 0;
-    s.J[r0 + 3 + r][3 + r] = 1;
-    s.J[r0 + 3 + r][9 + r] = -1;
+    double row[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    row[3 + r] = 1;
+    row[9 + r] = -1;
+    put_row(s, r0 + 3 + r, row);
     s.rhs[r0 + 3 + r] = 2 * k * e[r];
   }
   for (int r = 0; r < 6; r++) {
@@ -196,12 +215,10 @@ __device__ inline void contact_rows(L& s, int b, const hs_sim_params& P, double 
   cross3(j1, c1, t1);
   cross3(j2, c1, t2);
   for (int j = 0; j < 3; j++) {
-    s.J[r0][j] = normal[j]; s.J[r0][3 + j] = jn[j];
-    s.J[r0 + 1][j] = t1[j]; s.J[r0 + 1][3 + j] = j1[j];
-    s.J[r0 + 2][j] = t2[j]; s.J[r0 + 2][3 + j] = j2[j];
+    s.J[r0][j] = normal[j]; s.J[r0][3 + j] = jn[j]; s.J[r0][6 + j] = 0;
+    s.J[r0 + 1][j] = t1[j]; s.J[r0 + 1][3 + j] = j1[j]; s.J[r0 + 1][6 + j] = 0;
+    s.J[r0 + 2][j] = t2[j]; s.J[r0 + 2][3 + j] = j2[j]; s.J[r0 + 2][6 + j] = 0;
   }
-  for (int r = 0; r < 3; r++)
-    for (int j = 6; j < 12; j++) s.J[r0 + r][j] = 0;
   const double k = fps * P.erp;
   double depth = s.cdepth[b];
   if (depth < 0) depth = 0;
@@ -256,11 +273,14 @@ __device__ inline RowData load_row(const L& s, int row, int half) {
   r.body = row < 0 ? -1 : (half ? b2 : b1);
   r.b2 = b2;
   r.rt = s.rtype[rr];
-  const int c0 = half * 6;
   const int bb = r.body < 0 ? 0 : r.body;
   double Jb[6];
 #pragma unroll
-  for (int j = 0; j < 6; j++) Jb[j] = s.J[rr][c0 + j];
+  for (int j = 0; j < 3; j++) {
+    const double l = s.J[rr][j];
+    Jb[j] = half ? -l : l;                 // J2l = -J1l
+    Jb[3 + j] = s.J[rr][3 + 3 * half + j];  // J1a | J2a
+  }
   const double ad = s.Ad[rr];
 #pragma unroll
   for (int j = 0; j < 6; j++) r.Js[j] = Jb[j] * ad;  // SOR_LCP: J *= Ad
@@ -497,7 +517,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
     for (int i = lane; i < m; i += WAVE) {
       const int b1 = s.rb1[i], b2 = s.rb2[i];
       double Jr[12];
-      for (int j = 0; j < 12; j++) Jr[j] = s.J[i][j];
+      get_row(s, i, Jr);
       double sum = 0;
       for (int j = 0; j < 6; j++) sum += Jr[j] * s.fc[b1][j];  // fc holds tmp1 here
       if (b2 >= 0)
