@@ -294,15 +294,16 @@ def main():
         ms_per_step = 1e3 * elapsed / args.steps
         alg_bytes = B * Hh * (out_bytes + width * PARAM_BYTES / Hh)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = None
+        traffic = fp64_flops = None
         tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tf):
             try:
                 j = json.load(open(tf))
                 if j.get("workload") == traffic_key:
                     traffic = j.get("hbm_bytes_per_launch")
+                    fp64_flops = j.get("fp64_lane_flops_per_launch")
             except Exception:
-                traffic = None
+                traffic = fp64_flops = None
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -316,6 +317,11 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "hs_rollout_kernel", "kernel_ms": round(kern_ms, 5),
                          "alg_bytes_per_launch": alg_bytes},
+            # the bound that binds: FP64 VALU issue, from the committed PMC instruction counts of this
+            # workload (profiles/pmc_traffic.json) over the live kernel time (inactive lanes included)
+            "fp64_valu": None if fp64_flops is None else {
+                "issued_tflops": round(fp64_flops / (kern_ms * 1e-3) / 1e12, 3), "peak_tflops": FP64_PEAK_TFLOPS,
+                "frac": fp64_flops / (kern_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS},
             "best_rollout": {"id": best_id, "cot": best_cot},
             "nan_steps": nan_steps,
         }

@@ -57,13 +57,22 @@ def main():
     if "FETCH_SIZE" in med and "WRITE_SIZE" in med:
         traffic = int(round((2 * med["FETCH_SIZE"] + med["WRITE_SIZE"]) * 1024))
         lines.append(f"HBM traffic per launch (gfx950 correction: FETCH_SIZE x2): {traffic} bytes")
+    fp64 = None
+    if all(c in med for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64")):
+        # issued FP64 lane operations (64 lanes per wave instruction, FMA = 2): an upper bound on the
+        # useful FP64 work, inactive lanes included
+        fp64 = int(64 * (med["SQ_INSTS_VALU_ADD_F64"] + med["SQ_INSTS_VALU_MUL_F64"] +
+                         2 * med["SQ_INSTS_VALU_FMA_F64"]))
+        lines.append(f"issued FP64 lane flops per launch (64 x (ADD + MUL + 2 FMA)): {fp64}")
     with open(a.out, "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
     if a.traffic_json and traffic is not None:
         with open(a.traffic_json, "w") as f:
             json.dump({"workload": a.workload, "hbm_bytes_per_launch": traffic,
-                       "source": f"{a.out} (FETCH_SIZE x2 + WRITE_SIZE, KiB -> B)"}, f, indent=1)
+                       "fp64_lane_flops_per_launch": fp64,
+                       "source": f"{a.out} (FETCH_SIZE x2 + WRITE_SIZE, KiB -> B; FP64 instruction counts)"},
+                      f, indent=1)
             f.write("\n")
 
 
