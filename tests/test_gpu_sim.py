@@ -160,3 +160,29 @@ def test_bad_arguments_fail_loudly(gpu, hmodels):
     a.q_tab = None
     assert L.hs_sim_step(hmodels["hexapod"].handle, ctypes.byref(a)) == -1
     assert b"tables" in L.hs_last_error()
+
+
+@pytest.mark.parametrize("name", ["hexapod", "spider", "myant"])
+def test_every_part_in_contact(gpu, hmodels, oracle_mod, omodels, name):
+    """Maximum row count: the robot pushed into the plane so every capsule and sphere touches it
+    (hexapod: 108 joint rows + 22 contacts x 3 = 174 of the 176-row layout), 5 steps vs the oracle."""
+    import torch
+
+    sb = make_batch(gpu, hmodels[name], name, 4)
+    sb.body[:, :, 2] = 0.0  # every body centre on the plane: every capsule and sphere penetrates it
+    body0 = sb.body.cpu().numpy()
+    qt, dqt, tt = tables(sb)
+    out = sb.step(5)
+    torch.cuda.synchronize()
+    body = sb.body.cpu().numpy()
+    nc = out["n_contacts"].cpu().numpy()
+    import xml.etree.ElementTree as ET
+
+    bodies = ET.parse(os.path.join(MODELS, f"{name}.xml")).getroot().iter("body")
+    ncoll = sum(1 for bd in bodies if bd.find("geom") is not None and bd.find("geom").get("type") in ("capsule", "sphere"))
+    assert nc[:, 0].max() == ncoll
+    P = oracle_mod.SimParams()
+    for b in range(4):
+        r = oracle_mod.sim_run(omodels[name], P, sb.n_t, qt[b], dqt[b], tt[b], body0[b], 0, 2, 5)
+        assert (r["n_contacts"] == nc[b]).all()
+        assert np.abs(r["body"] - body[b]).max() < 1e-9 * max(1.0, np.abs(r["body"]).max())
