@@ -112,10 +112,10 @@ def sim_cpu_baseline(model, name, sb, seconds, threads):
     threads = max(1, min(threads, os.cpu_count() or 1))
     om = O.Model(os.path.join(ROOT, "models", f"{name}.xml"))
     nb = min(sb.B, 4 * threads)
-    qt = sb.tables.q[:nb].cpu().numpy().copy()
-    dqt = sb.tables.dq[:nb].cpu().numpy().copy()
-    tt = sb.tables.tau[:nb].cpu().numpy().copy()
-    body0 = sb.body[:nb].cpu().numpy().copy()
+    qt = sb.tables.q[:nb].cpu().numpy().astype(np.float64)
+    dqt = sb.tables.dq[:nb].cpu().numpy().astype(np.float64)
+    tt = sb.tables.tau[:nb].cpu().numpy().astype(np.float64)
+    body0 = sb.body[:nb].cpu().numpy().astype(np.float64)
     P = O.SimParams()
 
     def timed(nthr, budget):
@@ -134,7 +134,7 @@ def sim_cpu_baseline(model, name, sb, seconds, threads):
     rate, done, el = timed(threads, seconds)
     return {"value": round(rate, 1), "unit": "steps/s", "cores": threads, "kind": "port",
             "sample": f"{done} simulation steps ({name}, {nb} rollouts of the batch, 10-step calls) in {el:.1f}s, "
-                      f"oracle ODE-QuickStep restatement, g++ -O2, std::thread x{threads}; "
+                      f"oracle ODE-QuickStep restatement (double, as ODE computes), g++ -O2, std::thread x{threads}; "
                       f"single-thread {single:.1f} steps/s",
             "single_thread": round(single, 1)}
 
@@ -145,7 +145,8 @@ def main_sim(args, torch, dist, world, rank, dev):
 
     B = args.rollouts
     model = H.KinematicModel(os.path.join(ROOT, "models", f"{args.model}.xml"))
-    sb = H.SimBatch(model, synth.gen_sim_params(B, args.model, id0=rank * B), device=dev)
+    dtype = torch.float32 if args.fp32 else torch.float64
+    sb = H.SimBatch(model, synth.gen_sim_params(B, args.model, id0=rank * B), device=dev, dtype=dtype)
     stream = torch.cuda.current_stream(dev)
     sb.step(args.warmup, stream=stream, outputs=())
     torch.cuda.synchronize()
@@ -168,18 +169,20 @@ def main_sim(args, torch, dist, world, rank, dev):
     finite = bool(torch.isfinite(sb.body).all().item())
     if rank == 0:
         nmj = model.nmj
-        # per rollout-step the kernel must read the controller row (q0, dq0, tau_ff: 3 nmj doubles);
-        # the body state (n x 13 doubles) crosses HBM once per launch in each direction
-        alg_bytes = B * (args.steps * 3 * nmj * 8 + 2 * model.n_parts * 13 * 8)
+        # per rollout-step the kernel must read the controller row (q0, dq0, tau_ff: 3 nmj reals);
+        # the body state (n x 13 reals) crosses HBM once per launch in each direction
+        w = 4 if args.fp32 else 8
+        alg_bytes = B * (args.steps * 3 * nmj * w + 2 * model.n_parts * 13 * w)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         out = {
             "metric": SIM_METRIC, "value": round(B * args.steps * world / elapsed, 1), "unit": "steps/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64",
+            "vs_baseline": None, "dtype": "f32" if args.fp32 else "f64",
             "data": "synthetic (splitmix64 gait parameters around pgs id 8, period 3 -> n_t 300; SURVEY.md 8d)",
             "config": {"workload": f"{args.model}.xml B={B}/GPU closed-loop simulation, play_dt .01, QuickStep 20 "
-                                   f"iterations, {args.steps} steps per launch (SURVEY.md 8f row 4)",
+                                   f"iterations, {args.steps} steps per launch, "
+                                   f"{'fp32' if args.fp32 else 'fp64'} (SURVEY.md 8f row 4)",
                        "rollouts_per_gpu": B, "parallelism": f"rollout-sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "hs_sim_kernel",

@@ -281,7 +281,9 @@ class SimBatch:
     """
 
     def __init__(self, model: KinematicModel, params, dt: float = 0.01, tsi0: int = 2, device=None,
-                 ignore_reach: bool = True, **sim_overrides):
+                 ignore_reach: bool = True, dtype=None, **sim_overrides):
+        """dtype: torch.float64 (default) or torch.float32 (HS_PREC_F32: single-precision tables,
+        state and arithmetic, BASELINE configs[2])."""
         import torch
 
         self.torch = torch
@@ -302,10 +304,13 @@ class SimBatch:
             setattr(self.params, k, v)
         dev = device or torch.device("cuda", torch.cuda.current_device())
         self.device = dev
+        self.dtype = dtype or torch.float64
+        assert self.dtype in (torch.float64, torch.float32)
+        self.precision = capi.HS_PREC_F32 if self.dtype == torch.float32 else capi.HS_PREC_F64
         self.tables = DeviceBatch(model, arr, n_t=self.n_t, k0=0, horizon=self.n_t, ignore_reach=ignore_reach,
-                                  outputs=("q", "dq", "tau"), device=dev)
+                                  outputs=("q", "dq", "tau"), device=dev, dtype=self.dtype)
         self.tables.run(best=False)
-        self.body = torch.empty((self.B, model.n_parts, capi.SIM_BODY_STRIDE), dtype=torch.float64, device=dev)
+        self.body = torch.empty((self.B, model.n_parts, capi.SIM_BODY_STRIDE), dtype=self.dtype, device=dev)
         self.seed = torch.zeros(self.B, dtype=torch.int32, device=dev)
         self.tsi = torch.full((self.B,), int(tsi0), dtype=torch.int32, device=dev)
         self.reset(tsi0)
@@ -326,7 +331,7 @@ class SimBatch:
         config = self.tables.q[:, self.table_row(tsi0), :].contiguous()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         capi.check(capi.load().hs_sim_reset(self.model.handle, self.B, config.data_ptr(), config.shape[1],
-                                            self.body.data_ptr(), st.cuda_stream), "hs_sim_reset")
+                                            self.body.data_ptr(), self.precision, st.cuda_stream), "hs_sim_reset")
         self._config = config
         self.seed.zero_()
         self.tsi.fill_(int(tsi0))
@@ -337,7 +342,7 @@ class SimBatch:
         per-step outputs as device tensors [B][n_steps][...]."""
         torch = self.torch
         B, nmj = self.B, self.model.nmj
-        f64 = dict(dtype=torch.float64, device=self.device)
+        f64 = dict(dtype=self.dtype, device=self.device)
         out = {}
         if "tau_cmd" in outputs:
             out["tau_cmd"] = torch.empty((B, n_steps, nmj), **f64)
@@ -351,6 +356,7 @@ class SimBatch:
             out["normal_force"] = torch.empty((B, n_steps), **f64)
         a = capi.SimArgsC()
         a.n_rollouts, a.n_steps, a.n_t = B, n_steps, self.n_t
+        a.precision = self.precision
         a.params = self.params
         a.body, a.seed, a.tsi = self.body.data_ptr(), self.seed.data_ptr(), self.tsi.data_ptr()
         a.q_tab, a.dq_tab, a.tau_tab = self.tables.q.data_ptr(), self.tables.dq.data_ptr(), self.tables.tau.data_ptr()

@@ -11,7 +11,7 @@ import os
 
 from . import build as _build
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 HS_OK = 0
 HS_FLAG_RANK_RETRY = 1
@@ -93,7 +93,7 @@ class SimParamsC(ctypes.Structure):
 class SimArgsC(ctypes.Structure):
     """hs_sim_args."""
     _fields_ = [("n_rollouts", ctypes.c_int32), ("n_steps", ctypes.c_int32), ("n_t", ctypes.c_int32),
-                ("reserved", ctypes.c_int32), ("params", SimParamsC)] + \
+                ("precision", ctypes.c_int32), ("params", SimParamsC)] + \
                [(f, ctypes.c_void_p) for f in ("body", "seed", "tsi", "q_tab", "dq_tab", "tau_tab", "tau_cmd", "q_meas",
                                                "torso", "n_contacts", "normal_force", "stream")]
 
@@ -164,7 +164,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_best_key_decode.restype = None
     L.hs_sim_default_params.argtypes = [ctypes.POINTER(SimParamsC)]
     L.hs_sim_default_params.restype = None
-    L.hs_sim_reset.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int32, vp, vp]
+    L.hs_sim_reset.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int32, vp, ctypes.c_int32, vp]
     L.hs_sim_step.argtypes = [vp, ctypes.POINTER(SimArgsC)]
     L.hs_sim_create.argtypes = [vp, ctypes.POINTER(GaitParamsC), ctypes.c_int32, ctypes.POINTER(SimParamsC),
                                 ctypes.c_double, ctypes.POINTER(vp)]

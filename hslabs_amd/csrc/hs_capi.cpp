@@ -95,7 +95,8 @@ int device_state(hs_model_t m, int n_rollouts, void* stream, const hs_topo** top
 }
 
 // Device copies of the topology and the ODE world description for the current device.
-int sim_device_state(hs_model_t m, const hs_topo** topo, const hs_simtopo** sim) {
+int sim_device_state(hs_model_t m, const hs_topo** topo, const hs_simtopo** sim,
+                     const hs_simtopo_t<float>** sim_f32 = nullptr) {
   int rc = device_state(m, 0, nullptr, topo, nullptr);
   if (rc != HS_OK) return rc;
   int dev = 0;
@@ -110,7 +111,18 @@ int sim_device_state(hs_model_t m, const hs_topo** topo, const hs_simtopo** sim)
     if (e != hipSuccess) { (void)hipFree(d); return hip_fail(e, "hipMemcpy(simtopo)"); }
     m->sim_dev[dev] = d;
   }
+  if (sim_f32 && !m->sim_dev_f32[dev]) {
+    hs_simtopo_t<float> h;
+    hs_simtopo_round(h, m->sim);
+    hs_simtopo_t<float>* d = nullptr;
+    e = hipMalloc(&d, sizeof(h));
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(simtopo f32)");
+    e = hipMemcpy(d, &h, sizeof(h), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { (void)hipFree(d); return hip_fail(e, "hipMemcpy(simtopo f32)"); }
+    m->sim_dev_f32[dev] = d;
+  }
   *sim = m->sim_dev[dev];
+  if (sim_f32) *sim_f32 = m->sim_dev_f32[dev];
   return HS_OK;
 }
 
@@ -190,6 +202,7 @@ int hs_model_load_ex(const char* xml_path, int lik_variant, hs_model_t* out) {
   hs_model_s* m = new hs_model_s;
   memset(m->dev, 0, sizeof(m->dev));
   memset(m->sim_dev, 0, sizeof(m->sim_dev));
+  memset(m->sim_dev_f32, 0, sizeof(m->sim_dev_f32));
   std::string err;
   int rc = hs::load_model_file(xml_path, lik_variant, &m->host, err, &m->sim);
   if (rc != HS_OK) {
@@ -207,6 +220,7 @@ void hs_model_free(hs_model_t m) {
   for (int d = 0; d < HS_MAX_DEVICES; d++) {
     if (m->dev[d]) free_on_device(d, m->dev[d]);
     if (m->sim_dev[d]) free_on_device(d, m->sim_dev[d]);
+    if (m->sim_dev_f32[d]) free_on_device(d, m->sim_dev_f32[d]);
   }
   m->ws.release();
   delete m;
@@ -609,17 +623,18 @@ void hs_sim_default_params(hs_sim_params* p) {
 }
 
 int hs_sim_reset(hs_model_t m, int32_t n_rollouts, const double* config, int32_t config_stride, double* body,
-                 void* stream) {
+                 int32_t precision, void* stream) {
   if (!m) return fail(HS_E_ARG, "null model");
   if (n_rollouts < 0 || n_rollouts > (1 << 30)) return fail(HS_E_ARG, "bad n_rollouts");
   if (n_rollouts == 0) return HS_OK;
   if (!config || !body) return fail(HS_E_ARG, "null config or body");
   if (config_stride < m->host.cfg) return fail(HS_E_ARG, "config_stride < config_dim");
+  if (precision != HS_PREC_F64 && precision != HS_PREC_F32) return fail(HS_E_ARG, "unknown precision");
   const hs_topo* d = nullptr;
   const hs_simtopo* ds = nullptr;
   int rc = sim_device_state(m, &d, &ds);
   if (rc != HS_OK) return rc;
-  int e = hs::launch_sim_reset(d, ds, n_rollouts, config, config_stride, body, stream);
+  int e = hs::launch_sim_reset(d, ds, n_rollouts, config, config_stride, body, precision, stream);
   if (e != 0) return hip_fail((hipError_t)e, "hs_sim_reset launch");
   return HS_OK;
 }
@@ -639,13 +654,15 @@ int hs_sim_step(hs_model_t m, const hs_sim_args* a) {
     if (!a->q_tab || !a->dq_tab || !a->tau_tab) return fail(HS_E_ARG, "controller tables are required when k > 0");
   }
   if (m->sim.m_max > 9 * HS_NMAX) return fail(HS_E_TOPOLOGY, "too many constraint rows for the simulation kernel");
+  if (a->precision != HS_PREC_F64 && a->precision != HS_PREC_F32) return fail(HS_E_ARG, "unknown precision");
   const hs_topo* d = nullptr;
   const hs_simtopo* ds = nullptr;
-  int rc = sim_device_state(m, &d, &ds);
+  const hs_simtopo_t<float>* dsf = nullptr;
+  int rc = sim_device_state(m, &d, &ds, a->precision == HS_PREC_F32 ? &dsf : nullptr);
   if (rc != HS_OK) return rc;
   hs_sim_args c = *a;
   if (c.n_t < 1) c.n_t = 1;
-  int e = hs::launch_sim_steps(d, ds, m->sim, c);
+  int e = hs::launch_sim_steps(d, ds, dsf, m->sim, c);
   if (e != 0) return hip_fail((hipError_t)e, "hs_sim_step launch");
   return HS_OK;
 }
@@ -725,7 +742,8 @@ int hs_sim_create(hs_model_t m, const hs_gait_params* params, int32_t B, const h
   const int tsi0 = (int)(t0 / P.dt + .5);  // play_t = int(t0/play_dt+.5)*play_dt
   const int h0 = ((tsi0 % n_t) + n_t - 2) % n_t;
   if (rc == HS_OK)
-    rc = hs_sim_reset(m, B, (const double*)s->q + (size_t)h0 * t.cfg, n_t * t.cfg, (double*)s->body, s->stream);
+    rc = hs_sim_reset(m, B, (const double*)s->q + (size_t)h0 * t.cfg, n_t * t.cfg, (double*)s->body, HS_PREC_F64,
+                      s->stream);
   std::vector<int32_t> tsi(nb, tsi0);
   if (rc == HS_OK) {
     e = hipMemsetAsync(s->seed, 0, nb * sizeof(uint32_t), s->stream);

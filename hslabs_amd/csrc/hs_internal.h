@@ -47,9 +47,9 @@ launch_map single_model_map(const hs_topo& t, int32_t n_rollouts);
 
 // closed-loop simulation kernels (hs_sim.hip); return hipError_t values
 int launch_sim_reset(const hs_topo* d_topo, const hs_simtopo* d_sim, int32_t n_rollouts, const double* config,
-                     int32_t config_stride, double* body, void* stream);
-int launch_sim_steps(const hs_topo* d_topo, const hs_simtopo* d_sim, const hs_simtopo& host_sim,
-                     const hs_sim_args& a);
+                     int32_t config_stride, double* body, int32_t precision, void* stream);
+int launch_sim_steps(const hs_topo* d_topo, const hs_simtopo* d_sim, const hs_simtopo_t<float>* d_sim_f32,
+                     const hs_simtopo& host_sim, const hs_sim_args& a);
 
 }  // namespace hs
 
@@ -77,6 +77,7 @@ struct hs_model_s {
   hs_topo* dev[HS_MAX_DEVICES];  // per-device topology copy, created lazily
   hs_simtopo sim;                // ODE world of the model (closed-loop simulation)
   hs_simtopo* sim_dev[HS_MAX_DEVICES];
+  hs_simtopo_t<float>* sim_dev_f32[HS_MAX_DEVICES];  // rounded copy for the single-precision kernel
   ws_pool ws;
   std::mutex mu;
 };

@@ -1,5 +1,6 @@
 // hs_ode.h -- the ODE rigid-body formulas the closed-loop simulation needs,
-// restated for host (model load) and device (hs_sim.hip) in double precision.
+// restated for host (model load) and device (hs_sim.hip); templates on the real type
+// (double everywhere the reference computes, float for the single-precision simulation).
 //
 // Conventions follow ODE 0.13 (the reference links an unpinned -lode built in
 // double precision, makefile:7-9): dMatrix3 is row-major 3x4 (R[i*4+j]),
@@ -14,40 +15,48 @@ namespace hsode {
 
 #define HSODE_FN __host__ __device__ __attribute__((always_inline)) inline
 
-HSODE_FN double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-HSODE_FN double dot3_41(const double* a, const double* b) { return a[0] * b[0] + a[4] * b[1] + a[8] * b[2]; }
-HSODE_FN double dot3_14(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[4] + a[2] * b[8]; }
-HSODE_FN void cross3(double* r, const double* a, const double* b) {
-  double r0 = a[1] * b[2] - a[2] * b[1], r1 = a[2] * b[0] - a[0] * b[2], r2 = a[0] * b[1] - a[1] * b[0];
+template <class T>
+HSODE_FN T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+template <class T>
+HSODE_FN T dot3_41(const T* a, const T* b) { return a[0] * b[0] + a[4] * b[1] + a[8] * b[2]; }
+template <class T>
+HSODE_FN T dot3_14(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[4] + a[2] * b[8]; }
+template <class T>
+HSODE_FN void cross3(T* r, const T* a, const T* b) {
+  T r0 = a[1] * b[2] - a[2] * b[1], r1 = a[2] * b[0] - a[0] * b[2], r2 = a[0] * b[1] - a[1] * b[0];
   r[0] = r0; r[1] = r1; r[2] = r2;
 }
 // r = B c, B a dMatrix3 (dMultiply0_331)
-HSODE_FN void mul0_331(double* r, const double* B, const double* c) {
-  double r0 = dot3(B, c), r1 = dot3(B + 4, c), r2 = dot3(B + 8, c);
+template <class T>
+HSODE_FN void mul0_331(T* r, const T* B, const T* c) {
+  T r0 = dot3(B, c), r1 = dot3(B + 4, c), r2 = dot3(B + 8, c);
   r[0] = r0; r[1] = r1; r[2] = r2;
 }
 // r = B^T c (dMultiply1_331)
-HSODE_FN void mul1_331(double* r, const double* B, const double* c) {
-  double r0 = dot3_41(B, c), r1 = dot3_41(B + 1, c), r2 = dot3_41(B + 2, c);
+template <class T>
+HSODE_FN void mul1_331(T* r, const T* B, const T* c) {
+  T r0 = dot3_41(B, c), r1 = dot3_41(B + 1, c), r2 = dot3_41(B + 2, c);
   r[0] = r0; r[1] = r1; r[2] = r2;
 }
 
 // rotation.cpp dQtoR
-HSODE_FN void q_to_R(const double* q, double* R) {
-  double qq1 = 2 * q[1] * q[1], qq2 = 2 * q[2] * q[2], qq3 = 2 * q[3] * q[3];
+template <class T>
+HSODE_FN void q_to_R(const T* q, T* R) {
+  T qq1 = 2 * q[1] * q[1], qq2 = 2 * q[2] * q[2], qq3 = 2 * q[3] * q[3];
   R[0] = 1 - qq2 - qq3; R[1] = 2 * (q[1] * q[2] - q[0] * q[3]); R[2] = 2 * (q[1] * q[3] + q[0] * q[2]); R[3] = 0;
   R[4] = 2 * (q[1] * q[2] + q[0] * q[3]); R[5] = 1 - qq1 - qq3; R[6] = 2 * (q[2] * q[3] - q[0] * q[1]); R[7] = 0;
   R[8] = 2 * (q[1] * q[3] - q[0] * q[2]); R[9] = 2 * (q[2] * q[3] + q[0] * q[1]); R[10] = 1 - qq1 - qq2; R[11] = 0;
 }
 
 // rotation.cpp dQfromR
-HSODE_FN void q_from_R(double* q, const double* R) {
+template <class T>
+HSODE_FN void q_from_R(T* q, const T* R) {
 #define HSODE_R(i, j) R[(i) * 4 + (j)]
-  double tr = HSODE_R(0, 0) + HSODE_R(1, 1) + HSODE_R(2, 2), s;
+  T tr = HSODE_R(0, 0) + HSODE_R(1, 1) + HSODE_R(2, 2), s;
   if (tr >= 0) {
     s = sqrt(tr + 1);
-    q[0] = 0.5 * s;
-    s = 0.5 * (1.0 / s);
+    q[0] = T(0.5) * s;
+    s = T(0.5) * (T(1) / s);
     q[1] = (HSODE_R(2, 1) - HSODE_R(1, 2)) * s;
     q[2] = (HSODE_R(0, 2) - HSODE_R(2, 0)) * s;
     q[3] = (HSODE_R(1, 0) - HSODE_R(0, 1)) * s;
@@ -58,22 +67,22 @@ HSODE_FN void q_from_R(double* q, const double* R) {
   else c = (HSODE_R(2, 2) > HSODE_R(0, 0)) ? 2 : 0;
   if (c == 0) {
     s = sqrt((HSODE_R(0, 0) - (HSODE_R(1, 1) + HSODE_R(2, 2))) + 1);
-    q[1] = 0.5 * s;
-    s = 0.5 * (1.0 / s);
+    q[1] = T(0.5) * s;
+    s = T(0.5) * (T(1) / s);
     q[2] = (HSODE_R(0, 1) + HSODE_R(1, 0)) * s;
     q[3] = (HSODE_R(2, 0) + HSODE_R(0, 2)) * s;
     q[0] = (HSODE_R(2, 1) - HSODE_R(1, 2)) * s;
   } else if (c == 1) {
     s = sqrt((HSODE_R(1, 1) - (HSODE_R(2, 2) + HSODE_R(0, 0))) + 1);
-    q[2] = 0.5 * s;
-    s = 0.5 * (1.0 / s);
+    q[2] = T(0.5) * s;
+    s = T(0.5) * (T(1) / s);
     q[3] = (HSODE_R(1, 2) + HSODE_R(2, 1)) * s;
     q[1] = (HSODE_R(0, 1) + HSODE_R(1, 0)) * s;
     q[0] = (HSODE_R(0, 2) - HSODE_R(2, 0)) * s;
   } else {
     s = sqrt((HSODE_R(2, 2) - (HSODE_R(0, 0) + HSODE_R(1, 1))) + 1);
-    q[3] = 0.5 * s;
-    s = 0.5 * (1.0 / s);
+    q[3] = T(0.5) * s;
+    s = T(0.5) * (T(1) / s);
     q[1] = (HSODE_R(2, 0) + HSODE_R(0, 2)) * s;
     q[2] = (HSODE_R(1, 2) + HSODE_R(2, 1)) * s;
     q[0] = (HSODE_R(1, 0) - HSODE_R(0, 1)) * s;
@@ -82,10 +91,11 @@ HSODE_FN void q_from_R(double* q, const double* R) {
 }
 
 // odemath.cpp dSafeNormalize4
-HSODE_FN void normalize4(double* a) {
-  double l = a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3];
+template <class T>
+HSODE_FN void normalize4(T* a) {
+  T l = a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3];
   if (l > 0) {
-    l = 1.0 / sqrt(l);
+    l = T(1) / sqrt(l);
     a[0] *= l; a[1] *= l; a[2] *= l; a[3] *= l;
   } else {
     a[0] = 1; a[1] = a[2] = a[3] = 0;
@@ -93,8 +103,9 @@ HSODE_FN void normalize4(double* a) {
 }
 
 // odemath.cpp dSafeNormalize3 (scale by the largest magnitude first)
-HSODE_FN void normalize3(double* a) {
-  double aa0 = fabs(a[0]), aa1 = fabs(a[1]), aa2 = fabs(a[2]), l;
+template <class T>
+HSODE_FN void normalize3(T* a) {
+  T aa0 = fabs(a[0]), aa1 = fabs(a[1]), aa2 = fabs(a[2]), l;
   if (aa1 > aa0) l = (aa2 > aa1) ? aa2 : aa1;
   else if (aa2 > aa0) l = aa2;
   else {
@@ -102,37 +113,40 @@ HSODE_FN void normalize3(double* a) {
     l = aa0;
   }
   a[0] /= l; a[1] /= l; a[2] /= l;
-  l = 1.0 / sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+  l = T(1) / sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
   a[0] *= l; a[1] *= l; a[2] *= l;
 }
 
 // dQMultiply1: qa = conj(qb) qc
-HSODE_FN void qmul1(double* qa, const double* qb, const double* qc) {
-  double a0 = qb[0] * qc[0] + qb[1] * qc[1] + qb[2] * qc[2] + qb[3] * qc[3];
-  double a1 = qb[0] * qc[1] - qb[1] * qc[0] - qb[2] * qc[3] + qb[3] * qc[2];
-  double a2 = qb[0] * qc[2] - qb[2] * qc[0] - qb[3] * qc[1] + qb[1] * qc[3];
-  double a3 = qb[0] * qc[3] - qb[3] * qc[0] - qb[1] * qc[2] + qb[2] * qc[1];
+template <class T>
+HSODE_FN void qmul1(T* qa, const T* qb, const T* qc) {
+  T a0 = qb[0] * qc[0] + qb[1] * qc[1] + qb[2] * qc[2] + qb[3] * qc[3];
+  T a1 = qb[0] * qc[1] - qb[1] * qc[0] - qb[2] * qc[3] + qb[3] * qc[2];
+  T a2 = qb[0] * qc[2] - qb[2] * qc[0] - qb[3] * qc[1] + qb[1] * qc[3];
+  T a3 = qb[0] * qc[3] - qb[3] * qc[0] - qb[1] * qc[2] + qb[2] * qc[1];
   qa[0] = a0; qa[1] = a1; qa[2] = a2; qa[3] = a3;
 }
 // dQMultiply2: qa = qb conj(qc)
-HSODE_FN void qmul2(double* qa, const double* qb, const double* qc) {
-  double a0 = qb[0] * qc[0] + qb[1] * qc[1] + qb[2] * qc[2] + qb[3] * qc[3];
-  double a1 = -qb[0] * qc[1] + qb[1] * qc[0] - qb[2] * qc[3] + qb[3] * qc[2];
-  double a2 = -qb[0] * qc[2] + qb[2] * qc[0] - qb[3] * qc[1] + qb[1] * qc[3];
-  double a3 = -qb[0] * qc[3] + qb[3] * qc[0] - qb[1] * qc[2] + qb[2] * qc[1];
+template <class T>
+HSODE_FN void qmul2(T* qa, const T* qb, const T* qc) {
+  T a0 = qb[0] * qc[0] + qb[1] * qc[1] + qb[2] * qc[2] + qb[3] * qc[3];
+  T a1 = -qb[0] * qc[1] + qb[1] * qc[0] - qb[2] * qc[3] + qb[3] * qc[2];
+  T a2 = -qb[0] * qc[2] + qb[2] * qc[0] - qb[3] * qc[1] + qb[1] * qc[3];
+  T a3 = -qb[0] * qc[3] + qb[3] * qc[0] - qb[1] * qc[2] + qb[2] * qc[1];
   qa[0] = a0; qa[1] = a1; qa[2] = a2; qa[3] = a3;
 }
 
 // odemath.cpp dPlaneSpace
-HSODE_FN void plane_space(const double* n, double* p, double* q) {
-  if (fabs(n[2]) > M_SQRT1_2) {
-    double a = n[1] * n[1] + n[2] * n[2];
-    double k = 1.0 / sqrt(a);
+template <class T>
+HSODE_FN void plane_space(const T* n, T* p, T* q) {
+  if (fabs(n[2]) > T(M_SQRT1_2)) {
+    T a = n[1] * n[1] + n[2] * n[2];
+    T k = T(1) / sqrt(a);
     p[0] = 0; p[1] = -n[2] * k; p[2] = n[1] * k;
     q[0] = a * k; q[1] = -n[0] * p[2]; q[2] = n[0] * p[1];
   } else {
-    double a = n[0] * n[0] + n[1] * n[1];
-    double k = 1.0 / sqrt(a);
+    T a = n[0] * n[0] + n[1] * n[1];
+    T k = T(1) / sqrt(a);
     p[0] = -n[1] * k; p[1] = n[0] * k; p[2] = 0;
     q[0] = -n[2] * p[1]; q[1] = n[2] * p[0]; q[2] = a * k;
   }

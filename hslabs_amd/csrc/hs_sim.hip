@@ -68,22 +68,35 @@ __device__ unsigned long long g_sim_stamps[4096][16];
 #define SIM_ACC(slot) do {} while (0)
 #endif
 
-template <int NM, int MM>
+// the run's parameters in the kernel's precision (k1, k2 as player.cpp:393-394 forms them)
+template <class real>
+struct SimP {
+  real dt, h1, k, k1, k2, sor_w, erp, cfm, gravity, bounce, bounce_vel, soft_cfm, mu;
+  int iterations;
+  __device__ explicit SimP(const hs_sim_params& p)
+      : dt((real)p.dt), h1(real(1) / (real)p.dt), k((real)p.k), k1(-(real)p.k),
+        k2(real(-2) * sqrt((real)p.k)), sor_w((real)p.sor_w), erp((real)p.erp), cfm((real)p.cfm),
+        gravity((real)p.gravity), bounce((real)p.bounce), bounce_vel((real)p.bounce_vel),
+        soft_cfm((real)p.soft_cfm), mu((real)p.mu), iterations(p.iterations) {}
+};
+
+template <int NM, int MM, class Real>
 struct SimL {
+  using real = Real;
   // bodies (part ids index everything; ODE's island numbering does not change any arithmetic)
-  double pos[NM][3], q[NM][4], R[NM][12], lvel[NM][3], avel[NM][3], tacc[NM][3];
-  double invI[NM][12];
-  double invm[NM];         // 1 / mass, kept on chip: the SOR rows read it for every update
-  double fc[NM][6];        // v/h + M^-1 f while the rows are built (ODE's tmp1), then SOR's fc
-  double cpos[NM][3], cdepth[NM];
-  double tau[NM];
+  real pos[NM][3], q[NM][4], R[NM][12], lvel[NM][3], avel[NM][3], tacc[NM][3];
+  real invI[NM][12];
+  real invm[NM];         // 1 / mass, kept on chip: the SOR rows read it for every update
+  real fc[NM][6];        // v/h + M^-1 f while the rows are built (ODE's tmp1), then SOR's fc
+  real cpos[NM][3], cdepth[NM];
+  real tau[NM];
   // constraint rows
-  double J[MM][9];         // Jacobian rows, unscaled, as J1l | J1a | J2a: every two-body row here has
+  real J[MM][9];         // Jacobian rows, unscaled, as J1l | J1a | J2a: every two-body row here has
                            // J2l = -J1l (ball, fixed and hinge-axis rows), and contacts have no body2
-  double rhs[MM];          // c, then rhs, then rhs * Ad
-  double cfm[MM];          // cfm, then cfm / h, then Ad * cfm
-  double Ad[MM];
-  double lambda[MM];
+  real rhs[MM];          // c, then rhs, then rhs * Ad
+  real cfm[MM];          // cfm, then cfm / h, then Ad * cfm
+  real Ad[MM];
+  real lambda[MM];
   int8_t rb1[MM], rb2[MM], rtype[MM];
   int16_t order[MM];       // row at each sweep position (ODE's order)
   int16_t swp[MM];         // Fisher-Yates swap targets s_i of a reshuffle
@@ -100,26 +113,27 @@ struct SimL {
 
 // hinge.cpp getHingeAngle (body1 = part, body2 = parent; no dJOINT_REVERSE)
 template <class L>
-__device__ inline double hinge_angle(const L& s, const hs_simjoint& J) {
-  double qq[4], qr[4];
+__device__ inline typename L::real hinge_angle(const L& s, const hs_simjoint_t<typename L::real>& J) {
+  using real = typename L::real;
+  real qq[4], qr[4];
   qmul1(qq, s.q[J.b1], s.q[J.b2]);
   qmul2(qr, qq, J.qrel);
-  double cost2 = qr[0];
-  double sint2 = sqrt(qr[1] * qr[1] + qr[2] * qr[2] + qr[3] * qr[3]);
-  double theta = (dot3(qr + 1, J.axis1) >= 0) ? (2 * atan2(sint2, cost2)) : (2 * atan2(sint2, -cost2));
-  if (theta > M_PI) theta -= 2 * M_PI;
+  real cost2 = qr[0];
+  real sint2 = sqrt(qr[1] * qr[1] + qr[2] * qr[2] + qr[3] * qr[3]);
+  real theta = (dot3(qr + 1, J.axis1) >= 0) ? (2 * atan2(sint2, cost2)) : (2 * atan2(sint2, -cost2));
+  if (theta > real(M_PI)) theta -= real(2 * M_PI);
   return -theta;
 }
 
 template <class L>
-__device__ inline void put_row(L& s, int r, const double* j12) {
+__device__ inline void put_row(L& s, int r, const typename L::real* j12) {
 #pragma unroll
   for (int j = 0; j < 6; j++) s.J[r][j] = j12[j];
 #pragma unroll
   for (int j = 0; j < 3; j++) s.J[r][6 + j] = j12[9 + j];
 }
 template <class L>
-__device__ inline void get_row(const L& s, int r, double* j12) {
+__device__ inline void get_row(const L& s, int r, typename L::real* j12) {
 #pragma unroll
   for (int j = 0; j < 6; j++) j12[j] = s.J[r][j];
 #pragma unroll
@@ -130,12 +144,13 @@ __device__ inline void get_row(const L& s, int r, double* j12) {
 }
 
 template <class L>
-__device__ inline void set_ball(L& s, const hs_simjoint& J, double k, int r0) {
-  double a1[3], a2[3];
+__device__ inline void set_ball(L& s, const hs_simjoint_t<typename L::real>& J, typename L::real k, int r0) {
+  using real = typename L::real;
+  real a1[3], a2[3];
   mul0_331(a1, s.R[J.b1], J.anchor1);
   mul0_331(a2, s.R[J.b2], J.anchor2);
   // J1l = I, J1a = -[a1]x, J2l = -I, J2a = [a2]x
-  const double rows[3][12] = {
+  const real rows[3][12] = {
       {1, 0, 0, 0, a1[2], -a1[1], -1, 0, 0, 0, -a2[2], a2[1]},
       {0, 1, 0, -a1[2], 0, a1[0], 0, -1, 0, a2[2], 0, -a2[0]},
       {0, 0, 1, a1[1], -a1[0], 0, 0, 0, -1, -a2[1], a2[0], 0}};
@@ -146,16 +161,17 @@ __device__ inline void set_ball(L& s, const hs_simjoint& J, double k, int r0) {
 }
 
 template <class L>
-__device__ inline void hinge_rows(L& s, const hs_simjoint& J, double fps, double erp, double cfm, int r0) {
-  const double k = fps * erp;
+__device__ inline void hinge_rows(L& s, const hs_simjoint_t<typename L::real>& J, typename L::real fps, typename L::real erp, typename L::real cfm, int r0) {
+  using real = typename L::real;
+  const real k = fps * erp;
   set_ball(s, J, k, r0);
-  double ax1[3], p[3], qv[3], ax2[3], b[3];
+  real ax1[3], p[3], qv[3], ax2[3], b[3];
   mul0_331(ax1, s.R[J.b1], J.axis1);
   plane_space(ax1, p, qv);
   mul0_331(ax2, s.R[J.b2], J.axis2);
   cross3(b, ax1, ax2);
-  const double r3[12] = {0, 0, 0, p[0], p[1], p[2], 0, 0, 0, -p[0], -p[1], -p[2]};
-  const double r4[12] = {0, 0, 0, qv[0], qv[1], qv[2], 0, 0, 0, -qv[0], -qv[1], -qv[2]};
+  const real r3[12] = {0, 0, 0, p[0], p[1], p[2], 0, 0, 0, -p[0], -p[1], -p[2]};
+  const real r4[12] = {0, 0, 0, qv[0], qv[1], qv[2], 0, 0, 0, -qv[0], -qv[1], -qv[2]};
   put_row(s, r0 + 3, r3);
   put_row(s, r0 + 4, r4);
   s.rhs[r0 + 3] = k * dot3(b, p);
@@ -169,12 +185,13 @@ __device__ inline void hinge_rows(L& s, const hs_simjoint& J, double fps, double
 }
 
 template <class L>
-__device__ inline void fixed_rows(L& s, const hs_simjoint& J, double fps, double erp, double cfm, int r0) {
-  const double k = fps * erp;
+__device__ inline void fixed_rows(L& s, const hs_simjoint_t<typename L::real>& J, typename L::real fps, typename L::real erp, typename L::real cfm, int r0) {
+  using real = typename L::real;
+  const real k = fps * erp;
   // three linear rows: J1l = I, J1a = [ofs]x, J2l = -I
-  double ofs[3];
+  real ofs[3];
   mul0_331(ofs, s.R[J.b1], J.offset);
-  const double rows[3][12] = {
+  const real rows[3][12] = {
       {1, 0, 0, 0, -ofs[2], ofs[1], -1, 0, 0, 0, 0, 0},
       {0, 1, 0, ofs[2], 0, -ofs[0], 0, -1, 0, 0, 0, 0},
       {0, 0, 1, -ofs[1], ofs[0], 0, 0, 0, -1, 0, 0, 0}};
@@ -183,13 +200,13 @@ __device__ inline void fixed_rows(L& s, const hs_simjoint& J, double fps, double
     s.rhs[r0 + r] = k * (s.pos[J.b2][r] - s.pos[J.b1][r] + ofs[r]);
   }
   // setFixedOrientation: rows 3..5, J1a = I, J2a = -I
-  double qq[4], qerr[4], e[3];
+  real qq[4], qerr[4], e[3];
   qmul1(qq, s.q[J.b1], s.q[J.b2]);
   qmul2(qerr, qq, J.qrel);
   if (qerr[0] < 0) { qerr[1] = -qerr[1]; qerr[2] = -qerr[2]; qerr[3] = -qerr[3]; }
   mul0_331(e, s.R[J.b1], qerr + 1);
   for (int r = 0; r < 3; r++) {
-    double row[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    real row[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     row[3 + r] = 1;
     row[9 + r] = -1;
     put_row(s, r0 + 3 + r, row);
@@ -205,11 +222,12 @@ __device__ inline void fixed_rows(L& s, const hs_simjoint& J, double fps, double
 
 // contact.cpp getInfo2: body1 = the geom's body, body2 = the environment, normal (0,0,1)
 template <class L>
-__device__ inline void contact_rows(L& s, int b, const hs_sim_params& P, double fps, int r0) {
-  const double normal[3] = {0, 0, 1};
-  double c1[3];
+__device__ inline void contact_rows(L& s, int b, const SimP<typename L::real>& P, typename L::real fps, int r0) {
+  using real = typename L::real;
+  const real normal[3] = {0, 0, 1};
+  real c1[3];
   for (int i = 0; i < 3; i++) c1[i] = s.cpos[b][i] - s.pos[b][i];
-  double jn[3], t1[3], t2[3], j1[3], j2[3];
+  real jn[3], t1[3], t2[3], j1[3], j2[3];
   cross3(jn, c1, normal);
   plane_space(normal, t1, t2);
   cross3(j1, c1, t1);
@@ -219,13 +237,13 @@ __device__ inline void contact_rows(L& s, int b, const hs_sim_params& P, double 
     s.J[r0 + 1][j] = t1[j]; s.J[r0 + 1][3 + j] = j1[j]; s.J[r0 + 1][6 + j] = 0;
     s.J[r0 + 2][j] = t2[j]; s.J[r0 + 2][3 + j] = j2[j]; s.J[r0 + 2][6 + j] = 0;
   }
-  const double k = fps * P.erp;
-  double depth = s.cdepth[b];
+  const real k = fps * P.erp;
+  real depth = s.cdepth[b];
   if (depth < 0) depth = 0;
-  double c = k * depth;
-  double outgoing = dot3(normal, s.lvel[b]) + dot3(jn, s.avel[b]);
+  real c = k * depth;
+  real outgoing = dot3(normal, s.lvel[b]) + dot3(jn, s.avel[b]);
   if (P.bounce_vel >= 0 && (-outgoing) > P.bounce_vel) {
-    double newc = -P.bounce * outgoing;
+    real newc = -P.bounce * outgoing;
     if (newc > c) c = newc;
   }
   s.rhs[r0] = c;
@@ -245,8 +263,9 @@ __device__ inline void contact_rows(L& s, int b, const hs_sim_params& P, double 
 
 // iMJ block of one body: linear invMass * J, angular invI * J (compute_invM_JT)
 template <class L>
-__device__ inline void imj_block(const L& s, const hs_simtopo& T, int b, const double* Jb, double* out) {
-  const double k1 = s.invm[b];
+__device__ inline void imj_block(const L& s, const hs_simtopo_t<typename L::real>& T, int b, const typename L::real* Jb, typename L::real* out) {
+  using real = typename L::real;
+  const real k1 = s.invm[b];
   for (int j = 0; j < 3; j++) out[j] = k1 * Jb[j];
   mul0_331(out + 3, s.invI[b], Jb + 3);
 }
@@ -256,36 +275,41 @@ __device__ inline double swap_pair(double v) {  // value of the other lane of th
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
+__device__ inline float swap_pair(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
 
 // What one lane of a row's lane pair needs of the row: its body block of the scaled J and of
 // iMJ (half 0: body1 columns 0..5, half 1: body2 columns 6..11); the even lane also the row's
 // scalars. Nothing here changes during the sweeps, so it is loaded one run ahead of use.
+template <class real>
 struct RowData {
-  double Js[6], iM[6], rhs, adcfm;
+  real Js[6], iM[6], rhs, adcfm;
   int body, b2, rt;
 };
 
 template <class L>
-__device__ inline RowData load_row(const L& s, int row, int half) {
-  RowData r;
+__device__ inline RowData<typename L::real> load_row(const L& s, int row, int half) {
+  using real = typename L::real;
+  RowData<real> r;
   const int rr = row < 0 ? 0 : row;
   const int b1 = s.rb1[rr], b2 = s.rb2[rr];
   r.body = row < 0 ? -1 : (half ? b2 : b1);
   r.b2 = b2;
   r.rt = s.rtype[rr];
   const int bb = r.body < 0 ? 0 : r.body;
-  double Jb[6];
+  real Jb[6];
 #pragma unroll
   for (int j = 0; j < 3; j++) {
-    const double l = s.J[rr][j];
+    const real l = s.J[rr][j];
     Jb[j] = half ? -l : l;                 // J2l = -J1l
     Jb[3 + j] = s.J[rr][3 + 3 * half + j];  // J1a | J2a
   }
-  const double ad = s.Ad[rr];
+  const real ad = s.Ad[rr];
 #pragma unroll
   for (int j = 0; j < 6; j++) r.Js[j] = Jb[j] * ad;  // SOR_LCP: J *= Ad
   // compute_invM_JT: invMass J (linear), invI J (angular)
-  const double k1 = s.invm[bb];
+  const real k1 = s.invm[bb];
   for (int j = 0; j < 3; j++) r.iM[j] = k1 * Jb[j];
   mul0_331(r.iM + 3, s.invI[bb], Jb + 3);
   r.rhs = s.rhs[rr];
@@ -299,33 +323,34 @@ __device__ inline RowData load_row(const L& s, int row, int half) {
 // of the fc update are fused here (explicit fma; the file is otherwise unfused), which moves
 // lambda by ulps against the unfused restatement and never decides a contact.
 template <class L>
-__device__ inline void sor_pair(L& s, const RowData& r, int row, int half, double mu) {
+__device__ inline void sor_pair(L& s, const RowData<typename L::real>& r, int row, int half, typename L::real mu) {
+  using real = typename L::real;
   const bool act = row >= 0 && r.body >= 0;
-  const double* f = s.fc[act ? r.body : 0];
-  const double f0 = f[0], f1 = f[1], f2 = f[2], f3 = f[3], f4 = f[4], f5 = f[5];
-  const double lam = s.lambda[row < 0 ? 0 : row];
-  double sum = f0 * r.Js[0];
+  const real* f = s.fc[act ? r.body : 0];
+  const real f0 = f[0], f1 = f[1], f2 = f[2], f3 = f[3], f4 = f[4], f5 = f[5];
+  const real lam = s.lambda[row < 0 ? 0 : row];
+  real sum = f0 * r.Js[0];
   sum = fma(f1, r.Js[1], sum);
   sum = fma(f2, r.Js[2], sum);
   sum = fma(f3, r.Js[3], sum);
   sum = fma(f4, r.Js[4], sum);
   sum = fma(f5, r.Js[5], sum);
   if (!act) sum = 0;
-  const double other = swap_pair(sum);  // the body2 sum, on the even lane
-  double delta = r.rhs - lam * r.adcfm;
+  const real other = swap_pair(sum);  // the body2 sum, on the even lane
+  real delta = r.rhs - lam * r.adcfm;
   delta -= sum;
-  delta -= (r.b2 >= 0) ? other : 0.0;  // x - 0.0 == x
-  const double lo = (r.rt == ROW_BILATERAL) ? -INFINITY : (r.rt == ROW_NORMAL ? 0.0 : -mu);
-  const double hi = (r.rt == ROW_BILATERAL) ? INFINITY : mu;
-  const double nl = lam + delta;
+  delta -= (r.b2 >= 0) ? other : real(0);  // x - 0 == x
+  const real lo = (r.rt == ROW_BILATERAL) ? real(-INFINITY) : (r.rt == ROW_NORMAL ? real(0) : -mu);
+  const real hi = (r.rt == ROW_BILATERAL) ? real(INFINITY) : mu;
+  const real nl = lam + delta;
   const bool below = nl < lo, above = !below && nl > hi;
-  const double newl = below ? lo : (above ? hi : nl);
+  const real newl = below ? lo : (above ? hi : nl);
   delta = (below || above) ? newl - lam : delta;
   if (row >= 0 && half == 0) s.lambda[row] = newl;
-  const double d2 = swap_pair(delta);
+  const real d2 = swap_pair(delta);
   if (half) delta = d2;
   if (act) {
-    double* g = s.fc[r.body];
+    real* g = s.fc[r.body];
     g[0] = fma(delta, r.iM[0], f0);
     g[1] = fma(delta, r.iM[1], f1);
     g[2] = fma(delta, r.iM[2], f2);
@@ -340,25 +365,34 @@ __device__ inline int run_row(const L& s, int se, int pair) {  // row of a lane 
   return pair < (se >> 16) ? s.sched[(se & 0xFFFF) + pair] : -1;
 }
 
-template <int NM, int MM>
+template <int NM, int MM, class Real>
 __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restrict__ T0,
-                                                         const hs_simtopo* __restrict__ S, hs_sim_args a) {
-  __shared__ SimL<NM, MM> s;
+                                                         const hs_simtopo_t<Real>* __restrict__ S, hs_sim_args a) {
+  using real = Real;
+  __shared__ SimL<NM, MM, Real> s;
   const int lane = threadIdx.x;
   const int b = blockIdx.x;
   if (b >= a.n_rollouts) return;
-  const hs_simtopo& T = *S;
+  const hs_simtopo_t<Real>& T = *S;
   const int n = T.n, nmj = T.nmj, nj = T.nj, cfg = T0->cfg;
-  const hs_sim_params& P = a.params;
-  const double h = P.dt, h1 = 1.0 / h;
+  const SimP<real> P(a.params);
+  const real h = P.dt, h1 = P.h1;
+  // the ABI's arrays are double*; in the single-precision build they hold floats
+  const real* q_tab = reinterpret_cast<const real*>(a.q_tab);
+  const real* dq_tab = reinterpret_cast<const real*>(a.dq_tab);
+  const real* tau_tab = reinterpret_cast<const real*>(a.tau_tab);
+  real* o_tau = reinterpret_cast<real*>(a.tau_cmd);
+  real* o_q = reinterpret_cast<real*>(a.q_meas);
+  real* o_torso = reinterpret_cast<real*>(a.torso);
+  real* o_fn = reinterpret_cast<real*>(a.normal_force);
 #ifdef HS_SIM_STAMPS
   unsigned long long t_last = __builtin_amdgcn_s_memtime();
 #endif
-  double* gbody = a.body + (size_t)b * n * HS_SIM_BODY;
+  real* gbody = reinterpret_cast<real*>(a.body) + (size_t)b * n * HS_SIM_BODY;
   // load the world
   for (int e = lane; e < n * HS_SIM_BODY; e += WAVE) {
     const int p = e / HS_SIM_BODY, c = e % HS_SIM_BODY;
-    const double v = gbody[e];
+    const real v = gbody[e];
     if (c < 3) s.pos[p][c] = v;
     else if (c < 7) s.q[p][c - 3] = v;
     else if (c < 10) s.lvel[p][c - 7] = v;
@@ -369,7 +403,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
   wave_sync();
   if (lane < n) {
     q_to_R(s.q[lane], s.R[lane]);
-    s.invm[lane] = 1.0 / T.mass[lane];
+    s.invm[lane] = real(1) / T.mass[lane];
   }
   wave_sync();
 
@@ -378,40 +412,40 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
     const size_t orow = (size_t)b * a.n_steps + step;
     // ---- P: position control (set_position_control_torques, player.cpp:388-409)
     if (lane < nmj) {
-      const hs_simjoint& J = T.joint[T.motor_joint[lane]];
-      const double qm = hinge_angle(s, J);
-      double tq = 0;
+      const hs_simjoint_t<real>& J = T.joint[T.motor_joint[lane]];
+      const real qm = hinge_angle(s, J);
+      real tq = 0;
       if (P.k > 0) {
-        double ax[3];
+        real ax[3];
         mul0_331(ax, s.R[J.b1], J.axis1);
-        const double rate = dot3(ax, s.avel[J.b1]) - dot3(ax, s.avel[J.b2]);
+        const real rate = dot3(ax, s.avel[J.b1]) - dot3(ax, s.avel[J.b2]);
         const int t = tsi % a.n_t;
         const int hrow = (t + a.n_t - 2) % a.n_t;
         const size_t tb = (size_t)b * a.n_t + hrow;
-        double a1 = qm - a.q_tab[tb * cfg + 6 + lane];
-        double a2 = rate - a.dq_tab[tb * cfg + 6 + lane];
-        if (a1 > M_PI) a1 -= 2 * M_PI;  // arrayops::modulus (core.cpp:122-131)
-        else if (a1 <= -M_PI) a1 += 2 * M_PI;
-        a1 *= -P.k;
-        a2 *= -2 * sqrt(P.k);
+        real a1 = qm - q_tab[tb * cfg + 6 + lane];
+        real a2 = rate - dq_tab[tb * cfg + 6 + lane];
+        if (a1 > real(M_PI)) a1 -= real(2 * M_PI);  // arrayops::modulus (core.cpp:122-131)
+        else if (a1 <= -real(M_PI)) a1 += real(2 * M_PI);
+        a1 *= P.k1;
+        a2 *= P.k2;
         a1 += a2;
-        tq = a.tau_tab[tb * nmj + lane] + a1;
+        tq = tau_tab[tb * nmj + lane] + a1;
       }
       s.tau[lane] = tq;
-      if (a.q_meas) a.q_meas[orow * nmj + lane] = qm;
-      if (a.tau_cmd) a.tau_cmd[orow * nmj + lane] = tq;
+      if (o_q) o_q[orow * nmj + lane] = qm;
+      if (o_tau) o_tau[orow * nmj + lane] = tq;
     }
     wave_sync();
     SIM_ACC(1);
     // ---- B: per body accumulators, collision, inertia, v/h + M^-1 f
     if (lane < n) {
       const int p = lane;
-      double tq[3] = {0, 0, 0};
+      real tq[3] = {0, 0, 0};
       if (P.k > 0) {
         for (int c = 0; c < T.tq_n[p]; c++) {  // dJointAddHingeTorque in motor order
           const int j = T.tq_motor[p][c];
-          const hs_simjoint& J = T.joint[T.motor_joint[j]];
-          double ax[3];
+          const hs_simjoint_t<real>& J = T.joint[T.motor_joint[j]];
+          real ax[3];
           mul0_331(ax, s.R[J.b1], J.axis1);
           for (int i = 0; i < 3; i++) ax[i] *= s.tau[j];
           if (T.tq_sign[p][c] > 0)
@@ -422,34 +456,34 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
       }
       // collision with the plane (0,0,1,0)
       bool hit = false;
-      const double* R = s.R[p];
+      const real* R = s.R[p];
       if (T.gtype[p] == HS_GEOM_CAPSULE) {
-        const double sign = (R[10] > 0) ? -1.0 : 1.0;  // dCalcVectorDot3_14(plane normal, R + 2)
-        double pp[3];
-        pp[0] = s.pos[p][0] + R[2] * T.glen[p] * 0.5 * sign;
-        pp[1] = s.pos[p][1] + R[6] * T.glen[p] * 0.5 * sign;
-        pp[2] = s.pos[p][2] + R[10] * T.glen[p] * 0.5 * sign;
-        const double depth = 0 - (pp[0] * 0.0 + pp[1] * 0.0 + pp[2] * 1.0) + T.gr[p];
+        const real sign = (R[10] > 0) ? real(-1) : real(1);  // dCalcVectorDot3_14(plane normal, R + 2)
+        real pp[3];
+        pp[0] = s.pos[p][0] + R[2] * T.glen[p] * real(0.5) * sign;
+        pp[1] = s.pos[p][1] + R[6] * T.glen[p] * real(0.5) * sign;
+        pp[2] = s.pos[p][2] + R[10] * T.glen[p] * real(0.5) * sign;
+        const real depth = 0 - (pp[0] * real(0) + pp[1] * real(0) + pp[2] * real(1)) + T.gr[p];
         if (depth >= 0) {
           hit = true;
-          s.cpos[p][0] = pp[0] - 0.0 * T.gr[p];
-          s.cpos[p][1] = pp[1] - 0.0 * T.gr[p];
-          s.cpos[p][2] = pp[2] - 1.0 * T.gr[p];
+          s.cpos[p][0] = pp[0] - real(0) * T.gr[p];
+          s.cpos[p][1] = pp[1] - real(0) * T.gr[p];
+          s.cpos[p][2] = pp[2] - real(1) * T.gr[p];
           s.cdepth[p] = depth;
         }
       } else if (T.gtype[p] == HS_GEOM_SPHERE) {
-        const double depth = 0 - (s.pos[p][0] * 0.0 + s.pos[p][1] * 0.0 + s.pos[p][2] * 1.0) + T.gr[p];
+        const real depth = 0 - (s.pos[p][0] * real(0) + s.pos[p][1] * real(0) + s.pos[p][2] * real(1)) + T.gr[p];
         if (depth >= 0) {
           hit = true;
-          s.cpos[p][0] = s.pos[p][0] - 0.0 * T.gr[p];
-          s.cpos[p][1] = s.pos[p][1] - 0.0 * T.gr[p];
-          s.cpos[p][2] = s.pos[p][2] - 1.0 * T.gr[p];
+          s.cpos[p][0] = s.pos[p][0] - real(0) * T.gr[p];
+          s.cpos[p][1] = s.pos[p][1] - real(0) * T.gr[p];
+          s.cpos[p][2] = s.pos[p][2] - real(1) * T.gr[p];
           s.cdepth[p] = depth;
         }
       }
       s.contact[p] = hit ? 1 : 0;
       // world inverse inertia R invI_b R^T, gyroscopic torque, gravity (dxQuickStepper)
-      double Ib[12], iIb[12], tmp[12], I[12];
+      real Ib[12], iIb[12], tmp[12], I[12];
       for (int r = 0; r < 3; r++) {
         for (int c = 0; c < 3; c++) { Ib[r * 4 + c] = T.inertia[p][r * 3 + c]; iIb[r * 4 + c] = T.inv_inertia[p][r * 3 + c]; }
         Ib[r * 4 + 3] = iIb[r * 4 + 3] = 0;
@@ -464,20 +498,20 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
         for (int c = 0; c < 3; c++) tmp[r * 4 + c] = dot3(Ib + r * 4, R + c * 4);
       for (int r = 0; r < 3; r++)
         for (int c = 0; c < 3; c++) I[r * 4 + c] = dot3_14(R + r * 4, tmp + c);
-      double t3[3];
-      const double* w = s.avel[p];
+      real t3[3];
+      const real* w = s.avel[p];
       mul0_331(t3, I, w);
       tq[0] -= w[1] * t3[2] - w[2] * t3[1];
       tq[1] -= w[2] * t3[0] - w[0] * t3[2];
       tq[2] -= w[0] * t3[1] - w[1] * t3[0];
-      double fa[3] = {0, 0, 0};
+      real fa[3] = {0, 0, 0};
       if (P.gravity != 0) fa[2] += T.mass[p] * (-P.gravity);
-      const double im = s.invm[p];
+      const real im = s.invm[p];
       for (int i = 0; i < 3; i++) {
         s.tacc[p][i] = tq[i];
         s.fc[p][i] = fa[i] * im + s.lvel[p][i] * h1;  // tmp1
       }
-      double it[3];
+      real it[3];
       mul0_331(it, s.invI[p], tq);
       for (int i = 0; i < 3; i++) s.fc[p][3 + i] = it[i] + w[i] * h1;
     }
@@ -504,7 +538,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
     const int m = s.m;
     // ---- R: getInfo2 of every joint
     if (lane < nj) {
-      const hs_simjoint& J = T.joint[lane];
+      const hs_simjoint_t<real>& J = T.joint[lane];
       if (J.type == HS_SJ_HINGE) hinge_rows(s, J, h1, P.erp, P.cfm, s.joff[lane]);
       else fixed_rows(s, J, h1, P.erp, P.cfm, s.joff[lane]);
     } else if (lane < nj + n) {
@@ -516,22 +550,22 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
     // ---- A: rhs, CFM / h, Ad (SOR_LCP prologue)
     for (int i = lane; i < m; i += WAVE) {
       const int b1 = s.rb1[i], b2 = s.rb2[i];
-      double Jr[12];
+      real Jr[12];
       get_row(s, i, Jr);
-      double sum = 0;
+      real sum = 0;
       for (int j = 0; j < 6; j++) sum += Jr[j] * s.fc[b1][j];  // fc holds tmp1 here
       if (b2 >= 0)
         for (int j = 0; j < 6; j++) sum += Jr[6 + j] * s.fc[b2][j];
-      const double rhs = s.rhs[i] * h1 - sum;
-      const double cfm = s.cfm[i] * h1;
-      double iM[6], dsum = 0;
+      const real rhs = s.rhs[i] * h1 - sum;
+      const real cfm = s.cfm[i] * h1;
+      real iM[6], dsum = 0;
       imj_block(s, T, b1, Jr, iM);
       for (int j = 0; j < 6; j++) dsum += iM[j] * Jr[j];
       if (b2 >= 0) {
         imj_block(s, T, b2, Jr + 6, iM);
         for (int j = 0; j < 6; j++) dsum += iM[j] * Jr[6 + j];
       }
-      const double ad = P.sor_w / (dsum + cfm);
+      const real ad = P.sor_w / (dsum + cfm);
       s.Ad[i] = ad;
       s.rhs[i] = rhs * ad;
       s.cfm[i] = ad * cfm;
@@ -718,25 +752,25 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
       const int p = lane;
       for (int j = 0; j < 3; j++) s.lvel[p][j] += h * s.fc[p][j];
       for (int j = 0; j < 3; j++) s.avel[p][j] += h * s.fc[p][3 + j];
-      const double hm = h * s.invm[p];
-      double fa[3] = {0, 0, 0};  // facc: gravity only (the motors add torques)
+      const real hm = h * s.invm[p];
+      real fa[3] = {0, 0, 0};  // facc: gravity only (the motors add torques)
       if (P.gravity != 0) fa[2] += T.mass[p] * (-P.gravity);
-      double ta[3];
+      real ta[3];
       for (int j = 0; j < 3; j++) {
         s.lvel[p][j] += hm * fa[j];
         ta[j] = s.tacc[p][j] * h;
       }
-      double t3[3];
+      real t3[3];
       mul0_331(t3, s.invI[p], ta);
       for (int j = 0; j < 3; j++) s.avel[p][j] += t3[j];
       for (int j = 0; j < 3; j++) s.pos[p][j] += h * s.lvel[p][j];
-      const double* w = s.avel[p];
-      double* qv = s.q[p];
-      double dq[4];
-      dq[0] = 0.5 * (-w[0] * qv[1] - w[1] * qv[2] - w[2] * qv[3]);
-      dq[1] = 0.5 * (w[0] * qv[0] + w[1] * qv[3] - w[2] * qv[2]);
-      dq[2] = 0.5 * (-w[0] * qv[3] + w[1] * qv[0] + w[2] * qv[1]);
-      dq[3] = 0.5 * (w[0] * qv[2] - w[1] * qv[1] + w[2] * qv[0]);
+      const real* w = s.avel[p];
+      real* qv = s.q[p];
+      real dq[4];
+      dq[0] = real(0.5) * (-w[0] * qv[1] - w[1] * qv[2] - w[2] * qv[3]);
+      dq[1] = real(0.5) * (w[0] * qv[0] + w[1] * qv[3] - w[2] * qv[2]);
+      dq[2] = real(0.5) * (-w[0] * qv[3] + w[1] * qv[0] + w[2] * qv[1]);
+      dq[3] = real(0.5) * (w[0] * qv[2] - w[1] * qv[1] + w[2] * qv[0]);
       for (int j = 0; j < 4; j++) qv[j] += h * dq[j];
       normalize4(qv);
       q_to_R(qv, s.R[p]);
@@ -744,16 +778,16 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
     if (lane == 0) {
       if (a.n_contacts) a.n_contacts[orow] = s.nc;
       if (a.normal_force) {
-        double fsum = 0;
+        real fsum = 0;
         for (int v = 0; v < n; v++) {
           const int bv = T.border[v];
           if (s.contact[bv]) fsum += s.lambda[s.coff[bv]];
         }
-        a.normal_force[orow] = fsum;
+        o_fn[orow] = fsum;
       }
     }
     wave_sync();
-    if (a.torso && lane < 3) a.torso[orow * 3 + lane] = s.pos[0][lane];
+    if (o_torso && lane < 3) o_torso[orow * 3 + lane] = s.pos[0][lane];
     tsi++;
     SIM_ACC(8);
 #ifdef HS_SIM_STAMPS
@@ -763,7 +797,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
   // store the world
   for (int e = lane; e < n * HS_SIM_BODY; e += WAVE) {
     const int p = e / HS_SIM_BODY, c = e % HS_SIM_BODY;
-    double v;
+    real v;
     if (c < 3) v = s.pos[p][c];
     else if (c < 7) v = s.q[p][c - 3];
     else if (c < 10) v = s.lvel[p][c - 7];
@@ -777,14 +811,18 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
 }
 
 // init_play_config + orient_odebodys: lane = part, A_ground by walking the chain from the root
-// (each product in the reference's order: J_A_ground = A_parent J_A_parent, then * E(q) * A_pj_body)
+// (each product in the reference's order: J_A_ground = A_parent J_A_parent, then * E(q) * A_pj_body).
+// IO = the precision of the configuration and body arrays; the pose is built in double and
+// rounded once into a float state for the single-precision simulation.
+template <class IO>
 __global__ __launch_bounds__(WAVE) void hs_sim_reset_kernel(const hs_topo* __restrict__ T, const hs_simtopo* __restrict__ S,
-                                                             int32_t n_rollouts, const double* __restrict__ config,
-                                                             int32_t stride, double* __restrict__ body) {
+                                                             int32_t n_rollouts, const IO* __restrict__ config,
+                                                             int32_t stride, IO* __restrict__ body) {
   using namespace hsd;
   const int b = blockIdx.x, p = threadIdx.x;
   if (b >= n_rollouts || p >= T->n) return;
-  const double* cf = config + (size_t)b * stride;
+  double cf[6 + HS_NMAX];
+  for (int i = 0; i < T->cfg; i++) cf[i] = (double)config[(size_t)b * stride + i];
   int chain[HS_NMAX], len = 0;
   for (int a = p; a >= 0; a = T->node[a].parent) chain[len++] = a;
   A34 A;
@@ -809,9 +847,9 @@ __global__ __launch_bounds__(WAVE) void hs_sim_reset_kernel(const hs_topo* __res
   }
   q_from_R(q, Rin);
   normalize4(q);
-  double* o = body + ((size_t)b * T->n + p) * HS_SIM_BODY;
-  for (int i = 0; i < 3; i++) o[i] = G(i, 3);
-  for (int i = 0; i < 4; i++) o[3 + i] = q[i];
+  IO* o = body + ((size_t)b * T->n + p) * HS_SIM_BODY;
+  for (int i = 0; i < 3; i++) o[i] = (IO)G(i, 3);
+  for (int i = 0; i < 4; i++) o[3 + i] = (IO)q[i];
   for (int i = 7; i < 13; i++) o[i] = 0;
   (void)R;
 }
@@ -833,26 +871,38 @@ extern "C" int hs_debug_clear_sim_stamps() {
 namespace hs {
 
 int launch_sim_reset(const hs_topo* d_topo, const hs_simtopo* d_sim, int32_t n_rollouts, const double* config,
-                     int32_t config_stride, double* body, void* stream) {
+                     int32_t config_stride, double* body, int32_t precision, void* stream) {
   if (n_rollouts <= 0) return 0;
-  hipLaunchKernelGGL(hs_sim_reset_kernel, dim3(n_rollouts), dim3(WAVE), 0, (hipStream_t)stream, d_topo, d_sim,
-                     n_rollouts, config, config_stride, body);
+  hipStream_t st = (hipStream_t)stream;
+  if (precision == HS_PREC_F32)
+    hipLaunchKernelGGL(hs_sim_reset_kernel<float>, dim3(n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, n_rollouts,
+                       reinterpret_cast<const float*>(config), config_stride, reinterpret_cast<float*>(body));
+  else
+    hipLaunchKernelGGL(hs_sim_reset_kernel<double>, dim3(n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, n_rollouts,
+                       config, config_stride, body);
   return (int)hipGetLastError();
 }
 
-int launch_sim_steps(const hs_topo* d_topo, const hs_simtopo* d_sim, const hs_simtopo& hs, const hs_sim_args& a) {
-  if (a.n_rollouts <= 0 || a.n_steps <= 0) return 0;
+template <class R, class S>
+static int launch_sim_typed(const hs_topo* d_topo, const S* d_sim, const hs_simtopo& hs, const hs_sim_args& a) {
   hipStream_t st = (hipStream_t)a.stream;
   // smallest LDS layout holding the model: parts and rows (6 per fixed, 5 per hinge, 3 per contact)
   if (hs.n <= 18 && hs.m_max <= 144)
-    hipLaunchKernelGGL((hs_sim_kernel<18, 144>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
+    hipLaunchKernelGGL((hs_sim_kernel<18, 144, R>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
   else if (hs.n <= 22 && hs.m_max <= 176)
-    hipLaunchKernelGGL((hs_sim_kernel<22, 176>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
+    hipLaunchKernelGGL((hs_sim_kernel<22, 176, R>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
   else if (hs.n <= HS_NMAX && hs.m_max <= 9 * HS_NMAX)
-    hipLaunchKernelGGL((hs_sim_kernel<HS_NMAX, 9 * HS_NMAX>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
+    hipLaunchKernelGGL((hs_sim_kernel<HS_NMAX, 9 * HS_NMAX, R>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
   else
     return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
+}
+
+int launch_sim_steps(const hs_topo* d_topo, const hs_simtopo* d_sim, const hs_simtopo_t<float>* d_sim_f32,
+                     const hs_simtopo& hs, const hs_sim_args& a) {
+  if (a.n_rollouts <= 0 || a.n_steps <= 0) return 0;
+  if (a.precision == HS_PREC_F32) return launch_sim_typed<float>(d_topo, d_sim_f32, hs, a);
+  return launch_sim_typed<double>(d_topo, d_sim, hs, a);
 }
 
 }  // namespace hs

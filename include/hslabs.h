@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 4
+#define HSLABS_ABI_VERSION 5
 
 enum {
   HS_OK = 0,
@@ -260,15 +260,19 @@ void hs_sim_default_params(hs_sim_params* p);
 
 /* init_play_config (player.cpp:351-356) + orient_odebodys (model.cpp:295-305):
  * body states of B configurations (joint values, config [B][config_stride],
- * DEVICE), zero velocities. body: DEVICE [B][n_parts][HS_SIM_BODY_STRIDE]. */
+ * DEVICE), zero velocities. body: DEVICE [B][n_parts][HS_SIM_BODY_STRIDE].
+ * precision HS_PREC_F32: config and body hold floats (the pose is built in
+ * double and rounded once). */
 int hs_sim_reset(hs_model_t model, int32_t n_rollouts, const double* config, int32_t config_stride, double* body,
-                 void* stream);
+                 int32_t precision, void* stream);
 
 typedef struct {
   int32_t n_rollouts;
   int32_t n_steps;         /* simulation steps of this call (one launch runs them all) */
   int32_t n_t;             /* controller table rows (setup_per_controller: int(T / play_dt + .5)) */
-  int32_t reserved;
+  int32_t precision;       /* HS_PREC_F64, or HS_PREC_F32 (BASELINE configs[2]): single-precision
+                              arithmetic; body, the tables and the outputs hold floats (pointer types
+                              stay double*, like hs_run_args); seed/tsi/n_contacts unchanged */
   hs_sim_params params;
   /* per-rollout state, DEVICE, read and advanced */
   double* body;            /* [B][n_parts][HS_SIM_BODY_STRIDE] */

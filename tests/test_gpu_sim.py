@@ -186,3 +186,103 @@ def test_every_part_in_contact(gpu, hmodels, oracle_mod, omodels, name):
         r = oracle_mod.sim_run(omodels[name], P, sb.n_t, qt[b], dqt[b], tt[b], body0[b], 0, 2, 5)
         assert (r["n_contacts"] == nc[b]).all()
         assert np.abs(r["body"] - body[b]).max() < 1e-9 * max(1.0, np.abs(r["body"]).max())
+
+
+# ---- single precision (HS_PREC_F32, BASELINE configs[2] "fp32"): same algorithm in float.
+# Floats cannot follow the double trajectories bit for bit, so these check the reset against
+# the oracle to float rounding, closed-form physics, the fp32 path's own determinism, and that
+# its trajectories stay near the fp64 ones over configs[2]'s 32-step horizon.
+
+@pytest.mark.parametrize("name", ["hexapod", "spider", "myant"])
+def test_f32_reset_matches_oracle(gpu, hmodels, oracle_mod, omodels, name):
+    import torch
+
+    sb = make_batch(gpu, hmodels[name], name, 8, dtype=torch.float32)
+    assert sb.body.dtype == torch.float32
+    body = sb.body.cpu().numpy().astype(np.float64)
+    qt = sb.tables.q.cpu().numpy().astype(np.float64)
+    for b in range(8):
+        ob = oracle_mod.sim_reset(omodels[name], qt[b, sb.table_row(2)])
+        assert np.abs(ob - body[b]).max() < 1e-5 * max(1.0, np.abs(ob).max())
+
+
+def test_f32_free_fall(gpu, hmodels):
+    import torch
+
+    sb = make_batch(gpu, hmodels["hexapod"], "hexapod", 16, k=0.0, dtype=torch.float32)
+    sb.body[:, :, 2] += 10.0
+    n = 40
+    out = sb.step(n)
+    torch.cuda.synchronize()
+    b = sb.body.cpu().numpy().astype(np.float64)
+    # the joints are internal forces: the mean body velocity (all masses 1) falls freely to float
+    # rounding; single bodies carry the ERP corrections of float-sized joint drift (~1e-4)
+    assert np.abs(b[:, :, 9].mean(axis=1) + n * 0.01).max() < 1e-5
+    assert np.abs(b[:, :, 9] + n * 0.01).max() < 1e-3
+    assert (out["n_contacts"].cpu().numpy() == 0).all()
+
+
+def test_f32_launch_split_is_bitwise(gpu, hmodels):
+    import torch
+
+    a = make_batch(gpu, hmodels["spider"], "spider", 64, dtype=torch.float32)
+    b = make_batch(gpu, hmodels["spider"], "spider", 64, dtype=torch.float32)
+    oa = a.step(30)
+    parts = [b.step(10) for _ in range(3)]
+    torch.cuda.synchronize()
+    assert torch.equal(a.body, b.body) and torch.equal(a.seed, b.seed) and torch.equal(a.tsi, b.tsi)
+    assert torch.equal(oa["tau_cmd"], torch.cat([p["tau_cmd"] for p in parts], dim=1))
+
+
+@pytest.mark.parametrize("name", ["hexapod", "spider", "myant"])
+def test_f32_follows_f64_over_horizon(gpu, hmodels, name):
+    """configs[2]'s horizon (32 steps): fp32 torsos within 1e-2 of the fp64 ones (median 5e-4),
+    joint angles within 5e-2, the mean normal force within 1 % (median). Measured on MI355X
+    (tools/sim_f32_check.py, 256 rollouts): torso median 3e-5..1.1e-4, max 1.4e-3..2.4e-3;
+    angles max 3e-3..7e-3; force median 1.5e-4..3.8e-4; 6-8 % of contact counts differ (contacts
+    made or broken a step apart at depth ~0)."""
+    import torch
+    from hslabs_amd import synth
+
+    p = synth.gen_sim_params(256, name)
+    a = gpu.SimBatch(hmodels[name], p, dtype=torch.float64)
+    b = gpu.SimBatch(hmodels[name], p, dtype=torch.float32)
+    outs = ("torso", "q_meas", "normal_force")
+    oa, ob = a.step(32, outputs=outs), b.step(32, outputs=outs)
+    torch.cuda.synchronize()
+    assert torch.isfinite(b.body).all()
+    dt = (oa["torso"] - ob["torso"].double()).abs().amax(dim=(1, 2)).cpu().numpy()
+    assert np.median(dt) < 5e-4 and dt.max() < 1e-2
+    dq = oa["q_meas"] - ob["q_meas"].double()
+    dq = ((dq + np.pi) % (2 * np.pi) - np.pi).abs().max().item()
+    assert dq < 5e-2
+    fa, fb = oa["normal_force"].mean(dim=1), ob["normal_force"].double().mean(dim=1)
+    assert np.median(((fa - fb).abs() / fa.abs().clamp(min=1)).cpu().numpy()) < 1e-2
+
+
+def test_f32_full_batch_one_period(gpu, hmodels):
+    """4096 hexapods in fp32 over one gait period: the physics of the fp64 test holds."""
+    import torch
+
+    sb = make_batch(gpu, hmodels["hexapod"], "hexapod", 4096, dtype=torch.float32)
+    z0 = sb.body[:, 0, 2].clone()
+    out = sb.step(300, outputs=("torso", "normal_force", "n_contacts"))
+    torch.cuda.synchronize()
+    assert torch.isfinite(sb.body).all()
+    z = out["torso"][:, :, 2].cpu().numpy()
+    assert (z > 0).all()
+    assert np.median(np.abs(z[:, -1] - z0.cpu().numpy())) < 0.1
+    fn = out["normal_force"].cpu().numpy()[:, 100:]
+    assert abs(np.median(fn.mean(axis=1)) - 22.0) < 0.25 * 22.0
+
+
+def test_f32_configs2_shape(gpu, hmodels):
+    """BASELINE configs[2] shape: 16384 spiders x 32 steps in one launch, finite and on the ground."""
+    import torch
+
+    sb = make_batch(gpu, hmodels["spider"], "spider", 16384, dtype=torch.float32)
+    out = sb.step(32, outputs=("torso", "n_contacts"))
+    torch.cuda.synchronize()
+    assert torch.isfinite(sb.body).all()
+    assert (out["torso"][:, :, 2] > 0).all()
+    assert (out["n_contacts"][:, -1] > 0).float().mean().item() > 0.99
