@@ -333,12 +333,35 @@ __device__ inline void step_profiles(real t, real& sx, real& sz) {
   sz = s * s;
 }
 
-template <class W>
-__device__ __attribute__((always_inline)) inline void node_features(const hs_topo* T, int v, const A34& A, const A34* J, const W& w, int k) {
+// What the kinematics reads of one node, fetched in one batch of independent loads instead of
+// one round trip per branch that consumes it (fetching earlier measured slower: the values
+// stay live across the gait record and their waits land on its loads, vmcnt being in order).
+struct NodeK {
+  A34 Jp, pj;  // J_A_parent, A_pj_body
+  real com[3], cap[3];
+  int foot, hinge, owner;
+};
+__device__ __attribute__((always_inline)) inline NodeK load_nodek(const hs_topo* T, int v) {
   const hs_node& nd = T->node[v];
+  NodeK r;
+  r.Jp = load34(nd.J_A_parent);
+  r.pj = load34(nd.A_pj_body);
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    r.com[i] = (real)nd.com[i];
+    r.cap[i] = (real)nd.cap[i];
+  }
+  r.foot = nd.foot;
+  r.hinge = nd.hinge;
+  r.owner = nd.owner_limb;
+  return r;
+}
+
+template <class W>
+__device__ __attribute__((always_inline)) inline void node_features(const hs_topo* T, int v, const NodeK& nd, const A34& A, const A34* J, const W& w, int k) {
   if (w.want_pos(k)) {
-    real com[3] = {(real)nd.com[0], (real)nd.com[1], (real)nd.com[2]}, p[3];
-    mulp(A, com, p);
+    real p[3];
+    mulp(A, nd.com, p);
     real* P = w.pos(k, v);
     for (int i = 0; i < 3; i++) P[i] = p[i];
   }
@@ -359,8 +382,8 @@ __device__ __attribute__((always_inline)) inline void node_features(const hs_top
     for (int i = 0; i < 3; i++) Jp[i] = J ? (*J)(i, 3) : A(i, 3);
     for (int i = 0; i < 3; i++) Jz[i] = J ? (*J)(i, 2) : real(0);
     if (nd.foot >= 0) {
-      real cap[3] = {(real)nd.cap[0], (real)nd.cap[1], (real)nd.cap[2]}, fp[3];
-      mulp(A, cap, fp);
+      real fp[3];
+      mulp(A, nd.cap, fp);
       real* F = w.fpos(k, nd.foot);
       for (int i = 0; i < 3; i++) F[i] = fp[i];
       w.contact(k, nd.foot) = fp[2] < (real)(T->rcap + 1e-4);
@@ -371,6 +394,10 @@ __device__ __attribute__((always_inline)) inline void node_features(const hs_top
 template <class W>
 __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, int isample, int L,
                            bool ignore_reach, const W& w, int k) {
+  const int j = T->limb_pergen[L];
+  const int ysign = T->limb_ysign[L];
+  const int clen = T->limb_chain_len[L];
+  const int lv[3] = {T->limb_node[L][0], T->limb_node[L][1], T->limb_node[L][2]};
   real t = 0;  // t accumulates dt (periodic.cpp:171-181)
   for (int i = 0; i < isample; i++) t += st.dt;
   // pergensetup::set_rec -> turn_torso (pergen.cpp:386-397)
@@ -398,7 +425,6 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
     euler_from(A1, o1);
   }
   // periodicgenerator::limb_positions for this limb's pergen index (pergen.cpp:82-94)
-  int j = T->limb_pergen[L];
   real target[3];
   {
     real tt = t / g.period;
@@ -432,40 +458,45 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
     target[1] = dy + st.pos0[j][1];
     target[2] = dz + st.pos0[j][2];
   }
+  STAMP(20);
   // set_jvalues_with_lik: torso + body chain FK, then limb IK (model.cpp:354-359, lik.cpp:89-99)
   real q6[6] = {o0[0], o0[1], o0[2], o1[0], o1[1], o1[2]};
   const A34 F = turned ? free_joint(q6) : free_joint_sc(q6, st.tsc);  // straight gait: torso angles fixed
-  A34 A0 = mul(mul(node_joint_parent(T, 0), F), node_pj(T, 0));
+  const NodeK n0 = load_nodek(T, 0);  // the torso
+  A34 A0 = mul(mul(n0.Jp, F), n0.pj);
   const bool wq = w.want_q(k);
   if (L == 0) {
     if (wq) for (int i = 0; i < 6; i++) w.q(k)[i] = q6[i];
-    A34 J0 = node_joint_parent(T, 0);  // torso joint frame J = I * J_A_parent
-    node_features(T, 0, A0, &J0, w, k);
+    node_features(T, 0, n0, A0, &n0.Jp, w, k);  // torso joint frame J = I * J_A_parent
   }
   A34 A = A0;
-  for (int kk = 1; kk < T->limb_chain_len[L]; kk++) {
-    int v = T->limb_chain[L][kk];
-    A = mul(A, node_pj(T, v));
-    if (T->node[v].owner_limb == L) node_features(T, v, A, nullptr, w, k);
+  for (int kk = 1; kk < clen; kk++) {
+    const int v = T->limb_chain[L][kk];
+    const NodeK nc = load_nodek(T, v);
+    A = mul(A, nc.pj);
+    if (nc.owner == L) node_features(T, v, nc, A, nullptr, w, k);
   }
-  int c = T->limb_child[L];
-  A34 J = mul(A, node_joint_parent(T, c));  // poslimb (lik.cpp:341-347)
+  NodeK nk = load_nodek(T, lv[0]);  // limb_child
+  A34 J = mul(A, nk.Jp);  // poslimb (lik.cpp:341-347)
   A34 Jinv = invert(J);
+  STAMP(21);
   real pl[3], ja[3];
   mulp(Jinv, target, pl);
   bool unreach = false, fail = false;
   const real ls[3] = {(real)T->ls[0], (real)T->ls[1], (real)T->ls[2]};
-  limb_ik(T->lik_kind, ls, T->limb_ysign[L], pl, ja, ignore_reach, unreach, fail);
+  limb_ik(T->lik_kind, ls, ysign, pl, ja, ignore_reach, unreach, fail);
   if (w.want_centre(k)) w.unreach(k, L) = (unreach || fail) ? 1 : 0;
+  STAMP(22);
   // limb FK with the new joint values (compute_dynrecs' recompute_modelnodes)
-  int v = c;
-  for (int kk = 0; kk < 3; kk++) {
-    const hs_node& nd = T->node[v];
-    A34 Jv = (kk == 0) ? J : mul(A, node_joint_parent(T, v));
-    A = mul(mul(Jv, hinge_joint(ja[kk])), node_pj(T, v));
-    if (wq) w.q(k)[6 + nd.hinge] = ja[kk];
-    node_features(T, v, A, &Jv, w, k);
-    if (kk < 2) v = nd.kids[0];
+#pragma unroll
+  for (int kk = 0; kk < 3; kk++) {  // limb_child, its first kid, that one's first kid
+    if (kk > 0) nk = load_nodek(T, lv[kk]);
+    A34 Jv = (kk == 0) ? J : mul(A, nk.Jp);
+    real sq, cq;
+    sincos(ja[kk], &sq, &cq);
+    A = mul(mul_hinge(Jv, cq, sq), nk.pj);
+    if (wq) w.q(k)[6 + nk.hinge] = ja[kk];
+    node_features(T, lv[kk], nk, A, &Jv, w, k);
   }
 }
 

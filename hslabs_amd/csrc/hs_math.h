@@ -141,6 +141,21 @@ __device__ inline A34 free_joint_sc(const real* q6, const SC3& t) {
 __device__ inline A34 free_joint(const real* q6) { return free_joint_sc(q6, sincos3(q6[3], q6[4], q6[5])); }
 
 // hinge transformation Rz(q) (model.cpp:50-57)
+// mul(A, hinge_joint(q)) given (cos q, sin q), without the products by the hinge's zeros and
+// one: column 0 = A0 c + A1 s, column 1 = A0 (-s) + A1 c (mul's sums with the zero terms
+// dropped, which add exact zeros), columns 2 and 3 copied
+__device__ inline A34 mul_hinge(const A34& A, real c, real s) {
+  A34 C;
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    C.at(r, 0) = fma(A(r, 1), s, A(r, 0) * c);
+    C.at(r, 1) = fma(A(r, 1), c, A(r, 0) * (-1 * s));
+    C.at(r, 2) = A(r, 2);
+    C.at(r, 3) = A(r, 3);
+  }
+  return C;
+}
+
 __device__ inline A34 hinge_joint(real q) {
   real c, s;
   sincos(q, &s, &c);

@@ -454,6 +454,7 @@ int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& 
     int v = c;
     for (int j = 0; j < 3; j++) {
       if (b.jtype[v] != HS_J_HINGE) { err = "limb link without hinge"; return HS_E_TOPOLOGY; }
+      t->limb_node[L][j] = v;
       if (j < 2) {
         if (b.kids[v].empty()) { err = "limb too short"; return HS_E_TOPOLOGY; }
         v = b.kids[v][0];

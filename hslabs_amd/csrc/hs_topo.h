@@ -50,6 +50,7 @@ struct hs_topo {
   int32_t limb_foot[HS_LMAX];    // foot node of each limb (lik.cpp:453-455)
   int32_t limb_ysign[HS_LMAX];   // lik.cpp:230-245
   int32_t limb_pergen[HS_LMAX];  // likpergen_map (pergen.cpp:243-262)
+  int32_t limb_node[HS_LMAX][3];        // the limb's three hinged links, top first
   int32_t limb_chain_len[HS_LMAX];      // nodes from root to limb parent (inclusive)
   int32_t limb_chain[HS_LMAX][HS_NMAX]; // root ... limb parent
   // index tables that turn pointer chases into independent loads:
