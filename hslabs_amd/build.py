@@ -28,6 +28,10 @@ SOURCES = ["hs_kernels.hip", "hs_kernels_f32.hip", "hs_sim.hip", "hs_capi.cpp", 
 HEADERS = ["hs_topo.h", "hs_simtopo.h", "hs_ode.h", "hs_math.h", "hs_internal.h", os.path.join("..", "..", "include", "hslabs.h")]
 ARCH = os.environ.get("HSLABS_ARCH", "gfx950")
 CONTRACT = {"hs_sim.hip": "off"}  # per-source FMA contraction (default: fast)
+# per-source scheduler choice, measured (tools/gpu_sweep_libs.sh): the fp32 rollout kernel
+# (4 waves/SIMD, 128 VGPRs) gains 1.4 % with the iterative ILP scheduler; the fp64 rollout
+# kernel and the simulation are fastest with the default one
+SRC_FLAGS = {"hs_kernels_f32.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
 
 
 def _hipcc() -> str:
@@ -52,7 +56,8 @@ def _compile(out: str, defines=(), verbose: bool = False, flags=()) -> str:
     def obj(src):
         o = os.path.join(OUT_DIR, f"{tag}.{src}.o")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
-               f"-ffp-contract={CONTRACT.get(src, 'fast')}", "-Wall", "-Wno-unused-function", *flags,
+               f"-ffp-contract={CONTRACT.get(src, 'fast')}", "-Wall", "-Wno-unused-function",
+               *SRC_FLAGS.get(src, []), *flags,
                *[f"-D{d}" for d in defines], os.path.join(SRC, src), "-o", o]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
