@@ -32,6 +32,12 @@ HSODE_FN void mul0_331(T* r, const T* B, const T* c) {
   T r0 = dot3(B, c), r1 = dot3(B + 4, c), r2 = dot3(B + 8, c);
   r[0] = r0; r[1] = r1; r[2] = r2;
 }
+// r = B c, B 3x3 row-major (the same sums as mul0_331 on a compact matrix)
+template <class T>
+HSODE_FN void mul0_33(T* r, const T* B, const T* c) {
+  T r0 = dot3(B, c), r1 = dot3(B + 3, c), r2 = dot3(B + 6, c);
+  r[0] = r0; r[1] = r1; r[2] = r2;
+}
 // r = B^T c (dMultiply1_331)
 template <class T>
 HSODE_FN void mul1_331(T* r, const T* B, const T* c) {

@@ -82,14 +82,14 @@ struct SimP {
 
 template <int NM, int MM, class Real>
 struct SimL {
+  static_assert(MM < 256, "row ids, positions and levels are stored in bytes");
   using real = Real;
   // bodies (part ids index everything; ODE's island numbering does not change any arithmetic)
-  real pos[NM][3], q[NM][4], R[NM][12], lvel[NM][3], avel[NM][3], tacc[NM][3];
-  real invI[NM][12];
+  // (no rotation matrices: R = dQtoR(q) is formed where it is read, from the same q)
+  real pos[NM][3], q[NM][4], lvel[NM][3], avel[NM][3], tacc[NM][3];
+  real invI[NM][9];      // world inverse inertia, 3x3 row-major
   real invm[NM];         // 1 / mass, kept on chip: the SOR rows read it for every update
   real fc[NM][6];        // v/h + M^-1 f while the rows are built (ODE's tmp1), then SOR's fc
-  real cpos[NM][3], cdepth[NM];
-  real tau[NM];
   // constraint rows
   real J[MM][9];         // Jacobian rows, unscaled, as J1l | J1a | J2a: every two-body row here has
                            // J2l = -J1l (ball, fixed and hinge-axis rows), and contacts have no body2
@@ -98,13 +98,26 @@ struct SimL {
   real Ad[MM];
   real lambda[MM];
   int8_t rb1[MM], rb2[MM], rtype[MM];
-  int16_t order[MM];       // row at each sweep position (ODE's order)
-  int16_t swp[MM];         // Fisher-Yates swap targets s_i of a reshuffle
-  int16_t sched[MM];       // rows grouped by level
-  int16_t lv[MM];          // level of each position
-  int32_t cnt[MM];         // rows per level
-  uint64_t bmask[NM][4];   // positions touching each body
-  int32_t run_se[MM];      // levels: start in sched | length << 16
+  // LDS shared by lifetime: the step's setup scratch (torques, contact points) is dead once the
+  // rows are built, the sweep scheduling exists only during the sweeps (row ids, positions and
+  // levels are < MM <= 216 and fit a byte)
+  union {
+    struct {
+      real cpos[NM][3], cdepth[NM];
+      real tau[NM];
+    };
+    struct {
+      uint8_t order[MM];     // row at each sweep position (ODE's order)
+      uint8_t swp[MM];       // Fisher-Yates swap targets s_i of a reshuffle
+      uint8_t sched[MM];     // rows grouped by level
+      uint8_t lv[MM];        // level of each position
+      uint16_t run_se[MM];   // levels: start in sched | length << 8
+      union {
+        uint64_t bmask[NM][4];  // positions touching each body (dead once the levels are known)
+        int32_t cnt[MM];        // rows per level
+      };
+    };
+  };
   int16_t joff[HS_SIM_JMAX], coff[NM];
   int8_t contact[NM];
   int32_t m, nc, nruns;
@@ -144,11 +157,12 @@ __device__ inline void get_row(const L& s, int r, typename L::real* j12) {
 }
 
 template <class L>
-__device__ inline void set_ball(L& s, const hs_simjoint_t<typename L::real>& J, typename L::real k, int r0) {
+__device__ inline void set_ball(L& s, const hs_simjoint_t<typename L::real>& J, typename L::real k, int r0,
+                                const typename L::real* R1, const typename L::real* R2) {
   using real = typename L::real;
   real a1[3], a2[3];
-  mul0_331(a1, s.R[J.b1], J.anchor1);
-  mul0_331(a2, s.R[J.b2], J.anchor2);
+  mul0_331(a1, R1, J.anchor1);
+  mul0_331(a2, R2, J.anchor2);
   // J1l = I, J1a = -[a1]x, J2l = -I, J2a = [a2]x
   const real rows[3][12] = {
       {1, 0, 0, 0, a1[2], -a1[1], -1, 0, 0, 0, -a2[2], a2[1]},
@@ -164,11 +178,14 @@ template <class L>
 __device__ inline void hinge_rows(L& s, const hs_simjoint_t<typename L::real>& J, typename L::real fps, typename L::real erp, typename L::real cfm, int r0) {
   using real = typename L::real;
   const real k = fps * erp;
-  set_ball(s, J, k, r0);
+  real R1[12], R2[12];
+  q_to_R(s.q[J.b1], R1);
+  q_to_R(s.q[J.b2], R2);
+  set_ball(s, J, k, r0, R1, R2);
   real ax1[3], p[3], qv[3], ax2[3], b[3];
-  mul0_331(ax1, s.R[J.b1], J.axis1);
+  mul0_331(ax1, R1, J.axis1);
   plane_space(ax1, p, qv);
-  mul0_331(ax2, s.R[J.b2], J.axis2);
+  mul0_331(ax2, R2, J.axis2);
   cross3(b, ax1, ax2);
   const real r3[12] = {0, 0, 0, p[0], p[1], p[2], 0, 0, 0, -p[0], -p[1], -p[2]};
   const real r4[12] = {0, 0, 0, qv[0], qv[1], qv[2], 0, 0, 0, -qv[0], -qv[1], -qv[2]};
@@ -189,8 +206,9 @@ __device__ inline void fixed_rows(L& s, const hs_simjoint_t<typename L::real>& J
   using real = typename L::real;
   const real k = fps * erp;
   // three linear rows: J1l = I, J1a = [ofs]x, J2l = -I
-  real ofs[3];
-  mul0_331(ofs, s.R[J.b1], J.offset);
+  real ofs[3], R1[12];
+  q_to_R(s.q[J.b1], R1);
+  mul0_331(ofs, R1, J.offset);
   const real rows[3][12] = {
       {1, 0, 0, 0, -ofs[2], ofs[1], -1, 0, 0, 0, 0, 0},
       {0, 1, 0, ofs[2], 0, -ofs[0], 0, -1, 0, 0, 0, 0},
@@ -204,7 +222,7 @@ __device__ inline void fixed_rows(L& s, const hs_simjoint_t<typename L::real>& J
   qmul1(qq, s.q[J.b1], s.q[J.b2]);
   qmul2(qerr, qq, J.qrel);
   if (qerr[0] < 0) { qerr[1] = -qerr[1]; qerr[2] = -qerr[2]; qerr[3] = -qerr[3]; }
-  mul0_331(e, s.R[J.b1], qerr + 1);
+  mul0_331(e, R1, qerr + 1);
   for (int r = 0; r < 3; r++) {
     real row[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     row[3 + r] = 1;
@@ -267,7 +285,7 @@ __device__ inline void imj_block(const L& s, const hs_simtopo_t<typename L::real
   using real = typename L::real;
   const real k1 = s.invm[b];
   for (int j = 0; j < 3; j++) out[j] = k1 * Jb[j];
-  mul0_331(out + 3, s.invI[b], Jb + 3);
+  mul0_33(out + 3, s.invI[b], Jb + 3);
 }
 
 __device__ inline double swap_pair(double v) {  // value of the other lane of the pair (DPP quad_perm 1,0,3,2)
@@ -311,7 +329,7 @@ __device__ inline RowData<typename L::real> load_row(const L& s, int row, int ha
   // compute_invM_JT: invMass J (linear), invI J (angular)
   const real k1 = s.invm[bb];
   for (int j = 0; j < 3; j++) r.iM[j] = k1 * Jb[j];
-  mul0_331(r.iM + 3, s.invI[bb], Jb + 3);
+  mul0_33(r.iM + 3, s.invI[bb], Jb + 3);
   r.rhs = s.rhs[rr];
   r.adcfm = s.cfm[rr];
   return r;
@@ -362,11 +380,14 @@ __device__ inline void sor_pair(L& s, const RowData<typename L::real>& r, int ro
 
 template <class L>
 __device__ inline int run_row(const L& s, int se, int pair) {  // row of a lane pair in a level, -1 = idle
-  return pair < (se >> 16) ? s.sched[(se & 0xFFFF) + pair] : -1;
+  return pair < (se >> 8) ? s.sched[(se & 0xFF) + pair] : -1;
 }
 
-template <int NM, int MM, class Real>
-__global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restrict__ T0,
+// MINW: waves per SIMD the register budget is built for. 1 leaves every kernel its 256 VGPRs
+// (2 waves/SIMD); the fp32 kernel also exists at 3 (168 VGPRs, 32 B of spills), which fits 11
+// instead of 8 rollouts per CU but runs each ~20 % slower (launch_class picks per batch).
+template <int NM, int MM, class Real, int MINW>
+__global__ __launch_bounds__(WAVE, MINW) void hs_sim_kernel(const hs_topo* __restrict__ T0,
                                                          const hs_simtopo_t<Real>* __restrict__ S, hs_sim_args a) {
   using real = Real;
   __shared__ SimL<NM, MM, Real> s;
@@ -401,10 +422,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
   if (lane == 0) s.seed = a.seed[b];
   int tsi = a.tsi[b];
   wave_sync();
-  if (lane < n) {
-    q_to_R(s.q[lane], s.R[lane]);
-    s.invm[lane] = real(1) / T.mass[lane];
-  }
+  if (lane < n) s.invm[lane] = real(1) / T.mass[lane];
   wave_sync();
 
   SIM_ACC(0);
@@ -416,8 +434,9 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
       const real qm = hinge_angle(s, J);
       real tq = 0;
       if (P.k > 0) {
-        real ax[3];
-        mul0_331(ax, s.R[J.b1], J.axis1);
+        real ax[3], R1[12];
+        q_to_R(s.q[J.b1], R1);
+        mul0_331(ax, R1, J.axis1);
         const real rate = dot3(ax, s.avel[J.b1]) - dot3(ax, s.avel[J.b2]);
         const int t = tsi % a.n_t;
         const int hrow = (t + a.n_t - 2) % a.n_t;
@@ -445,8 +464,9 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
         for (int c = 0; c < T.tq_n[p]; c++) {  // dJointAddHingeTorque in motor order
           const int j = T.tq_motor[p][c];
           const hs_simjoint_t<real>& J = T.joint[T.motor_joint[j]];
-          real ax[3];
-          mul0_331(ax, s.R[J.b1], J.axis1);
+          real ax[3], R1[12];
+          q_to_R(s.q[J.b1], R1);
+          mul0_331(ax, R1, J.axis1);
           for (int i = 0; i < 3; i++) ax[i] *= s.tau[j];
           if (T.tq_sign[p][c] > 0)
             for (int i = 0; i < 3; i++) tq[i] += ax[i];
@@ -456,7 +476,8 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
       }
       // collision with the plane (0,0,1,0)
       bool hit = false;
-      const real* R = s.R[p];
+      real R[12];
+      q_to_R(s.q[p], R);
       if (T.gtype[p] == HS_GEOM_CAPSULE) {
         const real sign = (R[10] > 0) ? real(-1) : real(1);  // dCalcVectorDot3_14(plane normal, R + 2)
         real pp[3];
@@ -491,8 +512,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
       for (int r = 0; r < 3; r++)
         for (int c = 0; c < 3; c++) tmp[r * 4 + c] = dot3(iIb + r * 4, R + c * 4);
       for (int r = 0; r < 3; r++) {
-        for (int c = 0; c < 3; c++) s.invI[p][r * 4 + c] = dot3_14(R + r * 4, tmp + c);
-        s.invI[p][r * 4 + 3] = 0;
+        for (int c = 0; c < 3; c++) s.invI[p][r * 3 + c] = dot3_14(R + r * 4, tmp + c);
       }
       for (int r = 0; r < 3; r++)
         for (int c = 0; c < 3; c++) tmp[r * 4 + c] = dot3(Ib + r * 4, R + c * 4);
@@ -512,7 +532,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
         s.fc[p][i] = fa[i] * im + s.lvel[p][i] * h1;  // tmp1
       }
       real it[3];
-      mul0_331(it, s.invI[p], tq);
+      mul0_33(it, s.invI[p], tq);
       for (int i = 0; i < 3; i++) s.fc[p][3 + i] = it[i] + w[i] * h1;
     }
     wave_sync();
@@ -578,7 +598,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
     // ---- G: SOR sweeps
     {
       const int pair = lane >> 1, half = lane & 1;
-      for (int i = lane; i < m; i += WAVE) s.order[i] = (int16_t)i;  // findex all -1: identity order
+      for (int i = lane; i < m; i += WAVE) s.order[i] = (uint8_t)i;  // findex all -1: identity order
       uint32_t seed = __builtin_amdgcn_readfirstlane(s.seed);
       for (int it0 = 0; it0 < P.iterations; it0 += 8) {
         // RANDOMLY_REORDER_CONSTRAINTS: Fisher-Yates with dRandInt over the current order, i.e.
@@ -590,7 +610,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           const int p = lane + 64 * k;
-          if (p >= 1 && p < m) s.swp[p] = (int16_t)rand_int_from(T.lcg_a[p] * seed + T.lcg_c[p], p + 1);
+          if (p >= 1 && p < m) s.swp[p] = (uint8_t)rand_int_from(T.lcg_a[p] * seed + T.lcg_c[p], p + 1);
           src[k] = p;
         }
         if (m > 1) seed = T.lcg_a[m - 1] * seed + T.lcg_c[m - 1];
@@ -616,7 +636,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           const int p = lane + 64 * k;
-          if (p < m) s.order[p] = (int16_t)ordr[k];
+          if (p < m) s.order[p] = (uint8_t)ordr[k];
           pb1[k] = (p < m) ? s.rb1[ordr[k]] : -2;
           pb2[k] = (p < m) ? s.rb2[ordr[k]] : -2;
         }
@@ -672,7 +692,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
 #pragma unroll
           for (int k = 0; k < 4; k++) {
             lvr[k] = nl[k];
-            if (k < nblk && lane + 64 * k < m) s.lv[lane + 64 * k] = (int16_t)nl[k];
+            if (k < nblk && lane + 64 * k < m) s.lv[lane + 64 * k] = (uint8_t)nl[k];
           }
           wave_sync();
         }
@@ -703,14 +723,14 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
               const int up = __shfl_up(incl, off);
               if (lane >= off) incl += up;
             }
-            if (l < nlev) s.run_se[l] = (base + incl - size) | (size << 16);
+            if (l < nlev) s.run_se[l] = (uint16_t)((base + incl - size) | (size << 8));
             base += __shfl(incl, 63);
           }
           wave_sync();
 #pragma unroll
           for (int k = 0; k < 4; k++) {
             const int p = lane + 64 * k;
-            if (p < m) s.sched[(s.run_se[lvr[k]] & 0xFFFF) + rank[k]] = (int16_t)ordr[k];
+            if (p < m) s.sched[(s.run_se[lvr[k]] & 0xFF) + rank[k]] = (uint8_t)ordr[k];
           }
           if (lane == 0) s.nruns = nlev;
         }
@@ -761,7 +781,7 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
         ta[j] = s.tacc[p][j] * h;
       }
       real t3[3];
-      mul0_331(t3, s.invI[p], ta);
+      mul0_33(t3, s.invI[p], ta);
       for (int j = 0; j < 3; j++) s.avel[p][j] += t3[j];
       for (int j = 0; j < 3; j++) s.pos[p][j] += h * s.lvel[p][j];
       const real* w = s.avel[p];
@@ -773,7 +793,6 @@ __global__ __launch_bounds__(WAVE, 1) void hs_sim_kernel(const hs_topo* __restri
       dq[3] = real(0.5) * (w[0] * qv[2] - w[1] * qv[1] + w[2] * qv[0]);
       for (int j = 0; j < 4; j++) qv[j] += h * dq[j];
       normalize4(qv);
-      q_to_R(qv, s.R[p]);
     }
     if (lane == 0) {
       if (a.n_contacts) a.n_contacts[orow] = s.nc;
@@ -883,16 +902,41 @@ int launch_sim_reset(const hs_topo* d_topo, const hs_simtopo* d_sim, int32_t n_r
   return (int)hipGetLastError();
 }
 
+// rounds of resident rollouts a batch needs with kernel k (every rollout runs a whole launch)
+static long sim_rounds(const void* k, long B) {
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, WAVE, 0) != hipSuccess || per_cu <= 0) return -1;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -1;
+  const long slots = (long)per_cu * cus;
+  return (B + slots - 1) / slots;
+}
+
+template <int NM, int MM, class R, class S>
+static void launch_class(const hs_topo* d_topo, const S* d_sim, const hs_sim_args& a, hipStream_t st) {
+  if constexpr (sizeof(R) == 4) {
+    // the 3-waves/SIMD build when it saves more than its per-rollout slowdown in rounds
+    // (measured: spider B = 16384, 8 -> 6 rounds, +8 %; hexapod B = 4096, 2 -> 2 rounds, -9 %)
+    const long r2 = sim_rounds((const void*)hs_sim_kernel<NM, MM, R, 1>, a.n_rollouts);
+    const long r3 = sim_rounds((const void*)hs_sim_kernel<NM, MM, R, 3>, a.n_rollouts);
+    if (r2 > 0 && r3 > 0 && 5 * r3 < 4 * r2) {
+      hipLaunchKernelGGL((hs_sim_kernel<NM, MM, R, 3>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((hs_sim_kernel<NM, MM, R, 1>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
+}
+
 template <class R, class S>
 static int launch_sim_typed(const hs_topo* d_topo, const S* d_sim, const hs_simtopo& hs, const hs_sim_args& a) {
   hipStream_t st = (hipStream_t)a.stream;
   // smallest LDS layout holding the model: parts and rows (6 per fixed, 5 per hinge, 3 per contact)
   if (hs.n <= 18 && hs.m_max <= 144)
-    hipLaunchKernelGGL((hs_sim_kernel<18, 144, R>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
+    launch_class<18, 144, R>(d_topo, d_sim, a, st);
   else if (hs.n <= 22 && hs.m_max <= 176)
-    hipLaunchKernelGGL((hs_sim_kernel<22, 176, R>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
+    launch_class<22, 176, R>(d_topo, d_sim, a, st);
   else if (hs.n <= HS_NMAX && hs.m_max <= 9 * HS_NMAX)
-    hipLaunchKernelGGL((hs_sim_kernel<HS_NMAX, 9 * HS_NMAX, R>), dim3(a.n_rollouts), dim3(WAVE), 0, st, d_topo, d_sim, a);
+    launch_class<HS_NMAX, 9 * HS_NMAX, R>(d_topo, d_sim, a, st);
   else
     return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();

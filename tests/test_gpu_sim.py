@@ -286,3 +286,21 @@ def test_f32_configs2_shape(gpu, hmodels):
     assert torch.isfinite(sb.body).all()
     assert (out["torso"][:, :, 2] > 0).all()
     assert (out["n_contacts"][:, -1] > 0).float().mean().item() > 0.99
+
+
+def test_f32_occupancy_builds_agree(gpu, hmodels):
+    """A 16384-spider fp32 batch runs the 3-waves/SIMD build of the kernel (more rollouts per CU),
+    a small one the default build: the same rollouts come out bit for bit."""
+    import torch
+    from hslabs_amd import synth
+
+    params = synth.gen_sim_params(16384, "spider")
+    big = gpu.SimBatch(hmodels["spider"], params, dtype=torch.float32)
+    big.step(32, outputs=())
+    idx = [0, 5000, 16383]
+    small = gpu.SimBatch(hmodels["spider"], params[idx], dtype=torch.float32)
+    small.step(32, outputs=())
+    torch.cuda.synchronize()
+    for k, i in enumerate(idx):
+        assert torch.equal(small.body[k], big.body[i])
+        assert small.seed[k].item() == big.seed[i].item()
