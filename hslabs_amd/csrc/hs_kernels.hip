@@ -1279,11 +1279,17 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       real da[3], va[3][3];
       for (int r = 0; r < 3; r++) da[r] = Jp[r] - fp[r];
       cross_rows(da, va);
+      // (va[r][r] = 0: the products it enters add exact zeros and are skipped)
+#pragma unroll
       for (int r = 0; r < 3; r++) {
         real w2 = Jz[r] * Jz[r];
         if (w2 == 0) continue;
+#pragma unroll
         for (int i = 0; i < 3; i++) {
-          for (int j = 0; j < 3; j++) D[3 * i + j] += w2 * va[r][i] * va[r][j];
+          if (i == r) continue;
+#pragma unroll
+          for (int j = 0; j < 3; j++)
+            if (j != r) D[3 * i + j] += w2 * va[r][i] * va[r][j];
           g[i] += w2 * va[r][i] * sv.x[3 * n + 3 * p + r];
         }
       }
@@ -1303,17 +1309,36 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
           chol_solve_n<3>(L, e);
           for (int i = 0; i < 3; i++) Dinv[3 * i + j] = e[i];
         }
+        // E = A_c D_c^-1 and S_c = E A_c^T with A_c = [-I; [d0]x]: the products by A_c's zeros
+        // (identity off-diagonal, cross-matrix diagonal) add exact zeros and are skipped, the
+        // remaining terms are summed in the same order
         real E[18];
+#pragma unroll
         for (int r = 0; r < 6; r++)
+#pragma unroll
           for (int j = 0; j < 3; j++) {
             real s = 0;
-            for (int i = 0; i < 3; i++) s += Ac[r * 3 + i] * Dinv[3 * i + j];
+            if (r < 3) {
+              s += real(-1) * Dinv[3 * r + j];
+            } else {
+#pragma unroll
+              for (int i = 0; i < 3; i++)
+                if (i != r - 3) s += Ac[r * 3 + i] * Dinv[3 * i + j];
+            }
             E[r * 3 + j] = s;
           }
+#pragma unroll
         for (int r = 0; r < 6; r++) {
-          for (int q = 0; q < 6; q++) {
+#pragma unroll
+          for (int q = 0; q <= r; q++) {  // lower triangle: all the Cholesky below reads
             real s = 0;
-            for (int j = 0; j < 3; j++) s += E[r * 3 + j] * Ac[q * 3 + j];
+            if (q < 3) {
+              s += E[r * 3 + q] * real(-1);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 3; j++)
+                if (j != q - 3) s += E[r * 3 + j] * Ac[q * 3 + j];
+            }
             fl.sc.S[c][6 * r + q] = s;
           }
           real s = 0;
@@ -1391,7 +1416,16 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       fl.ok[0] = ok;
     }
   } else {  // Schur complement of the 6 zeroth-order constraints
-    for (int e = lane; e < 42; e += HALF) {  // entry sums in contact order (lane per entry)
+    // entry sums in contact order, one lane per entry of the lower triangle (21) and of h (6)
+    if (lane < 27) {
+      int e = lane;
+      if (lane < 21) {
+        int r = 0;
+        while ((r + 1) * (r + 2) / 2 <= lane) r++;
+        e = 6 * r + (lane - r * (r + 1) / 2);
+      } else {
+        e = 36 + (lane - 21);
+      }
       real s = 0;
       for (int c = 0; c < nc; c++) s += (e < 36) ? fl.sc.S[c][e] : fl.sc.h[c][e - 36];
       fl.sc.Ssum[e] = s;
@@ -1399,7 +1433,10 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
     wave_sync();
     if (lane == 0) {
       real Sm[36], h[6];
-      for (int i = 0; i < 36; i++) Sm[i] = fl.sc.Ssum[i];
+#pragma unroll
+      for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j < 6; j++) Sm[6 * i + j] = (j <= i) ? fl.sc.Ssum[6 * i + j] : real(0);  // upper: unread
       for (int i = 0; i < 6; i++) h[i] = fl.sc.Ssum[36 + i];
       real lam[6];
       for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
@@ -1417,9 +1454,15 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       const int c = lane;
       const real* Ac = fl.A[c];
       real t[3];
-      for (int i = 0; i < 3; i++) {
+#pragma unroll
+      for (int i = 0; i < 3; i++) {  // g + A_c^T lam, A_c's zero entries skipped (exact zeros)
         real s = fl.g[c][i];
-        for (int r = 0; r < 6; r++) s += Ac[r * 3 + i] * fl.sc.lam[r];
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+          if (r < 3 && r != i) continue;
+          if (r >= 3 && r - 3 == i) continue;
+          s += Ac[r * 3 + i] * fl.sc.lam[r];
+        }
         t[i] = s;
       }
       for (int i = 0; i < 3; i++) {
@@ -1487,10 +1530,13 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
       const real* fp = w.fpos(0, fi);
       for (int rr = 0; rr < 3; rr++) d[rr] = Jp[rr] - fp[rr];
     }
+#pragma unroll
     for (int r = 0; r < 3; r++) {
       real s = real(0);
       if (cc >= 0)
-        for (int jj = 0; jj < 3; jj++) s = s + cross_e(d, jj, r) * sv.y[3 * cc + jj];
+#pragma unroll
+        for (int jj = 0; jj < 3; jj++)
+          if (jj != r) s = s + cross_e(d, jj, r) * sv.y[3 * cc + jj];  // (d x e_r)[r] = 0: skipped
       real xr = sv.x[3 * n + 3 * h_id + r] + s;
       tq = tq + Jz[r] * xr;
     }
