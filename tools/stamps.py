@@ -55,6 +55,8 @@ def main():
     st = np.zeros((4096, 24), dtype=np.uint64)
     L.hs_debug_read_stamps(st.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), 4096)
     st = st[:min((n + 1) // 2, 4096)].astype(np.int64)  # one row per wavefront (two rollouts)
+    if os.environ.get("STAMPS_RAW"):
+        np.save(os.environ["STAMPS_RAW"], st)
     gen = st[:, 9] != 0
     sch = (st[:, 18] != 0) & (st[:, 19] != 0) & ~gen  # Schur tier: contact blocks | 6x6 solve | back-sub
     if sch.any():
