@@ -148,6 +148,47 @@ def run_host(model: KinematicModel, params, n_t: int = 20, k0: int = 0, horizon:
     return out
 
 
+class ShardedBatch:
+    """hs_batch_*: a batch sharded over the devices of this process (device_mask bit d = HIP
+    device d), host parameters in, host outputs out, and the best-rollout reduce
+    (hs_select_best). The in-process counterpart of one process per GPU (dist.py)."""
+
+    def __init__(self, model: KinematicModel, params, horizon: int = 1, n_t: int = 20, fp32: bool = False,
+                 device_mask: int = 1):
+        self.model = model
+        self.params = params_array(params)
+        self.B, self.H, self.n_t = len(self.params), horizon, n_t
+        self.dtype = np.float32 if fp32 else np.float64
+        L = capi.load()
+        h = ctypes.c_void_p()
+        capi.check(L.hs_batch_create(model.handle, self.B, horizon, n_t, capi.HS_PREC_F32 if fp32 else capi.HS_PREC_F64,
+                                     device_mask, ctypes.byref(h)), "hs_batch_create")
+        self.handle = h
+        capi.check(L.hs_batch_set_params(h, self.params.ctypes.data_as(ctypes.POINTER(capi.GaitParamsC))),
+                   "hs_batch_set_params")
+
+    def run(self, k0: int = 0, ignore_reach: bool = True, want=("tau", "cf", "flags", "work", "cot")) -> dict:
+        m, B, H, f = self.model, self.B, self.H, self.dtype
+        shapes = {"q": (B, H, m.config_dim), "tau": (B, H, m.nmj), "cf": (B, H, 3 * m.nfeet),
+                  "x": (B, H, 6 * m.n_parts), "flags": (B, H), "work": (B,), "cot": (B,)}
+        out = {k: np.zeros(shapes[k], np.uint32 if k == "flags" else f) for k in want}
+        o = capi.BatchOutputsC(**{k: v.ctypes.data for k, v in out.items()})
+        capi.check(capi.load().hs_batch_run(self.handle, k0, int(ignore_reach), ctypes.byref(o)), "hs_batch_run")
+        return out
+
+    def select_best(self):
+        """(cot as float32, rollout id) of the last run's best rollout."""
+        c, i = ctypes.c_float(), ctypes.c_int64()
+        capi.check(capi.load().hs_select_best(self.handle, ctypes.byref(c), ctypes.byref(i)), "hs_select_best")
+        return c.value, i.value
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and capi._lib is not None:
+            capi._lib.hs_batch_free(h)
+            self.handle = None
+
+
 class DeviceBatch:
     """Device-resident batch (torch tensors on the current HIP device) for hs_run.
 

@@ -11,7 +11,7 @@ import os
 
 from . import build as _build
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 HS_OK = 0
 HS_FLAG_RANK_RETRY = 1
@@ -31,7 +31,8 @@ EXPORTS = [
     "hs_mixed_get_dims", "hs_complete_traj", "hs_traj_save", "hs_run_forces_host",
     "hs_run_mixed", "hs_run_mixed_steps", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
     "hs_sim_default_params", "hs_sim_reset", "hs_sim_step", "hs_sim_create", "hs_sim_advance", "hs_sim_get_state",
-    "hs_sim_free",
+    "hs_sim_free", "hs_batch_create", "hs_batch_set_params", "hs_batch_run", "hs_select_best",
+    "hs_batch_best_key_device", "hs_batch_free",
 ]
 SIM_BODY_STRIDE = 13
 
@@ -55,6 +56,12 @@ class GaitParamsC(ctypes.Structure):
 
 
 assert ctypes.sizeof(GaitParamsC) == 128
+
+
+class BatchOutputsC(ctypes.Structure):
+    """hs_batch_outputs: host arrays (NULL = not wanted)."""
+
+    _fields_ = [(f, ctypes.c_void_p) for f in ("q", "tau", "cf", "x", "flags", "work", "cot")]
 
 
 class ModelDimsC(ctypes.Structure):
@@ -172,6 +179,15 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_sim_get_state.argtypes = [vp, dp, ctypes.POINTER(ctypes.c_int32)]
     L.hs_sim_free.argtypes = [vp]
     L.hs_sim_free.restype = None
+    L.hs_batch_create.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
+                                  ctypes.POINTER(vp)]
+    L.hs_batch_set_params.argtypes = [vp, ctypes.POINTER(GaitParamsC)]
+    L.hs_batch_run.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(BatchOutputsC)]
+    L.hs_select_best.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64)]
+    L.hs_batch_best_key_device.argtypes = [vp, ctypes.c_int32]
+    L.hs_batch_best_key_device.restype = vp
+    L.hs_batch_free.argtypes = [vp]
+    L.hs_batch_free.restype = None
     L.hs_last_error.argtypes = []
     L.hs_last_error.restype = ctypes.c_char_p
     L.hs_abi_version.argtypes = []

@@ -823,3 +823,238 @@ int hs_sim_get_state(hs_sim_t s, double* body, int32_t* tsi) {
 }
 
 }  // extern "C"
+
+// ---- batch handle sharded over the devices of one process -------------------------------------
+struct hs_batch_s {
+  struct shard {
+    int dev = 0;
+    int32_t id0 = 0, count = 0;  // contiguous rollout range (hslabs_amd/dist.py shard)
+    hipStream_t stream = nullptr;
+    hs_gait_params* params = nullptr;
+    void *q = nullptr, *tau = nullptr, *cf = nullptr, *x = nullptr, *work_cot = nullptr;
+    uint32_t* flags = nullptr;
+    uint64_t* best_key = nullptr;
+  };
+  hs_model_t model = nullptr;
+  int32_t B = 0, H = 0, n_t = 0, precision = HS_PREC_F64;
+  bool have_params = false, ran = false;
+  std::vector<shard> shards;
+};
+
+namespace {
+
+// restores the caller's current device when a batch call returns
+struct device_guard {
+  int cur = 0;
+  bool ok = false;
+  device_guard() { ok = hipGetDevice(&cur) == hipSuccess; }
+  ~device_guard() {
+    if (ok) (void)hipSetDevice(cur);
+  }
+};
+
+void batch_release(hs_batch_s* b) {
+  for (auto& sh : b->shards) {
+    if (hipSetDevice(sh.dev) != hipSuccess) continue;
+    for (void* p : {(void*)sh.params, sh.q, sh.tau, sh.cf, sh.x, sh.work_cot, (void*)sh.flags, (void*)sh.best_key})
+      if (p) (void)hipFree(p);
+    if (sh.stream) (void)hipStreamDestroy(sh.stream);
+  }
+  b->shards.clear();
+}
+
+}  // namespace
+
+extern "C" {
+
+int hs_batch_create(hs_model_t m, int32_t B, int32_t H, int32_t n_t, int32_t precision, uint32_t mask,
+                    hs_batch_t* out) {
+  if (!m || !out) return fail(HS_E_ARG, "null argument");
+  *out = nullptr;
+  if (B <= 0 || H <= 0 || n_t <= 0) return fail(HS_E_ARG, "empty batch");
+  if (precision != HS_PREC_F64 && precision != HS_PREC_F32) return fail(HS_E_ARG, "unknown precision");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+  std::vector<int> devs;
+  for (int d = 0; d < 32; d++)
+    if (mask & (1u << d)) {
+      if (d >= ndev || d >= HS_MAX_DEVICES) return fail(HS_E_DEVICE, "device_mask names a missing device");
+      devs.push_back(d);
+    }
+  if (devs.empty()) return fail(HS_E_ARG, "empty device_mask");
+  device_guard guard;
+  auto* b = new hs_batch_s;
+  b->model = m;
+  b->B = B;
+  b->H = H;
+  b->n_t = n_t;
+  b->precision = precision;
+  const hs_topo& t = m->host;
+  const size_t w = precision == HS_PREC_F32 ? sizeof(float) : sizeof(double);
+  const int n = (int)devs.size();
+  const int32_t base = B / n, rem = B % n;
+  for (int r = 0; r < n; r++) {
+    hs_batch_s::shard sh;
+    sh.dev = devs[r];
+    sh.count = base + (r < rem ? 1 : 0);
+    sh.id0 = r * base + std::min<int32_t>(r, rem);
+    b->shards.push_back(sh);
+  }
+  for (auto& sh : b->shards) {
+    const size_t rows = (size_t)std::max(sh.count, 1) * H;
+    e = hipSetDevice(sh.dev);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&sh.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&sh.params, (size_t)std::max(sh.count, 1) * sizeof(hs_gait_params));
+    if (e == hipSuccess) e = hipMalloc(&sh.q, rows * t.cfg * w);
+    if (e == hipSuccess) e = hipMalloc(&sh.tau, rows * t.nmj * w);
+    if (e == hipSuccess) e = hipMalloc(&sh.cf, rows * 3 * t.nf * w);
+    if (e == hipSuccess) e = hipMalloc(&sh.x, rows * 6 * t.n * w);
+    if (e == hipSuccess) e = hipMalloc(&sh.flags, rows * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&sh.work_cot, (size_t)std::max(sh.count, 1) * 2 * w);
+    if (e == hipSuccess) e = hipMalloc(&sh.best_key, sizeof(uint64_t));
+    if (e != hipSuccess) {
+      batch_release(b);
+      delete b;
+      return hip_fail(e, "hs_batch_create");
+    }
+  }
+  *out = b;
+  return HS_OK;
+}
+
+int hs_batch_set_params(hs_batch_t b, const hs_gait_params* params) {
+  if (!b || !params) return fail(HS_E_ARG, "null argument");
+  device_guard guard;
+  hipError_t e = hipSuccess;
+  for (auto& sh : b->shards) {
+    if (sh.count == 0) continue;
+    e = hipSetDevice(sh.dev);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(sh.params, params + sh.id0, (size_t)sh.count * sizeof(hs_gait_params),
+                         hipMemcpyHostToDevice, sh.stream);
+    if (e != hipSuccess) return hip_fail(e, "hs_batch_set_params");
+  }
+  for (auto& sh : b->shards) {
+    e = hipSetDevice(sh.dev);
+    if (e == hipSuccess) e = hipStreamSynchronize(sh.stream);
+    if (e != hipSuccess) return hip_fail(e, "hs_batch_set_params");
+  }
+  b->have_params = true;
+  return HS_OK;
+}
+
+int hs_batch_run(hs_batch_t b, int32_t k0, int32_t ignore_reach, const hs_batch_outputs* out) {
+  if (!b) return fail(HS_E_ARG, "null batch");
+  if (!b->have_params) return fail(HS_E_ARG, "hs_batch_set_params not called");
+  if (k0 < 0) return fail(HS_E_ARG, "k0 < 0");
+  device_guard guard;
+  const hs_topo& t = b->model->host;
+  const size_t w = b->precision == HS_PREC_F32 ? sizeof(float) : sizeof(double);
+  const uint64_t init = ~0ull;
+  hipError_t e = hipSuccess;
+  // launch every shard, then collect: the devices run concurrently
+  for (auto& sh : b->shards) {
+    if (sh.count == 0) continue;
+    e = hipSetDevice(sh.dev);
+    if (e == hipSuccess) e = hipMemcpyAsync(sh.best_key, &init, sizeof(init), hipMemcpyHostToDevice, sh.stream);
+    if (e != hipSuccess) return hip_fail(e, "hs_batch_run");
+    hs_run_args a;
+    memset(&a, 0, sizeof(a));
+    a.n_rollouts = sh.count;
+    a.horizon = b->H;
+    a.k0 = k0;
+    a.n_t = b->n_t;
+    a.ignore_reach = ignore_reach;
+    a.params = sh.params;
+    a.q = (out && out->q) ? (double*)sh.q : nullptr;
+    a.tau = (double*)sh.tau;
+    a.cf = (double*)sh.cf;
+    a.x = (out && out->x) ? (double*)sh.x : nullptr;
+    a.flags = sh.flags;
+    a.work_cot = (double*)sh.work_cot;
+    a.best_key = sh.best_key;
+    a.rollout_id_base = sh.id0;
+    a.stream = sh.stream;
+    a.precision = b->precision;
+    int rc = hs_run(b->model, &a);
+    if (rc != HS_OK) return rc;
+  }
+  for (auto& sh : b->shards) {
+    if (sh.count == 0) continue;
+    e = hipSetDevice(sh.dev);
+    const size_t rows = (size_t)sh.count * b->H, row0 = (size_t)sh.id0 * b->H;
+    auto copy = [&](void* host, const void* dev, size_t per_row, size_t elem, size_t host_row0) {
+      if (e == hipSuccess && host)
+        e = hipMemcpyAsync((char*)host + host_row0 * per_row * elem, dev, rows * per_row * elem, hipMemcpyDeviceToHost,
+                           sh.stream);
+    };
+    if (out) {
+      copy(out->q, sh.q, t.cfg, w, row0);
+      copy(out->tau, sh.tau, t.nmj, w, row0);
+      copy(out->cf, sh.cf, 3 * t.nf, w, row0);
+      copy(out->x, sh.x, 6 * t.n, w, row0);
+      copy(out->flags, sh.flags, 1, sizeof(uint32_t), row0);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(sh.stream);
+    if (e == hipSuccess && out && (out->work || out->cot)) {
+      std::vector<char> wc((size_t)sh.count * 2 * w);
+      e = hipMemcpy(wc.data(), sh.work_cot, wc.size(), hipMemcpyDeviceToHost);
+      for (int32_t i = 0; e == hipSuccess && i < sh.count; i++) {
+        double wk, ct;
+        if (w == sizeof(float)) {
+          wk = ((const float*)wc.data())[2 * i];
+          ct = ((const float*)wc.data())[2 * i + 1];
+        } else {
+          wk = ((const double*)wc.data())[2 * i];
+          ct = ((const double*)wc.data())[2 * i + 1];
+        }
+        const size_t gi = (size_t)sh.id0 + i;
+        if (w == sizeof(float)) {
+          if (out->work) ((float*)out->work)[gi] = (float)wk;
+          if (out->cot) ((float*)out->cot)[gi] = (float)ct;
+        } else {
+          if (out->work) out->work[gi] = wk;
+          if (out->cot) out->cot[gi] = ct;
+        }
+      }
+    }
+    if (e != hipSuccess) return hip_fail(e, "hs_batch_run");
+  }
+  b->ran = true;
+  return HS_OK;
+}
+
+int hs_select_best(hs_batch_t b, float* cot, int64_t* rollout_id) {
+  if (!b) return fail(HS_E_ARG, "null batch");
+  if (!b->ran) return fail(HS_E_ARG, "hs_batch_run not called");
+  device_guard guard;
+  uint64_t best = ~0ull;
+  for (auto& sh : b->shards) {
+    if (sh.count == 0) continue;
+    uint64_t k = ~0ull;
+    hipError_t e = hipSetDevice(sh.dev);
+    if (e == hipSuccess) e = hipMemcpy(&k, sh.best_key, sizeof(k), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "hs_select_best");
+    best = std::min(best, k);
+  }
+  hs_best_key_decode(best, cot, rollout_id);
+  return HS_OK;
+}
+
+uint64_t* hs_batch_best_key_device(hs_batch_t b, int32_t i) {
+  if (!b || i < 0 || i >= (int32_t)b->shards.size()) {
+    fail(HS_E_ARG, "no such device in the batch");
+    return nullptr;
+  }
+  return b->shards[i].best_key;
+}
+
+void hs_batch_free(hs_batch_t b) {
+  if (!b) return;
+  device_guard guard;
+  batch_release(b);
+  delete b;
+}
+
+}  // extern "C"

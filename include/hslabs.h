@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 5
+#define HSLABS_ABI_VERSION 6
 
 enum {
   HS_OK = 0,
@@ -217,6 +217,42 @@ int hs_traj_save(const char* path, const double* rec, int32_t n_rows, int32_t re
  * NaN COT maps to the largest key. Initial value for a reduction: UINT64_MAX. */
 uint64_t hs_best_key_encode(double cot, int64_t rollout_id);
 void hs_best_key_decode(uint64_t key, float* cot, int64_t* rollout_id);
+
+/*
+ * Batch handle sharded over the devices of one process (SURVEY.md 8b exports 2-5): the
+ * in-process counterpart of one process per GPU. Rollouts split into contiguous ranges, one per
+ * device set in device_mask (bit d = HIP device d; the same ranges as hslabs_amd/dist.py shard),
+ * each range run on its device's own stream with rollout_id_base = its first id. Parameters and
+ * outputs live on the devices; hs_batch_run copies the requested outputs to caller-owned HOST
+ * arrays laid out for the whole batch. Replaces the loop of pgssweeper::setup_pergen +
+ * modelplayer::measure_cot over a parameter sweep (player.cpp:259-321).
+ */
+typedef struct hs_batch_s* hs_batch_t;
+
+typedef struct {         /* host arrays, any may be NULL; float instead of double with HS_PREC_F32 */
+  double* q;             /* [B][H][config_dim] */
+  double* tau;           /* [B][H][nmj] */
+  double* cf;            /* [B][H][3*nfeet] */
+  double* x;             /* [B][H][6*n_parts] */
+  uint32_t* flags;       /* [B][H] */
+  double* work;          /* [B]: positive work of the run's steps (work_over_period) */
+  double* cot;           /* [B]: work / (sum m * step_length) (player.cpp:269-285) */
+} hs_batch_outputs;
+
+int hs_batch_create(hs_model_t model, int32_t n_rollouts, int32_t horizon, int32_t n_t, int32_t precision,
+                    uint32_t device_mask, hs_batch_t* out);
+/* host params[n_rollouts] (pgsconfigparams fields, pergen.h:137-146) -> the devices' shards */
+int hs_batch_set_params(hs_batch_t batch, const hs_gait_params* params);
+/* steps k0 .. k0+H-1 of every rollout (hs_run semantics), synchronous; resets and refills the
+ * per-device best keys */
+int hs_batch_run(hs_batch_t batch, int32_t k0, int32_t ignore_reach, const hs_batch_outputs* out);
+/* The best-rollout reduce: minimum of the per-device keys of the last run (lowest COT, ties to the
+ * lowest id). Across processes, all-reduce the key that hs_batch_best_key_device exposes with
+ * RCCL instead (ncclUint64, ncclMin). */
+int hs_select_best(hs_batch_t batch, float* cot, int64_t* rollout_id);
+/* device pointer of the uint64 best key of the i-th device of the batch (in mask order) */
+uint64_t* hs_batch_best_key_device(hs_batch_t batch, int32_t i);
+void hs_batch_free(hs_batch_t batch);
 
 /*
  * Closed-loop simulation: modelplayer::simulate_ode with position control

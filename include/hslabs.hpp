@@ -239,9 +239,35 @@ class periodic {
   }
 };
 
+// hs_batch_*: rollouts sharded over the devices of device_mask (bit d = HIP device d), host
+// parameters in, host outputs out, best-rollout reduce across the devices
+class batch {
+  hs_batch_t h_ = nullptr;
+
+ public:
+  batch(const kinematicmodel& m, int n_rollouts, int horizon, int n_t, uint32_t device_mask = 1u,
+        int precision = HS_PREC_F64) {
+    check(hs_batch_create(m.handle(), n_rollouts, horizon, n_t, precision, device_mask, &h_), "hs_batch_create");
+  }
+  ~batch() { hs_batch_free(h_); }
+  batch(const batch&) = delete;
+  batch& operator=(const batch&) = delete;
+  void set_params(const std::vector<hs_gait_params>& p) { check(hs_batch_set_params(h_, p.data()), "hs_batch_set_params"); }
+  void run(int k0, const hs_batch_outputs& out, bool ignore_reach = true) {
+    check(hs_batch_run(h_, k0, ignore_reach ? 1 : 0, &out), "hs_batch_run");
+  }
+  std::pair<float, int64_t> select_best() {
+    float c = 0;
+    int64_t id = -1;
+    check(hs_select_best(h_, &c, &id), "hs_select_best");
+    return {c, id};
+  }
+};
+
 class modelplayer {
   kinematicmodel model_;
   bool contact_force_flag_ = false;
+  uint32_t device_mask_ = 1u;  // devices a sweep is sharded over (hs_batch_create)
   hs_sim_t sim_ = nullptr;  // the ODE world of setup_per_controller (one rollout)
   double play_t_ = 0, play_dt_ = 0.01;
   std::vector<double> last_tau_, last_q_;
@@ -354,18 +380,23 @@ class modelplayer {
       params.push_back(p.to_c());
       vals.push_back(val);
     }
-    std::vector<double> wc(2 * params.size());
-    check(hs_run_host(model_.handle(), params.data(), (int)params.size(), n_t, 0, n_t, 1, nullptr, nullptr, nullptr,
-                      nullptr, nullptr, wc.data()),
-          "measure_cot_sweep");
+    std::vector<double> cot(params.size());
+    batch b(model_, (int)params.size(), n_t, n_t, device_mask_);
+    b.set_params(params);
+    hs_batch_outputs o;
+    std::memset(&o, 0, sizeof(o));
+    o.cot = cot.data();
+    b.run(0, o);
     std::vector<std::pair<double, double>> out;
     if (print) std::cout << "sweeping over " << param_name << ":" << std::endl;
     for (size_t i = 0; i < vals.size(); i++) {
-      out.emplace_back(vals[i], wc[2 * i + 1]);
-      if (print) std::cout << "val = " << vals[i] << " COT = " << wc[2 * i + 1] << std::endl;
+      out.emplace_back(vals[i], cot[i]);
+      if (print) std::cout << "val = " << vals[i] << " COT = " << cot[i] << std::endl;
     }
     return out;
   }
+  // devices measure_cot_sweep shards its rollouts over (bit d = HIP device d)
+  void set_device_mask(uint32_t mask) { device_mask_ = mask; }
   // player.cpp:617-629: one cycle's complete trajectory records to traj.txt
   void record_per_traj(const pergensetup* pgs, int n_t, const std::string& fname = "traj.txt") {
     const int len = 2 * model_.get_config_dim() + model_.number_of_motor_joints();

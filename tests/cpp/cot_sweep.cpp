@@ -3,7 +3,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
+#include <vector>
 
 #include "hslabs.hpp"
 
@@ -17,6 +19,29 @@ int main(int argc, char** argv) {
   std::printf("COT = %.12f\n", cot);
   auto sweep = player0.measure_cot_sweep(pgs, 20, "period", 3, 18, 15, false);        // main.cpp:69
   for (auto& vc : sweep) std::printf("val = %g COT = %.12f\n", vc.first, vc.second);
+  {  // the same sweep as a device-sharded batch and its best-rollout reduce
+    std::vector<hs_gait_params> ps;
+    for (size_t i = 0; i < sweep.size(); i++) {
+      pgsconfigparams p = pgs->params();
+      p.TLh[0] = sweep[i].first;  // period
+      ps.push_back(p.to_c());
+    }
+    batch b(*player0.get_model(), (int)ps.size(), 20, 20);
+    b.set_params(ps);
+    std::vector<double> cot_b(ps.size());
+    hs_batch_outputs o;
+    std::memset(&o, 0, sizeof(o));
+    o.cot = cot_b.data();
+    b.run(0, o);
+    auto best = b.select_best();
+    size_t imin = 0;
+    for (size_t i = 0; i < cot_b.size(); i++) {
+      if (cot_b[i] != sweep[i].second) return 4;
+      if ((float)cot_b[i] < (float)cot_b[imin]) imin = i;
+    }
+    std::printf("best = %.9g id %lld\n", (double)best.first, (long long)best.second);
+    if (best.second != (int64_t)imin || best.first != (float)cot_b[imin]) return 5;
+  }
   periodic per(player0.get_model());                                                  // main.cpp:81-89
   per.record_trajectory(pgs, 20);
   per.compute_dynrecs();

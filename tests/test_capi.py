@@ -204,3 +204,24 @@ def test_traj_save_format(product, tmp_path):
     want = [" ".join("%g" % v for v in row) for row in rec] + [" ".join("%g" % v for v in rec[0])]
     assert lines == want
     assert lines[0] == "0.1 -2.5e-07 1.23457e+08 0"
+
+
+def test_batch_handle_without_device_fails_loudly(product):
+    """hs_batch_create reports an error code and message (no GPU in this container), never
+    a CPU fallback; invalid arguments are rejected before any device call."""
+    import ctypes
+
+    L = product.capi.load()
+    m = product.KinematicModel(os.path.join(MODELS, "hexapod.xml"))
+    h = ctypes.c_void_p()
+    assert L.hs_batch_create(m.handle, 0, 1, 20, 0, 1, ctypes.byref(h)) != 0
+    assert b"empty batch" in L.hs_last_error()
+    assert L.hs_batch_create(m.handle, 16, 1, 20, 9, 1, ctypes.byref(h)) != 0
+    rc = L.hs_batch_create(m.handle, 16, 1, 20, 0, 1, ctypes.byref(h))
+    if rc == 0:  # a GPU is present after all
+        L.hs_batch_free(h)
+    else:
+        assert h.value is None and L.hs_last_error()
+    c, i = ctypes.c_float(), ctypes.c_int64()
+    assert L.hs_select_best(None, ctypes.byref(c), ctypes.byref(i)) != 0
+    assert L.hs_batch_best_key_device(None, 0) is None

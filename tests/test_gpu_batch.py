@@ -1,0 +1,96 @@
+"""GPU tests of the device-sharded batch handle (hs_batch_create / set_params / run /
+hs_select_best, SURVEY.md 8b exports 2-5) through the C ABI.
+
+On the one-GPU test box the mask holds device 0 only; the sharding arithmetic is the
+one of hslabs_amd/dist.py (tests/test_dist.py), the per-device launches are hs_run's.
+Bit-for-bit equality is expected against hs_run_host (same kernel, same inputs).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import MODELS
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu(product):
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return product
+
+
+@pytest.fixture(scope="module")
+def hexapod(gpu):
+    return gpu.KinematicModel(os.path.join(MODELS, "hexapod.xml"))
+
+
+def test_batch_matches_run_host(gpu, hexapod):
+    from hslabs_amd import synth
+
+    params = synth.gen_params(1000, "hexapod")
+    sb = gpu.ShardedBatch(hexapod, params, horizon=20, n_t=20)
+    out = sb.run(k0=0, want=("q", "tau", "cf", "x", "flags", "work", "cot"))
+    ref = gpu.run_host(hexapod, params, n_t=20, k0=0, horizon=20)
+    for k in ("q", "tau", "cf", "x", "flags"):
+        assert np.array_equal(out[k], ref[k]), k
+    assert np.array_equal(out["work"], ref["work_cot"][:, 0])
+    assert np.array_equal(out["cot"], ref["work_cot"][:, 1])
+
+
+def test_select_best_is_min_key(gpu, hexapod):
+    """hs_select_best = the lowest (float32 COT, id) key over the batch (measure_cot_sweep's
+    minimum, ties to the lowest id)."""
+    from hslabs_amd import capi, synth
+
+    params = synth.gen_params(777, "hexapod")
+    sb = gpu.ShardedBatch(hexapod, params, horizon=20, n_t=20)
+    out = sb.run(k0=0)
+    L = capi.load()
+    keys = [L.hs_best_key_encode(float(c), i) for i, c in enumerate(out["cot"])]
+    cot, rid = sb.select_best()
+    kmin = min(keys)
+    assert rid == kmin & 0xFFFFFFFF
+    assert cot == np.float32(out["cot"][rid])
+
+
+def test_batch_steps_and_fp32(gpu, hexapod):
+    """H = 1 runs at successive k0 give the H = n_t rows; the fp32 batch follows the fp64 one."""
+    from hslabs_amd import synth
+
+    params = synth.gen_params(64, "hexapod")
+    full = gpu.ShardedBatch(hexapod, params, horizon=20, n_t=20).run(k0=0)
+    one = gpu.ShardedBatch(hexapod, params, horizon=1, n_t=20)
+    for k0 in (0, 7, 19):
+        o = one.run(k0=k0)
+        assert np.array_equal(o["tau"][:, 0], full["tau"][:, k0])
+    f32 = gpu.ShardedBatch(hexapod, params, horizon=20, n_t=20, fp32=True).run(k0=0)
+    assert f32["tau"].dtype == np.float32
+    same = (f32["flags"] == full["flags"]).all(axis=1)
+    err = np.abs(f32["tau"][same] - full["tau"][same]) / np.maximum(1, np.abs(full["tau"][same]))
+    assert same.mean() > 0.9 and err.max() < 1e-3
+
+
+def test_batch_argument_errors(gpu, hexapod):
+    import ctypes
+
+    from hslabs_amd import capi
+
+    L = capi.load()
+    h = ctypes.c_void_p()
+    assert L.hs_batch_create(hexapod.handle, 16, 1, 20, 0, 0, ctypes.byref(h)) != 0  # empty mask
+    assert b"mask" in L.hs_last_error()
+    assert L.hs_batch_create(hexapod.handle, 16, 1, 20, 0, 1 << 31, ctypes.byref(h)) != 0  # no such device
+    assert L.hs_batch_create(hexapod.handle, 0, 1, 20, 0, 1, ctypes.byref(h)) != 0
+    assert L.hs_batch_create(hexapod.handle, 16, 1, 20, 7, 1, ctypes.byref(h)) != 0  # precision
+    assert L.hs_batch_create(hexapod.handle, 16, 1, 20, 0, 1, ctypes.byref(h)) == 0
+    o = capi.BatchOutputsC()
+    assert L.hs_batch_run(h, 0, 1, ctypes.byref(o)) != 0  # params not set
+    c, i = ctypes.c_float(), ctypes.c_int64()
+    assert L.hs_select_best(h, ctypes.byref(c), ctypes.byref(i)) != 0  # nothing run
+    assert L.hs_batch_best_key_device(h, 0) is not None
+    assert L.hs_batch_best_key_device(h, 1) is None
+    L.hs_batch_free(h)
