@@ -240,9 +240,11 @@ def main():
         batch = H.DeviceBatch(model, params, n_t=n_t, k0=0, horizon=Hh, outputs=outs, device=dev,
                               rollout_id_base=id0, dtype=dtype)
         out_bytes = OUT_BYTES_PER_STEP[args.model]
-        if args.model == "hexapod" and Hh == 1 and not args.fp32:
+        if args.model == "hexapod" and Hh == 1 and not args.fp32 and B == 4096:
             cfg = "configs[1]"
-        elif args.model == "spider" and Hh == 32 and args.fp32:
+        elif args.model == "hexapod" and Hh == 1 and not args.fp32 and B * world == 262144:
+            cfg = "configs[3]"  # 262144 rollouts sharded over the ranks
+        elif args.model == "spider" and Hh == 32 and args.fp32 and B == 16384:
             cfg = "configs[2]"
         else:
             cfg = "custom"
