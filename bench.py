@@ -56,6 +56,10 @@ def parse():
                          "--rollouts 16384 --horizon 32 --fp32")
     ap.add_argument("--mixed", action="store_true",
                     help="BASELINE configs[4]: myant.xml + hexapod.xml 50/50, interleaved, one launch")
+    ap.add_argument("--launch", choices=["fused", "steps"], default="fused",
+                    help="fused: the K control steps in launches of 16 steps over (step, rollout) "
+                         "(hs_run_calls, every step its own output rows); steps: one launch per step "
+                         "(hs_run_steps, the online loop)")
     ap.add_argument("--sim", action="store_true",
                     help="closed-loop simulation (PD control + ODE QuickStep, 20 SOR iterations) steps/s")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -227,6 +231,7 @@ def main():
         model_names = list(synth.MIXED_MODELS)
         models = [H.KinematicModel(os.path.join(ROOT, "models", f"{n}.xml")) for n in model_names]
         params, midx = synth.gen_mixed(B, id0=id0, curved=args.curved)
+        fused = False  # fused steps run one model per launch
         batch = H.MixedBatch(models, midx, params, n_t=n_t, k0=0, horizon=Hh, outputs=outs, device=dev,
                              rollout_id_base=id0, dtype=dtype)
         out_bytes = float(np.mean([OUT_BYTES_PER_STEP[model_names[k]] for k in midx]))
@@ -237,7 +242,9 @@ def main():
         model_names = [args.model]
         model = H.KinematicModel(os.path.join(ROOT, "models", f"{args.model}.xml"))
         params = synth.gen_params(B, args.model, id0=id0, curved=args.curved)
-        batch = H.DeviceBatch(model, params, n_t=n_t, k0=0, horizon=Hh, outputs=outs, device=dev,
+        fused = args.launch == "fused"
+        rows = Hh * max(args.steps, args.warmup) if fused else Hh  # fused: one output row per step
+        batch = H.DeviceBatch(model, params, n_t=n_t, k0=0, horizon=rows, outputs=outs, device=dev,
                               rollout_id_base=id0, dtype=dtype)
         out_bytes = OUT_BYTES_PER_STEP[args.model]
         if args.model == "hexapod" and Hh == 1 and not args.fp32 and B == 4096:
@@ -256,7 +263,14 @@ def main():
     # warmup (untimed): the same native launch loop as the timed region
     batch.work_cot.zero_()
     batch.k0 = 0
-    batch.run_steps(args.warmup, stream=stream, best=False, accumulate=True)
+
+    def run_k(k):
+        if fused:
+            batch.run_calls(k, call_horizon=Hh, stream=stream, best=False, accumulate=True)
+        else:
+            batch.run_steps(k, stream=stream, best=False, accumulate=True)
+
+    run_k(args.warmup)
     torch.cuda.synchronize()
     batch.work_cot.zero_()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -273,12 +287,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    # K steps: native launch loop, k0 = (s * H) mod n_t. Two HIP events on the launch stream
-    # bracket the K back-to-back launches (per-launch events would drain the queue between
-    # kernels and add ~8 us each): average launch duration = GPU time / K.
+    # K steps, k0 = (s * H) mod n_t: fused (a setup pass, launches of 16 steps, the in-order work
+    # sum) or the native loop of K launches. Two HIP events on the launch stream bracket them
+    # (per-launch events would drain the queue between kernels and add ~8 us each): GPU time per
+    # step of the batch = GPU time / K.
     batch.k0 = 0
     ev0.record(stream)
-    batch.run_steps(args.steps, stream=stream, best=False, accumulate=True)
+    run_k(args.steps)
     ev1.record(stream)
     key = hdist.reduce_best(best_key_local())  # the single RCCL collective (8 B)
     torch.cuda.synchronize()
@@ -317,6 +332,9 @@ def main():
             "data": "synthetic (splitmix64 gait parameters around pgs id 8; SURVEY.md 8d)",
             "config": {"workload": workload,
                        "rollouts_per_gpu": B, "horizon": Hh, "n_t": n_t,
+                       "launch": ("fused: K calls in launches of 16 steps over (step, rollout), every step "
+                                  "its own output rows (hs_run_calls)") if fused else
+                                 "one launch per step (hs_run_steps)",
                        "parallelism": f"rollout-sharded x{world}, 1 RCCL all_reduce(MIN, 8 B) per job"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -308,6 +308,19 @@ class DeviceBatch:
         self._launch(a, n_calls, ev)
 
 
+    def run_calls(self, n_calls: int, call_horizon: int = 1, stream=None, best: bool = False,
+                  accumulate: bool = True) -> None:
+        """The n_calls control steps of run_steps(n_calls) with call horizon ``call_horizon``
+        fused into few launches (hs_run_calls): every step keeps its own output row, rows packed
+        per rollout with stride n_calls * call_horizon, so this batch's horizon must be at least
+        that (equal: the [B][H] views hold the steps in order)."""
+        assert self.H >= n_calls * call_horizon, "outputs need one row per fused step"
+        assert not isinstance(self, MixedBatch), "fused steps run one model"
+        a = self._args(stream, best, accumulate)
+        a.horizon = call_horizon
+        capi.check(capi.load().hs_run_calls(self.model.handle, ctypes.byref(a), n_calls), "hs_run_calls")
+
+
 class SimBatch:
     """Closed-loop simulation of a batch of robots (hs_sim_reset / hs_sim_step).
 

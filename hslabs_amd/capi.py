@@ -11,7 +11,7 @@ import os
 
 from . import build as _build
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 HS_OK = 0
 HS_FLAG_RANK_RETRY = 1
@@ -27,7 +27,7 @@ HS_PREC_F32 = 1
 # every symbol declared in include/hslabs.h
 EXPORTS = [
     "hs_model_load", "hs_model_load_ex", "hs_model_free", "hs_model_get_dims", "hs_pgs_config_read",
-    "hs_run", "hs_run_steps", "hs_run_pd", "hs_run_forces", "hs_mixed_create", "hs_mixed_free",
+    "hs_run", "hs_run_steps", "hs_run_calls", "hs_run_pd", "hs_run_forces", "hs_mixed_create", "hs_mixed_free",
     "hs_mixed_get_dims", "hs_complete_traj", "hs_traj_save", "hs_run_forces_host",
     "hs_run_mixed", "hs_run_mixed_steps", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
     "hs_sim_default_params", "hs_sim_reset", "hs_sim_step", "hs_sim_create", "hs_sim_advance", "hs_sim_get_state",
@@ -147,6 +147,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
                                      ctypes.c_char_p, ctypes.c_int32]
     L.hs_run.argtypes = [vp, ctypes.POINTER(RunArgsC)]
     L.hs_run_steps.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32, ctypes.POINTER(vp)]
+    L.hs_run_calls.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32]
     L.hs_run_forces.argtypes = [vp, ctypes.POINTER(RunArgsC), vp]
     L.hs_run_forces_host.argtypes = [vp, ctypes.POINTER(GaitParamsC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                      ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_double),

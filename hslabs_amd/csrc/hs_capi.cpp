@@ -223,6 +223,8 @@ void hs_model_free(hs_model_t m) {
     if (m->sim_dev_f32[d]) free_on_device(d, m->sim_dev_f32[d]);
   }
   m->ws.release();
+  m->fused_gen.release();
+  m->fused_work.release();
   delete m;
 }
 
@@ -263,6 +265,54 @@ int hs_run_steps(hs_model_t m, const hs_run_args* a, int32_t n_calls, void* cons
   rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);  // + the idle half-wave of an odd batch
   if (rc != HS_OK) return rc;
   return launch_steps(d, *a, ws, hs::single_model_map(m->host, a->n_rollouts), n_calls, kernel_events);
+}
+
+int hs_run_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls) {
+  int rc = check_args(m, a);
+  if (rc != HS_OK) return rc;
+  if (n_calls < 0) return fail(HS_E_ARG, "n_calls < 0");
+  if (a->n_rollouts == 0 || n_calls == 0) return HS_OK;
+  const int64_t S = (int64_t)n_calls * a->horizon;  // steps, one output row each
+  if (S > (1 << 24)) return fail(HS_E_ARG, "too many steps");
+  const hs_topo* d = nullptr;
+  void* ws = nullptr;
+  rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);
+  if (rc != HS_OK) return rc;
+  // steps per launch: the launch refills the SIMDs from its queue of wavefronts (the batch's last
+  // wavefronts no longer end every step); each step in flight has its own general-path scratch
+  constexpr int32_t CHUNK = 16;
+  const int32_t B = a->n_rollouts;
+  const size_t gwb = hs::general_workspace_bytes();
+  void *gen = nullptr, *work = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(m->mu);
+    hipError_t e = (hipError_t)m->fused_gen.get(a->stream, (size_t)CHUNK * (B + 1), &gen);
+    if (e == hipSuccess) e = (hipError_t)m->fused_work.get(a->stream, ((size_t)S * B * sizeof(double) + gwb - 1) / gwb, &work);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(fused workspace)");
+  }
+  const bool f32 = a->precision == HS_PREC_F32;
+  hs_run_args c = *a;
+  c.horizon = (int32_t)S;  // output rows per rollout
+  c.best_key = nullptr;    // taken by the reduce, after the last step
+  hs::launch_map mp = hs::single_model_map(m->host, B);
+  mp.fused_h = a->horizon;
+  mp.fused_work = work;
+  mp.fused_gen = gen;
+  mp.setup_only = 1;  // gait setup once per rollout, stored for every step
+  mp.setup_io = hs::SETUP_STORE;
+  int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+  mp.setup_only = 0;
+  mp.setup_io = hs::SETUP_LOAD;
+  for (int64_t s0 = 0; le == 0 && s0 < S; s0 += CHUNK) {
+    mp.fused_s0 = (int32_t)s0;
+    mp.fused_n = (int32_t)std::min<int64_t>(CHUNK, S - s0);
+    le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+  }
+  if (le == 0)
+    le = f32 ? hs::launch_fused_reduce_f32(*a, m->host.total_mass, work, (int32_t)S)
+             : hs::launch_fused_reduce(*a, m->host.total_mass, work, (int32_t)S);
+  if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
+  return HS_OK;
 }
 
 int hs_run_pd(hs_model_t m, const hs_run_args* a, const hs_pd_args* pd) {

@@ -33,6 +33,15 @@ struct launch_map {
   double pd_k1, pd_k2;
   double *pd_tau, *pd_q0, *pd_dq0;
   int32_t st_tau, st_cf, st_q, st_x;  // output row strides (mixed: maxima over the models)
+  // fused steps (hs_run_calls): one launch runs fused_n steps x fused_w wavefronts, wavefront
+  // blockIdx = local step * fused_w + batch wavefront; global step s = fused_s0 + local step is
+  // call s / fused_h, step s % fused_h of that call, output row s; the step's work goes to
+  // fused_work[s][b] (summed in order afterwards), the general-path scratch to
+  // fused_gen[local step][b]. setup_only: store the gait setup and return.
+  int32_t fused_w, fused_s0, fused_n, fused_h;
+  void* fused_work;
+  void* fused_gen;
+  int32_t setup_only;
 };
 
 // Kernel launcher (hs_kernels.hip). `workspace` holds general_workspace_bytes()
@@ -44,6 +53,13 @@ int launch_rollouts(const hs_topo* d_topo, const hs_run_args& a, void* workspace
 size_t general_workspace_bytes_f32();
 int launch_rollouts_f32(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
 launch_map single_model_map(const hs_topo& t, int32_t n_rollouts);
+// one launch of mp.fused_n fused steps (or the setup-only pass when mp.setup_only)
+int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
+int launch_fused_f32(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
+// work_cot[b] = (w, w / (total_mass * step_length)) with w = (accumulate ? work_cot[b][0] : 0) + the steps'
+// work in step order, then the best key
+int launch_fused_reduce(const hs_run_args& a, double total_mass, const void* work_steps, int32_t n_steps);
+int launch_fused_reduce_f32(const hs_run_args& a, double total_mass, const void* work_steps, int32_t n_steps);
 
 // closed-loop simulation kernels (hs_sim.hip); return hipError_t values
 int launch_sim_reset(const hs_topo* d_topo, const hs_simtopo* d_sim, int32_t n_rollouts, const double* config,
@@ -79,5 +95,6 @@ struct hs_model_s {
   hs_simtopo* sim_dev[HS_MAX_DEVICES];
   hs_simtopo_t<float>* sim_dev_f32[HS_MAX_DEVICES];  // rounded copy for the single-precision kernel
   ws_pool ws;
+  ws_pool fused_gen, fused_work;  // hs_run_calls: general-path scratch per (step in a launch, rollout), step work
   std::mutex mu;
 };

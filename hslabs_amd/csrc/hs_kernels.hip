@@ -1609,8 +1609,10 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   wave_sync();
   real work_dt = 0;  // summed in joint order like work_over_period
   for (int jj = 0; jj < nmj; jj++) work_dt += wk.wd[jj];
-  work_dt *= st.dt;
-  work += work_dt;
+  // work_over_period: work += work_dt * dt, one rounding (explicit, so the fused path's in-order
+  // sum performs the same operation); fused steps hand back the joint sum itself
+  if (mp.fused_w) work = work_dt;
+  else work = fma(work_dt, st.dt, work);
   STAMP(8);
   RSTAMP(17);
 }
@@ -1816,20 +1818,31 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
   // one model per wavefront: the topology pointer stays wave-uniform (scalar loads)
   // (indexing the kernel argument keeps T a known-global pointer: global_load, not flat_load)
   const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[blockIdx.x] : T0;
+  // fused steps: this wavefront's step and its wavefront within the batch
+  const int fstep = mp.fused_w ? (int)(blockIdx.x / mp.fused_w) : 0;
+  const int wid = mp.fused_w ? (int)(blockIdx.x % mp.fused_w) : (int)blockIdx.x;
   int b, bb;
   bool live;  // an idle half (odd group) computes a copy of its neighbour and stores nothing
   if (mp.wave_rollouts) {
-    b = mp.wave_rollouts[2 * blockIdx.x + sub];
+    b = mp.wave_rollouts[2 * wid + sub];
     live = b >= 0;
-    bb = live ? b : mp.wave_rollouts[2 * blockIdx.x];
+    bb = live ? b : mp.wave_rollouts[2 * wid];
   } else {
-    b = blockIdx.x * 2 + sub;
+    b = wid * 2 + sub;
     live = b < a.n_rollouts;
     bb = live ? b : a.n_rollouts - 1;
   }
-  GenWS* G = &rws[live ? b : a.n_rollouts].gen;
+  GenWS* G = mp.fused_gen
+                 ? &((RolloutWS*)mp.fused_gen)[(size_t)fstep * (a.n_rollouts + 1) + (live ? b : a.n_rollouts)].gen
+                 : &rws[live ? b : a.n_rollouts].gen;
   Smem<NM, FORCES>& sm = smem[sub];
-  real work = (live && a.accumulate && a.work_cot) ? outp(a.work_cot)[2 * (size_t)b] : real(0);
+  real work = (live && a.accumulate && a.work_cot && !mp.fused_w) ? outp(a.work_cot)[2 * (size_t)b] : real(0);
+  int k0 = a.k0, h_row = mp.h_row;
+  if (mp.fused_w) {
+    const int s = mp.fused_s0 + fstep, c = s / mp.fused_h;
+    k0 = (int)(((int64_t)a.k0 + (int64_t)c * mp.fused_h) % a.n_t) + s % mp.fused_h;
+    h_row = s;
+  }
   const GaitR g = load_gait(a.params[bb]);
   const int nl = T->n_limbs;
   const bool ignore_reach = a.ignore_reach != 0;
@@ -1848,10 +1861,11 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
         for (int e = lane; e < NW; e += HALF) cache[e] = lds[e];
     }
   }
+  if (mp.setup_only) return;
   STAMP(1);
 
   // K: the five-sample window, lane = (sample, limb)
-  const int i = a.k0 + 2;  // centre sample of this launch's step
+  const int i = k0 + 2;  // centre sample of this launch's step
   {
     const int sl = lane / nl, L = lane % nl;
     if (sl < NS) kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2);
@@ -1859,11 +1873,16 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
   }
   STAMP(2);
   if constexpr (FORCES) {
-    forces_step(T, a, mp, sm.st, sm.sv, sm.d.fr, OneWin<NM, FORCES>{&sm.d}, b, live, mp.h_row, lane);
+    forces_step(T, a, mp, sm.st, sm.sv, sm.d.fr, OneWin<NM, FORCES>{&sm.d}, b, live, h_row, lane);
     return;
   } else {
-    step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.gl, sm.d.wk, OneWin<NM, FORCES>{&sm.d}, G, b, live, mp.h_row, work,
+    step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.gl, sm.d.wk, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
          lane);
+  }
+  if (mp.fused_w) {  // this step's joint sum of positive work, summed over the steps in order by the reduce
+    if (lane == 0 && live)
+      reinterpret_cast<real*>(mp.fused_work)[(size_t)(mp.fused_s0 + fstep) * a.n_rollouts + b] = work;
+    return;
   }
   if (lane == 0 && live) {
     real cot = work / ((real)T->total_mass * g.step_length);
@@ -1931,6 +1950,47 @@ int launch_rollouts(const hs_topo* d_topo, const hs_run_args& a, void* workspace
     if (e != hipSuccess) return (int)e;
   }
   return 0;
+}
+
+
+#if HS_REAL_IS_FLOAT
+int launch_fused_f32(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp) {
+#else
+int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp) {
+#endif
+  if (a.n_rollouts <= 0 || mp.n_waves <= 0) return 0;
+  hipStream_t st = (hipStream_t)a.stream;
+  RolloutWS* ws = (RolloutWS*)workspace;
+  launch_map m = mp;
+  m.fused_w = mp.setup_only ? 0 : mp.n_waves;
+  m.n_waves = mp.setup_only ? mp.n_waves : mp.n_waves * mp.fused_n;  // the grid
+  if (mp.max_parts <= 18) launch_nm<18>(d_topo, a, ws, m, st);
+  else if (mp.max_parts <= 22) launch_nm<22>(d_topo, a, ws, m, st);
+  else launch_nm<HS_NMAX>(d_topo, a, ws, m, st);
+  return (int)hipGetLastError();
+}
+
+__global__ void hs_fused_reduce_kernel(hs_run_args a, real total_mass, const real* __restrict__ ws, int n_steps) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= a.n_rollouts) return;
+  real w = a.accumulate ? outp(a.work_cot)[2 * (size_t)b] : real(0);
+  const real dt = (real)a.params[b].period / a.n_t;  // gait_setup's st.dt
+  for (int s = 0; s < n_steps; s++) w = fma(ws[(size_t)s * a.n_rollouts + b], dt, w);  // periodic.cpp:302-303
+  const real cot = w / (total_mass * (real)a.params[b].step_length);
+  outp(a.work_cot)[2 * (size_t)b] = w;
+  outp(a.work_cot)[2 * (size_t)b + 1] = cot;
+  if (a.best_key) atomicMin((unsigned long long*)a.best_key, (unsigned long long)best_key(cot, a.rollout_id_base + b));
+}
+
+#if HS_REAL_IS_FLOAT
+int launch_fused_reduce_f32(const hs_run_args& a, double total_mass, const void* work_steps, int32_t n_steps) {
+#else
+int launch_fused_reduce(const hs_run_args& a, double total_mass, const void* work_steps, int32_t n_steps) {
+#endif
+  if (a.n_rollouts <= 0 || !a.work_cot) return 0;
+  hipLaunchKernelGGL(hs_fused_reduce_kernel, dim3((a.n_rollouts + 255) / 256), dim3(256), 0, (hipStream_t)a.stream, a,
+                     (real)total_mass, (const real*)work_steps, n_steps);
+  return (int)hipGetLastError();
 }
 
 }  // namespace hs

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 6
+#define HSLABS_ABI_VERSION 7
 
 enum {
   HS_OK = 0,
@@ -158,6 +158,15 @@ typedef struct {
   double* q_target;       /* out, optional: get_motor_adas angles */
   double* dq_target;      /* out, optional: get_motor_adas rates */
 } hs_pd_args;
+/* The n_calls control steps of hs_run_steps (call c solves steps k0_c .. k0_c + H - 1 with
+ * k0_c = (k0 + c H) mod n_t) fused into few launches over (step, rollout), so the SIMDs are
+ * refilled from one queue of wavefronts instead of each step ending on its batch's slowest ones.
+ * Every step keeps its own output rows: q, dq, tau, cf, x, flags are [B][n_calls * H][...]
+ * (row c H + h). work_cot receives the same work (summed in step order, bitwise equal to
+ * hs_run_steps with accumulate) and COT; the best key is taken once, after the last step
+ * (needs work_cot). Asynchronous on args->stream like hs_run. */
+int hs_run_calls(hs_model_t model, const hs_run_args* args, int32_t n_calls);
+
 int hs_run_pd(hs_model_t model, const hs_run_args* args, const hs_pd_args* pd);
 
 /* Contact forces given motor torques: forcetorquesolver::solve_forces via
