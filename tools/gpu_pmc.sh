@@ -5,7 +5,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out/${PMC_OUT:-pmc}; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-ARGS="${BENCH_ARGS:---steps 10 --warmup 2} --no-cpu"
+ARGS="${BENCH_ARGS:---steps 10 --warmup 2 --launch steps} --no-cpu"  # per-step launches: one dispatch = one step of the batch
 if [ "${PMC_SET:-traffic}" = diag ]; then
   GROUPS_=("SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH"
            "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_LDS"
