@@ -231,8 +231,9 @@ def main():
         model_names = list(synth.MIXED_MODELS)
         models = [H.KinematicModel(os.path.join(ROOT, "models", f"{n}.xml")) for n in model_names]
         params, midx = synth.gen_mixed(B, id0=id0, curved=args.curved)
-        fused = False  # fused steps run one model per launch
-        batch = H.MixedBatch(models, midx, params, n_t=n_t, k0=0, horizon=Hh, outputs=outs, device=dev,
+        fused = args.launch == "fused"
+        rows = Hh * max(args.steps, args.warmup) if fused else Hh  # fused: one output row per step
+        batch = H.MixedBatch(models, midx, params, n_t=n_t, k0=0, horizon=rows, outputs=outs, device=dev,
                              rollout_id_base=id0, dtype=dtype)
         out_bytes = float(np.mean([OUT_BYTES_PER_STEP[model_names[k]] for k in midx]))
         workload = (f"myant.xml+hexapod.xml 50/50 interleaved B={B}/GPU H={Hh} n_t={n_t} {prec} "

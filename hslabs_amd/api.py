@@ -315,10 +315,13 @@ class DeviceBatch:
         per rollout with stride n_calls * call_horizon, so this batch's horizon must be at least
         that (equal: the [B][H] views hold the steps in order)."""
         assert self.H >= n_calls * call_horizon, "outputs need one row per fused step"
-        assert not isinstance(self, MixedBatch), "fused steps run one model"
         a = self._args(stream, best, accumulate)
         a.horizon = call_horizon
-        capi.check(capi.load().hs_run_calls(self.model.handle, ctypes.byref(a), n_calls), "hs_run_calls")
+        L = capi.load()
+        if isinstance(self, MixedBatch):
+            capi.check(L.hs_run_mixed_calls(self.plan, ctypes.byref(a), n_calls), "hs_run_mixed_calls")
+        else:
+            capi.check(L.hs_run_calls(self.model.handle, ctypes.byref(a), n_calls), "hs_run_calls")
 
 
 class SimBatch:

@@ -29,7 +29,7 @@ EXPORTS = [
     "hs_model_load", "hs_model_load_ex", "hs_model_free", "hs_model_get_dims", "hs_pgs_config_read",
     "hs_run", "hs_run_steps", "hs_run_calls", "hs_run_pd", "hs_run_forces", "hs_mixed_create", "hs_mixed_free",
     "hs_mixed_get_dims", "hs_complete_traj", "hs_traj_save", "hs_run_forces_host",
-    "hs_run_mixed", "hs_run_mixed_steps", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
+    "hs_run_mixed", "hs_run_mixed_steps", "hs_run_mixed_calls", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
     "hs_sim_default_params", "hs_sim_reset", "hs_sim_step", "hs_sim_create", "hs_sim_advance", "hs_sim_get_state",
     "hs_sim_free", "hs_batch_create", "hs_batch_set_params", "hs_batch_run", "hs_select_best",
     "hs_batch_best_key_device", "hs_batch_free",
@@ -148,6 +148,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_run.argtypes = [vp, ctypes.POINTER(RunArgsC)]
     L.hs_run_steps.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32, ctypes.POINTER(vp)]
     L.hs_run_calls.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32]
+    L.hs_run_mixed_calls.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32]
     L.hs_run_forces.argtypes = [vp, ctypes.POINTER(RunArgsC), vp]
     L.hs_run_forces_host.argtypes = [vp, ctypes.POINTER(GaitParamsC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                      ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_double),

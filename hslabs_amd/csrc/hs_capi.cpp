@@ -161,6 +161,48 @@ int check_args(const hs_model_s* m, const hs_run_args* a) {
   return HS_OK;
 }
 
+// hs_run_calls / hs_run_mixed_calls: a setup-only pass, launches of CHUNK steps over (step, wavefront),
+// the in-order work reduce. Each step in flight in a launch has its own general-path scratch.
+int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map mp, ws_pool& gen_pool,
+              ws_pool& work_pool, std::mutex& mu, double total_mass, const double* rollout_mass, int32_t n_calls) {
+  const int64_t S = (int64_t)n_calls * a.horizon;  // steps, one output row each
+  if (S > (1 << 24)) return fail(HS_E_ARG, "too many steps");
+  // steps per launch: the launch refills the SIMDs from its queue of wavefronts (the batch's last
+  // wavefronts no longer end every step)
+  constexpr int32_t CHUNK = 16;
+  const int32_t B = a.n_rollouts;
+  const size_t gwb = hs::general_workspace_bytes();
+  void *gen = nullptr, *work = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    hipError_t e = (hipError_t)gen_pool.get(a.stream, (size_t)CHUNK * (B + 1), &gen);
+    if (e == hipSuccess) e = (hipError_t)work_pool.get(a.stream, ((size_t)S * B * sizeof(double) + gwb - 1) / gwb, &work);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(fused workspace)");
+  }
+  const bool f32 = a.precision == HS_PREC_F32;
+  hs_run_args c = a;
+  c.horizon = (int32_t)S;  // output rows per rollout
+  c.best_key = nullptr;    // taken by the reduce, after the last step
+  mp.fused_h = a.horizon;
+  mp.fused_work = work;
+  mp.fused_gen = gen;
+  mp.setup_only = 1;  // gait setup once per rollout, stored for every step
+  mp.setup_io = hs::SETUP_STORE;
+  int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+  mp.setup_only = 0;
+  mp.setup_io = hs::SETUP_LOAD;
+  for (int64_t s0 = 0; le == 0 && s0 < S; s0 += CHUNK) {
+    mp.fused_s0 = (int32_t)s0;
+    mp.fused_n = (int32_t)std::min<int64_t>(CHUNK, S - s0);
+    le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+  }
+  if (le == 0)
+    le = f32 ? hs::launch_fused_reduce_f32(a, total_mass, rollout_mass, work, (int32_t)S)
+             : hs::launch_fused_reduce(a, total_mass, rollout_mass, work, (int32_t)S);
+  if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
+  return HS_OK;
+}
+
 }  // namespace
 
 namespace hs {
@@ -187,7 +229,9 @@ struct hs_mixed_s {
   hs_topo* d_topos = nullptr;  // the models' topologies, contiguous (wave_model indexes it)
   int32_t* d_wave_model = nullptr;
   int32_t* d_wave_rollouts = nullptr;
+  double* d_rollout_mass = nullptr;  // total mass of each rollout's model (the fused reduce's COT)
   ws_pool ws;
+  ws_pool fused_gen, fused_work;
   std::mutex mu;
 };
 
@@ -272,47 +316,12 @@ int hs_run_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls) {
   if (rc != HS_OK) return rc;
   if (n_calls < 0) return fail(HS_E_ARG, "n_calls < 0");
   if (a->n_rollouts == 0 || n_calls == 0) return HS_OK;
-  const int64_t S = (int64_t)n_calls * a->horizon;  // steps, one output row each
-  if (S > (1 << 24)) return fail(HS_E_ARG, "too many steps");
   const hs_topo* d = nullptr;
   void* ws = nullptr;
   rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);
   if (rc != HS_OK) return rc;
-  // steps per launch: the launch refills the SIMDs from its queue of wavefronts (the batch's last
-  // wavefronts no longer end every step); each step in flight has its own general-path scratch
-  constexpr int32_t CHUNK = 16;
-  const int32_t B = a->n_rollouts;
-  const size_t gwb = hs::general_workspace_bytes();
-  void *gen = nullptr, *work = nullptr;
-  {
-    std::lock_guard<std::mutex> lk(m->mu);
-    hipError_t e = (hipError_t)m->fused_gen.get(a->stream, (size_t)CHUNK * (B + 1), &gen);
-    if (e == hipSuccess) e = (hipError_t)m->fused_work.get(a->stream, ((size_t)S * B * sizeof(double) + gwb - 1) / gwb, &work);
-    if (e != hipSuccess) return hip_fail(e, "hipMalloc(fused workspace)");
-  }
-  const bool f32 = a->precision == HS_PREC_F32;
-  hs_run_args c = *a;
-  c.horizon = (int32_t)S;  // output rows per rollout
-  c.best_key = nullptr;    // taken by the reduce, after the last step
-  hs::launch_map mp = hs::single_model_map(m->host, B);
-  mp.fused_h = a->horizon;
-  mp.fused_work = work;
-  mp.fused_gen = gen;
-  mp.setup_only = 1;  // gait setup once per rollout, stored for every step
-  mp.setup_io = hs::SETUP_STORE;
-  int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
-  mp.setup_only = 0;
-  mp.setup_io = hs::SETUP_LOAD;
-  for (int64_t s0 = 0; le == 0 && s0 < S; s0 += CHUNK) {
-    mp.fused_s0 = (int32_t)s0;
-    mp.fused_n = (int32_t)std::min<int64_t>(CHUNK, S - s0);
-    le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
-  }
-  if (le == 0)
-    le = f32 ? hs::launch_fused_reduce_f32(*a, m->host.total_mass, work, (int32_t)S)
-             : hs::launch_fused_reduce(*a, m->host.total_mass, work, (int32_t)S);
-  if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
-  return HS_OK;
+  return run_fused(d, *a, ws, hs::single_model_map(m->host, a->n_rollouts), m->fused_gen, m->fused_work, m->mu,
+                   m->host.total_mass, nullptr, n_calls);
 }
 
 int hs_run_pd(hs_model_t m, const hs_run_args* a, const hs_pd_args* pd) {
@@ -402,6 +411,12 @@ int hs_mixed_create(const hs_model_t* models, int32_t n_models, const int32_t* m
   if (e == hipSuccess) e = hipMemcpy(p->d_topos, topos.data(), nt, hipMemcpyHostToDevice);
   if (e == hipSuccess && nw) e = hipMemcpy(p->d_wave_model, wave_model.data(), nw, hipMemcpyHostToDevice);
   if (e == hipSuccess && nw) e = hipMemcpy(p->d_wave_rollouts, wave_rollouts.data(), 2 * nw, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n_rollouts > 0) {
+    std::vector<double> mass((size_t)n_rollouts);
+    for (int32_t r = 0; r < n_rollouts; r++) mass[(size_t)r] = models[model_index[r]]->host.total_mass;
+    e = hipMalloc(&p->d_rollout_mass, mass.size() * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpy(p->d_rollout_mass, mass.data(), mass.size() * sizeof(double), hipMemcpyHostToDevice);
+  }
   if (e != hipSuccess) {
     hs_mixed_free(p);
     return hip_fail(e, "mixed plan upload");
@@ -415,7 +430,10 @@ void hs_mixed_free(hs_mixed_t p) {
   if (p->d_topos) free_on_device(p->dev, p->d_topos);
   if (p->d_wave_model) free_on_device(p->dev, p->d_wave_model);
   if (p->d_wave_rollouts) free_on_device(p->dev, p->d_wave_rollouts);
+  if (p->d_rollout_mass) free_on_device(p->dev, p->d_rollout_mass);
   p->ws.release();
+  p->fused_gen.release();
+  p->fused_work.release();
   delete p;
 }
 
@@ -454,6 +472,35 @@ int hs_run_mixed_steps(hs_mixed_t p, const hs_run_args* a, int32_t n_calls, void
   }
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
   return launch_steps(p->d_topos, *a, ws, mp, n_calls, kernel_events);
+}
+
+int hs_run_mixed_calls(hs_mixed_t p, const hs_run_args* a, int32_t n_calls) {
+  if (!p) return fail(HS_E_ARG, "null plan");
+  int rc = check_args(p->models[0], a);
+  if (rc != HS_OK) return rc;
+  if (a->n_rollouts != p->n_rollouts) return fail(HS_E_ARG, "n_rollouts differs from the plan's");
+  if (n_calls < 0) return fail(HS_E_ARG, "n_calls < 0");
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  if (dev != p->dev) return fail(HS_E_DEVICE, "plan was created on another device");
+  if (a->n_rollouts == 0 || n_calls == 0) return HS_OK;
+  hs::launch_map mp{};
+  mp.wave_model = p->d_wave_model;
+  mp.wave_rollouts = p->d_wave_rollouts;
+  mp.n_waves = p->n_waves;
+  mp.max_parts = p->max_dims.n_parts;
+  mp.st_tau = p->st_tau;
+  mp.st_cf = p->st_cf;
+  mp.st_q = p->st_q;
+  mp.st_x = p->st_x;
+  void* ws = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(p->mu);
+    e = (hipError_t)p->ws.get(a->stream, (size_t)p->n_rollouts + 1, &ws);
+  }
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
+  return run_fused(p->d_topos, *a, ws, mp, p->fused_gen, p->fused_work, p->mu, 0.0, p->d_rollout_mass, n_calls);
 }
 
 int hs_complete_traj(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n_t, int32_t ignore_reach,

@@ -58,8 +58,11 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
 int launch_fused_f32(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
 // work_cot[b] = (w, w / (total_mass * step_length)) with w = (accumulate ? work_cot[b][0] : 0) + the steps'
 // work in step order, then the best key
-int launch_fused_reduce(const hs_run_args& a, double total_mass, const void* work_steps, int32_t n_steps);
-int launch_fused_reduce_f32(const hs_run_args& a, double total_mass, const void* work_steps, int32_t n_steps);
+// (rollout_mass: per-rollout total mass of a mixed plan, else null and total_mass)
+int launch_fused_reduce(const hs_run_args& a, double total_mass, const double* rollout_mass, const void* work_steps,
+                        int32_t n_steps);
+int launch_fused_reduce_f32(const hs_run_args& a, double total_mass, const double* rollout_mass,
+                            const void* work_steps, int32_t n_steps);
 
 // closed-loop simulation kernels (hs_sim.hip); return hipError_t values
 int launch_sim_reset(const hs_topo* d_topo, const hs_simtopo* d_sim, int32_t n_rollouts, const double* config,

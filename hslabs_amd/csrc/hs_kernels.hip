@@ -1817,10 +1817,10 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
   const int lane = threadIdx.x % HALF; // lane within the rollout
   // one model per wavefront: the topology pointer stays wave-uniform (scalar loads)
   // (indexing the kernel argument keeps T a known-global pointer: global_load, not flat_load)
-  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[blockIdx.x] : T0;
   // fused steps: this wavefront's step and its wavefront within the batch
   const int fstep = mp.fused_w ? (int)(blockIdx.x / mp.fused_w) : 0;
   const int wid = mp.fused_w ? (int)(blockIdx.x % mp.fused_w) : (int)blockIdx.x;
+  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
   int b, bb;
   bool live;  // an idle half (odd group) computes a copy of its neighbour and stores nothing
   if (mp.wave_rollouts) {
@@ -1970,9 +1970,11 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   return (int)hipGetLastError();
 }
 
-__global__ void hs_fused_reduce_kernel(hs_run_args a, real total_mass, const real* __restrict__ ws, int n_steps) {
+__global__ void hs_fused_reduce_kernel(hs_run_args a, real total_mass, const double* __restrict__ rollout_mass,
+                                       const real* __restrict__ ws, int n_steps) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= a.n_rollouts) return;
+  if (rollout_mass) total_mass = (real)rollout_mass[b];  // a mixed plan: the rollout's model
   real w = a.accumulate ? outp(a.work_cot)[2 * (size_t)b] : real(0);
   const real dt = (real)a.params[b].period / a.n_t;  // gait_setup's st.dt
   for (int s = 0; s < n_steps; s++) w = fma(ws[(size_t)s * a.n_rollouts + b], dt, w);  // periodic.cpp:302-303
@@ -1983,13 +1985,15 @@ __global__ void hs_fused_reduce_kernel(hs_run_args a, real total_mass, const rea
 }
 
 #if HS_REAL_IS_FLOAT
-int launch_fused_reduce_f32(const hs_run_args& a, double total_mass, const void* work_steps, int32_t n_steps) {
+int launch_fused_reduce_f32(const hs_run_args& a, double total_mass, const double* rollout_mass,
+                            const void* work_steps, int32_t n_steps) {
 #else
-int launch_fused_reduce(const hs_run_args& a, double total_mass, const void* work_steps, int32_t n_steps) {
+int launch_fused_reduce(const hs_run_args& a, double total_mass, const double* rollout_mass, const void* work_steps,
+                        int32_t n_steps) {
 #endif
   if (a.n_rollouts <= 0 || !a.work_cot) return 0;
   hipLaunchKernelGGL(hs_fused_reduce_kernel, dim3((a.n_rollouts + 255) / 256), dim3(256), 0, (hipStream_t)a.stream, a,
-                     (real)total_mass, (const real*)work_steps, n_steps);
+                     (real)total_mass, rollout_mass, (const real*)work_steps, n_steps);
   return (int)hipGetLastError();
 }
 

@@ -201,6 +201,8 @@ int hs_mixed_get_dims(hs_mixed_t plan, hs_model_dims* out);
 /* hs_run / hs_run_steps over a plan (args->n_rollouts must equal the plan's). */
 int hs_run_mixed(hs_mixed_t plan, const hs_run_args* args);
 int hs_run_mixed_steps(hs_mixed_t plan, const hs_run_args* args, int32_t n_calls, void* const* kernel_events);
+/* hs_run_calls for a mixed plan (rows with the plan's strides) */
+int hs_run_mixed_calls(hs_mixed_t plan, const hs_run_args* args, int32_t n_calls);
 
 /* Host-buffer convenience wrapper of hs_run (copies in/out, synchronous).
  * Replaces periodic::compute_torques_over_period + get_motor_torques +

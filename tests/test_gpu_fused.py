@@ -105,3 +105,35 @@ def test_fused_argument_errors(gpu, hmodels):
     assert L.hs_run_calls(hmodels["hexapod"].handle, ctypes.byref(a), 0) == 0
     a.horizon = 0
     assert L.hs_run_calls(hmodels["hexapod"].handle, ctypes.byref(a), 2) != 0
+
+
+def test_fused_mixed_plan_equals_steps(gpu, hmodels):
+    """configs[4]'s plan (myant + hexapod interleaved): fused calls = one launch per call."""
+    import torch
+    from hslabs_amd import synth
+
+    models = [hmodels[n] for n in synth.MIXED_MODELS]
+    params, midx = synth.gen_mixed(301)
+    n_calls = 25
+    seq = gpu.MixedBatch(models, midx, params, n_t=20, k0=0, horizon=1, outputs=("tau", "cf", "flags", "work_cot"))
+    seq.work_cot.zero_()
+    rows = {k: [] for k in ("tau", "cf", "flags")}
+    for c in range(n_calls):
+        seq.k0 = c % 20
+        seq.run(best=False, accumulate=True)
+        for k in rows:
+            rows[k].append(npy(getattr(seq, k)))
+    fz = gpu.MixedBatch(models, midx, params, n_t=20, k0=0, horizon=n_calls,
+                        outputs=("tau", "cf", "flags", "work_cot"))
+    fz.work_cot.zero_()
+    fz.run_calls(n_calls, call_horizon=1, accumulate=True, best=True)
+    torch.cuda.synchronize()
+    for k in rows:
+        assert np.array_equal(np.concatenate(rows[k], axis=1), npy(getattr(fz, k)), equal_nan=True), k
+    assert np.array_equal(npy(seq.work_cot), npy(fz.work_cot))
+    key = npy(fz.best_key).view(np.uint64)[0]
+    from hslabs_amd import capi
+
+    L = capi.load()
+    want = min(L.hs_best_key_encode(float(c), i) for i, c in enumerate(npy(fz.work_cot)[:, 1]))
+    assert int(key) == want
