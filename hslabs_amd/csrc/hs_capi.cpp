@@ -168,20 +168,33 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   const int64_t S = (int64_t)n_calls * a.horizon;  // steps, one output row each
   if (S > (1 << 24)) return fail(HS_E_ARG, "too many steps");
   // steps per launch: the launch refills the SIMDs from its queue of wavefronts (the batch's last
-  // wavefronts no longer end every step). About 128k wavefronts per launch (64 rounds of a full
-  // MI355X at 2 per SIMD; measured B = 4096: 16 steps -2.5 %, 32 steps -0.5 % against 64), and
-  // each step in flight holds general-path scratch for its rollouts (~3.3 GB at 128k wavefronts).
+  // wavefronts no longer end every step). Up to 512k wavefronts per launch (256 rounds of a full
+  // MI355X at 2 per SIMD; measured B = 4096, 200 steps, interleaved A/B: 16 steps -2.5 %, 32 steps
+  // -0.5 % against 64; 128 steps +0.5 %, 256 steps +1.2 % against 64), and each step in flight
+  // holds general-path scratch for its rollouts (~13 GB at 512k wavefronts, of 288 GB HBM).
 #ifndef HS_FUSED_WAVES
-#define HS_FUSED_WAVES 131072
+#define HS_FUSED_WAVES 524288
+#endif
+#ifndef HS_FUSED_MAX_STEPS
+#define HS_FUSED_MAX_STEPS 256
+#endif
+#ifndef HS_FUSED_RESERVE_STEPS
+#define HS_FUSED_RESERVE_STEPS 1024
 #endif
   const int32_t B = a.n_rollouts;
-  const int32_t CHUNK = std::max(1, std::min(64, HS_FUSED_WAVES / std::max(1, mp.n_waves)));
+  const int32_t CHUNK = std::max(1, std::min(HS_FUSED_MAX_STEPS, HS_FUSED_WAVES / std::max(1, mp.n_waves)));
   const size_t gwb = hs::general_workspace_bytes();
   void *gen = nullptr, *work = nullptr;
   {
     std::lock_guard<std::mutex> lk(mu);
     hipError_t e = (hipError_t)gen_pool.get(a.stream, (size_t)CHUNK * (B + 1), &gen);
-    if (e == hipSuccess) e = (hipError_t)work_pool.get(a.stream, ((size_t)S * B * sizeof(double) + gwb - 1) / gwb, &work);
+    // the [step][rollout] work buffer is reserved for at least HS_FUSED_RESERVE_STEPS steps (at most
+    // 512 MB) on first use, so a caller growing its call length (a short warmup, then the real run)
+    // does not hit a hipMalloc between its launches
+    const size_t need = (size_t)S * B * sizeof(double);
+    const size_t want =
+        std::max(need, std::min((size_t)HS_FUSED_RESERVE_STEPS * B * sizeof(double), (size_t)512 << 20));
+    if (e == hipSuccess) e = (hipError_t)work_pool.get(a.stream, (want + gwb - 1) / gwb, &work);
     if (e != hipSuccess) return hip_fail(e, "hipMalloc(fused workspace)");
   }
   const bool f32 = a.precision == HS_PREC_F32;
