@@ -1977,7 +1977,16 @@ __global__ void hs_fused_reduce_kernel(hs_run_args a, real total_mass, const dou
   if (rollout_mass) total_mass = (real)rollout_mass[b];  // a mixed plan: the rollout's model
   real w = a.accumulate ? outp(a.work_cot)[2 * (size_t)b] : real(0);
   const real dt = (real)a.params[b].period / a.n_t;  // gait_setup's st.dt
-  for (int s = 0; s < n_steps; s++) w = fma(ws[(size_t)s * a.n_rollouts + b], dt, w);  // periodic.cpp:302-303
+  // periodic.cpp:302-303, in step order; the loads of 16 steps issue together ahead of their FMAs
+  int s = 0;
+  for (; s + 16 <= n_steps; s += 16) {
+    real v[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[j] = ws[(size_t)(s + j) * a.n_rollouts + b];
+#pragma unroll
+    for (int j = 0; j < 16; j++) w = fma(v[j], dt, w);
+  }
+  for (; s < n_steps; s++) w = fma(ws[(size_t)s * a.n_rollouts + b], dt, w);
   const real cot = w / (total_mass * (real)a.params[b].step_length);
   outp(a.work_cot)[2 * (size_t)b] = w;
   outp(a.work_cot)[2 * (size_t)b + 1] = cot;
@@ -1992,7 +2001,8 @@ int launch_fused_reduce(const hs_run_args& a, double total_mass, const double* r
                         int32_t n_steps) {
 #endif
   if (a.n_rollouts <= 0 || !a.work_cot) return 0;
-  hipLaunchKernelGGL(hs_fused_reduce_kernel, dim3((a.n_rollouts + 255) / 256), dim3(256), 0, (hipStream_t)a.stream, a,
+  // one wavefront per workgroup: B = 4096 spreads over 64 CUs instead of 16
+  hipLaunchKernelGGL(hs_fused_reduce_kernel, dim3((a.n_rollouts + 63) / 64), dim3(64), 0, (hipStream_t)a.stream, a,
                      (real)total_mass, rollout_mass, (const real*)work_steps, n_steps);
   return (int)hipGetLastError();
 }
