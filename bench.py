@@ -265,9 +265,9 @@ def main():
     batch.work_cot.zero_()
     batch.k0 = 0
 
-    def run_k(k):
+    def run_k(k, best=False):
         if fused:
-            batch.run_calls(k, call_horizon=Hh, stream=stream, best=False, accumulate=True)
+            batch.run_calls(k, call_horizon=Hh, stream=stream, best=best, accumulate=True)
         else:
             batch.run_steps(k, stream=stream, best=False, accumulate=True)
 
@@ -281,9 +281,17 @@ def main():
     def best_key_local():
         return hdist.best_key(batch.work_cot[:, 1], id0)
 
+    def job_key():
+        # fused: the work reduce already took the shard's min key (atomicMin, hs_best_key_encode's
+        # encoding); per-step launches: the key of the accumulated COTs, taken after the last step
+        if fused:
+            return batch.best_key ^ hdist._FLIP
+        return best_key_local()
+
     # warm the key computation and the collective too (first use loads code objects)
-    warm = best_key_local()
+    warm = job_key()
     hdist.reduce_best(warm)
+    batch.reset_best()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -294,9 +302,9 @@ def main():
     # step of the batch = GPU time / K.
     batch.k0 = 0
     ev0.record(stream)
-    run_k(args.steps)
+    run_k(args.steps, best=True)
     ev1.record(stream)
-    key = hdist.reduce_best(best_key_local())  # the single RCCL collective (8 B)
+    key = hdist.reduce_best(job_key())  # the single RCCL collective (8 B)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -307,6 +315,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms = float(t[0]), float(t[1])
     best_cot, best_id = hdist.decode(key)
+    check = hdist.reduce_best(best_key_local())  # untimed: the device key equals the host-side encoding
+    if int(check.item()) != int(key.item()):
+        raise RuntimeError(f"best key mismatch: kernel {int(key.item())} vs torch {int(check.item())}")
     nan_steps = int(((batch.flags & 8) != 0).sum().item())
 
     if rank == 0:
