@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--mixed", action="store_true",
                     help="BASELINE configs[4]: myant.xml + hexapod.xml 50/50, interleaved, one launch")
     ap.add_argument("--launch", choices=["fused", "steps"], default="fused",
-                    help="fused: the K control steps in launches of ~128k wavefronts over (step, rollout) "
+                    help="fused: the K control steps in launches of up to 512k wavefronts over (step, rollout) "
                          "(hs_run_calls, every step its own output rows); steps: one launch per step "
                          "(hs_run_steps, the online loop)")
     ap.add_argument("--sim", action="store_true",
@@ -296,7 +296,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    # K steps, k0 = (s * H) mod n_t: fused (a setup pass, launches of ~128k wavefronts, the in-order work
+    # K steps, k0 = (s * H) mod n_t: fused (a setup pass, launches of up to 512k wavefronts, the in-order work
     # sum) or the native loop of K launches. Two HIP events on the launch stream bracket them
     # (per-launch events would drain the queue between kernels and add ~8 us each): GPU time per
     # step of the batch = GPU time / K.
@@ -344,7 +344,7 @@ def main():
             "data": "synthetic (splitmix64 gait parameters around pgs id 8; SURVEY.md 8d)",
             "config": {"workload": workload,
                        "rollouts_per_gpu": B, "horizon": Hh, "n_t": n_t,
-                       "launch": ("fused: K calls in launches of ~128k wavefronts over (step, rollout), every step "
+                       "launch": ("fused: K calls in launches of up to 512k wavefronts over (step, rollout), every step "
                                   "its own output rows (hs_run_calls)") if fused else
                                  "one launch per step (hs_run_steps)",
                        "parallelism": f"rollout-sharded x{world}, 1 RCCL all_reduce(MIN, 8 B) per job"},
