@@ -176,10 +176,23 @@ class ShardedBatch:
         capi.check(capi.load().hs_batch_run(self.handle, k0, int(ignore_reach), ctypes.byref(o)), "hs_batch_run")
         return out
 
-    def select_best(self):
-        """(cot as float32, rollout id) of the last run's best rollout."""
+    def run_device(self, out: dict, k0: int = 0, ignore_reach: bool = True) -> None:
+        """hs_batch_run_device: the requested outputs into caller-owned device tensors (any device of
+        the process; keys as in run(), whole-batch layouts)."""
+        o = capi.BatchOutputsC(**{k: v.data_ptr() for k, v in out.items()})
+        capi.check(capi.load().hs_batch_run_device(self.handle, k0, int(ignore_reach), ctypes.byref(o)),
+                   "hs_batch_run_device")
+
+    def select_best(self, comm: "Comm | None" = None):
+        """(selection cot as float32, rollout id) of the last run's best rollout; with a Comm, the
+        best over all ranks (hs_select_best_comm, one RCCL all-reduce)."""
         c, i = ctypes.c_float(), ctypes.c_int64()
-        capi.check(capi.load().hs_select_best(self.handle, ctypes.byref(c), ctypes.byref(i)), "hs_select_best")
+        L = capi.load()
+        if comm is None:
+            capi.check(L.hs_select_best(self.handle, ctypes.byref(c), ctypes.byref(i)), "hs_select_best")
+        else:
+            capi.check(L.hs_select_best_comm(self.handle, comm.handle, ctypes.byref(c), ctypes.byref(i)),
+                       "hs_select_best_comm")
         return c.value, i.value
 
     def __del__(self):
@@ -187,6 +200,42 @@ class ShardedBatch:
         if h and capi._lib is not None:
             capi._lib.hs_batch_free(h)
             self.handle = None
+
+
+class Comm:
+    """hs_comm_t: the RCCL communicator of the best-rollout reduce, one process per GPU
+    (SURVEY.md 8e). Rank 0 makes the id (``unique_id``), the caller broadcasts it, every rank
+    constructs a Comm with its device current."""
+
+    def __init__(self, n_ranks: int, rank: int, uid: bytes):
+        assert len(uid) == capi.COMM_ID_BYTES
+        h = ctypes.c_void_p()
+        capi.check(capi.load().hs_comm_init(n_ranks, rank, uid, ctypes.byref(h)), "hs_comm_init")
+        self.handle, self.n_ranks, self.rank = h, n_ranks, rank
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(capi.COMM_ID_BYTES)
+        capi.check(capi.load().hs_comm_unique_id(buf), "hs_comm_unique_id")
+        return buf.raw
+
+    def reduce_best(self, key, stream=None) -> None:
+        """In-place all-reduce(MIN) of a device key tensor (int64 [1] holding the uint64 bits)."""
+        import torch
+
+        st = stream if stream is not None else torch.cuda.current_stream(key.device)
+        capi.check(capi.load().hs_comm_reduce_best(self.handle, key.data_ptr(), st.cuda_stream), "hs_comm_reduce_best")
+
+    def free(self) -> None:
+        if self.handle:
+            capi.load().hs_comm_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class DeviceBatch:
@@ -229,6 +278,8 @@ class DeviceBatch:
         self.flags = torch.empty((B, H), dtype=torch.int32, device=dev) if "flags" in outputs else None
         self.work_cot = torch.empty((B, 2), **f64) if "work_cot" in outputs else None
         self.best_key = torch.full((1,), -1, dtype=torch.int64, device=dev)  # UINT64_MAX bit pattern
+        self.solve_mode = capi.HS_SOLVE_AUTO  # HS_SOLVE_REFERENCE: every step through the Eigen-style path
+        self.key_steps = 0  # steps the best key's work covers (0: those of the call)
 
     def reset_best(self):
         self.best_key.fill_(-1)
@@ -249,6 +300,8 @@ class DeviceBatch:
         a.best_key = ptr(self.best_key) if best else None
         a.rollout_id_base = self.rollout_id_base
         a.precision = self.precision
+        a.solve_mode = self.solve_mode
+        a.key_steps = self.key_steps
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         a.stream = st.cuda_stream
         return a
@@ -294,8 +347,8 @@ class DeviceBatch:
     def run_steps(self, n_calls: int, stream=None, best: bool = False, accumulate: bool = True,
                   events=None) -> None:
         """n_calls launches marching k0 through the cycle (hs_run_steps); the launch loop is
-        native. ``events``: 2*n_calls torch.cuda.Event(enable_timing=True), recorded around
-        each launch."""
+        native; the best key (``best``) is taken after the last launch. ``events``: 2*n_calls
+        torch.cuda.Event(enable_timing=True), recorded around each launch."""
         a = self._args(stream, best, accumulate)
         ev = None
         if events is not None:

@@ -24,7 +24,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT_DIR, "libhslabs.so")
-SOURCES = ["hs_kernels.hip", "hs_kernels_f32.hip", "hs_sim.hip", "hs_capi.cpp", "hs_model.cpp"]
+SOURCES = ["hs_kernels.hip", "hs_kernels_f32.hip", "hs_sim.hip", "hs_capi.cpp", "hs_model.cpp", "hs_comm.cpp"]
+# the best-rollout all-reduce (hs_comm.cpp) links RCCL; under torch the process's librccl.so.1
+# (same SONAME) is the one bound
+LIBS = ["-L/opt/rocm/lib", "-lrccl"]
+VARIANT_DIR = os.path.join(OUT_DIR, "variants")
 HEADERS = ["hs_topo.h", "hs_simtopo.h", "hs_ode.h", "hs_math.h", "hs_internal.h", os.path.join("..", "..", "include", "hslabs.h")]
 ARCH = os.environ.get("HSLABS_ARCH", "gfx950")
 CONTRACT = {"hs_sim.hip": "off"}  # per-source FMA contraction (default: fast)
@@ -50,11 +54,11 @@ def _stale() -> bool:
 
 
 def _compile(out: str, defines=(), verbose: bool = False, flags=()) -> str:
-    os.makedirs(OUT_DIR, exist_ok=True)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     tag = os.path.splitext(os.path.basename(out))[0]
 
     def obj(src):
-        o = os.path.join(OUT_DIR, f"{tag}.{src}.o")
+        o = os.path.join(os.path.dirname(out), f"{tag}.{src}.o")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
                f"-ffp-contract={CONTRACT.get(src, 'fast')}", "-Wall", "-Wno-unused-function",
                *SRC_FLAGS.get(src, []), *flags,
@@ -67,7 +71,7 @@ def _compile(out: str, defines=(), verbose: bool = False, flags=()) -> str:
     jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(obj, SOURCES))
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, *LIBS, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
@@ -84,9 +88,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 
 def build_variant(name: str, defines, verbose: bool = False, flags=()) -> str:
-    """Tuning builds (e.g. HS_MIN_WAVES=N) next to the product library; select one with
-    HSLABS_LIB=<path> for a measurement sweep."""
-    return _compile(os.path.join(OUT_DIR, f"libhslabs_{name}.so"), defines, verbose, flags)
+    """Tuning builds (e.g. HS_MIN_WAVES=N) in _build/variants/, never the product library; an A/B
+    sweep selects one by name with HSLABS_VARIANT=<name> (capi.load reports the library it loaded,
+    and bench.py prints its path and hash). Delete them after the sweep."""
+    os.makedirs(VARIANT_DIR, exist_ok=True)
+    return _compile(os.path.join(VARIANT_DIR, f"libhslabs_{name}.so"), defines, verbose, flags)
 
 
 if __name__ == "__main__":

@@ -7,11 +7,12 @@ in-tree gfx950 library is missing, loading fails loudly.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 
 from . import build as _build
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 HS_OK = 0
 HS_FLAG_RANK_RETRY = 1
@@ -23,16 +24,22 @@ HS_FLAG_NO_CONTACT = 32
 HS_FLAG_GENERAL = 64
 HS_PREC_F64 = 0
 HS_PREC_F32 = 1
+HS_SOLVE_AUTO = 0
+HS_SOLVE_REFERENCE = 1
+KEY_MIN_STEP_LENGTH = 1e-3
+COMM_ID_BYTES = 128
 
 # every symbol declared in include/hslabs.h
 EXPORTS = [
     "hs_model_load", "hs_model_load_ex", "hs_model_free", "hs_model_get_dims", "hs_pgs_config_read",
     "hs_run", "hs_run_steps", "hs_run_calls", "hs_run_pd", "hs_run_forces", "hs_mixed_create", "hs_mixed_free",
     "hs_mixed_get_dims", "hs_complete_traj", "hs_traj_save", "hs_run_forces_host",
-    "hs_run_mixed", "hs_run_mixed_steps", "hs_run_mixed_calls", "hs_run_host", "hs_best_key_encode", "hs_best_key_decode", "hs_last_error", "hs_abi_version",
+    "hs_run_mixed", "hs_run_mixed_steps", "hs_run_mixed_calls", "hs_run_host", "hs_best_key_cot", "hs_best_key_encode",
+    "hs_best_key_decode", "hs_last_error", "hs_abi_version",
     "hs_sim_default_params", "hs_sim_reset", "hs_sim_step", "hs_sim_create", "hs_sim_advance", "hs_sim_get_state",
-    "hs_sim_free", "hs_batch_create", "hs_batch_set_params", "hs_batch_run", "hs_select_best",
-    "hs_batch_best_key_device", "hs_batch_free",
+    "hs_sim_free", "hs_batch_create", "hs_batch_set_params", "hs_batch_run", "hs_batch_run_device", "hs_select_best",
+    "hs_batch_best_key_device", "hs_batch_free", "hs_comm_unique_id", "hs_comm_init", "hs_comm_free", "hs_comm_size",
+    "hs_comm_reduce_best", "hs_select_best_comm",
 ]
 SIM_BODY_STRIDE = 13
 
@@ -86,7 +93,7 @@ class RunArgsC(ctypes.Structure):
         ("cf", ctypes.c_void_p), ("x", ctypes.c_void_p), ("flags", ctypes.c_void_p),
         ("work_cot", ctypes.c_void_p), ("best_key", ctypes.c_void_p),
         ("rollout_id_base", ctypes.c_int64), ("stream", ctypes.c_void_p), ("dq", ctypes.c_void_p),
-        ("precision", ctypes.c_int32),
+        ("precision", ctypes.c_int32), ("solve_mode", ctypes.c_int32), ("key_steps", ctypes.c_int32),
     ]
 
 
@@ -110,6 +117,7 @@ class HSError(RuntimeError):
 
 
 _lib = None
+LOADED = None  # {"path", "sha256"} of the library load() mapped
 
 
 def lib_path() -> str:
@@ -130,12 +138,23 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
         import torch  # noqa: F401
     except ImportError:
         pass
-    path = os.environ.get("HSLABS_LIB") or _build.LIB  # tuning-variant override (build.build_variant)
+    path = _build.LIB
+    variant = os.environ.get("HSLABS_VARIANT")  # an A/B tuning build (build.build_variant), by name only
+    if variant:
+        if not variant.replace("_", "").isalnum():
+            raise HSError(f"bad HSLABS_VARIANT {variant!r}")
+        path = os.path.join(_build.VARIANT_DIR, f"libhslabs_{variant}.so")
+        if not os.path.exists(path):
+            raise HSError(f"HSLABS_VARIANT={variant}: {path} not built")
     if not os.path.exists(path):
         if not build_if_missing:
             raise HSError(f"libhslabs.so not built ({path}); run `python -m hslabs_amd.build`")
         _build.build()
     L = ctypes.CDLL(path)
+    global LOADED
+    with open(path, "rb") as f:
+        LOADED = {"path": os.path.relpath(path, os.path.dirname(_build.HERE)),
+                  "sha256": hashlib.sha256(f.read()).hexdigest()[:16]}
     dp = ctypes.POINTER(ctypes.c_double)
     vp = ctypes.c_void_p
     L.hs_model_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
@@ -167,6 +186,8 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_run_mixed_steps.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32, ctypes.POINTER(vp)]
     L.hs_run_host.argtypes = [vp, ctypes.POINTER(GaitParamsC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                               ctypes.c_int32, ctypes.c_int32, dp, dp, dp, dp, ctypes.POINTER(ctypes.c_uint32), dp]
+    L.hs_best_key_cot.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int32, ctypes.c_int32]
+    L.hs_best_key_cot.restype = ctypes.c_double
     L.hs_best_key_encode.argtypes = [ctypes.c_double, ctypes.c_int64]
     L.hs_best_key_encode.restype = ctypes.c_uint64
     L.hs_best_key_decode.argtypes = [ctypes.c_uint64, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64)]
@@ -185,7 +206,15 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
                                   ctypes.POINTER(vp)]
     L.hs_batch_set_params.argtypes = [vp, ctypes.POINTER(GaitParamsC)]
     L.hs_batch_run.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(BatchOutputsC)]
+    L.hs_batch_run_device.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(BatchOutputsC)]
     L.hs_select_best.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64)]
+    L.hs_select_best_comm.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64)]
+    L.hs_comm_unique_id.argtypes = [ctypes.c_char_p]
+    L.hs_comm_init.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, ctypes.POINTER(vp)]
+    L.hs_comm_free.argtypes = [vp]
+    L.hs_comm_free.restype = None
+    L.hs_comm_size.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
+    L.hs_comm_reduce_best.argtypes = [vp, vp, vp]
     L.hs_batch_best_key_device.argtypes = [vp, ctypes.c_int32]
     L.hs_batch_best_key_device.restype = vp
     L.hs_batch_free.argtypes = [vp]

@@ -21,6 +21,12 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+}  // namespace
+
+int hs::set_error(int code, const std::string& msg) { return fail(code, msg); }
+
+namespace {
+
 int hip_fail(hipError_t e, const char* what) {
   g_err = std::string(what) + ": " + hipGetErrorString(e);
   return HS_E_DEVICE;
@@ -131,10 +137,13 @@ int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::lau
                  void* const* kernel_events) {
   hs_run_args c = a;
   hipStream_t st = (hipStream_t)a.stream;
+  // the best key covers the work of all n_calls calls: taken after the last one only
+  if (c.key_steps == 0) c.key_steps = (int32_t)std::min<int64_t>((int64_t)n_calls * a.horizon, INT32_MAX);
   // one gait setup per rollout per call: the first launch stores it, later launches load it
   const bool several = (int64_t)n_calls * a.horizon > 1;
   for (int32_t i = 0; i < n_calls; i++) {
     c.k0 = (int32_t)(((int64_t)a.k0 + (int64_t)i * a.horizon) % a.n_t);
+    c.best_key = (i + 1 == n_calls) ? a.best_key : nullptr;
     hs::launch_map mi = mp;
     mi.setup_io = !several ? hs::SETUP_COMPUTE : (i == 0 ? hs::SETUP_STORE : hs::SETUP_LOAD);
     hipError_t e = hipSuccess;
@@ -158,6 +167,9 @@ int check_args(const hs_model_s* m, const hs_run_args* a) {
   if (a->n_t < 1) return fail(HS_E_ARG, "n_t must be >= 1");
   if (a->n_rollouts > 0 && !a->params) return fail(HS_E_ARG, "params is null");
   if (a->n_rollouts > (1 << 30)) return fail(HS_E_ARG, "too many rollouts");
+  if (a->solve_mode != HS_SOLVE_AUTO && a->solve_mode != HS_SOLVE_REFERENCE) return fail(HS_E_ARG, "unknown solve_mode");
+  if (a->key_steps < 0) return fail(HS_E_ARG, "key_steps < 0");
+  if (a->best_key && !a->work_cot) return fail(HS_E_ARG, "best_key needs work_cot (the key is the work's COT)");
   return HS_OK;
 }
 
@@ -201,6 +213,8 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   hs_run_args c = a;
   c.horizon = (int32_t)S;  // output rows per rollout
   c.best_key = nullptr;    // taken by the reduce, after the last step
+  hs_run_args r = a;       // the reduce: its key covers the call's S steps unless told otherwise
+  if (r.key_steps == 0) r.key_steps = (int32_t)S;
   mp.fused_h = a.horizon;
   mp.fused_work = work;
   mp.fused_gen = gen;
@@ -215,8 +229,8 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
     le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   }
   if (le == 0)
-    le = f32 ? hs::launch_fused_reduce_f32(a, total_mass, rollout_mass, work, (int32_t)S)
-             : hs::launch_fused_reduce(a, total_mass, rollout_mass, work, (int32_t)S);
+    le = f32 ? hs::launch_fused_reduce_f32(r, total_mass, rollout_mass, work, (int32_t)S)
+             : hs::launch_fused_reduce(r, total_mass, rollout_mass, work, (int32_t)S);
   if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
   return HS_OK;
 }
@@ -696,6 +710,12 @@ int hs_run_host(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n
   return rc;
 }
 
+double hs_best_key_cot(double work, double total_mass, double step_length, int32_t n_t, int32_t steps) {
+  const double aL = std::fabs(step_length);  // the device computes the same expression (key_cot)
+  if (!(aL >= HS_KEY_MIN_STEP_LENGTH) || n_t < 1 || steps < 1) return NAN;
+  return work * ((double)n_t / (double)steps) / (total_mass * aL);
+}
+
 uint64_t hs_best_key_encode(double cot, int64_t id) {
   float c = (float)cot;
   uint32_t bits;
@@ -1059,7 +1079,13 @@ int hs_batch_set_params(hs_batch_t b, const hs_gait_params* params) {
   return HS_OK;
 }
 
-int hs_batch_run(hs_batch_t b, int32_t k0, int32_t ignore_reach, const hs_batch_outputs* out) {
+}  // extern "C"
+
+namespace {
+
+// hs_batch_run (host outputs) and hs_batch_run_device (device outputs, any device of the process:
+// the copies go through unified addressing, peer-to-peer where the buffer is on another GPU)
+int batch_run(hs_batch_t b, int32_t k0, int32_t ignore_reach, const hs_batch_outputs* out, bool device_out) {
   if (!b) return fail(HS_E_ARG, "null batch");
   if (!b->have_params) return fail(HS_E_ARG, "hs_batch_set_params not called");
   if (k0 < 0) return fail(HS_E_ARG, "k0 < 0");
@@ -1099,10 +1125,10 @@ int hs_batch_run(hs_batch_t b, int32_t k0, int32_t ignore_reach, const hs_batch_
     if (sh.count == 0) continue;
     e = hipSetDevice(sh.dev);
     const size_t rows = (size_t)sh.count * b->H, row0 = (size_t)sh.id0 * b->H;
+    const hipMemcpyKind kind = device_out ? hipMemcpyDefault : hipMemcpyDeviceToHost;
     auto copy = [&](void* host, const void* dev, size_t per_row, size_t elem, size_t host_row0) {
       if (e == hipSuccess && host)
-        e = hipMemcpyAsync((char*)host + host_row0 * per_row * elem, dev, rows * per_row * elem, hipMemcpyDeviceToHost,
-                           sh.stream);
+        e = hipMemcpyAsync((char*)host + host_row0 * per_row * elem, dev, rows * per_row * elem, kind, sh.stream);
     };
     if (out) {
       copy(out->q, sh.q, t.cfg, w, row0);
@@ -1111,8 +1137,16 @@ int hs_batch_run(hs_batch_t b, int32_t k0, int32_t ignore_reach, const hs_batch_
       copy(out->x, sh.x, 6 * t.n, w, row0);
       copy(out->flags, sh.flags, 1, sizeof(uint32_t), row0);
     }
+    if (device_out && out) {  // work / cot: the columns of work_cot [B][2], strided copies
+      for (int col = 0; col < 2; col++) {
+        void* dst = col == 0 ? (void*)out->work : (void*)out->cot;
+        if (e == hipSuccess && dst)
+          e = hipMemcpy2DAsync((char*)dst + (size_t)sh.id0 * w, w, (const char*)sh.work_cot + col * w, 2 * w, w,
+                               (size_t)sh.count, hipMemcpyDefault, sh.stream);
+      }
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(sh.stream);
-    if (e == hipSuccess && out && (out->work || out->cot)) {
+    if (e == hipSuccess && !device_out && out && (out->work || out->cot)) {
       std::vector<char> wc((size_t)sh.count * 2 * w);
       e = hipMemcpy(wc.data(), sh.work_cot, wc.size(), hipMemcpyDeviceToHost);
       for (int32_t i = 0; e == hipSuccess && i < sh.count; i++) {
@@ -1140,19 +1174,59 @@ int hs_batch_run(hs_batch_t b, int32_t k0, int32_t ignore_reach, const hs_batch_
   return HS_OK;
 }
 
-int hs_select_best(hs_batch_t b, float* cot, int64_t* rollout_id) {
+int local_best(hs_batch_t b, uint64_t* best) {
   if (!b) return fail(HS_E_ARG, "null batch");
   if (!b->ran) return fail(HS_E_ARG, "hs_batch_run not called");
   device_guard guard;
-  uint64_t best = ~0ull;
+  *best = ~0ull;
   for (auto& sh : b->shards) {
     if (sh.count == 0) continue;
     uint64_t k = ~0ull;
     hipError_t e = hipSetDevice(sh.dev);
     if (e == hipSuccess) e = hipMemcpy(&k, sh.best_key, sizeof(k), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_fail(e, "hs_select_best");
-    best = std::min(best, k);
+    *best = std::min(*best, k);
   }
+  return HS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hs_batch_run(hs_batch_t b, int32_t k0, int32_t ignore_reach, const hs_batch_outputs* out) {
+  return batch_run(b, k0, ignore_reach, out, false);
+}
+
+int hs_batch_run_device(hs_batch_t b, int32_t k0, int32_t ignore_reach, const hs_batch_outputs* out) {
+  return batch_run(b, k0, ignore_reach, out, true);
+}
+
+int hs_select_best(hs_batch_t b, float* cot, int64_t* rollout_id) {
+  uint64_t best = ~0ull;
+  int rc = local_best(b, &best);
+  if (rc != HS_OK) return rc;
+  hs_best_key_decode(best, cot, rollout_id);
+  return HS_OK;
+}
+
+int hs_select_best_comm(hs_batch_t b, hs_comm_t comm, float* cot, int64_t* rollout_id) {
+  if (!comm) return fail(HS_E_ARG, "null comm");
+  uint64_t best = ~0ull;
+  int rc = local_best(b, &best);
+  if (rc != HS_OK) return rc;
+  for (auto& sh : b->shards)
+    if (sh.dev != hs::comm_device(comm)) return fail(HS_E_ARG, "the batch runs on a device the comm does not");
+  device_guard guard;
+  const hs_batch_s::shard& sh = b->shards[0];
+  hipError_t e = hipSetDevice(sh.dev);
+  if (e == hipSuccess) e = hipMemcpyAsync(sh.best_key, &best, sizeof(best), hipMemcpyHostToDevice, sh.stream);
+  if (e != hipSuccess) return hip_fail(e, "hs_select_best_comm");
+  rc = hs::comm_reduce_min(comm, sh.best_key, sh.stream);
+  if (rc != HS_OK) return rc;
+  e = hipMemcpyAsync(&best, sh.best_key, sizeof(best), hipMemcpyDeviceToHost, sh.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(sh.stream);
+  if (e != hipSuccess) return hip_fail(e, "hs_select_best_comm");
   hs_best_key_decode(best, cot, rollout_id);
   return HS_OK;
 }

@@ -1476,6 +1476,14 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
   return fl.ok[0] != 0;
 }
 
+// selection COT of the best-rollout key (hs_best_key_cot, include/hslabs.h): one cycle's work over
+// sum m * |L|; |L| under HS_KEY_MIN_STEP_LENGTH gives NaN (never selected)
+__device__ inline real key_cot(real work, real mass, real L, int n_t, int steps) {
+  const real aL = fabs(L);
+  if (!(aL >= (real)HS_KEY_MIN_STEP_LENGTH) || steps < 1) return (real)NAN;
+  return work * ((real)n_t / (real)steps) / (mass * aL);
+}
+
 __device__ inline uint64_t best_key(real cot, int64_t id) {
   float c = (float)cot;
   uint32_t bits = __float_as_uint(c);
@@ -1504,7 +1512,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   int k = 3 * nc;
   uint32_t flags = 0;
   STAMP(6);
-  if (fast_solve(T, sv, fl, w, nc, lane)) {
+  if (a.solve_mode == HS_SOLVE_AUTO && fast_solve(T, sv, fl, w, nc, lane)) {
     if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
     if (nc == 1) flags |= HS_FLAG_FULL_RANK;
   } else if (k <= GenLDS::LD) {
@@ -1890,7 +1898,10 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
       outp(a.work_cot)[2 * (size_t)b] = work;
       outp(a.work_cot)[2 * (size_t)b + 1] = cot;
     }
-    if (a.best_key) atomicMin((unsigned long long*)a.best_key, (unsigned long long)best_key(cot, a.rollout_id_base + b));
+    if (a.best_key) {
+      const real kc = key_cot(work, (real)T->total_mass, g.step_length, a.n_t, a.key_steps);
+      atomicMin((unsigned long long*)a.best_key, (unsigned long long)best_key(kc, a.rollout_id_base + b));
+    }
   }
 }
 
@@ -1987,10 +1998,14 @@ __global__ void hs_fused_reduce_kernel(hs_run_args a, real total_mass, const dou
     for (int j = 0; j < 16; j++) w = fma(v[j], dt, w);
   }
   for (; s < n_steps; s++) w = fma(ws[(size_t)s * a.n_rollouts + b], dt, w);
-  const real cot = w / (total_mass * (real)a.params[b].step_length);
+  const real L = (real)a.params[b].step_length;
+  const real cot = w / (total_mass * L);
   outp(a.work_cot)[2 * (size_t)b] = w;
   outp(a.work_cot)[2 * (size_t)b + 1] = cot;
-  if (a.best_key) atomicMin((unsigned long long*)a.best_key, (unsigned long long)best_key(cot, a.rollout_id_base + b));
+  if (a.best_key) {
+    const real kc = key_cot(w, total_mass, L, a.n_t, a.key_steps);
+    atomicMin((unsigned long long*)a.best_key, (unsigned long long)best_key(kc, a.rollout_id_base + b));
+  }
 }
 
 #if HS_REAL_IS_FLOAT

@@ -11,10 +11,26 @@ from __future__ import annotations
 import torch
 
 _FLIP = -(2 ** 63)  # xor with the sign bit maps uint64 order onto int64 order
+KEY_MIN_STEP_LENGTH = 1e-3  # HS_KEY_MIN_STEP_LENGTH
+
+
+def select_cot(work: torch.Tensor, step_length: torch.Tensor, total_mass, n_t: int, steps: int) -> torch.Tensor:
+    """hs_best_key_cot on a shard: one cycle's COT for forward or backward walking,
+    work * (n_t / steps) / (total_mass * |L|), NaN where |L| < 1e-3 (include/hslabs.h). The same
+    expression in the same precision and order as the device's key_cot, so the keys agree
+    bitwise (work's dtype: float64, or float32 for HS_PREC_F32 runs)."""
+    dt = work.dtype
+    L = step_length.to(dt)
+    aL = L.abs()
+    r = torch.tensor(n_t, dtype=dt) / torch.tensor(steps, dtype=dt)
+    m = torch.as_tensor(total_mass, dtype=dt, device=work.device)
+    c = work * r.to(work.device) / (m * aL)
+    return torch.where(aL >= KEY_MIN_STEP_LENGTH, c, torch.full_like(c, float("nan")))
 
 
 def best_key(cot: torch.Tensor, id0: int) -> torch.Tensor:
-    """Min key over one shard; cot is float64 [B] (NaN sorts last). Returns int64 [1] (sign-flipped)."""
+    """Min key over one shard of selection COTs (float64 or float32 [B], NaN sorts last).
+    Returns int64 [1] (sign-flipped, so int64 MIN is the uint64 key's MIN)."""
     c = cot.to(torch.float32)
     bits = c.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
     ordk = torch.where(bits >= 0x80000000, (~bits) & 0xFFFFFFFF, bits | 0x80000000)
@@ -25,7 +41,9 @@ def best_key(cot: torch.Tensor, id0: int) -> torch.Tensor:
 
 
 def reduce_best(key: torch.Tensor, group=None) -> torch.Tensor:
-    """The single collective of the path: all_reduce(MIN) of the 8-byte key (in place)."""
+    """all_reduce(MIN) of a sign-flipped 8-byte key through torch.distributed (the gloo CPU
+    tests and the bench's untimed cross-check; the GPU path's collective is hs_comm_reduce_best,
+    RCCL inside libhslabs)."""
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:

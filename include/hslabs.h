@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 7
+#define HSLABS_ABI_VERSION 8
 
 enum {
   HS_OK = 0,
@@ -33,7 +33,7 @@ enum {
 };
 
 /* Per-step flag bits (hs_run_args.flags). */
-#define HS_FLAG_RANK_RETRY   1u  /* adaptive-rank loop iterated (ftsolver.cpp:279-303) */
+#define HS_FLAG_RANK_RETRY   1u  /* adaptive-rank loop iterated (ftsolver.cpp:208-232) */
 #define HS_FLAG_FULL_RANK    2u  /* zeroth-order Gram full rank (reference asserts in its comma initializer) */
 #define HS_FLAG_LOOP_EXHAUST 4u  /* rank loop reached rank 0 without converging */
 #define HS_FLAG_NAN          8u  /* NaN in torques or contact forces */
@@ -115,7 +115,8 @@ typedef struct {
   double* x;              /* [B][H][6*n_parts]: joint forces/torques (ftsolver.cpp:166) */
   uint32_t* flags;        /* [B][H] */
   double* work_cot;       /* [B][2]: positive work, work/(sum m * step_length) */
-  uint64_t* best_key;     /* scalar; atomically min-reduced (cot key, see hs_best_key_decode) */
+  uint64_t* best_key;     /* scalar; atomically min-reduced with the rollouts' keys after the LAST
+                             step of the call (hs_best_key_encode of hs_best_key_cot; needs work_cot) */
   int64_t rollout_id_base;/* global id of rollout 0 (shard offset) */
   void* stream;           /* hipStream_t */
   double* dq;             /* [B][H][config_dim]: rates at each solved sample (compute_vel_traj,
@@ -124,10 +125,20 @@ typedef struct {
                              arithmetic is single precision and every floating-point array of the
                              call (q, dq, tau, cf, x, work_cot; hs_pd_args; hs_run_forces' tau_in)
                              holds float (the pointer types stay double*). params stay double. */
+  int32_t solve_mode;     /* HS_SOLVE_AUTO (0): the contact solve's closed form, the Eigen-style
+                             path only where the minimizer is not unique; HS_SOLVE_REFERENCE (1):
+                             every step through the Eigen-style FullPivLU / ColPivHouseholderQR
+                             adaptive-rank loop of ftsolver.cpp:185-236 (same results where the
+                             minimizer is unique; much slower; flags carry HS_FLAG_GENERAL) */
+  int32_t key_steps;      /* control steps whose work the best key covers (0: the steps of this
+                             call, i.e. H for hs_run, n_calls * H for hs_run_steps / hs_run_calls);
+                             callers that accumulate work over several calls pass the total */
 } hs_run_args;
 
 #define HS_PREC_F64 0
 #define HS_PREC_F32 1
+#define HS_SOLVE_AUTO 0
+#define HS_SOLVE_REFERENCE 1
 
 int hs_run(hs_model_t model, const hs_run_args* args);
 
@@ -135,7 +146,9 @@ int hs_run(hs_model_t model, const hs_run_args* args);
  * k0_c = (args->k0 + c * horizon) mod n_t .. k0_c + horizon - 1, i.e. the
  * control loop marching through the gait cycle (compute_torques_over_period's
  * step order, periodic.cpp:377-391, wrapped); outputs are overwritten per call
- * and work_cot accumulates when args->accumulate is set. kernel_events, if not
+ * and work_cot accumulates when args->accumulate is set. The best key (if
+ * args->best_key) is taken once, after the last call, over the accumulated work
+ * (key_steps 0 = n_calls * horizon steps). kernel_events, if not
  * NULL, holds 2 * n_calls caller-created hipEvent_t recorded immediately before
  * and after each launch (per-launch kernel timing on the launch stream). */
 int hs_run_steps(hs_model_t model, const hs_run_args* args, int32_t n_calls, void* const* kernel_events);
@@ -224,8 +237,19 @@ int hs_complete_traj(hs_model_t model, const hs_gait_params* params, int32_t n_r
  * separated, default ostream formatting, appended when append != 0. */
 int hs_traj_save(const char* path, const double* rec, int32_t n_rows, int32_t rec_len, int32_t append);
 
-/* Best-rollout key: (order-preserving bits of (float)cot) << 32 | (uint32)rollout id.
- * NaN COT maps to the largest key. Initial value for a reduction: UINT64_MAX. */
+/* Best-rollout key: (order-preserving bits of (float)c) << 32 | (uint32)rollout id, where c is
+ * the selection COT of hs_best_key_cot. NaN maps to the largest key (never selected); ties go to
+ * the lowest id. Initial value for a reduction: UINT64_MAX.
+ *
+ * Selection COT (a deliberate deviation from the signed COT player.cpp:269-285 prints, which
+ * work_cot[1] keeps): the cost of transport of ONE gait cycle of forward or backward walking,
+ *   c = work * (n_t / steps) / (total_mass * |step_length|),
+ * steps = the control steps the accumulated work covers (hs_run_args.key_steps), so a key taken
+ * after K != n_t steps ranks rollouts like measure_cot over one cycle would; |step_length| <
+ * HS_KEY_MIN_STEP_LENGTH gives NaN (a gait that does not travel has no meaningful COT). The
+ * reference only prints per-setup COTs of its sweep (player.cpp:311-321) and never selects. */
+#define HS_KEY_MIN_STEP_LENGTH 1e-3
+double hs_best_key_cot(double work, double total_mass, double step_length, int32_t n_t, int32_t steps);
 uint64_t hs_best_key_encode(double cot, int64_t rollout_id);
 void hs_best_key_decode(uint64_t key, float* cot, int64_t* rollout_id);
 
@@ -257,13 +281,39 @@ int hs_batch_set_params(hs_batch_t batch, const hs_gait_params* params);
 /* steps k0 .. k0+H-1 of every rollout (hs_run semantics), synchronous; resets and refills the
  * per-device best keys */
 int hs_batch_run(hs_batch_t batch, int32_t k0, int32_t ignore_reach, const hs_batch_outputs* out);
-/* The best-rollout reduce: minimum of the per-device keys of the last run (lowest COT, ties to the
- * lowest id). Across processes, all-reduce the key that hs_batch_best_key_device exposes with
- * RCCL instead (ncclUint64, ncclMin). */
+/* hs_batch_run into caller-owned DEVICE buffers (same [B] layouts; each may be on any device of the
+ * process: a shard's rows are copied device-to-device, peer-to-peer when the buffer is on another
+ * GPU; float arrays with HS_PREC_F32), synchronous. periodic::get_motor_torques and
+ * solve_torques_contforces write caller-allocated arrays the same way (periodic.cpp:328-343). */
+int hs_batch_run_device(hs_batch_t batch, int32_t k0, int32_t ignore_reach, const hs_batch_outputs* out);
+/* The best-rollout reduce inside one process: minimum of the per-device keys of the last run
+ * (lowest selection COT, ties to the lowest id), by host reads of the devices' 8-byte keys. */
 int hs_select_best(hs_batch_t batch, float* cot, int64_t* rollout_id);
 /* device pointer of the uint64 best key of the i-th device of the batch (in mask order) */
 uint64_t* hs_batch_best_key_device(hs_batch_t batch, int32_t i);
 void hs_batch_free(hs_batch_t batch);
+
+/*
+ * One process per GPU: the path's single collective, the best-rollout reduce, as
+ * ONE RCCL all-reduce (ncclUint64, ncclMin) of the 8-byte key over xGMI. It replaces the serial
+ * sweep whose minimum a caller of player.cpp:311-321 would take. The communicator spans the ranks
+ * of the job, one HIP device each: rank 0 creates the id with hs_comm_unique_id, the caller
+ * broadcasts its HS_COMM_ID_BYTES bytes (MPI, torch.distributed, a file ...), every rank calls
+ * hs_comm_init with the device it runs on current. Rollouts are sharded in contiguous id ranges
+ * (rollout_id_base), so the reduced key names the global winner.
+ */
+#define HS_COMM_ID_BYTES 128
+typedef struct hs_comm_s* hs_comm_t;
+int hs_comm_unique_id(char id[HS_COMM_ID_BYTES]);
+int hs_comm_init(int32_t n_ranks, int32_t rank, const char id[HS_COMM_ID_BYTES], hs_comm_t* out);
+void hs_comm_free(hs_comm_t comm);
+int hs_comm_size(hs_comm_t comm, int32_t* n_ranks, int32_t* rank);
+/* in-place all-reduce(MIN) of the uint64 key at key (DEVICE pointer, the comm's device), async
+ * on stream (a hipStream_t, NULL = default stream) */
+int hs_comm_reduce_best(hs_comm_t comm, uint64_t* key, void* stream);
+/* hs_select_best across the ranks: this process's minimum over its batch's devices (the batch
+ * must run on the comm's device only), all-reduced over the communicator, decoded on every rank */
+int hs_select_best_comm(hs_batch_t batch, hs_comm_t comm, float* cot, int64_t* rollout_id);
 
 /*
  * Closed-loop simulation: modelplayer::simulate_ode with position control

@@ -124,6 +124,7 @@ def build() -> str:
 
 
 _lib = None
+_perf = {}
 
 
 def lib():
@@ -131,39 +132,54 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             build()
-        L = ctypes.CDLL(LIB_PATH)
-        dp = ctypes.POINTER(ctypes.c_double)
-        L.hso_model_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
-        L.hso_model_free.argtypes = [ctypes.c_void_p]
-        L.hso_model_dims.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
-        L.hso_rollout.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                  ctypes.c_int, ctypes.c_int, dp, dp, dp, dp,
-                                  ctypes.POINTER(ctypes.c_uint32), dp, dp]
-        L.hso_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, dp,
-                                ctypes.POINTER(ctypes.c_uint32)]
-        L.hso_forces.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                 ctypes.c_int, dp, dp, ctypes.POINTER(ctypes.c_uint32)]
-        L.hso_lik_roundtrip.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]
-        L.hso_lik_roundtrip.restype = ctypes.c_double
-        L.hso_euler_roundtrip.argtypes = [dp, dp]
-        L.hso_rot_ztov.argtypes = [dp, dp]
-        L.hso_fk_ik_check.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_double, ctypes.c_int]
-        L.hso_fk_ik_check.restype = ctypes.c_double
-        L.hso_residuals.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int,
-                                    ctypes.c_int, dp]
-        ip = ctypes.POINTER(ctypes.c_int32)
-        L.hso_dynrec_dump.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int,
-                                      dp, dp, dp, dp, dp, dp, ip, ip, ip, ip]
-        up = ctypes.POINTER(ctypes.c_uint32)
-        L.hso_sim_reset.argtypes = [ctypes.c_void_p, dp, dp]
-        L.hso_sim_hinges.argtypes = [ctypes.c_void_p, dp, dp, dp]
-        L.hso_sim_run.argtypes = [ctypes.c_void_p, dp, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, up, ip,
-                                  ctypes.c_int, dp, dp, dp, ip, dp]
-        L.hso_sim_batch.argtypes = [ctypes.c_void_p, dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp,
-                                    up, ip, ctypes.c_int, ctypes.c_int]
-        _lib = L
+        _lib = _bind(LIB_PATH)
     return _lib
+
+
+def perf_lib(tag: str, timeout: float = 180.0):
+    """The CPU-baseline build (-O3 -march=native) for this machine's CPU (tag), built on first use
+    (bench.py cpu_baseline only; the parity checker is lib()). Returns (CDLL, path) or raises."""
+    if tag not in _perf:
+        safe = "".join(c if c.isalnum() else "_" for c in tag)[:48]
+        subprocess.run(["make", "-s", "-C", HERE, "perf", f"PERF_TAG={safe}"], check=True, timeout=timeout)
+        path = os.path.join(HERE, "_build", f"perf_{safe}", "libhs_oracle.so")
+        _perf[tag] = (_bind(path), path)
+    return _perf[tag]
+
+
+def _bind(path):
+    L = ctypes.CDLL(path)
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.hso_model_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
+    L.hso_model_free.argtypes = [ctypes.c_void_p]
+    L.hso_model_dims.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+    L.hso_rollout.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                              ctypes.c_int, ctypes.c_int, dp, dp, dp, dp,
+                              ctypes.POINTER(ctypes.c_uint32), dp, dp]
+    L.hso_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, dp,
+                            ctypes.POINTER(ctypes.c_uint32)]
+    L.hso_forces.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                             ctypes.c_int, dp, dp, ctypes.POINTER(ctypes.c_uint32)]
+    L.hso_lik_roundtrip.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]
+    L.hso_lik_roundtrip.restype = ctypes.c_double
+    L.hso_euler_roundtrip.argtypes = [dp, dp]
+    L.hso_rot_ztov.argtypes = [dp, dp]
+    L.hso_fk_ik_check.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_double, ctypes.c_int]
+    L.hso_fk_ik_check.restype = ctypes.c_double
+    L.hso_residuals.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int,
+                                ctypes.c_int, dp]
+    ip = ctypes.POINTER(ctypes.c_int32)
+    L.hso_dynrec_dump.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int,
+                                  dp, dp, dp, dp, dp, dp, ip, ip, ip, ip]
+    up = ctypes.POINTER(ctypes.c_uint32)
+    L.hso_sim_reset.argtypes = [ctypes.c_void_p, dp, dp]
+    L.hso_sim_hinges.argtypes = [ctypes.c_void_p, dp, dp, dp]
+    L.hso_sim_run.argtypes = [ctypes.c_void_p, dp, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, up, ip,
+                              ctypes.c_int, dp, dp, dp, ip, dp]
+    L.hso_sim_batch.argtypes = [ctypes.c_void_p, dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp,
+                                up, ip, ctypes.c_int, ctypes.c_int]
+    return L
 
 
 def _ptr(a):
@@ -180,21 +196,23 @@ class Model:
     cfg: int = 0
     lik_index: int = -1
     n_limbs: int = 0
+    L: object = field(default=None, repr=False)  # the build that owns the handle (default lib())
 
     def __post_init__(self):
+        self.L = self.L or lib()
         h = ctypes.c_void_p()
-        rc = lib().hso_model_load(self.path.encode(), ctypes.byref(h))
+        rc = self.L.hso_model_load(self.path.encode(), ctypes.byref(h))
         if rc != 0:
             raise RuntimeError(f"oracle: cannot load {self.path} (rc={rc})")
         self.handle = h
         d = (ctypes.c_int * 6)()
-        lib().hso_model_dims(h, d)
+        self.L.hso_model_dims(h, d)
         self.n, self.nmj, self.nf, self.cfg, self.lik_index, self.n_limbs = list(d)
 
     def __del__(self):
         try:
             if self.handle:
-                lib().hso_model_free(self.handle)
+                self.L.hso_model_free(self.handle)
         except Exception:
             pass
 
@@ -267,14 +285,17 @@ def forces(model: Model, gait: GaitParams, tau_in, n_t: int = 20, k0: int = 0, i
 
 
 def batch(model: Model, gaits: list, n_t: int, k0: int, H: int, basis: int = BASIS_TREE,
-          ignore_reach: bool = True, n_threads: int = 1) -> dict:
+          ignore_reach: bool = True, n_threads: int = 1, L=None) -> dict:
+    """B rollouts on n_threads threads. L: another build of the same restatement (perf_lib) whose
+    hso_model the Model was loaded with (Model(path, L=...))."""
+    L = L or lib()
     B = len(gaits)
     arr = (Gait * B)(*[g.to_c() for g in gaits])
     tau = np.zeros((B, H, model.nmj))
     cf = np.zeros((B, H, 3 * model.nf))
     wc = np.zeros((B, 2))
     flags = np.zeros((B, H), dtype=np.uint32)
-    rc = lib().hso_batch(model.handle, arr, B, n_t, k0, H, basis, int(ignore_reach), n_threads,
+    rc = L.hso_batch(model.handle, arr, B, n_t, k0, H, basis, int(ignore_reach), n_threads,
                          _ptr(tau), _ptr(cf), _ptr(wc), flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
     if rc != 0:
         raise RuntimeError(f"oracle batch failed rc={rc}")

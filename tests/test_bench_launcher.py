@@ -1,0 +1,71 @@
+"""bench.py --gpus N launches N ranks: the parent starts
+torch.distributed.run as a child before any GPU call, every rank checks WORLD_SIZE == N, the
+rollouts are sharded in contiguous ranges, and one all-reduce(MIN) of the 8-byte key picks the
+global winner. --stub-cpu runs that skeleton on CPU ranks over gloo with a stub in place of the
+kernel (the GPU run uses the same functions with RCCL and the HIP kernel)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+
+
+def run_bench(*argv, env=None, timeout=240):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], capture_output=True, text=True,
+                          timeout=timeout, env=e, cwd=ROOT)
+
+
+@pytest.mark.parametrize("world,total", [(2, 1000), (3, 1001)])
+def test_gpus_n_spawns_n_ranks_with_distinct_shards(world, total):
+    r = run_bench("--gpus", str(world), "--stub-cpu", "--steps", "3", "--warmup", "1", "--total-rollouts",
+                  str(total))
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout  # rank 0 prints one JSON line
+    out = json.loads(line[0])
+    assert out["n_gpus"] == world and out["scaling"] == "strong"
+    shards = sorted(out["stub_shards"])
+    assert [s[0] for s in shards] == list(range(world))
+    assert len({s[3] for s in shards}) == world  # one process per rank
+    pos = 0
+    for _, id0, count, _ in shards:  # contiguous, disjoint, covering [0, total)
+        assert id0 == pos and count > 0
+        pos += count
+    assert pos == total
+    # the global winner: the stub's per-cycle COT over ALL rollouts, ties to the lowest id
+    from hslabs_amd import dist as hdist
+    from hslabs_amd import synth
+
+    p = synth.gen_params(total, "hexapod")
+    work = torch.from_numpy(p["period"] * p["step_height"] * (3 / 20))
+    sel = hdist.select_cot(work, torch.from_numpy(p["step_length"]), 22.0, 20, 3).numpy()
+    want = int(np.nanargmin(sel.astype(np.float32)))
+    assert out["best_rollout"]["id"] == want
+    assert abs(p["step_length"][want]) >= 1e-3
+
+
+def test_default_layout_is_configs3_over_ranks():
+    import bench
+
+    a = bench.parse(["--gpus", "8"])
+    lay = [bench.job_layout(a, 8, r) for r in range(8)]
+    assert all(l["cfg"] == "configs[3]" and l["B"] == 32768 and l["scaling"] == "strong" for l in lay)
+    assert [l["id0"] for l in lay] == [32768 * r for r in range(8)]
+    one = bench.job_layout(bench.parse([]), 1, 0)
+    assert one["cfg"] == "configs[1]" and one["B"] == 4096
+    weak = bench.job_layout(bench.parse(["--gpus", "2", "--rollouts", "4096"]), 2, 1)
+    assert weak["scaling"] == "weak" and weak["id0"] == 4096 and weak["B"] == 4096
+
+
+def test_world_size_mismatch_is_an_error():
+    r = run_bench("--gpus", "2", "--stub-cpu", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)

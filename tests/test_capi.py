@@ -101,6 +101,30 @@ def test_torch_key_matches_c_encoding(product):
     assert u == L.hs_best_key_encode(-2.0, 1001)
 
 
+def test_selection_cot_is_per_cycle_with_abs_step_length(product):
+    """hs_best_key_cot (include/hslabs.h) and its torch twin (dist.select_cot) agree bitwise:
+    one cycle's work over sum m * |L|, NaN for gaits under 1e-3 of travel per cycle."""
+    import torch
+
+    from hslabs_amd import dist as hdist
+
+    L = product.capi.load()
+    assert L.hs_best_key_cot(2.0, 22.0, 0.5, 20, 20) == 2.0 / (22.0 * 0.5)
+    assert L.hs_best_key_cot(2.0, 22.0, -0.5, 20, 20) == 2.0 / (22.0 * 0.5)
+    assert L.hs_best_key_cot(20.0, 22.0, 0.5, 20, 200) == 20.0 * (20 / 200) / (22.0 * 0.5)
+    assert np.isnan(L.hs_best_key_cot(2.0, 22.0, 0.0009, 20, 20))
+    assert np.isnan(L.hs_best_key_cot(2.0, 22.0, -0.0009, 20, 20))
+    rng = np.random.default_rng(3)
+    work = rng.uniform(0, 50, 64)
+    sl = rng.uniform(-0.5, 0.5, 64)
+    for steps in (1, 20, 37, 200):
+        got = hdist.select_cot(torch.from_numpy(work), torch.from_numpy(sl), 22.0, 20, steps).numpy()
+        want = np.array([L.hs_best_key_cot(w, 22.0, s, 20, steps) for w, s in zip(work, sl)])
+        assert np.array_equal(got, want, equal_nan=True)
+        got32 = hdist.select_cot(torch.from_numpy(work.astype(np.float32)), torch.from_numpy(sl), 22.0, 20, steps)
+        assert got32.dtype == torch.float32
+
+
 def test_run_argument_validation(product):
     L = product.capi.load()
     m = product.KinematicModel(os.path.join(MODELS, "hexapod.xml"))

@@ -194,12 +194,18 @@ def test_device_batch_best_key(gpu, hmodels):
     b.reset_best()
     b.run(best=True)
     torch.cuda.synchronize()
-    cot = b.work_cot[:, 1].cpu().numpy().astype(np.float32)
+    L = torch.from_numpy(params["step_length"].copy()).to(b.work_cot.device)
+    sel = hdist.select_cot(b.work_cot[:, 0], L, hmodels["hexapod"].total_mass, 20, 20)
     c_kernel, id_kernel = gpu.decode_best_key(int(b.best_key.item()) & 0xFFFFFFFFFFFFFFFF)
-    c_torch, id_torch = hdist.decode(hdist.best_key(b.work_cot[:, 1], 4096))
+    c_torch, id_torch = hdist.decode(hdist.best_key(sel, 4096))
+    cot = sel.cpu().numpy().astype(np.float32)
     ref = int(np.nanargmin(cot))
     assert id_kernel == id_torch == 4096 + ref
     assert c_kernel == c_torch == cot[ref]
+    # one cycle (key_steps = n_t): the selection COT is |reference COT|
+    wc = b.work_cot.cpu().numpy()
+    ok = np.abs(params["step_length"]) >= 1e-3
+    np.testing.assert_array_equal(sel.cpu().numpy()[ok], np.abs(wc[ok, 1]))
 
 
 def test_full_size_properties(gpu, hmodels):

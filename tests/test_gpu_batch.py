@@ -50,11 +50,53 @@ def test_select_best_is_min_key(gpu, hexapod):
     sb = gpu.ShardedBatch(hexapod, params, horizon=20, n_t=20)
     out = sb.run(k0=0)
     L = capi.load()
-    keys = [L.hs_best_key_encode(float(c), i) for i, c in enumerate(out["cot"])]
+    sel = [L.hs_best_key_cot(float(w), hexapod.total_mass, float(l), 20, 20)
+           for w, l in zip(out["work"], params["step_length"])]
+    keys = [L.hs_best_key_encode(c, i) for i, c in enumerate(sel)]
     cot, rid = sb.select_best()
     kmin = min(keys)
     assert rid == kmin & 0xFFFFFFFF
-    assert cot == np.float32(out["cot"][rid])
+    assert cot == np.float32(abs(out["cot"][rid]))
+
+
+def test_select_best_over_a_one_rank_comm(gpu, hexapod):
+    """hs_select_best_comm / hs_comm_reduce_best: the RCCL all-reduce(MIN) of the 8-byte key inside
+    libhslabs, on a communicator of one rank (the one-GPU box); the N-rank layout is the launcher's
+    (tests/test_bench_launcher.py)."""
+    import torch
+
+    from hslabs_amd import synth
+
+    params = synth.gen_params(333, "hexapod")
+    sb = gpu.ShardedBatch(hexapod, params, horizon=20, n_t=20)
+    sb.run(k0=0)
+    comm = gpu.Comm(1, 0, gpu.Comm.unique_id())
+    assert sb.select_best(comm) == sb.select_best()
+    key = torch.tensor([0x0123456789ABCDEF], dtype=torch.int64, device="cuda")
+    comm.reduce_best(key)
+    torch.cuda.synchronize()
+    assert int(key.item()) == 0x0123456789ABCDEF
+    comm.free()
+
+
+def test_batch_run_into_device_buffers(gpu, hexapod):
+    """hs_batch_run_device writes caller-owned device tensors; the same values as host outputs."""
+    import torch
+
+    from hslabs_amd import synth
+
+    params = synth.gen_params(100, "hexapod")
+    sb = gpu.ShardedBatch(hexapod, params, horizon=20, n_t=20)
+    host = sb.run(k0=0, want=("tau", "cf", "flags", "work", "cot"))
+    dev = {"tau": torch.zeros((100, 20, 18), dtype=torch.float64, device="cuda"),
+           "cf": torch.zeros((100, 20, 18), dtype=torch.float64, device="cuda"),
+           "flags": torch.zeros((100, 20), dtype=torch.int32, device="cuda"),
+           "work": torch.zeros(100, dtype=torch.float64, device="cuda"),
+           "cot": torch.zeros(100, dtype=torch.float64, device="cuda")}
+    sb.run_device(dev, k0=0)
+    for k, v in dev.items():
+        got = v.cpu().numpy()
+        assert np.array_equal(got.view(np.uint32) if k == "flags" else got, host[k]), k
 
 
 def test_batch_steps_and_fp32(gpu, hexapod):

@@ -135,5 +135,113 @@ def test_fused_mixed_plan_equals_steps(gpu, hmodels):
     from hslabs_amd import capi
 
     L = capi.load()
-    want = min(L.hs_best_key_encode(float(c), i) for i, c in enumerate(npy(fz.work_cot)[:, 1]))
+    wc = npy(fz.work_cot)
+    want = min(L.hs_best_key_encode(L.hs_best_key_cot(float(wc[i, 0]), models[midx[i]].total_mass,
+                                                      float(params["step_length"][i]), 20, n_calls), i)
+               for i in range(len(midx)))
     assert int(key) == want
+
+
+def host_key(L, work, step_length, mass, n_t, steps, id0=0):
+    return min(L.hs_best_key_encode(L.hs_best_key_cot(float(w), mass, float(l), n_t, steps), id0 + i)
+               for i, (w, l) in enumerate(zip(work, step_length)))
+
+
+def test_best_key_after_the_last_call(gpu, hmodels):
+    """hs_run_steps(n, best) takes the key once, after the last call, over the accumulated work
+    (ADVICE r1): equal to hs_run_calls(n, best)'s key and to the host encoding of the final work."""
+    import torch
+
+    from hslabs_amd import capi, synth
+
+    m = hmodels["hexapod"]
+    p = synth.gen_params(300, "hexapod", id0=50)
+    keys = []
+    for fused in (False, True):
+        b = gpu.DeviceBatch(m, p, n_t=20, horizon=30 if fused else 1, outputs=("tau", "work_cot"),
+                            rollout_id_base=50)
+        b.work_cot.zero_()
+        b.reset_best()
+        if fused:
+            b.run_calls(30, best=True, accumulate=True)
+        else:
+            b.run_steps(30, best=True, accumulate=True)
+        torch.cuda.synchronize()
+        keys.append(int(npy(b.best_key).view(np.uint64)[0]))
+        want = host_key(capi.load(), npy(b.work_cot)[:, 0], p["step_length"], m.total_mass, 20, 30, 50)
+        assert keys[-1] == want
+    assert keys[0] == keys[1]
+
+
+def test_forward_gait_beats_near_zero_backward_gaits(gpu, hmodels, oracle_mod, omodels):
+    """The selection key ranks per-cycle COT with |L| (include/hslabs.h hs_best_key_cot): gaits that
+    barely travel (|L| < 1e-3) are never selected and a slow backward gait no longer wins by a huge
+    negative COT, which the signed COT of player.cpp:269-285 would give it."""
+    import dataclasses
+
+    import torch
+
+    from conftest import PGS_CONFIG, to_oracle_gait
+
+    base = gpu.read_pgs_config(PGS_CONFIG, 8)  # hexapod walking forward, L = 0.5
+    lengths = [-0.0005, 0.0008, -0.01, -0.05, 0.5, 0.3, -0.5]
+    gaits = [dataclasses.replace(base, step_length=L) for L in lengths]
+    m = hmodels["hexapod"]
+    b = gpu.DeviceBatch(m, gaits, n_t=20, horizon=20, outputs=("work_cot",))
+    b.reset_best()
+    b.run(best=True)
+    torch.cuda.synchronize()
+    _, rid = gpu.decode_best_key(int(npy(b.best_key).view(np.uint64)[0]))
+    om = omodels["hexapod"]
+    ref = [oracle_mod.rollout(om, to_oracle_gait(oracle_mod, g), 20, basis=oracle_mod.BASIS_FAST) for g in gaits]
+    per_cycle = [r["work"] / (m.total_mass * abs(L)) if abs(L) >= 1e-3 else np.inf for r, L in zip(ref, lengths)]
+    # the key holds float32 COTs, ties to the lowest id (L = +-0.5 mirror each other's work)
+    assert rid == int(np.argmin(np.array(per_cycle, dtype=np.float32)))
+    assert abs(lengths[rid]) >= 0.05
+    signed = [r["cot"] for r in ref]
+    assert lengths[int(np.argmin(signed))] < 0  # what a signed-COT minimum would have picked
+
+
+def test_fused_more_steps_than_a_launch(gpu, hmodels):
+    """S > CHUNK (ADVICE r1): 300 steps of 200 rollouts run as two fused launches (256 + 44 steps);
+    every row, the work and the key equal the launch-per-step loop bitwise."""
+    import torch
+
+    from hslabs_amd import synth
+
+    m = hmodels["hexapod"]
+    p = synth.gen_params(200, "hexapod", curved=True)
+    S = 300
+    seq = gpu.DeviceBatch(m, p, n_t=20, horizon=1, outputs=("tau", "cf", "flags", "work_cot"))
+    seq.work_cot.zero_()
+    seq.reset_best()
+    rows = {k: [] for k in ("tau", "cf", "flags")}
+    for c in range(S):
+        seq.k0 = c % 20
+        seq.key_steps = S
+        seq.run(best=c == S - 1, accumulate=True)
+        for k in rows:
+            rows[k].append(npy(getattr(seq, k)))
+    fz = gpu.DeviceBatch(m, p, n_t=20, horizon=S, outputs=("tau", "cf", "flags", "work_cot"))
+    fz.work_cot.zero_()
+    fz.reset_best()
+    fz.run_calls(S, best=True, accumulate=True)
+    torch.cuda.synchronize()
+    for k in rows:
+        assert np.array_equal(np.concatenate(rows[k], axis=1), npy(getattr(fz, k))), k
+    assert np.array_equal(npy(seq.work_cot), npy(fz.work_cot))
+    assert np.array_equal(npy(seq.best_key), npy(fz.best_key))
+
+
+def test_best_key_needs_work(gpu, hmodels):
+    """A best key without work_cot is an argument error on every entry point."""
+    import ctypes
+
+    from hslabs_amd import capi, synth
+
+    b = gpu.DeviceBatch(hmodels["hexapod"], synth.gen_params(4, "hexapod"), horizon=2, outputs=("tau",))
+    a = b._args(None, True, True)
+    L = capi.load()
+    assert L.hs_run_calls(hmodels["hexapod"].handle, ctypes.byref(a), 2) != 0
+    assert b"work_cot" in L.hs_last_error()
+    assert L.hs_run_steps(hmodels["hexapod"].handle, ctypes.byref(a), 2, None) != 0

@@ -1,0 +1,200 @@
+"""GPU parity at BASELINE sizes and on the solve paths round 1 left untested.
+
+The oracle is the CPU restatement (oracle/, parity with the reference binary unpinned: SURVEY.md
+8c); its three modes agree with each other to ~1e-12 on every step of these
+batches, full-rank steps included (measured on CPU: fast vs tree <= 3e-12, ortho vs tree <= 5e-13).
+
+Tolerances (written here, per the north_star): fp64 per-joint motor torque |GPU - oracle| <
+1e-6 N*m on EVERY step (the north_star bound) and < 1e-9 * max(1, |tau|) on every step (what the
+kernel achieves: ULPs of the device transcendentals amplified by the 1 / (4 dt^2) stencil); contact
+forces < 1e-8 * max(1, |f|); flags identical (HS_FLAG_GENERAL aside). fp32 (configs[2]): 1e-3 *
+max(1, |tau|) wherever the fp32 run chose the same contact set as the fp64 oracle.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import MODELS, PGS_CONFIG, PGS_IDS, record_to_oracle_gait, to_oracle_gait
+
+pytestmark = pytest.mark.gpu
+
+TAU_REL = 1e-9
+TAU_ABS = 1e-6  # north_star
+CF_REL = 1e-8
+FP32_TOL = 1e-3
+GEN = np.uint32(64)  # HS_FLAG_GENERAL: which solve path ran, not a property of the step
+
+
+@pytest.fixture(scope="module")
+def gpu(product):
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return product
+
+
+@pytest.fixture(scope="module")
+def hmodels(gpu):
+    return {n: gpu.KinematicModel(os.path.join(MODELS, f"{n}.xml")) for n in ("hexapod", "spider", "myant")}
+
+
+def threads():
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(16, int(omp) if omp.isdigit() else (os.cpu_count() or 1)))
+
+
+def npy(t):
+    return t.cpu().numpy()
+
+
+def check_tau(tau, ref, what):
+    scale = np.maximum(1, np.abs(ref).max(axis=-1, keepdims=True))
+    err = np.abs(tau - ref)
+    assert err.max() < TAU_ABS, f"{what}: max |dtau| {err.max():.3e} over the north_star bound"
+    rel = (err / scale).max(axis=-1)
+    assert (rel < TAU_REL).all(), f"{what}: {(rel >= TAU_REL).sum()} steps over {TAU_REL} (max {rel.max():.3e})"
+
+
+def check_cf(cf, ref, what):
+    scale = np.maximum(1, np.abs(ref).max(axis=-1, keepdims=True))
+    rel = (np.abs(cf - ref) / scale).max()
+    assert rel < CF_REL, f"{what}: contact forces off by {rel:.3e}"
+
+
+def fused_cycle(gpu, model, params, solve_mode=0, dtype=None, H=20):
+    """H control steps of every rollout from k0 = 0 (H calls of horizon 1 through hs_run_calls, the
+    bench's path): tau/cf/flags [B][H][...] on the host."""
+    import torch
+
+    b = gpu.DeviceBatch(model, params, n_t=20, k0=0, horizon=H, outputs=("tau", "cf", "flags", "work_cot"),
+                        dtype=dtype)
+    b.solve_mode = solve_mode
+    b.work_cot.zero_()
+    b.run_calls(H, call_horizon=1, best=False, accumulate=True)
+    torch.cuda.synchronize()
+    return {k: npy(getattr(b, k)) for k in ("tau", "cf", "flags", "work_cot")}
+
+
+def test_configs1_full_size_matches_oracle_tree(gpu, hmodels, oracle_mod, omodels):
+    """BASELINE configs[1] at full size: 4096 hexapod rollouts x the 20 steps of a cycle, the bench's
+    fused path, every step against the oracle's tree mode (the same null basis)."""
+    from hslabs_amd import synth
+
+    params = synth.gen_params(4096, "hexapod")
+    g = fused_cycle(gpu, hmodels["hexapod"], params)
+    gaits = [record_to_oracle_gait(oracle_mod, r) for r in params]
+    r = oracle_mod.batch(omodels["hexapod"], gaits, 20, 0, 20, basis=oracle_mod.BASIS_TREE, n_threads=threads())
+    check_tau(g["tau"], r["tau"], "configs[1] vs tree")
+    check_cf(g["cf"], r["cf"], "configs[1] vs tree")
+    assert np.array_equal(g["flags"].astype(np.uint32) & ~GEN, r["flags"])
+    np.testing.assert_allclose(g["work_cot"][:, 0], r["work"], rtol=1e-9, atol=1e-12)
+
+
+def test_configs1_sample_matches_oracle_ortho(gpu, hmodels, oracle_mod, omodels):
+    """256 rollouts of the same batch against the reference-faithful orthonormal null basis (the
+    Q of a QR of B^T that SparseQR spans, ftsolver.cpp:185-202): basis invariance on the GPU."""
+    from hslabs_amd import synth
+
+    params = synth.gen_params(4096, "hexapod")[:256]
+    g = fused_cycle(gpu, hmodels["hexapod"], params)
+    gaits = [record_to_oracle_gait(oracle_mod, r) for r in params]
+    r = oracle_mod.batch(omodels["hexapod"], gaits, 20, 0, 20, basis=oracle_mod.BASIS_ORTHO, n_threads=threads())
+    check_tau(g["tau"], r["tau"], "configs[1] sample vs ortho")
+    check_cf(g["cf"], r["cf"], "configs[1] sample vs ortho")
+    assert np.array_equal(g["flags"].astype(np.uint32) & ~GEN, r["flags"])
+
+
+@pytest.mark.parametrize("sid", PGS_IDS)
+def test_reference_solve_mode_pgs_setups(gpu, hmodels, oracle_mod, omodels, sid):
+    """HS_SOLVE_REFERENCE sends every step through the kernel's Eigen-style FullPivLU threshold
+    loop + ColPivHouseholderQR (ftsolver.cpp:208-232): the same as the oracle's tree mode."""
+    import torch
+
+    p = gpu.read_pgs_config(PGS_CONFIG, sid)
+    name = p.fname.replace(".xml", "")
+    b = gpu.DeviceBatch(hmodels[name], [p], n_t=20, k0=0, horizon=20, outputs=("tau", "cf", "flags", "work_cot"))
+    b.solve_mode = gpu.capi.HS_SOLVE_REFERENCE
+    b.run(best=False)
+    torch.cuda.synchronize()
+    r = oracle_mod.rollout(omodels[name], to_oracle_gait(oracle_mod, p), 20, basis=oracle_mod.BASIS_TREE)
+    flags = npy(b.flags)[0].astype(np.uint32)
+    assert ((flags & GEN) != 0).all(), "every step must take the Eigen-style path"
+    assert np.array_equal(flags & ~GEN, r["flags"] & ~GEN)
+    check_tau(npy(b.tau)[0], r["tau"], f"pgs {sid} reference mode")
+    check_cf(npy(b.cf)[0], r["cf"], f"pgs {sid} reference mode")
+    assert float(npy(b.work_cot)[0, 1]) == pytest.approx(r["cot"], rel=1e-9, abs=1e-12)
+
+
+@pytest.mark.parametrize("name,curved", [("hexapod", False), ("hexapod", True), ("spider", True), ("myant", False)])
+def test_reference_solve_mode_synthetic(gpu, hmodels, oracle_mod, omodels, name, curved):
+    """The Eigen-style path on synthetic batches: 4-6 contacts of a hexapod (k = 12..18, the
+    global-memory workspace), 1-4 of myant (the LDS workspace), rank retries where they occur;
+    the fused path's per-step scratch equals the launch-per-call one bitwise."""
+    import torch
+
+    from hslabs_amd import synth
+
+    params = synth.gen_params(256, name, id0=777, curved=curved)
+    g = fused_cycle(gpu, hmodels[name], params, solve_mode=1)
+    gaits = [record_to_oracle_gait(oracle_mod, r) for r in params]
+    r = oracle_mod.batch(omodels[name], gaits, 20, 0, 20, basis=oracle_mod.BASIS_TREE, n_threads=threads())
+    assert ((g["flags"] & GEN) != 0).all()
+    assert np.array_equal(g["flags"].astype(np.uint32) & ~GEN, r["flags"])
+    check_tau(g["tau"], r["tau"], f"{name} reference mode")
+    check_cf(g["cf"], r["cf"], f"{name} reference mode")
+    seq = gpu.DeviceBatch(hmodels[name], params, n_t=20, k0=0, horizon=20, outputs=("tau", "cf", "flags"))
+    seq.solve_mode = 1
+    seq.run(best=False)
+    torch.cuda.synchronize()
+    assert np.array_equal(npy(seq.tau), g["tau"]) and np.array_equal(npy(seq.cf), g["cf"])
+
+
+def test_full_rank_steps_match_oracle(gpu, hmodels, oracle_mod, omodels):
+    """Steps with one foot down (k = 3): the zeroth-order Gram is full rank, and the reference's
+    comma initializer `m << ntn1*Ny, ntn0*Ry` (ftsolver.cpp:223-224) gets a one-column empty kernel
+    plus a k x k image, k + 1 columns for a k x k matrix: the reference, built without -DNDEBUG
+    (makefile:1), aborts on Eigen's assertion there. The kernel returns the unique least-squares
+    answer and flags the step HS_FLAG_FULL_RANK; the oracle's modes agree on it. Compared here on
+    their own (round 1 excluded them)."""
+    from hslabs_amd import synth
+
+    params = synth.gen_params(1024, "myant")
+    g = fused_cycle(gpu, hmodels["myant"], params)
+    gaits = [record_to_oracle_gait(oracle_mod, r) for r in params]
+    fr = (g["flags"] & 2) != 0
+    assert fr.sum() >= 100, "the batch must contain single-contact steps"
+    for basis in (oracle_mod.BASIS_TREE, oracle_mod.BASIS_FAST):
+        r = oracle_mod.batch(omodels["myant"], gaits, 20, 0, 20, basis=basis, n_threads=threads())
+        assert np.array_equal(fr, (r["flags"] & 2) != 0)
+        check_tau(g["tau"][fr], r["tau"][fr], "full-rank steps")
+        check_cf(g["cf"][fr], r["cf"][fr], "full-rank steps")
+        check_tau(g["tau"], r["tau"], "myant batch")
+
+
+def test_fp32_configs2_matches_fp64_oracle(gpu, hmodels, oracle_mod, omodels):
+    """BASELINE configs[2] (spider, 16384 rollouts x horizon 32, fp32) against the fp64 oracle
+    directly (round 1 compared fp32 only with the fp64 kernel). A foot whose height is within
+    rounding of the contact threshold (rcap + 1e-4) may switch contact sets between precisions; such
+    steps are counted, and must be rare."""
+    import torch
+
+    from hslabs_amd import synth
+
+    B, H = 16384, 32
+    params = synth.gen_params(B, "spider")
+    b = gpu.DeviceBatch(hmodels["spider"], params, n_t=20, k0=0, horizon=H, outputs=("tau", "cf", "flags"),
+                        dtype=torch.float32)
+    b.run(best=False)
+    torch.cuda.synchronize()
+    tau, cf, flags = npy(b.tau).astype(np.float64), npy(b.cf).astype(np.float64), npy(b.flags).astype(np.uint32)
+    gaits = [record_to_oracle_gait(oracle_mod, r) for r in params]
+    r = oracle_mod.batch(omodels["spider"], gaits, 20, 0, H, basis=oracle_mod.BASIS_TREE, n_threads=threads())
+    down32 = (np.abs(cf.reshape(B, H, -1, 3)).max(axis=3) > 0)
+    down64 = (np.abs(r["cf"].reshape(B, H, -1, 3)).max(axis=3) > 0)
+    same = (down32 == down64).all(axis=2) & ((flags & ~GEN) == r["flags"])
+    assert same.mean() > 0.995, f"contact sets differ on {(~same).sum()} of {same.size} steps"
+    scale = np.maximum(1, np.abs(r["tau"]).max(axis=2))
+    err = np.abs(tau - r["tau"]).max(axis=2) / scale
+    assert err[same].max() < FP32_TOL, f"fp32 vs fp64 oracle: {err[same].max():.3e}"
+    assert np.median(err[same]) < 1e-5
