@@ -1876,7 +1876,10 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
   const int i = k0 + 2;  // centre sample of this launch's step
   {
     const int sl = lane / nl, L = lane % nl;
-    if (sl < NS) kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2);
+#ifndef HS_EXP_KIN_FIRST
+#define HS_EXP_KIN_FIRST 0  // timing experiment only: samples below this offset are not computed
+#endif
+    if (sl < NS && sl >= HS_EXP_KIN_FIRST) kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2);
     wave_sync();
   }
   STAMP(2);
