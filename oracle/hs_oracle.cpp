@@ -2202,4 +2202,6 @@ int hso_residuals(const hso_model* m0, const hso_gait* g, int n_t, int step, int
 }  // extern "C"
 
 // closed-loop simulation restatement (same translation unit: uses the model code above)
+#ifndef HSO_FLOPCOUNT
 #include "hs_oracle_sim.cpp"
+#endif

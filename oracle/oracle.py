@@ -173,6 +173,8 @@ def _bind(path):
     L.hso_dynrec_dump.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int,
                                   dp, dp, dp, dp, dp, dp, ip, ip, ip, ip]
     up = ctypes.POINTER(ctypes.c_uint32)
+    if not hasattr(L, "hso_sim_reset"):  # the FLOP-counting build has no simulation part
+        return L
     L.hso_sim_reset.argtypes = [ctypes.c_void_p, dp, dp]
     L.hso_sim_hinges.argtypes = [ctypes.c_void_p, dp, dp, dp]
     L.hso_sim_run.argtypes = [ctypes.c_void_p, dp, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, up, ip,

@@ -1,11 +1,13 @@
 #!/bin/bash
-# PMC passes for hs_rollout_kernel (run under gpurun). One counter group per pass.
+# PMC passes for hs_rollout_kernel (run under gpurun), one counter group per pass, on the bench's
+# own command (default: the driver's, fused launches). tools/pmc_summary.py divides each fused
+# dispatch's counts by the steps it ran (grid / wavefronts per step) and skips the setup-only pass.
 #   PMC_SET=traffic (default: HBM bytes + instruction mix) | diag (stall/i-cache breakdown)
-#   PMC_OUT=<dir under gpurun_out> ; HSLABS_LIB selects a tuning build
+#   PMC_OUT=<dir under gpurun_out>   BENCH_ARGS=<bench.py arguments>
 set -o pipefail
 R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out/${PMC_OUT:-pmc}; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-ARGS="${BENCH_ARGS:---steps 10 --warmup 2 --launch steps} --no-cpu"  # per-step launches: one dispatch = one step of the batch
+ARGS="${BENCH_ARGS:---steps 20 --warmup 5} --no-cpu"
 if [ "${PMC_SET:-traffic}" = diag ]; then
   GROUPS_=("SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH"
            "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_LDS"
@@ -20,6 +22,6 @@ fi
 i=0
 for grp in "${GROUPS_[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 $R/bench.py $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+  timeout -k 10 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 $R/bench.py $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
 echo "pmc done ($OUT)"
