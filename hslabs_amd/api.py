@@ -102,6 +102,56 @@ class KinematicModel:
     def number_of_motor_joints(self) -> int:
         return self.nmj
 
+    def get_mnode(self, i: int) -> dict:
+        """kinematicmodel::get_mnode (model.h:108) as the node's topology record (hs_node_info)."""
+        c = capi.NodeInfoC()
+        capi.check(capi.load().hs_model_get_node(self.handle, i, ctypes.byref(c)), "hs_model_get_node")
+        return {"parent": c.parent, "jtype": c.jtype, "hinge": c.hinge, "foot": c.foot, "limb": c.limb,
+                "kids": list(c.kids[:c.n_kids]), "com": np.array(c.com), "foot_pos": np.array(c.foot_pos),
+                "mass": c.mass}
+
+    # batched per-configuration kinematics (hs_pergen_rec / hs_model_lik / hs_model_fk, host buffers)
+    def pergen_rec(self, params, times) -> np.ndarray:
+        """pergensetup::set_rec (pergen.cpp:225-239) of every gait at every time: [B][n_times][6 + 3 n_limbs]."""
+        arr = params_array(params)
+        t = np.ascontiguousarray(times, dtype=np.float64).reshape(-1)
+        rec = np.zeros((len(arr), len(t), 6 + 3 * self.n_limbs))
+        dp = ctypes.POINTER(ctypes.c_double)
+        capi.check(capi.load().hs_pergen_rec_host(self.handle, arr.ctypes.data_as(ctypes.POINTER(capi.GaitParamsC)),
+                                                  len(arr), t.ctypes.data_as(dp), len(t), rec.ctypes.data_as(dp)),
+                   "hs_pergen_rec_host")
+        return rec
+
+    def set_jvalues_with_lik(self, rec, ignore_reach: bool = False, config=None):
+        """kinematicmodel::set_jvalues_with_lik (model.cpp:354-359) for rows rec [n][6 + 3 n_limbs]:
+        returns (config [n][config_dim], status [n]); raises HSError when a target is out of reach
+        and ignore_reach is off (lik.cpp:321-330)."""
+        r = np.ascontiguousarray(rec, dtype=np.float64).reshape(-1, 6 + 3 * self.n_limbs)
+        n = len(r)
+        q = np.zeros((n, self.config_dim)) if config is None else np.array(config, np.float64).reshape(n, -1)
+        st = np.zeros(n, np.uint32)
+        dp = ctypes.POINTER(ctypes.c_double)
+        capi.check(capi.load().hs_model_lik_host(self.handle, n, r.ctypes.data_as(dp), int(ignore_reach),
+                                                 q.ctypes.data_as(dp), st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))),
+                   "hs_model_lik_host")
+        return q, st
+
+    def recompute_modelnodes(self, config, joints: bool = False):
+        """kinematicmodel::recompute_modelnodes (model.cpp:314-318) for configurations [n][config_dim]:
+        A_ground of every model node as [n][n_parts][3][4] (and the joints' A_ground if joints)."""
+        q = np.ascontiguousarray(config, dtype=np.float64).reshape(-1, self.config_dim)
+        n = len(q)
+        ag = np.zeros((n, self.n_parts, 12))
+        aj = np.zeros((n, self.n_parts, 12)) if joints else None
+        dp = ctypes.POINTER(ctypes.c_double)
+        capi.check(capi.load().hs_model_fk_host(self.handle, n, q.ctypes.data_as(dp), self.config_dim,
+                                                ag.ctypes.data_as(dp), None if aj is None else aj.ctypes.data_as(dp)),
+                   "hs_model_fk_host")
+
+        def rows(a):  # [c * 3 + r] -> [r][c]
+            return a.reshape(n, self.n_parts, 4, 3).transpose(0, 1, 3, 2).copy()
+        return (rows(ag), rows(aj)) if joints else rows(ag)
+
     def __del__(self):
         try:
             if self.handle:

@@ -24,14 +24,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT_DIR, "libhslabs.so")
-SOURCES = ["hs_kernels.hip", "hs_kernels_f32.hip", "hs_sim.hip", "hs_capi.cpp", "hs_model.cpp", "hs_comm.cpp"]
+SOURCES = ["hs_kernels.hip", "hs_kernels_f32.hip", "hs_sim.hip", "hs_config.hip", "hs_capi.cpp", "hs_model.cpp",
+           "hs_comm.cpp"]
 # the best-rollout all-reduce (hs_comm.cpp) links RCCL; under torch the process's librccl.so.1
 # (same SONAME) is the one bound
 LIBS = ["-L/opt/rocm/lib", "-lrccl"]
 VARIANT_DIR = os.path.join(OUT_DIR, "variants")
 HEADERS = ["hs_topo.h", "hs_simtopo.h", "hs_ode.h", "hs_math.h", "hs_internal.h", os.path.join("..", "..", "include", "hslabs.h")]
 ARCH = os.environ.get("HSLABS_ARCH", "gfx950")
-CONTRACT = {"hs_sim.hip": "off"}  # per-source FMA contraction (default: fast)
+CONTRACT = {"hs_sim.hip": "off", "hs_config.hip": "off"}  # per-source FMA contraction (default: fast)
 # per-source scheduler choice, measured (tools/gpu_sweep_libs.sh): the fp32 rollout kernel
 # (4 waves/SIMD, 128 VGPRs) gains 1.4 % with the iterative ILP scheduler; the fp64 rollout
 # kernel and the simulation are fastest with the default one

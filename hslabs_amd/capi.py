@@ -12,7 +12,7 @@ import os
 
 from . import build as _build
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 HS_OK = 0
 HS_FLAG_RANK_RETRY = 1
@@ -39,8 +39,10 @@ EXPORTS = [
     "hs_sim_default_params", "hs_sim_reset", "hs_sim_step", "hs_sim_create", "hs_sim_advance", "hs_sim_get_state",
     "hs_sim_free", "hs_batch_create", "hs_batch_set_params", "hs_batch_run", "hs_batch_run_device", "hs_select_best",
     "hs_batch_best_key_device", "hs_batch_free", "hs_comm_unique_id", "hs_comm_init", "hs_comm_free", "hs_comm_size",
-    "hs_comm_reduce_best", "hs_select_best_comm",
+    "hs_comm_reduce_best", "hs_select_best_comm", "hs_pergen_rec", "hs_pergen_rec_host", "hs_model_lik",
+    "hs_model_lik_host", "hs_model_fk", "hs_model_fk_host", "hs_model_get_node",
 ]
+HS_FLAG_LIK_FAILED = 128
 SIM_BODY_STRIDE = 13
 
 
@@ -77,6 +79,13 @@ class ModelDimsC(ctypes.Structure):
         ("config_dim", ctypes.c_int32), ("n_limbs", ctypes.c_int32), ("lik_kind", ctypes.c_int32),
         ("total_mass", ctypes.c_double), ("rcap", ctypes.c_double),
     ]
+
+
+class NodeInfoC(ctypes.Structure):
+    """hs_node_info."""
+    _fields_ = [(f, ctypes.c_int32) for f in ("parent", "jtype", "hinge", "foot", "limb", "n_kids")] + \
+               [("kids", ctypes.c_int32 * 6), ("com", ctypes.c_double * 3), ("foot_pos", ctypes.c_double * 3),
+                ("mass", ctypes.c_double)]
 
 
 class PdArgsC(ctypes.Structure):
@@ -219,6 +228,14 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_batch_best_key_device.restype = vp
     L.hs_batch_free.argtypes = [vp]
     L.hs_batch_free.restype = None
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    L.hs_pergen_rec.argtypes = [vp, vp, ctypes.c_int32, vp, ctypes.c_int32, vp, vp]
+    L.hs_pergen_rec_host.argtypes = [vp, ctypes.POINTER(GaitParamsC), ctypes.c_int32, dp, ctypes.c_int32, dp]
+    L.hs_model_lik.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int32, vp, vp, vp]
+    L.hs_model_lik_host.argtypes = [vp, ctypes.c_int32, dp, ctypes.c_int32, dp, u32p]
+    L.hs_model_fk.argtypes = [vp, ctypes.c_int32, vp, ctypes.c_int32, vp, vp, vp]
+    L.hs_model_fk_host.argtypes = [vp, ctypes.c_int32, dp, ctypes.c_int32, dp, dp]
+    L.hs_model_get_node.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(NodeInfoC)]
     L.hs_last_error.argtypes = []
     L.hs_last_error.restype = ctypes.c_char_p
     L.hs_abi_version.argtypes = []

@@ -318,6 +318,29 @@ int hs_model_get_dims(hs_model_t m, hs_model_dims* o) {
   return HS_OK;
 }
 
+int hs_model_get_node(hs_model_t m, int32_t i, hs_node_info* o) {
+  if (!m || !o) return fail(HS_E_ARG, "null argument");
+  const hs_topo& t = m->host;
+  if (i < 0 || i >= t.n) return fail(HS_E_ARG, "node index out of range");
+  const hs_node& nd = t.node[i];
+  memset(o, 0, sizeof(*o));
+  o->parent = nd.parent;
+  o->jtype = nd.jtype;
+  o->hinge = nd.hinge;
+  o->foot = nd.foot;
+  o->limb = -1;
+  for (int L = 0; L < t.n_limbs; L++)
+    if (t.limb_child[L] == i) o->limb = L;
+  o->n_kids = nd.nkids;
+  for (int k = 0; k < nd.nkids && k < HS_NODE_MAX_KIDS; k++) o->kids[k] = nd.kids[k];
+  for (int r = 0; r < 3; r++) {
+    o->com[r] = nd.com[r];
+    o->foot_pos[r] = nd.foot >= 0 ? nd.cap[r] : 0.0;
+  }
+  o->mass = t.mass[i];
+  return HS_OK;
+}
+
 int hs_pgs_config_read(const char* path, int setup_id, hs_gait_params* out, char* xml_file, int32_t xml_file_len) {
   if (!path || !out) return fail(HS_E_ARG, "null argument");
   std::string xml, err;
@@ -708,6 +731,138 @@ int hs_run_host(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n
   (void)hipFree(dfl);
   (void)hipFree(dwc);
   return rc;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// per-configuration kinematics (hs_config.hip, hs_kernels.hip)
+// ---------------------------------------------------------------------------
+namespace {
+
+// device scratch of a synchronous host-buffer call: freed on scope exit
+struct dev_buf {
+  void* p = nullptr;
+  hipError_t alloc(size_t bytes) { return bytes ? hipMalloc(&p, bytes) : hipSuccess; }
+  ~dev_buf() { (void)hipFree(p); }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+}  // namespace
+
+extern "C" {
+
+int hs_pergen_rec(hs_model_t m, const hs_gait_params* params, int32_t B, const double* times, int32_t n_times,
+                  double* rec, void* stream) {
+  if (!m) return fail(HS_E_ARG, "null model");
+  if (B < 0 || n_times < 0 || (int64_t)B * n_times > (int64_t(1) << 31)) return fail(HS_E_ARG, "bad batch size");
+  if ((int64_t)B * n_times == 0) return HS_OK;
+  if (!params || !times || !rec) return fail(HS_E_ARG, "null params, times or rec");
+  const hs_topo* d = nullptr;
+  int rc = device_state(m, 0, nullptr, &d, nullptr);
+  if (rc != HS_OK) return rc;
+  int e = hs::launch_pergen_rec(d, params, B, times, n_times, rec, stream);
+  return e ? hip_fail((hipError_t)e, "hs_pergen_rec launch") : HS_OK;
+}
+
+int hs_pergen_rec_host(hs_model_t m, const hs_gait_params* params, int32_t B, const double* times, int32_t n_times,
+                       double* rec) {
+  if (!m) return fail(HS_E_ARG, "null model");
+  if (B < 0 || n_times < 0 || (int64_t)B * n_times > (int64_t(1) << 31)) return fail(HS_E_ARG, "bad batch size");
+  if ((int64_t)B * n_times == 0) return HS_OK;
+  if (!params || !times || !rec) return fail(HS_E_ARG, "null params, times or rec");
+  const size_t len = 6 + 3 * (size_t)m->host.n_limbs, nrec = (size_t)B * n_times * len;
+  dev_buf dp, dt, dr;
+  hipError_t e = dp.alloc((size_t)B * sizeof(hs_gait_params));
+  if (e == hipSuccess) e = dt.alloc((size_t)n_times * sizeof(double));
+  if (e == hipSuccess) e = dr.alloc(nrec * sizeof(double));
+  if (e == hipSuccess) e = hipMemcpy(dp.p, params, (size_t)B * sizeof(hs_gait_params), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dt.p, times, (size_t)n_times * sizeof(double), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "alloc/copy");
+  int rc = hs_pergen_rec(m, dp.as<hs_gait_params>(), B, dt.as<double>(), n_times, dr.as<double>(), nullptr);
+  if (rc != HS_OK) return rc;
+  e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(rec, dr.p, nrec * sizeof(double), hipMemcpyDeviceToHost);
+  return e == hipSuccess ? HS_OK : hip_fail(e, "run/copy back");
+}
+
+int hs_model_lik(hs_model_t m, int32_t n, const double* rec, int32_t ignore_reach, double* config, uint32_t* status,
+                 void* stream) {
+  if (!m) return fail(HS_E_ARG, "null model");
+  if (n < 0 || n > (1 << 30)) return fail(HS_E_ARG, "bad n");
+  if (n == 0) return HS_OK;
+  if (!rec || !config) return fail(HS_E_ARG, "null rec or config");
+  const hs_topo* d = nullptr;
+  int rc = device_state(m, 0, nullptr, &d, nullptr);
+  if (rc != HS_OK) return rc;
+  int e = hs::launch_lik(d, n, rec, ignore_reach, config, status, stream);
+  return e ? hip_fail((hipError_t)e, "hs_model_lik launch") : HS_OK;
+}
+
+int hs_model_lik_host(hs_model_t m, int32_t n, const double* rec, int32_t ignore_reach, double* config,
+                      uint32_t* status) {
+  if (!m) return fail(HS_E_ARG, "null model");
+  if (n < 0 || n > (1 << 30)) return fail(HS_E_ARG, "bad n");
+  if (n == 0) return HS_OK;
+  if (!rec || !config) return fail(HS_E_ARG, "null rec or config");
+  const size_t nrec = (size_t)n * (6 + 3 * (size_t)m->host.n_limbs), ncfg = (size_t)n * m->host.cfg;
+  dev_buf dr, dc, ds;
+  hipError_t e = dr.alloc(nrec * sizeof(double));
+  if (e == hipSuccess) e = dc.alloc(ncfg * sizeof(double));
+  if (e == hipSuccess) e = ds.alloc((size_t)n * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemcpy(dr.p, rec, nrec * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dc.p, config, ncfg * sizeof(double), hipMemcpyHostToDevice);  // kept entries
+  if (e != hipSuccess) return hip_fail(e, "alloc/copy");
+  int rc = hs_model_lik(m, n, dr.as<double>(), ignore_reach, dc.as<double>(), ds.as<uint32_t>(), nullptr);
+  if (rc != HS_OK) return rc;
+  std::vector<uint32_t> st((size_t)n);
+  e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(config, dc.p, ncfg * sizeof(double), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(st.data(), ds.p, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "run/copy back");
+  if (status) std::copy(st.begin(), st.end(), status);
+  for (int32_t i = 0; i < n; i++)
+    if (st[i] & HS_FLAG_LIK_FAILED)
+      return fail(HS_E_ARG, "limb target out of reach in configuration " + std::to_string(i) +
+                                " (lik.cpp:321-330; set ignore_reach to clamp it)");
+  return HS_OK;
+}
+
+int hs_model_fk(hs_model_t m, int32_t n, const double* config, int32_t stride, double* a_ground, double* a_joint,
+                void* stream) {
+  if (!m) return fail(HS_E_ARG, "null model");
+  if (n < 0 || n > (1 << 26)) return fail(HS_E_ARG, "bad n");
+  if (n == 0) return HS_OK;
+  if (!config || !a_ground) return fail(HS_E_ARG, "null config or a_ground");
+  if (stride < m->host.cfg) return fail(HS_E_ARG, "config_stride < config_dim");
+  const hs_topo* d = nullptr;
+  int rc = device_state(m, 0, nullptr, &d, nullptr);
+  if (rc != HS_OK) return rc;
+  int e = hs::launch_fk(d, m->host.n, n, config, stride, a_ground, a_joint, stream);
+  return e ? hip_fail((hipError_t)e, "hs_model_fk launch") : HS_OK;
+}
+
+int hs_model_fk_host(hs_model_t m, int32_t n, const double* config, int32_t stride, double* a_ground,
+                     double* a_joint) {
+  if (!m) return fail(HS_E_ARG, "null model");
+  if (n < 0 || n > (1 << 26)) return fail(HS_E_ARG, "bad n");
+  if (n == 0) return HS_OK;
+  if (!config || !a_ground) return fail(HS_E_ARG, "null config or a_ground");
+  if (stride < m->host.cfg) return fail(HS_E_ARG, "config_stride < config_dim");
+  const size_t ncfg = (size_t)n * stride, na = (size_t)n * m->host.n * 12;
+  dev_buf dc, dg, dj;
+  hipError_t e = dc.alloc(ncfg * sizeof(double));
+  if (e == hipSuccess) e = dg.alloc(na * sizeof(double));
+  if (e == hipSuccess && a_joint) e = dj.alloc(na * sizeof(double));
+  if (e == hipSuccess) e = hipMemcpy(dc.p, config, ncfg * sizeof(double), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "alloc/copy");
+  int rc = hs_model_fk(m, n, dc.as<double>(), stride, dg.as<double>(), dj.as<double>(), nullptr);
+  if (rc != HS_OK) return rc;
+  e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(a_ground, dg.p, na * sizeof(double), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && a_joint) e = hipMemcpy(a_joint, dj.p, na * sizeof(double), hipMemcpyDeviceToHost);
+  return e == hipSuccess ? HS_OK : hip_fail(e, "run/copy back");
 }
 
 double hs_best_key_cot(double work, double total_mass, double step_length, int32_t n_t, int32_t steps) {

@@ -70,6 +70,15 @@ int launch_fused_reduce(const hs_run_args& a, double total_mass, const double* r
 int launch_fused_reduce_f32(const hs_run_args& a, double total_mass, const double* rollout_mass,
                             const void* work_steps, int32_t n_steps);
 
+// pergensetup::set_rec for n_rollouts x n_times items (hs_kernels.hip), rec [B][n_times][6 + 3 n_limbs]
+int launch_pergen_rec(const hs_topo* d_topo, const hs_gait_params* params, int32_t n_rollouts, const double* times,
+                      int32_t n_times, double* rec, void* stream);
+// per-configuration kinematics (hs_config.hip): recompute_modelnodes and set_jvalues_with_lik
+int launch_fk(const hs_topo* d_topo, int32_t n_parts, int32_t n_cfg, const double* config, int32_t stride,
+              double* a_ground, double* a_joint, void* stream);
+int launch_lik(const hs_topo* d_topo, int32_t n_cfg, const double* rec, int32_t ignore_reach, double* config,
+               uint32_t* status, void* stream);
+
 // closed-loop simulation kernels (hs_sim.hip); return hipError_t values
 int launch_sim_reset(const hs_topo* d_topo, const hs_simtopo* d_sim, int32_t n_rollouts, const double* config,
                      int32_t config_stride, double* body, int32_t precision, void* stream);

@@ -391,20 +391,15 @@ __device__ __attribute__((always_inline)) inline void node_features(const hs_top
   }
 }
 
-template <class W>
-__device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, int isample, int L,
-                           bool ignore_reach, const W& w, int k) {
-  const int j = T->limb_pergen[L];
-  const int ysign = T->limb_ysign[L];
-  const int clen = T->limb_chain_len[L];
-  const int lv[3] = {T->limb_node[L][0], T->limb_node[L][1], T->limb_node[L][2]};
-  real t = 0;  // t accumulates dt (periodic.cpp:171-181)
-  for (int i = 0; i < isample; i++) t += st.dt;
-  // pergensetup::set_rec -> turn_torso (pergen.cpp:386-397)
-  real o0[3] = {g.torso_pos[0], g.torso_pos[1], g.torso_pos[2]};
-  real o1[3] = {g.torso_angles[0], g.torso_angles[1], g.torso_angles[2]};
+// pergensetup::set_rec at time t for lik limb L (pergen.cpp:225-239): torso position o0 and Euler
+// angles o1 (turn_torso, pergen.cpp:386-397; `turned` when the torso frame was rotated), and the
+// limb's foot target (limb_positions of its pergen index, pergen.cpp:82-94, 160-183)
+__device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g, const SetupL& st, real t, int j,
+                                                                  real* o0, real* o1, bool& turned, real* target) {
+  o0[0] = g.torso_pos[0]; o0[1] = g.torso_pos[1]; o0[2] = g.torso_pos[2];
+  o1[0] = g.torso_angles[0]; o1[1] = g.torso_angles[1]; o1[2] = g.torso_angles[2];
   real tv = t * st.v;
-  bool turned = false;
+  turned = false;
   real psi = 0;
   if (g.curvature != 0) {
     int s = (g.curvature > 0) ? 1 : -1;
@@ -425,39 +420,50 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
     euler_from(A1, o1);
   }
   // periodicgenerator::limb_positions for this limb's pergen index (pergen.cpp:82-94)
-  real target[3];
-  {
-    real tt = t / g.period;
-    int t_int = int(tt);
-    real t_frac = tt - t_int;
-    real t_lift = st.ts[j], stepf;
-    if (t_frac < t_lift) stepf = 0;
-    else if (t_frac < t_lift + st.t_step) stepf = (t_frac - t_lift) / st.t_step;
-    else stepf = 1;
-    real sx, sz;
-    step_profiles(stepf, sx, sz);
-    real dx = (t_int + st.xs[j] + sx) * g.step_length;
-    real dy = 0;
-    real dz = sz * g.step_height;
-    if (g.curvature != 0) {  // turn_position (pergen.cpp:160-183)
-      int s = (g.curvature > 0) ? 1 : -1;
-      real x0 = st.pos0[j][0], y0 = st.pos0[j][1];
-      real rc = real(1) / g.curvature;
-      real rx = x0, ry = y0 - rc;
-      real r = sqrt(rx * rx + ry * ry);
-      real alpha = atan2(ry, rx);
-      real beta = -s * dx / st.max_radius;
-      real gamma = alpha - beta / 2;
-      real sb = 2 * sin(beta / 2);
-      real sg, cg;
-      sincos(gamma, &sg, &cg);
-      dx = r * sg * sb;
-      dy += -r * cg * sb;
-    }
-    target[0] = dx + st.pos0[j][0];
-    target[1] = dy + st.pos0[j][1];
-    target[2] = dz + st.pos0[j][2];
+  real tt = t / g.period;
+  int t_int = int(tt);
+  real t_frac = tt - t_int;
+  real t_lift = st.ts[j], stepf;
+  if (t_frac < t_lift) stepf = 0;
+  else if (t_frac < t_lift + st.t_step) stepf = (t_frac - t_lift) / st.t_step;
+  else stepf = 1;
+  real sx, sz;
+  step_profiles(stepf, sx, sz);
+  real dx = (t_int + st.xs[j] + sx) * g.step_length;
+  real dy = 0;
+  real dz = sz * g.step_height;
+  if (g.curvature != 0) {  // turn_position (pergen.cpp:160-183)
+    int s = (g.curvature > 0) ? 1 : -1;
+    real x0 = st.pos0[j][0], y0 = st.pos0[j][1];
+    real rc = real(1) / g.curvature;
+    real rx = x0, ry = y0 - rc;
+    real r = sqrt(rx * rx + ry * ry);
+    real alpha = atan2(ry, rx);
+    real beta = -s * dx / st.max_radius;
+    real gamma = alpha - beta / 2;
+    real sb = 2 * sin(beta / 2);
+    real sg, cg;
+    sincos(gamma, &sg, &cg);
+    dx = r * sg * sb;
+    dy += -r * cg * sb;
   }
+  target[0] = dx + st.pos0[j][0];
+  target[1] = dy + st.pos0[j][1];
+  target[2] = dz + st.pos0[j][2];
+}
+
+template <class W>
+__device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, int isample, int L,
+                           bool ignore_reach, const W& w, int k) {
+  const int j = T->limb_pergen[L];
+  const int ysign = T->limb_ysign[L];
+  const int clen = T->limb_chain_len[L];
+  const int lv[3] = {T->limb_node[L][0], T->limb_node[L][1], T->limb_node[L][2]};
+  real t = 0;  // t accumulates dt (periodic.cpp:171-181)
+  for (int i = 0; i < isample; i++) t += st.dt;
+  real o0[3], o1[3], target[3];
+  bool turned;
+  gait_record(g, st, t, j, o0, o1, turned, target);
   STAMP(20);
   // set_jvalues_with_lik: torso + body chain FK, then limb IK (model.cpp:354-359, lik.cpp:89-99)
   real q6[6] = {o0[0], o0[1], o0[2], o1[0], o1[1], o1[2]};
@@ -1908,6 +1914,37 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
   }
 }
 
+#if !HS_REAL_IS_FLOAT
+// pergensetup::set_rec (pergen.cpp:225-239) after setup_pergen (pergen.cpp:453-507), for
+// n_rollouts x n_times (rollout, time) items, two per wavefront: the gait setup of the item's
+// rollout on its half-wave, then lane L < n_limbs writes lik limb L's foot target, lane 0 the
+// torso position and angles. rec rows: [torso_pos(3), torso_angles(3), foot targets (3 n_limbs)].
+__global__ __launch_bounds__(WAVE) void hs_pergen_rec_kernel(const hs_topo* __restrict__ T,
+                                                             const hs_gait_params* __restrict__ params,
+                                                             int32_t n_rollouts, const double* __restrict__ times,
+                                                             int32_t n_times, double* __restrict__ rec) {
+  __shared__ SetupL st[2];
+  const int sub = threadIdx.x / HALF, lane = threadIdx.x % HALF;
+  const int64_t n_items = (int64_t)n_rollouts * n_times;
+  const int64_t item = (int64_t)blockIdx.x * 2 + sub;
+  const bool live = item < n_items;
+  const int64_t it = live ? item : n_items - 1;  // an idle half computes its neighbour's item, stores nothing
+  const int b = (int)(it / n_times), ti = (int)(it % n_times);
+  const GaitR g = load_gait(params[b]);
+  gait_setup(T, g, 1, st[sub], lane);  // every lane of the wave takes part (wave_sync inside)
+  const int nl = T->n_limbs;
+  if (live && lane < nl) {
+    real o0[3], o1[3], target[3];
+    bool turned;
+    gait_record(g, st[sub], (real)times[ti], T->limb_pergen[lane], o0, o1, turned, target);
+    double* r = rec + it * (6 + 3 * nl);
+    if (lane == 0)
+      for (int i = 0; i < 3; i++) { r[i] = o0[i]; r[3 + i] = o1[i]; }
+    for (int i = 0; i < 3; i++) r[6 + 3 * lane + i] = target[i];
+  }
+}
+#endif
+
 }  // namespace
 
 #if defined(HS_STAMPS) && !HS_REAL_IS_FLOAT
@@ -1928,6 +1965,15 @@ namespace hs {
 size_t general_workspace_bytes_f32() { return sizeof(RolloutWS); }
 #else
 size_t general_workspace_bytes() { return sizeof(RolloutWS); }
+
+int launch_pergen_rec(const hs_topo* d_topo, const hs_gait_params* params, int32_t n_rollouts, const double* times,
+                      int32_t n_times, double* rec, void* stream) {
+  const int64_t items = (int64_t)n_rollouts * n_times;
+  if (items <= 0) return 0;
+  hipLaunchKernelGGL(hs_pergen_rec_kernel, dim3((unsigned)((items + 1) / 2)), dim3(WAVE), 0, (hipStream_t)stream,
+                     d_topo, params, n_rollouts, times, n_times, rec);
+  return (int)hipGetLastError();
+}
 #endif
 
 template <int NM>

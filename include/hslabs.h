@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 8
+#define HSLABS_ABI_VERSION 9
 
 enum {
   HS_OK = 0,
@@ -81,6 +81,25 @@ int hs_model_load(const char* xml_path, hs_model_t* out);
 int hs_model_load_ex(const char* xml_path, int lik_variant, hs_model_t* out);
 void hs_model_free(hs_model_t model);
 int hs_model_get_dims(hs_model_t model, hs_model_dims* out);
+
+/* One model node (modelnode, model.h:64-86; kinematicmodel::get_mnode, model.h:108), nodes in XML
+ * preorder (the order of mnodes, odeparts and dynparts). */
+#define HS_NODE_MAX_KIDS 6
+typedef struct {
+  int32_t parent;     /* get_parent() index, -1 for the root */
+  int32_t jtype;      /* get_joint()->get_type(): -1 no joint (ODE fixed joint), 0 free6, 1 hinge (model.h:26) */
+  int32_t hinge;      /* hinge: motor index, its value at configuration index 6 + hinge; else -1 */
+  int32_t foot;       /* foot index (periodic::get_nfeet order, periodic.cpp:34-58), else -1 */
+  int32_t limb;       /* lik limb whose top link this node is (liklimb::child, lik.cpp:295-301), else -1 */
+  int32_t n_kids;
+  int32_t kids[HS_NODE_MAX_KIDS]; /* child_nodes in order (get_first_child = kids[0]) */
+  double com[3];      /* odepart body position in the node frame (A_body_geom translation,
+                         visualization.cpp:541-545) */
+  double foot_pos[3]; /* foot: capsule end in the node frame (odepart::get_foot_pos,
+                         visualization.cpp:553-568); else 0 */
+  double mass;        /* dBodyGetMass (dynpart::set_inertial_params, dynrec.cpp:62-68) */
+} hs_node_info;
+int hs_model_get_node(hs_model_t model, int32_t i, hs_node_info* out);
 
 /* Replaces modelplayer::get_rec_str + get_pgs_config_params (player.cpp:170-244):
  * reads line `setup_id` of a pgs_config.txt. xml_file receives the model name. */
@@ -236,6 +255,56 @@ int hs_complete_traj(hs_model_t model, const hs_gait_params* params, int32_t n_r
 /* save_2d_array (core.cpp:46-61): n_rows rows of rec_len doubles, space
  * separated, default ostream formatting, appended when append != 0. */
 int hs_traj_save(const char* path, const double* rec, int32_t n_rows, int32_t rec_len, int32_t append);
+
+/*
+ * Per-configuration kinematics: the kinematicmodel / pergensetup entry points every caller
+ * outside periodic binds (model.h:122-130, pergen.h:68-108; player.cpp:69, 122, 354,
+ * ghost.cpp:53-54, periodic.cpp:89-90), for batches of n configurations. DEVICE arrays on the
+ * current HIP device, asynchronous on stream (a hipStream_t, NULL = default stream); the _host
+ * forms take host arrays and are synchronous. fp64 only.
+ */
+/* Row length of a trajectory record: torso position and Euler angles, then the foot position of
+ * every limb in lik order (liksolver::place_limbs, lik.cpp:87-99; pergensetup::set_rec,
+ * pergen.cpp:220-239). = 6 + 3 * n_limbs = config_dim for the shipped models. */
+#define HS_REC_LEN(dims) (6 + 3 * (dims).n_limbs)
+
+/* pergensetup::set_rec (pergen.cpp:225-239) after pgssweeper::setup_pergen (pergen.cpp:453-507):
+ * rec[b][i] = the record of rollout b's gait at time times[i] (t in the units of period), for
+ * n_rollouts x n_times items. params [n_rollouts], times [n_times], rec [B][n_times][rec_len]. */
+int hs_pergen_rec(hs_model_t model, const hs_gait_params* params, int32_t n_rollouts, const double* times,
+                  int32_t n_times, double* rec, void* stream);
+int hs_pergen_rec_host(hs_model_t model, const hs_gait_params* params, int32_t n_rollouts, const double* times,
+                       int32_t n_times, double* rec);
+
+#define HS_FLAG_LIK_FAILED 128u /* hs_model_lik status: a foot target out of reach with ignore_reach = 0
+                                   (the reference prints the limb and exits, lik.cpp:321-330); the
+                                   limb's angles are then NaN */
+#define HS_LIK_LIMB_BIT(L) (1u << (16 + (L))) /* hs_model_lik status: limb L's target was out of reach */
+/* kinematicmodel::set_jvalues_with_lik (model.cpp:354-359 -> liksolver::place_limbs,
+ * lik.cpp:89-99, liklimb::place_limb / poslimb, lik.cpp:316-347): rec [n][rec_len] -> config
+ * [n][config_dim] (joint values in get_jvalues order, model.cpp:368-372). Only the torso's six
+ * values and the limbs' hinge values are written; other entries keep what config held (the
+ * reference leaves the other joint values as they were). ignore_reach as
+ * liksolver::set_ignore_reach_flag (lik.cpp:142-147): a target beyond reach is clamped to the
+ * stretched limb (status HS_FLAG_UNREACH); without it status gets HS_FLAG_LIK_FAILED; either way
+ * HS_LIK_LIMB_BIT(L) names the limb. status [n] may be NULL. The host form returns HS_E_ARG when any row failed (after writing all rows). */
+int hs_model_lik(hs_model_t model, int32_t n, const double* rec, int32_t ignore_reach, double* config,
+                 uint32_t* status, void* stream);
+int hs_model_lik_host(hs_model_t model, int32_t n, const double* rec, int32_t ignore_reach, double* config,
+                      uint32_t* status);
+
+/* kinematicmodel::recompute_modelnodes (model.cpp:314-318; modelnode::recompute_A_ground,
+ * model.cpp:183-201) for n configurations config [n][config_stride] (config_stride >=
+ * config_dim): the ground transform of every model node, get_mnode(i)->get_A_ground()
+ * (model.h:73, 108), into a_ground [n][n_parts][12], and of every node's joint,
+ * get_joint()->get_A_ground() (model.h:45), into a_joint [n][n_parts][12] (may be NULL; zeros
+ * for a node without a joint). Each transform is the 3x4 top of the reference's column-major 4x4
+ * affine (matrix.h:27-28): element (row r, column c) at [c * 3 + r], c = 3 the translation. Node
+ * order = model nodes in XML preorder (kinematicmodel::mnodes). */
+int hs_model_fk(hs_model_t model, int32_t n, const double* config, int32_t config_stride, double* a_ground,
+                double* a_joint, void* stream);
+int hs_model_fk_host(hs_model_t model, int32_t n, const double* config, int32_t config_stride, double* a_ground,
+                     double* a_joint);
 
 /* Best-rollout key: (order-preserving bits of (float)c) << 32 | (uint32)rollout id, where c is
  * the selection COT of hs_best_key_cot. NaN maps to the largest key (never selected); ties go to

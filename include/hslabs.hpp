@@ -2,7 +2,15 @@
 // call shapes for the hot path, so player.cpp-style callers switch by changing
 // includes. Header-only; link with -lhslabs.
 //
-//   kinematicmodel::load_fromxml / get_config_dim / number_of_motor_joints  (model.h:96-137)
+//   kinematicmodel::load_fromxml / get_config_dim / number_of_motor_joints /
+//            get_mnode / get_joint_values / get_lik / recompute_modelnodes /
+//            set_jvalues_with_lik / set_jvalues / get_jvalues / orient_torso /
+//            get_foot_mnodes                                               (model.h:96-137)
+//   modelnode / modeljoint (read side), affine / extvec (read side)        (model.h:34-86, matrix.h)
+//   liksolver::place_limbs / place_limb / get_limb_hip_pos /
+//            set_ignore_reach_flag / get_number_of_limbs                   (lik.h, lik.cpp:82-146)
+//   pergensetup::set_rec                                                   (pergen.cpp:225-239)
+//   arrayops, str_to_val                                                   (core.h:13, 27-48)
 //   pgsconfigparams                                                        (pergen.h:137-146)
 //   pergensetup (setup parameters of one gait)                             (pergen.h:68-108)
 //   periodic::record_trajectory / compute_dynrecs / compute_dynrec_ders /
@@ -27,10 +35,13 @@
 #ifndef HSLABS_HPP
 #define HSLABS_HPP
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <set>
+#include <sstream>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -68,23 +79,177 @@ inline void save_2d_array(double** a, int n, int m, const std::string& fname, bo
   }
 }
 
+// core.h:13 (core.cpp:8-12): reads whitespace-separated doubles from str into val until one
+// fails to parse
+inline void str_to_val(const char* str, double* val) {
+  std::istringstream in(str ? str : "");
+  double d;
+  while (in >> d) *val++ = d;
+}
+
+// core.h:27-48: arithmetic on double arrays of length n
+class arrayops {
+  int n_ = 0;
+  std::vector<double> tmp_;
+
+ public:
+  arrayops() {}
+  explicit arrayops(int n) : n_(n) {}
+  void set_n(int n) { n_ = n; tmp_.clear(); }
+  void print(const double* a) const {
+    for (int i = 0; i < n_; i++) std::cout << (i ? " " : "") << a[i];
+    std::cout << std::endl;
+  }
+  void assign(double* a, const double* a1) const { std::copy(a1, a1 + n_, a); }
+  double* add(double* a, const double* a1) const { for (int i = 0; i < n_; i++) a[i] += a1[i]; return a; }
+  double* subtract(double* a, const double* a1) const { for (int i = 0; i < n_; i++) a[i] -= a1[i]; return a; }
+  double* times(double* a, double b) const { for (int i = 0; i < n_; i++) a[i] *= b; return a; }
+  // period-b wrap into (-b/2, b/2] of arguments in (-3b/2, 3b/2] (core.cpp:120-131)
+  double* modulus(double* a, double b) const {
+    const double bh = b / 2;
+    for (int i = 0; i < n_; i++) {
+      if (a[i] > bh) a[i] -= b;
+      else if (a[i] <= -bh) a[i] += b;
+    }
+    return a;
+  }
+  double dot(const double* a, const double* a1) const {
+    double s = 0;
+    for (int i = 0; i < n_; i++) s += a[i] * a1[i];
+    return s;
+  }
+  double norm(const double* a) const { return std::sqrt(dot(a, a)); }
+  double distance(const double* a, const double* a1) {
+    tmp_.assign(a, a + n_);
+    subtract(tmp_.data(), a1);
+    return norm(tmp_.data());
+  }
+  void assign_scalar(double* a, double b) const { std::fill(a, a + n_, b); }
+  double l1_norm(const double* a) const {
+    double s = 0;
+    for (int i = 0; i < n_; i++) s += std::fabs(a[i]);
+    return s;
+  }
+  double** new_2d_array(int m) const { return hslabs::new_2d_array(m, n_); }
+  void delete_2d_array(double** a, int m) const { hslabs::delete_2d_array(a, m); }
+};
+
+// matrix.h:57-88 (the part callers of the kinematic model use): a point (x, y, z, 1)
+class extvec {
+  double v_[4] = {0, 0, 0, 1};
+
+ public:
+  extvec() {}
+  extvec(double x, double y, double z) { set(x, y, z); }
+  void set(double x, double y, double z) { v_[0] = x; v_[1] = y; v_[2] = z; }
+  void set(const double* a) { set(a[0], a[1], a[2]); }
+  void set_v(int i, double val) { v_[i] = val; }
+  double get_v(int i) const { return v_[i]; }
+  double* get_data() { return v_; }
+  const double* get_data() const { return v_; }
+  void get_components(double& x, double& y, double& z) const { x = v_[0]; y = v_[1]; z = v_[2]; }
+  void get_components(double* p) const { std::copy(v_, v_ + 3, p); }
+  void print() const { std::cout << v_[0] << " " << v_[1] << " " << v_[2] << std::endl; }
+};
+
+// matrix.h:16-55 (read side): a rigid transform [rot, transl; 0 0 0 1], stored column-wise in 16
+// doubles like the reference, so get_data() + 8 is the z axis (dynrec.cpp:84-93)
+class affine {
+  double a_[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+
+ public:
+  double* get_data() { return a_; }
+  const double* get_data() const { return a_; }
+  double get_a(int i, int j) const { return a_[4 * j + i]; }
+  void get_translation(extvec& t) const { t.set(a_[12], a_[13], a_[14]); }
+  // u = A (v, 1) (matrix.cpp:149-164)
+  void mult(const extvec& v, extvec& u) const {
+    double r[3];
+    for (int i = 0; i < 3; i++) {
+      double s = 0;
+      for (int k = 0; k < 3; k++) s += a_[4 * k + i] * v.get_v(k);
+      r[i] = s + a_[12 + i];
+    }
+    u.set(r);
+  }
+  // from the ABI's 3x4 column-major block ([c * 3 + r])
+  void set_from34(const double* m) {
+    for (int c = 0; c < 4; c++) {
+      for (int r = 0; r < 3; r++) a_[4 * c + r] = m[3 * c + r];
+      a_[4 * c + 3] = (c == 3) ? 1.0 : 0.0;
+    }
+  }
+  void print() const {
+    for (int i = 0; i < 4; i++) {
+      for (int j = 0; j < 4; j++) std::cout << (j ? " " : "") << get_a(i, j);
+      std::cout << std::endl;
+    }
+  }
+};
+
+enum joint_type { free6, hinge, slider };  // model.h:26
+
+class kinematicmodel;
+
+// model.h:34-51 (read side): the joint of a model node, its values and ground frame
+class modeljoint {
+  friend class kinematicmodel;
+  joint_type type_ = hinge;
+  affine A_ground_;
+  double* values_ = nullptr;
+
+ public:
+  double* get_values() { return values_; }
+  affine* get_A_ground() { return &A_ground_; }
+  joint_type get_type() const { return type_; }
+};
+
+// model.h:64-86 (read side)
+class modelnode {
+  friend class kinematicmodel;
+  affine A_ground_;
+  modeljoint joint_;
+  bool has_joint_ = false;
+  modelnode* parent_ = nullptr;
+  std::vector<modelnode*> kids_;
+  hs_node_info info_{};
+
+ public:
+  const affine* get_A_ground() const { return &A_ground_; }
+  modeljoint* get_joint() const { return has_joint_ ? const_cast<modeljoint*>(&joint_) : nullptr; }
+  modelnode* get_first_child() const { return kids_.empty() ? nullptr : kids_.front(); }
+  modelnode* get_parent() const { return parent_; }
+  const std::vector<modelnode*>& get_child_nodes() const { return kids_; }
+  // hs_node_info: odepart positions (com, foot capsule end), mass, foot / limb / motor indices
+  const hs_node_info& info() const { return info_; }
+};
+
+// lik.cpp:142: one process-wide flag, like the reference's global ignore_reach_flag
+inline bool& lik_ignore_reach_flag() {
+  static bool flag = false;
+  return flag;
+}
+
+class liksolver;
+
+// kinematicmodel (model.h:96-137): the per-configuration API runs on the GPU through hs_model_lik /
+// hs_model_fk (one configuration per call here; the ABI takes batches)
 class kinematicmodel {
   hs_model_t h_ = nullptr;
   hs_model_dims d_{};
   std::string xmlfname_;
+  mutable std::vector<double> jv_;       // joint_values (model.h:100), get_jvalues order
+  std::vector<double*> jv_ptrs_;
+  mutable std::vector<modelnode> nodes_;  // mnodes, XML preorder
+  liksolver* lik_ = nullptr;
 
  public:
   explicit kinematicmodel(bool /*vis_flag*/ = false) {}
-  ~kinematicmodel() { hs_model_free(h_); }
+  ~kinematicmodel();
   kinematicmodel(const kinematicmodel&) = delete;
   kinematicmodel& operator=(const kinematicmodel&) = delete;
-  void load_fromxml(const std::string& fname, int lik_variant = -1) {
-    hs_model_free(h_);
-    h_ = nullptr;
-    check(hs_model_load_ex(fname.c_str(), lik_variant, &h_), "load_fromxml");
-    check(hs_model_get_dims(h_, &d_), "hs_model_get_dims");
-    xmlfname_ = fname;
-  }
+  // model.cpp:224-242: load, build the node tree, recompute_modelnodes
+  void load_fromxml(const std::string& fname, int lik_variant = -1);
   bool if_loaded() const { return h_ != nullptr; }
   std::string get_xmlfname() const { return xmlfname_; }
   int get_config_dim() const { return d_.config_dim; }
@@ -93,7 +258,132 @@ class kinematicmodel {
   int number_of_feet() const { return d_.nfeet; }
   double total_mass() const { return d_.total_mass; }
   hs_model_t handle() const { return h_; }
+  // model.h:108-111
+  const modelnode* get_mnode(int i) const { return &nodes_.at((size_t)i); }
+  std::vector<double*>* get_joint_values() { return &jv_ptrs_; }
+  const liksolver* get_lik() const { return lik_; }
+  // model.cpp:314-318: every node's A_ground (and its joint's) from the current joint values
+  void recompute_modelnodes() const {
+    std::vector<double> ag((size_t)d_.n_parts * 12), aj((size_t)d_.n_parts * 12);
+    check(hs_model_fk_host(h_, 1, jv_.data(), d_.config_dim, ag.data(), aj.data()), "recompute_modelnodes");
+    for (size_t i = 0; i < nodes_.size(); i++) {
+      nodes_[i].A_ground_.set_from34(&ag[12 * i]);
+      nodes_[i].joint_.A_ground_.set_from34(&aj[12 * i]);
+    }
+  }
+  // model.cpp:354-359: torso values from rec, recompute_modelnodes, then liksolver::place_limbs
+  // (lik.cpp:89-99) with the foot positions rec[6 ..]; throws where the reference exits
+  // (lik.cpp:321-330)
+  void set_jvalues_with_lik(const double* rec) const {
+    std::copy(rec, rec + 6, jv_.begin());
+    recompute_modelnodes();
+    place_limbs(rec + 6);
+  }
+  // model.cpp:361-372
+  void set_jvalues(const double* values) const { std::copy(values, values + d_.config_dim, jv_.begin()); }
+  void get_jvalues(double* values) const { std::copy(jv_.begin(), jv_.end(), values); }
+  // model.cpp:403-409
+  void orient_torso(const extvec* orientation) const {
+    for (int i = 0; i < 2; i++)
+      for (int j = 0; j < 3; j++) jv_[(size_t)(3 * i + j)] = orientation[i].get_v(j);
+    recompute_modelnodes();
+  }
+  // model.cpp:411-420: the feet's model nodes
+  void get_foot_mnodes(std::set<modelnode*>& foot_set) const {
+    for (modelnode& n : nodes_)
+      if (n.info_.foot >= 0) foot_set.insert(&n);
+  }
+  // liksolver::place_limbs on this model: the limb values for foot positions feet[3 * n_limbs]
+  // in the ground frame, from the torso's current values (rows of hs_model_lik). only_limb >= 0
+  // sets that limb's values alone (liksolver::place_limb, lik.cpp:82-85; the other rows of feet
+  // are then ignored). A target out of reach throws unless lik_ignore_reach_flag() (where the
+  // reference prints the limb and exits, lik.cpp:321-330).
+  void place_limbs(const double* feet, int only_limb = -1) const {
+    std::vector<double> rec(6 + 3 * (size_t)d_.n_limbs), q(jv_);
+    std::copy(jv_.begin(), jv_.begin() + 6, rec.begin());
+    std::copy(feet, feet + 3 * d_.n_limbs, rec.begin() + 6);
+    uint32_t status = 0;
+    check(hs_model_lik_host(h_, 1, rec.data(), 1, q.data(), &status), "place_limbs");
+    for (int L = 0; L < d_.n_limbs; L++) {
+      if (only_limb >= 0 && L != only_limb) continue;
+      if ((status & HS_LIK_LIMB_BIT(L)) && !lik_ignore_reach_flag())
+        throw error(HS_E_ARG, "place_limbs: the target of limb " + std::to_string(L) + " is out of reach");
+    }
+    if (only_limb < 0) {
+      jv_ = q;
+      return;
+    }
+    const modelnode* n = nullptr;
+    for (const modelnode& c : nodes_)
+      if (c.info_.limb == only_limb) n = &c;
+    for (int k = 0; k < 3 && n; k++, n = n->get_first_child()) jv_[6 + (size_t)n->info_.hinge] = q[6 + (size_t)n->info_.hinge];
+  }
 };
+
+// liksolver (lik.h:27-58, the caller-facing part), over its kinematicmodel
+class liksolver {
+  const kinematicmodel* model_;
+  std::vector<const modelnode*> limb_child_;
+
+ public:
+  explicit liksolver(const kinematicmodel* model) : model_(model) {
+    for (int i = 0; i < model->number_of_parts(); i++)
+      if (model->get_mnode(i)->info().limb >= 0) {
+        const int L = model->get_mnode(i)->info().limb;
+        if ((int)limb_child_.size() <= L) limb_child_.resize((size_t)L + 1);
+        limb_child_[(size_t)L] = model->get_mnode(i);
+      }
+  }
+  int get_number_of_limbs() const { return (int)limb_child_.size(); }
+  void set_ignore_reach_flag(bool value) const { lik_ignore_reach_flag() = value; }  // lik.cpp:144-146
+  void place_limbs(const double* feet) const { model_->place_limbs(feet); }        // lik.cpp:89-99
+  // lik.cpp:82-85: one limb, the others kept
+  void place_limb(int limbi, double x, double y, double z) const {
+    std::vector<double> feet(3 * (size_t)get_number_of_limbs());
+    for (int L = 0; L < get_number_of_limbs(); L++) {  // every row the target (only limbi's is kept)
+      feet[3 * (size_t)L] = x;
+      feet[3 * (size_t)L + 1] = y;
+      feet[3 * (size_t)L + 2] = z;
+    }
+    model_->place_limbs(feet.data(), limbi);
+  }
+  // lik.cpp:104-106, 358-361: the limb's top-link body position
+  void get_limb_hip_pos(int limbi, extvec& pos) const { limb_child_.at((size_t)limbi)->get_A_ground()->get_translation(pos); }
+  // lik.cpp:364-366: child -> first child -> first child
+  const modelnode* get_foot(int limbi) const {
+    return limb_child_.at((size_t)limbi)->get_first_child()->get_first_child();
+  }
+};
+
+inline kinematicmodel::~kinematicmodel() {
+  delete lik_;
+  hs_model_free(h_);
+}
+
+inline void kinematicmodel::load_fromxml(const std::string& fname, int lik_variant) {
+  delete lik_;
+  lik_ = nullptr;
+  hs_model_free(h_);
+  h_ = nullptr;
+  check(hs_model_load_ex(fname.c_str(), lik_variant, &h_), "load_fromxml");
+  check(hs_model_get_dims(h_, &d_), "hs_model_get_dims");
+  xmlfname_ = fname;
+  jv_.assign((size_t)d_.config_dim, 0.0);
+  jv_ptrs_.clear();
+  for (double& v : jv_) jv_ptrs_.push_back(&v);
+  nodes_.assign((size_t)d_.n_parts, modelnode());
+  for (int i = 0; i < d_.n_parts; i++) {
+    modelnode& n = nodes_[(size_t)i];
+    check(hs_model_get_node(h_, i, &n.info_), "hs_model_get_node");
+    n.parent_ = n.info_.parent >= 0 ? &nodes_[(size_t)n.info_.parent] : nullptr;
+    for (int k = 0; k < n.info_.n_kids; k++) n.kids_.push_back(&nodes_[(size_t)n.info_.kids[k]]);
+    n.has_joint_ = n.info_.jtype >= 0;
+    n.joint_.type_ = n.info_.jtype == 0 ? free6 : hinge;
+    n.joint_.values_ = n.info_.jtype == 0 ? &jv_[0] : (n.info_.hinge >= 0 ? &jv_[6 + (size_t)n.info_.hinge] : nullptr);
+  }
+  lik_ = new liksolver(this);
+  recompute_modelnodes();
+}
 
 struct pgsconfigparams {
   std::string fname;
@@ -132,9 +422,18 @@ struct pgsconfigparams {
 class pergensetup {
   pgsconfigparams pcp_;
   int n_;
+  const kinematicmodel* model_;
 
  public:
-  pergensetup(int n_limbs, const pgsconfigparams& pcp) : pcp_(pcp), n_(n_limbs) {}
+  pergensetup(int n_limbs, const pgsconfigparams& pcp, const kinematicmodel* model = nullptr)
+      : pcp_(pcp), n_(n_limbs), model_(model) {}
+  // pergen.cpp:225-239: torso position and angles, then the feet in lik order, at time t
+  // (needs the model the gait was set up for: make_pergensu passes it)
+  void set_rec(double* rec, double t) const {
+    if (!model_) throw error(HS_E_ARG, "pergensetup without a model");
+    hs_gait_params g = pcp_.to_c();
+    check(hs_pergen_rec_host(model_->handle(), &g, 1, &t, 1, rec), "set_rec");
+  }
   int get_limb_number() const { return n_; }
   int get_config_dim() const { return 6 + 3 * n_; }
   double get_period() const { return pcp_.TLh[0]; }
@@ -262,6 +561,14 @@ class batch {
     check(hs_select_best(h_, &c, &id), "hs_select_best");
     return {c, id};
   }
+  // across the ranks of an RCCL communicator (hs_select_best_comm): one all-reduce(MIN) of 8 bytes
+  std::pair<float, int64_t> select_best(hs_comm_t comm) {
+    float c = 0;
+    int64_t id = -1;
+    check(hs_select_best_comm(h_, comm, &c, &id), "hs_select_best_comm");
+    return {c, id};
+  }
+  hs_batch_t handle() const { return h_; }
 };
 
 class modelplayer {
@@ -344,7 +651,7 @@ class modelplayer {
     if (!model_.if_loaded()) model_.load_fromxml(path);
     else if (model_.get_xmlfname() != path) throw error(HS_E_ARG, "model not from " + pcp.fname);
     int n_limbs = (model_.get_config_dim() - 6) / 3;
-    return new pergensetup(n_limbs, pcp);
+    return new pergensetup(n_limbs, pcp, &model_);
   }
   // player.cpp:269-285
   double measure_cot(const pergensetup* pgs, int n_t) {

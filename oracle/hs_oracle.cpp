@@ -2057,6 +2057,43 @@ void hso_rot_ztov(const double* v3, double* R9) {
   for (int j = 0; j < 3; j++) for (int i = 0; i < 3; i++) R9[j * 3 + i] = A.a[j * 4 + i];
 }
 
+int hso_pergen_rec(const hso_model* m0, const hso_gait* g, double t, double* rec) {
+  hso_model mm = *m0;
+  hso_model* m = &mm;
+  PGS pgs;
+  setup_pergen(m, pgs, g);
+  pgs.set_rec(rec, t);
+  return 0;
+}
+
+int hso_lik(const hso_model* m0, const double* rec, int ignore_reach, double* config, int* unreach) {
+  hso_model mm = *m0;
+  hso_model* m = &mm;
+  for (int j = 0; j < m->cfg; j++) jv(m, j) = config[j];
+  tl_ignore_reach = ignore_reach != 0;
+  tl_unreach = false;
+  const bool ok = set_jvalues_with_lik(m, rec);
+  for (int j = 0; j < m->cfg; j++) config[j] = jv(m, j);
+  if (unreach) *unreach = tl_unreach ? 1 : 0;
+  return ok ? 0 : -10;
+}
+
+int hso_fk(const hso_model* m0, const double* config, double* a_ground, double* a_joint) {
+  hso_model mm = *m0;
+  hso_model* m = &mm;
+  for (int j = 0; j < m->cfg; j++) jv(m, j) = config[j];  // kinematicmodel::set_jvalues
+  recompute_modelnodes(m);
+  for (int i = 0; i < m->n; i++) {
+    const Node& nd = m->nodes[i];
+    for (int c = 0; c < 4; c++)
+      for (int r = 0; r < 3; r++) {
+        a_ground[12 * i + 3 * c + r] = nd.A_ground.a[4 * c + r];
+        if (a_joint) a_joint[12 * i + 3 * c + r] = nd.jtype != J_NONE ? nd.J_A_ground.a[4 * c + r] : 0.0;
+      }
+  }
+  return 0;
+}
+
 double hso_fk_ik_check(const hso_model* m0, const hso_gait* g, double t, int ignore_reach) {
   hso_model mm = *m0;
   hso_model* m = &mm;

@@ -96,6 +96,16 @@ void hso_euler_roundtrip(const double* angles3, double* out3);
 void hso_rot_ztov(const double* v3, double* R9);
 /* FK after IK: foot positions vs pergen targets for record at time t; out: max |err| */
 double hso_fk_ik_check(const hso_model* m, const hso_gait* g, double t, int ignore_reach);
+/* per-configuration kinematics (the product's hs_pergen_rec / hs_model_lik / hs_model_fk):
+ * pergensetup::set_rec at time t (pergen.cpp:225-239) after setup_pergen: rec [6 + 3 n_limbs] */
+int hso_pergen_rec(const hso_model* m, const hso_gait* g, double t, double* rec);
+/* kinematicmodel::set_jvalues_with_lik (model.cpp:354-359) on a copy of the model holding config
+ * (in/out, [config_dim]); returns 0, or -10 when a target is out of reach without ignore_reach
+ * (lik.cpp:321-330); *unreach = 1 when a target was clamped */
+int hso_lik(const hso_model* m, const double* rec, int ignore_reach, double* config, int* unreach);
+/* kinematicmodel::set_jvalues + recompute_modelnodes (model.cpp:314-318, 361-366): A_ground of every
+ * node and of its joint (zeros without one), 3x4 column-major (12 doubles, [c*3 + r]) per node */
+int hso_fk(const hso_model* m, const double* config, double* a_ground, double* a_joint);
 /* static residual checks for one step: |B0 x0 - f|, |[B0 Bc] N| (both bases) */
 int hso_residuals(const hso_model* m, const hso_gait* g, int n_t, int step, int basis, double* out2);
 

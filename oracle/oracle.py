@@ -169,6 +169,9 @@ def _bind(path):
     L.hso_fk_ik_check.restype = ctypes.c_double
     L.hso_residuals.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int,
                                 ctypes.c_int, dp]
+    L.hso_pergen_rec.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_double, dp]
+    L.hso_lik.argtypes = [ctypes.c_void_p, dp, ctypes.c_int, dp, ctypes.POINTER(ctypes.c_int)]
+    L.hso_fk.argtypes = [ctypes.c_void_p, dp, dp, dp]
     ip = ctypes.POINTER(ctypes.c_int32)
     L.hso_dynrec_dump.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int,
                                   dp, dp, dp, dp, dp, dp, ip, ip, ip, ip]
@@ -325,6 +328,32 @@ def rot_ztov(v) -> np.ndarray:
 def fk_ik_check(model: Model, gait: GaitParams, t: float, ignore_reach: bool = True) -> float:
     g = gait.to_c()
     return lib().hso_fk_ik_check(model.handle, ctypes.byref(g), t, int(ignore_reach))
+
+
+def pergen_rec(model: Model, gait: GaitParams, t: float) -> np.ndarray:
+    """pergensetup::set_rec (pergen.cpp:225-239): [6 + 3 n_limbs]."""
+    g = gait.to_c()
+    rec = np.zeros(6 + 3 * model.n_limbs)
+    lib().hso_pergen_rec(model.handle, ctypes.byref(g), t, _ptr(rec))
+    return rec
+
+
+def set_jvalues_with_lik(model: Model, rec, ignore_reach: bool = False, config=None):
+    """kinematicmodel::set_jvalues_with_lik (model.cpp:354-359) -> (config, ok, unreach)."""
+    r = np.ascontiguousarray(rec, dtype=np.float64)
+    q = np.zeros(model.cfg) if config is None else np.array(config, dtype=np.float64)
+    u = ctypes.c_int(0)
+    rc = lib().hso_lik(model.handle, _ptr(r), int(ignore_reach), _ptr(q), ctypes.byref(u))
+    return q, rc == 0, bool(u.value)
+
+
+def recompute_modelnodes(model: Model, config):
+    """set_jvalues + recompute_modelnodes (model.cpp:314-318, 361-366): (A_ground, joint A_ground) of
+    every node as [n][3][4] (zeros for a node without a joint)."""
+    q = np.ascontiguousarray(config, dtype=np.float64)
+    ag, aj = np.zeros(model.n * 12), np.zeros(model.n * 12)
+    lib().hso_fk(model.handle, _ptr(q), _ptr(ag), _ptr(aj))
+    return (ag.reshape(model.n, 4, 3).transpose(0, 2, 1).copy(), aj.reshape(model.n, 4, 3).transpose(0, 2, 1).copy())
 
 
 def residuals(model: Model, gait: GaitParams, n_t: int, step: int, basis: int):

@@ -22,6 +22,7 @@ def test_shim_compiles_and_links(product, tmp_path):
     exe = compile_prog(product, tmp_path / "cot_sweep")
     assert os.path.exists(exe)
     assert os.path.exists(compile_prog(product, tmp_path / "position_control", "position_control.cpp"))
+    assert os.path.exists(compile_prog(product, tmp_path / "model_api", "model_api.cpp"))
     # the C header alone is valid C (no C++ or HIP types leak through the boundary)
     src = tmp_path / "c_only.c"
     src.write_text('#include "hslabs.h"\nint main(void){return hs_abi_version()==HSLABS_ABI_VERSION?0:1;}\n')
@@ -76,3 +77,45 @@ def test_shim_position_control_walks(product, tmp_path):
     out = sb.step(600, outputs=("torso",))
     torch.cuda.synchronize()
     assert np.abs(out["torso"][0, -1].cpu().numpy() - t1).max() < 2e-9
+
+
+@pytest.mark.gpu
+def test_shim_model_api(product, oracle_mod, omodels, tmp_path):
+    """model.h / core.h through the shim (set_rec -> set_jvalues_with_lik -> get_jvalues ->
+    recompute_modelnodes -> feet, orient_torso, get_limb_hip_pos, arrayops, str_to_val) reproduces
+    the oracle's configurations and its FK-after-IK check to 1e-12."""
+    from conftest import to_oracle_gait
+
+    O = oracle_mod
+    exe = compile_prog(product, tmp_path / "model_api", "model_api.cpp")
+    ids = [0, 8, 10, 17, 24, 25]  # myant, hexapod, turned hexapod, myant, spider x2
+    out = subprocess.run([str(exe), MODELS, PGS_CONFIG, *map(str, ids)], check=True, capture_output=True, text=True,
+                         timeout=300).stdout
+    rows = [ln.split() for ln in out.splitlines()]
+    n_q = 0
+    for r in rows:
+        if r[0] == "q":
+            i, t, q = int(r[1]), float(r[2]), np.array([float(v) for v in r[3:]])
+            p = product.read_pgs_config(PGS_CONFIG, i)
+            om = omodels[p.fname.split(".")[0]]
+            rec = O.pergen_rec(om, to_oracle_gait(O, p), t)
+            qr, ok, _ = O.set_jvalues_with_lik(om, rec, ignore_reach=True)
+            assert ok and np.abs(q - qr).max() < 1e-12, (i, t)
+            n_q += 1
+        elif r[0] == "fkik":
+            assert float(r[3]) < 1e-12, r
+        elif r[0] == "zaxis":
+            assert float(r[3]) < 1e-14, r
+        elif r[0] == "jvalues":
+            assert float(r[2]) == 0.0, r
+        elif r[0] == "orient":
+            assert np.allclose([float(v) for v in r[2:5]], [0.5, -0.25, 1.0], atol=1e-12), r
+        elif r[0] == "feet":
+            assert int(r[2]) in (4, 6), r
+        elif r[0] == "unreach_throws":
+            assert r[2] == "1", r
+    assert n_q == 4 * len(ids)
+    kv = {r[0]: r[1:] for r in rows}
+    assert [float(v) for v in kv["str_to_val"]] == [1.5, -2.0, 0.3]
+    assert np.allclose([float(v) for v in kv["modulus"]], [4 - 2 * np.pi, -4 + 2 * np.pi, 1.0], atol=1e-15)
+    assert float(kv["dot"][0]) == pytest.approx(-0.2)

@@ -328,3 +328,27 @@ def test_solve_forces_matches_independent_lstsq(oracle_mod, omodels, name):
         for step in (0, 6, 15):
             ref = dense_forces(oracle_mod.dynrec_dump(m, g, 20, step), m.n, z[step])
             assert np.abs(fo["cf"][step] - ref).max() < 1e-10 * max(1.0, np.abs(ref).max())
+
+
+def test_oracle_per_configuration_kinematics(oracle_mod, omodels):
+    """The oracle's set_rec / set_jvalues_with_lik / recompute_modelnodes exports (checkers of
+    hs_pergen_rec / hs_model_lik / hs_model_fk): FK after IK puts the feet (the nodes whose joint
+    A_ground the oracle reports last in each limb chain) where fk_ik_check says, and the joint
+    frames are rigid."""
+    O = oracle_mod
+    for name, gid in (("hexapod", 8), ("myant", 0), ("spider", 24)):
+        m = omodels[name]
+        p = O.load_pgs_config(os.path.join(MODELS, "pgs_config.txt"), gid)
+        for t in (0.0, 0.7, 2.3):
+            rec = O.pergen_rec(m, p, t)
+            assert rec.shape == (6 + 3 * m.n_limbs,)
+            q, ok, _ = O.set_jvalues_with_lik(m, rec, ignore_reach=True)
+            assert ok and np.all(q[:6] == rec[:6])
+            ag, aj = O.recompute_modelnodes(m, q)
+            for A in list(ag) + [a for a in aj if np.any(a)]:
+                R = A[:, :3]
+                assert np.abs(R @ R.T - np.eye(3)).max() < 1e-14
+            assert O.fk_ik_check(m, p, t) < 1e-12
+            # the configuration is a fixed point: IK of the FK'd feet returns it
+            q2, ok2, _ = O.set_jvalues_with_lik(m, rec, ignore_reach=True, config=q)
+            assert ok2 and np.array_equal(q, q2)
