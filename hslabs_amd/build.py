@@ -10,6 +10,8 @@ The closed-loop simulation (hs_sim.hip) is the exception, built with
 -ffp-contract=off: its contact test (depth >= 0) is decided within rounding for
 stance feet, so it keeps the oracle's unfused rounding (clang ignores
 `#pragma clang fp contract` under -ffp-contract=fast, hence a per-file flag).
+So is hs_config.hip (the per-configuration FK / IK of the model.h API), which is
+not on the hot path and keeps the reference's rounding.
 Sources compile to objects in parallel, then link.
 """
 from __future__ import annotations

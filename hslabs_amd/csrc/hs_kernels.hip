@@ -25,9 +25,12 @@
 // is latency-bound, so recomputing the window on 30 lanes costs about what a
 // sliding window's one new sample on 6 lanes would, at twice the occupancy.
 //
-// Every floating-point operation sequence matches oracle/hs_oracle.cpp
-// (compiled with -ffp-contract=off), so the only expected differences against
-// it are ULP differences of the device sin/cos/atan2/acos/asin.
+// The floating-point operation sequences follow oracle/hs_oracle.cpp's fast mode
+// (built with -ffp-contract=off like the reference's x86-64 g++ -O2), but this
+// file is compiled with -ffp-contract=fast (hslabs_amd/build.py): a*b+c is one
+// FMA, so results differ from the oracle by FMA roundings (<= 2.3e-12 on the
+// per-joint torques, profiles/r01_parity_report.txt) and by ULPs of the device
+// sin/cos/atan2/acos/asin.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -1003,7 +1006,7 @@ __device__ void qr_solve(G& g, int k, int np, int lane) {
   gsync<G>();
 }
 
-// S3 general: adaptive-rank two-stage least squares (ftsolver.cpp:277-303) -> sv.y.
+// S3 general: adaptive-rank two-stage least squares (ftsolver.cpp:185-236) -> sv.y.
 // The reference re-runs FullPivLU on the same zeroth-order Gram every pass; it
 // is factorized once here (identical factors), only the rank threshold moves.
 template <class SV, class G>

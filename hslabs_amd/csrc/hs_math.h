@@ -3,9 +3,10 @@
 // Rigid transforms are 3x4 column-major (hs_aff34); every product sums k = 0..2
 // from an explicit 0 and adds the translation last, which is the rounding of
 // the reference's 4x4 affine::mult (matrix.cpp:78-97) with its exact (0,0,0,1)
-// bottom row. The file is compiled with -ffp-contract=off so a*b+c is never
-// fused: device results round like the reference's x86-64 -O2 build. `real`
-// is double, or float for the fp32 build (hs_kernels_f32.hip).
+// bottom row. Its rounding follows the compiling file's contraction flag
+// (hslabs_amd/build.py): hs_config.hip and hs_sim.hip (-ffp-contract=off) round
+// like the reference's x86-64 -O2 build; the rollout kernels (fast) fuse a*b+c.
+// `real` is double, or float for the fp32 build (hs_kernels_f32.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -42,7 +42,7 @@ enum { HSO_BASIS_ORTHO = 0, /* reference-faithful: orthonormal Q of QR(B^T) (fts
                                falling back to the TREE path when ill-conditioned */ };
 
 /* flag bits per step (also used by the product, see include/hslabs.h) */
-#define HSO_FLAG_RANK_RETRY   1u  /* adaptive-rank loop ran more than once (ftsolver.cpp:279-303) */
+#define HSO_FLAG_RANK_RETRY   1u  /* adaptive-rank loop ran more than once (ftsolver.cpp:207-232) */
 #define HSO_FLAG_FULL_RANK    2u  /* zeroth-order Gram full rank: reference would assert in comma init */
 #define HSO_FLAG_LOOP_EXHAUST 4u  /* rank loop reached rank 0 without converging */
 #define HSO_FLAG_NAN          8u  /* NaN in torques / contact forces */
