@@ -52,7 +52,10 @@ constexpr int HALF = 32;     // lanes per rollout: two rollouts per wavefront
 constexpr int NS = 5;        // samples in the derivative stencil (periodic.cpp:192-202)
 static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a rollout's lane maps exceed 32");
 #ifndef HS_MIN_WAVES
-#define HS_MIN_WAVES 2  // waves per SIMD the fp64 register budget allows (8 workgroups/CU at 19.5 KB LDS)
+#define HS_MIN_WAVES 3  // fp64: 12 workgroups/CU at 13.0 KB LDS (hexapod), <= 168 VGPRs
+#endif
+#ifndef HS_MIN_WAVES_FORCES
+#define HS_MIN_WAVES_FORCES 2  // solve_forces mode (hs_run_forces): its LDS layout holds a 24 x 24 system
 #endif
 #ifndef HS_MIN_WAVES_F32
 #define HS_MIN_WAVES_F32 4  // fp32: 9.9 KB LDS per hexapod workgroup; 128 VGPRs (216 B scratch)
@@ -64,24 +67,28 @@ static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a
 // NM = part capacity of the LDS layouts (the host picks the smallest instantiation >= n,
 // so LDS per rollout follows the model: hexapod 9.5 KB).
 
+// packed per-contact Schur entries: the lower triangle of S_c row by row (r (r + 1) / 2 + q), then h_c
+constexpr int SCH_H = 21, SCH_N = 27;
+__host__ __device__ constexpr int sch_lower(int r, int q) { return r * (r + 1) / 2 + q; }
+
 struct SchurL {  // per-contact Schur complement (all D_c invertible)
-  real Dinv[HS_LMAX][9], S[HS_LMAX][36], h[HS_LMAX][6];
-  real Ssum[42];  // sum over contacts of [S_c | h_c] (lane per entry)
+  real Dinv[HS_LMAX][9], S[HS_LMAX][SCH_N];
+  real Ssum[SCH_N];  // sum over contacts of the packed [S_c | h_c] (lane per entry)
   real lam[6];
 };
 
-struct AugL {  // augmented system K = D + rho A^T A (a singular D_c)
+// augmented system K = D + rho A^T A (tier 2: a singular D_c); rare, so it lives in the rollout's
+// global workspace (aliasing the general path's, which runs only after it declines)
+struct AugL {
   real K[HS_KMAX * HS_KMAX], X[HS_KMAX * 7], St[36], lam[6], rdiag[HS_KMAX];
   int ok;
 };
 
 struct FastL {  // blocks of the closed-form solve
-  real A[HS_LMAX][18], D[HS_LMAX][9], g[HS_LMAX][3];
+  real d0[HS_LMAX][3];  // A_c = [-I; [d0_c]x] (d0_c = torso COM - contact foot), kept as d0_c
+  real D[HS_LMAX][9], g[HS_LMAX][3];
   int ok[HS_LMAX];
-  union {
-    SchurL sc;
-    AugL ag;
-  };
+  SchurL sc;
 };
 
 struct WorkL {  // per-joint positive work of the step (outputs phase; FastL is dead by then)
@@ -89,8 +96,7 @@ struct WorkL {  // per-joint positive work of the step (outputs phase; FastL is 
 };
 
 // Workspace of the general path (k x k matrices, leading dimension LD >= k).
-// SHARED: in LDS (the dead stencil block, k <= 12: any 4-legged model, up to 4
-// contacts of a 6-legged one); otherwise one global-memory slot per rollout.
+// SHARED: in LDS; otherwise (GenWS, the only instance) one global-memory slot per rollout.
 template <int LD_, bool SHARED_>
 struct GenMats {
   static constexpr int LD = LD_;
@@ -100,20 +106,18 @@ struct GenMats {
   real ntx0[LD], ntx1[LD], y0[LD], b[LD], z[LD], c[LD], hc[LD], nu[LD], nd[LD];
   int8_t rowsT[LD], colsT[LD], q[LD], piv[LD], rycol[LD], cperm[LD];
 };
-using GenLDS = GenMats<12, true>;
 using GenWS = GenMats<HS_KMAX, false>;
 
 template <int NM>
 struct StencilL {  // fields only the finite differences read
   real pos[2][NM][3];  // t-2dt, t+2dt
   real ust[3][NM][3];  // t-2dt, t, t+2dt
-  real rot[2][NM][9];  // t-dt, t+dt
 };
 
 template <int NM>
 struct CentreL {  // fields read after D
   real pos[NM][3], jpos[NM][3], jz[NM][3], fpos[HS_LMAX][3];
-  real q[3][6 + NM];  // t-dt, t, t+dt
+  real q[3][6 + 3 * HS_LMAX];  // t-dt, t, t+dt (every hinge is a limb hinge: config_dim <= 24)
   int contact[HS_LMAX];
   int unreach[HS_LMAX];
 };
@@ -129,7 +133,6 @@ struct OneStore {
   union {
     StencilL<NM> sten;
     FastL fl;  // written only after D has consumed the stencil
-    GenLDS gl;  // general path, k <= 12 (fast solve declined)
     WorkL wk;
     typename std::conditional<FORCES, ForceL, WorkL>::type fr;  // forces-given-torques mode
   };
@@ -217,12 +220,10 @@ struct OneWin {
   OneStore<NM, FORCES>* d;
   __device__ bool want_pos(int k) const { return (k & 1) == 0; }
   __device__ bool want_ust(int k) const { return (k & 1) == 0; }
-  __device__ bool want_rot(int k) const { return (k & 1) != 0; }
   __device__ bool want_q(int k) const { return k >= -1 && k <= 1; }
   __device__ bool want_centre(int k) const { return k == 0; }
   __device__ real* pos(int k, int v) const { return k == 0 ? d->c.pos[v] : d->sten.pos[k > 0][v]; }
   __device__ real* ust(int k, int v) const { return d->sten.ust[(k + 2) >> 1][v]; }
-  __device__ real* rot(int k, int v) const { return d->sten.rot[k > 0][v]; }
   __device__ real* q(int k) const { return d->c.q[k + 1]; }
   __device__ real* jpos(int, int v) const { return d->c.jpos[v]; }
   __device__ real* jz(int, int v) const { return d->c.jz[v]; }
@@ -374,11 +375,6 @@ __device__ __attribute__((always_inline)) inline void node_features(const hs_top
     U[1] = (A(0, 2) - A(2, 0)) / 2;
     U[2] = (A(1, 0) - A(0, 1)) / 2;
   }
-  if (w.want_rot(k)) {
-    real* R = w.rot(k, v);
-    for (int c = 0; c < 3; c++)
-      for (int r = 0; r < 3; r++) R[c * 3 + r] = A(r, c);
-  }
   if (w.want_centre(k)) {
     real* Jp = w.jpos(k, v);
     real* Jz = w.jz(k, v);
@@ -521,7 +517,7 @@ __device__ __attribute__((always_inline)) inline void dynamics(const hs_topo* T,
     const real m = (real)T->mass[i];
     const real *Pp = w.pos(2, i), *P0 = w.pos(0, i), *Pm = w.pos(-2, i);
     const real *Up = w.ust(2, i), *U0 = w.ust(0, i), *Um = w.ust(-2, i);
-    real vp[3], vm[3], mr[3], wp[3], wm[3], amp[3], amm[3], amr[3];
+    real vp[3], vm[3], mr[3], wp[3], wm[3], amr[3];
     for (int j = 0; j < 3; j++) {
       vp[j] = Pp[j] - P0[j];
       vp[j] *= inv;
@@ -535,24 +531,13 @@ __device__ __attribute__((always_inline)) inline void dynamics(const hs_topo* T,
       wm[j] = U0[j] - Um[j];
       wm[j] *= inv;
     }
-    // ang_mom = R (I (R^T w)), I = identity (compute_ang_mom, dynrec.cpp:205-216)
-    const real* Rp = w.rot(1, i);
-    const real* Rm = w.rot(-1, i);
-    real up[3], um[3];
-    for (int r = 0; r < 3; r++) {
-      real s = real(0), t = real(0);
-      for (int k = 0; k < 3; k++) { s = s + Rp[r * 3 + k] * wp[k]; t = t + Rm[r * 3 + k] * wm[k]; }
-      up[r] = s;
-      um[r] = t;
-    }
-    for (int r = 0; r < 3; r++) {
-      real s = real(0), t = real(0);
-      for (int k = 0; k < 3; k++) { s = s + Rp[k * 3 + r] * up[k]; t = t + Rm[k * 3 + r] * um[k]; }
-      amp[r] = s;
-      amm[r] = t;
-    }
+    // ang_mom = R (I (R^T w)) (compute_ang_mom, dynrec.cpp:205-216) with I the identity: every
+    // inertia is ODE's default dMass (dBodyCreate; the reference sets no other, dynrec.cpp:62-68),
+    // so R R^T w = w exactly in exact arithmetic and the two rotations (9 + 9 products and the
+    // t +- dt rotations kept for them, 3.2 KB of LDS per hexapod rollout) are skipped: this rounds
+    // ang_mom once instead of through R^T and R (a few ULPs of |w|, ~1e-15 relative)
     for (int j = 0; j < 3; j++) {
-      amr[j] = amp[j] - amm[j];
+      amr[j] = wp[j] - wm[j];
       amr[j] *= inv;
     }
     for (int j = 0; j < 3; j++) {
@@ -1073,9 +1058,18 @@ __device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
   return flags;
 }
 
+// The general path is an out-of-line call: it keeps its own register allocation apart from the
+// kernel body's 168-VGPR budget (3 waves/SIMD). Inlined at that budget the compiler spilled SGPRs
+// across it, and the Eigen-style path returned wrong forces on every step on the GPU (HS_SOLVE_
+// REFERENCE, tests/test_gpu_parity.py; correct with the 2-wave budget or out of line). The call
+// costs only the steps that take it (stack frame in scratch, 288 B per lane).
+#ifndef HS_GENERAL_INLINE
+#define HS_GENERAL_ATTR __attribute__((noinline))
+#else
+#define HS_GENERAL_ATTR __attribute__((always_inline)) inline
+#endif
 template <class W, class SV, class G>
-__device__ __attribute__((always_inline)) inline uint32_t general_solve(const hs_topo* T, SV& sv, G& g, const W& w,
-                                                                        int k, int lane) {
+__device__ HS_GENERAL_ATTR uint32_t general_solve(const hs_topo* T, SV& sv, G& g, const W& w, int k, int lane) {
   build_grams(T, sv, g, w, k, lane);
   STAMP(9);
   return contact_solve(sv, g, k, lane);
@@ -1146,11 +1140,28 @@ __device__ inline void cross_rows(const real* d, real v[3][3]) {
   v[2][0] = -d[1]; v[2][1] = d[0];  v[2][2] = 0;
 }
 
+// entry (r, j) of A_c = [-I; [d0]x] (the values cross_rows lays out)
+__device__ inline real a_entry(const real* d0, int r, int j) {
+  if (r < 3) return (r == j) ? real(-1) : real(0);
+  const int i = r - 3;
+  if (i == j) return real(0);
+  const real v = d0[3 - i - j];
+  return ((j - i + 3) % 3 == 1) ? -v : v;
+}
+
 // In-place Cholesky of a k x k SPD matrix (row-major, lower triangle used) by
 // the half-wave, right-looking: element (i, j) gets its products subtracted in
 // increasing order, exactly like the oracle's left-looking chol(). False (wave-
 // uniform) when a pivot falls to guard * (max original diagonal) or below.
 // rdiag (optional) receives 1 / L_jj.
+// (GLOBAL: K lives in global memory, so the exchanges need the workgroup's global-memory fences)
+template <bool GLOBAL>
+__device__ inline void ws_sync() {
+  if constexpr (GLOBAL) __syncthreads();
+  else wave_sync();
+}
+
+template <bool GLOBAL>
 __device__ __attribute__((always_inline)) inline bool chol_half(real* K, int k, real guard, int lane,
                                                                  real* rdiag = nullptr) {
   real mx = 0;
@@ -1164,13 +1175,13 @@ __device__ __attribute__((always_inline)) inline bool chol_half(real* K, int k, 
       if (rdiag) rdiag[j] = rl;
     }
     for (int i = j + 1 + lane; i < k; i += HALF) K[i * k + j] = K[i * k + j] * rl;
-    wave_sync();
+    ws_sync<GLOBAL>();
     const int m = k - 1 - j;
     for (int e = lane; e < m * m; e += HALF) {
       const int i = j + 1 + e / m, c2 = j + 1 + e % m;
       if (c2 <= i) K[i * k + c2] -= K[i * k + j] * K[c2 * k + j];
     }
-    wave_sync();
+    ws_sync<GLOBAL>();
   }
   return true;
 }
@@ -1181,10 +1192,10 @@ __device__ __attribute__((always_inline)) inline bool chol_half(real* K, int k, 
 // half-wave right-looking Cholesky subtracts in the oracle's left-looking order).
 // False when the minimizer is not unique (a pivot under the guard).
 template <class SV>
-__device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, SV& sv, const real* a, int nc, int lane) {
-  AugL& ag = fl.ag;
+__device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, AugL& ag, SV& sv, const real* a, int nc,
+                                                                int lane) {
   const int k = 3 * nc;
-  auto Aat = [&](int r, int i) { return fl.A[i / 3][r * 3 + i % 3]; };  // A (6 x k)
+  auto Aat = [&](int r, int i) { return a_entry(fl.d0[i / 3], r, i % 3); };  // A (6 x k)
   real md = 0, ma = 0;
   for (int c = 0; c < nc; c++)
     for (int i = 0; i < 3; i++) {
@@ -1212,9 +1223,9 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, SV& s
     }
     ag.X[i * 7 + q] = v;
   }
-  wave_sync();
-  if (!chol_half(ag.K, k, kFastPivotGuard, lane, ag.rdiag)) return false;
-  wave_sync();
+  __syncthreads();
+  if (!chol_half<true>(ag.K, k, kFastPivotGuard, lane, ag.rdiag)) return false;
+  __syncthreads();
   if (lane < 7) {  // K X = [A^T | g~], one right-hand column per lane
     const int q = lane;
     for (int i = 0; i < k; i++) {
@@ -1228,7 +1239,7 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, SV& s
       ag.X[i * 7 + q] = s * ag.rdiag[i];
     }
   }
-  wave_sync();
+  __syncthreads();
   for (int e = lane; e < 42; e += HALF) {
     const int r = e / 7, q = e % 7;
     real s = 0;
@@ -1236,7 +1247,7 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, SV& s
     if (q < 6) ag.St[6 * r + q] = s;
     else ag.lam[r] = a[r] - s;
   }
-  wave_sync();
+  __syncthreads();
   if (lane == 0) {
     real St[36], lam[6];
     for (int i = 0; i < 36; i++) St[i] = ag.St[i];
@@ -1248,19 +1259,20 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, SV& s
     }
     ag.ok = ok;
   }
-  wave_sync();
+  __syncthreads();
   if (!ag.ok) return false;
   for (int i = lane; i < k; i += HALF) {
     real s = ag.X[i * 7 + 6];
     for (int r = 0; r < 6; r++) s += ag.X[i * 7 + r] * ag.lam[r];
     sv.y[i] = -s;
   }
-  wave_sync();
+  __syncthreads();
   return true;
 }
 
 template <class W, class SV>
-__device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* T, SV& sv, FastL& fl, const W& w, int nc, int lane) {
+__device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* T, SV& sv, FastL& fl, AugL& ag, const W& w,
+                                                                 int nc, int lane) {
   const int n = T->n;
   if (nc == 0) return true;
   const real* P0 = w.pos(0, 0);
@@ -1273,7 +1285,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
     real Ac[18];
     for (int r = 0; r < 3; r++)
       for (int j = 0; j < 3; j++) { Ac[r * 3 + j] = (r == j) ? real(-1) : real(0); Ac[(3 + r) * 3 + j] = v[r][j]; }
-    for (int i = 0; i < 18; i++) fl.A[c][i] = Ac[i];
+    for (int r = 0; r < 3; r++) fl.d0[c][r] = d0[r];
     real D[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
     const int nch = T->foot_chain_len[fi];
     int chain[HS_CHAIN_MAX];  // independent loads instead of a parent-pointer chase
@@ -1348,11 +1360,11 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
               for (int j = 0; j < 3; j++)
                 if (j != q - 3) s += E[r * 3 + j] * Ac[q * 3 + j];
             }
-            fl.sc.S[c][6 * r + q] = s;
+            fl.sc.S[c][sch_lower(r, q)] = s;
           }
           real s = 0;
           for (int j = 0; j < 3; j++) s += E[r * 3 + j] * g[j];
-          fl.sc.h[c][r] = s;
+          fl.sc.S[c][SCH_H + r] = s;
         }
         for (int i = 0; i < 9; i++) fl.sc.Dinv[c][i] = Dinv[i];
       }
@@ -1363,16 +1375,16 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
   STAMP(18);
   const real a[6] = {sv.x[0], sv.x[1], sv.x[2], sv.x[3 * n], sv.x[3 * n + 1], sv.x[3 * n + 2]};
   for (int c = 0; c < nc; c++)
-    if (!fl.ok[c]) return aug_solve(fl, sv, a, nc, lane);  // only nc >= 3 factors D_c
+    if (!fl.ok[c]) return aug_solve(fl, ag, sv, a, nc, lane);  // only nc >= 3 factors D_c
   int ok = 1;
   if (nc == 1) {  // unique least-squares solution (A^T A) w = -A^T a
     if (lane == 0) {
       real M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-      const real* A = fl.A[0];
+      const real* d0 = fl.d0[0];
       for (int i = 0; i < 3; i++) {
         for (int j = 0; j < 3; j++)
-          for (int r = 0; r < 6; r++) M[3 * i + j] += A[r * 3 + i] * A[r * 3 + j];
-        for (int r = 0; r < 6; r++) b[i] -= A[r * 3 + i] * a[r];
+          for (int r = 0; r < 6; r++) M[3 * i + j] += a_entry(d0, r, i) * a_entry(d0, r, j);
+        for (int r = 0; r < 6; r++) b[i] -= a_entry(d0, r, i) * a[r];
       }
       ok = chol_n<3>(M, kFastPivotGuard);
       if (ok) {
@@ -1393,15 +1405,15 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       if (ok) {
         for (int r = 0; r < 3; r++) { nv[r] = u[r] / un / sqrt(real(2)); nv[3 + r] = -nv[r]; }
         for (int i = 0; i < 6; i++) {
-          const real* Ai = fl.A[i / 3];
+          const real* di = fl.d0[i / 3];
           for (int j = 0; j < 6; j++) {
-            const real* Aj = fl.A[j / 3];
+            const real* dj = fl.d0[j / 3];
             real s = 0;
-            for (int r = 0; r < 6; r++) s += Ai[r * 3 + i % 3] * Aj[r * 3 + j % 3];
+            for (int r = 0; r < 6; r++) s += a_entry(di, r, i % 3) * a_entry(dj, r, j % 3);
             M[6 * i + j] = s + nv[i] * nv[j];
           }
           real s = 0;
-          for (int r = 0; r < 6; r++) s += Ai[r * 3 + i % 3] * a[r];
+          for (int r = 0; r < 6; r++) s += a_entry(di, r, i % 3) * a[r];
           b[i] = -s;
         }
         ok = chol_n<6>(M, kFastPivotGuard);
@@ -1425,19 +1437,11 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       fl.ok[0] = ok;
     }
   } else {  // Schur complement of the 6 zeroth-order constraints
-    // entry sums in contact order, one lane per entry of the lower triangle (21) and of h (6)
-    if (lane < 27) {
-      int e = lane;
-      if (lane < 21) {
-        int r = 0;
-        while ((r + 1) * (r + 2) / 2 <= lane) r++;
-        e = 6 * r + (lane - r * (r + 1) / 2);
-      } else {
-        e = 36 + (lane - 21);
-      }
+    // entry sums in contact order, one lane per packed entry: the lower triangle (21) and h (6)
+    if (lane < SCH_N) {
       real s = 0;
-      for (int c = 0; c < nc; c++) s += (e < 36) ? fl.sc.S[c][e] : fl.sc.h[c][e - 36];
-      fl.sc.Ssum[e] = s;
+      for (int c = 0; c < nc; c++) s += fl.sc.S[c][lane];
+      fl.sc.Ssum[lane] = s;
     }
     wave_sync();
     if (lane == 0) {
@@ -1445,8 +1449,8 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
 #pragma unroll
       for (int i = 0; i < 6; i++)
 #pragma unroll
-        for (int j = 0; j < 6; j++) Sm[6 * i + j] = (j <= i) ? fl.sc.Ssum[6 * i + j] : real(0);  // upper: unread
-      for (int i = 0; i < 6; i++) h[i] = fl.sc.Ssum[36 + i];
+        for (int j = 0; j < 6; j++) Sm[6 * i + j] = (j <= i) ? fl.sc.Ssum[sch_lower(i, j)] : real(0);  // upper: unread
+      for (int i = 0; i < 6; i++) h[i] = fl.sc.Ssum[SCH_H + i];
       real lam[6];
       for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
       ok = chol_n<6>(Sm, kFastPivotGuard);
@@ -1458,10 +1462,10 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
     }
     wave_sync();
     STAMP(19);
-    if (!fl.ok[0]) return aug_solve(fl, sv, a, nc, lane);
+    if (!fl.ok[0]) return aug_solve(fl, ag, sv, a, nc, lane);
     if (lane < nc) {
       const int c = lane;
-      const real* Ac = fl.A[c];
+      const real* d0 = fl.d0[c];
       real t[3];
 #pragma unroll
       for (int i = 0; i < 3; i++) {  // g + A_c^T lam, A_c's zero entries skipped (exact zeros)
@@ -1470,7 +1474,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
         for (int r = 0; r < 6; r++) {
           if (r < 3 && r != i) continue;
           if (r >= 3 && r - 3 == i) continue;
-          s += Ac[r * 3 + i] * fl.sc.lam[r];
+          s += a_entry(d0, r, i) * fl.sc.lam[r];
         }
         t[i] = s;
       }
@@ -1505,7 +1509,7 @@ __device__ inline uint64_t best_key(real cot, int64_t id) {
 // ---------------------------------------------------------------------------
 template <class W, class SV>
 __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st, SV& sv,
-                     FastL& fl, GenLDS& gl, WorkL& wk, const W& w, GenWS* G, int b, bool live, int h,
+                     FastL& fl, WorkL& wk, const W& w, GenWS* G, int b, bool live, int h,
                      real& work, int lane) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
   STAMP(3);
@@ -1521,11 +1525,11 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   int k = 3 * nc;
   uint32_t flags = 0;
   STAMP(6);
-  if (a.solve_mode == HS_SOLVE_AUTO && fast_solve(T, sv, fl, w, nc, lane)) {
+  // tier 2 (aug_solve) and the general path share the rollout's global workspace: the general
+  // path runs only after tier 2 declined
+  if (a.solve_mode == HS_SOLVE_AUTO && fast_solve(T, sv, fl, *reinterpret_cast<AugL*>(G), w, nc, lane)) {
     if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
     if (nc == 1) flags |= HS_FLAG_FULL_RANK;
-  } else if (k <= GenLDS::LD) {
-    flags = general_solve(T, sv, gl, w, k, lane) | HS_FLAG_GENERAL;
   } else {
     flags = general_solve(T, sv, *G, w, k, lane) | HS_FLAG_GENERAL;
   }
@@ -1751,7 +1755,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     fr.Ct[r * ld + q] = v;
   }
   wave_sync();
-  chol_half(fr.W, m, real(0), lane);  // I + G G^T: eigenvalues >= 1
+  chol_half<false>(fr.W, m, real(0), lane);  // I + G G^T: eigenvalues >= 1
   if (lane < ld) {                // L^-1 [C | d], one column per lane
     for (int i = 0; i < m; i++) {
       real s = fr.Ct[i * ld + lane];
@@ -1780,7 +1784,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
       else fr.y[p] = s;
     }
     wave_sync();
-    if (chol_half(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) break;
+    if (chol_half<false>(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) break;
     flags = HS_FLAG_GENERAL;  // least squares not unique
   }
   if (lane == 0) {
@@ -1818,13 +1822,14 @@ __device__ __attribute__((always_inline)) inline void forces_step(const hs_topo*
 // Global per-rollout workspace: the general path's scratch and the gait-setup cache that
 // carries SetupL from the first launch of a call to the later ones (hs::SETUP_*).
 struct RolloutWS {
-  GenWS gen;
+  GenWS gen;  // also the tier-2 AugL (aliased)
   SetupL st;
 };
+static_assert(sizeof(AugL) <= sizeof(GenWS), "the augmented system aliases the general workspace");
 static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 
 template <int NM, bool FORCES>
-__global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_F32 : HS_MIN_WAVES) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
+__global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FLOAT ? HS_MIN_WAVES_F32 : HS_MIN_WAVES)) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
                                                                                  hs_run_args a, RolloutWS* __restrict__ rws,
                                                                                  hs::launch_map mp) {
   __shared__ Smem<NM, FORCES> smem[2];
@@ -1896,7 +1901,7 @@ __global__ __launch_bounds__(WAVE, (HS_REAL_IS_FLOAT && !FORCES) ? HS_MIN_WAVES_
     forces_step(T, a, mp, sm.st, sm.sv, sm.d.fr, OneWin<NM, FORCES>{&sm.d}, b, live, h_row, lane);
     return;
   } else {
-    step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.gl, sm.d.wk, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
+    step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.wk, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
          lane);
   }
   if (mp.fused_w) {  // this step's joint sum of positive work, summed over the steps in order by the reduce
