@@ -1453,9 +1453,16 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       for (int i = 0; i < 6; i++) h[i] = fl.sc.Ssum[SCH_H + i];
       real lam[6];
       for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
+#ifdef HS_EXP_NO_SCHUR  // timing experiment only: no 6x6 factorization
+      ok = 1;
+      (void)Sm;
+#else
       ok = chol_n<6>(Sm, kFastPivotGuard);
+#endif
       if (ok) {
+#ifndef HS_EXP_NO_SCHUR
         chol_solve_n<6>(Sm, lam);
+#endif
         for (int r = 0; r < 6; r++) fl.sc.lam[r] = lam[r];
       }
       fl.ok[0] = ok;
@@ -1527,7 +1534,13 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   STAMP(6);
   // tier 2 (aug_solve) and the general path share the rollout's global workspace: the general
   // path runs only after tier 2 declined
+#ifdef HS_EXP_NO_SOLVE  // timing experiment only: no contact solve (y = 0)
+  if (lane < k) sv.y[lane] = 0;
+  wave_sync();
+  if (true) {
+#else
   if (a.solve_mode == HS_SOLVE_AUTO && fast_solve(T, sv, fl, *reinterpret_cast<AugL*>(G), w, nc, lane)) {
+#endif
     if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
     if (nc == 1) flags |= HS_FLAG_FULL_RANK;
   } else {
