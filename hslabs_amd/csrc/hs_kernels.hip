@@ -1089,8 +1089,9 @@ __device__ HS_GENERAL_ATTR uint32_t general_solve(const hs_topo* T, SV& sv, G& g
 #endif
 constexpr real kFastPivotGuard = HS_REAL_IS_FLOAT ? real(HS_F32_GUARD) : real(1e-10);
 
+// rl (N): receives 1 / L_jj, the reciprocal each pivot's column was scaled by, for chol_solve_n
 template <int N>
-__device__ inline bool chol_n(real* a, real guard) {  // row-major, in place
+__device__ inline bool chol_n(real* a, real guard, real* rl_out) {  // row-major, in place
   real mx = 0;
 #pragma unroll
   for (int i = 0; i < N; i++) mx = fmax(mx, a[i * N + i]);
@@ -1102,6 +1103,7 @@ __device__ inline bool chol_n(real* a, real guard) {  // row-major, in place
     if (!(s > guard * mx)) return false;
     const real l = sqrt(s), rl = real(1) / l;  // one division per pivot (oracle chol)
     a[j * N + j] = l;
+    rl_out[j] = rl;
 #pragma unroll
     for (int i = j + 1; i < N; i++) {
       real t = a[i * N + j];
@@ -1113,11 +1115,9 @@ __device__ inline bool chol_n(real* a, real guard) {  // row-major, in place
   return true;
 }
 
+// rl: chol_n's reciprocals of the pivots (1 / L_ii, the same divisions, not recomputed)
 template <int N>
-__device__ inline void chol_solve_n(const real* L, real* b) {
-  real rl[N];  // 1 / L_ii (bitwise the reciprocals chol_n formed)
-#pragma unroll
-  for (int i = 0; i < N; i++) rl[i] = real(1) / L[i * N + i];
+__device__ inline void chol_solve_n(const real* L, const real* rl, real* b) {
 #pragma unroll
   for (int i = 0; i < N; i++) {
     real s = b[i];
@@ -1252,9 +1252,10 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, AugL&
     real St[36], lam[6];
     for (int i = 0; i < 36; i++) St[i] = ag.St[i];
     for (int i = 0; i < 6; i++) lam[i] = ag.lam[i];
-    int ok = chol_n<6>(St, kFastPivotGuard);
+    real rl[6];
+    int ok = chol_n<6>(St, kFastPivotGuard, rl);
     if (ok) {
-      chol_solve_n<6>(St, lam);
+      chol_solve_n<6>(St, rl, lam);
       for (int i = 0; i < 6; i++) ag.lam[i] = lam[i];
     }
     ag.ok = ok;
@@ -1321,13 +1322,14 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
     if (nc >= 3) {
       real L[9];
       for (int i = 0; i < 9; i++) L[i] = D[i];
-      ok = chol_n<3>(L, kFastPivotGuard);
+      real rl[3];
+      ok = chol_n<3>(L, kFastPivotGuard, rl);
       if (ok) {
         real Dinv[9];
         for (int j = 0; j < 3; j++) {
           real e[3] = {0, 0, 0};
           e[j] = 1;
-          chol_solve_n<3>(L, e);
+          chol_solve_n<3>(L, rl, e);
           for (int i = 0; i < 3; i++) Dinv[3 * i + j] = e[i];
         }
         // E = A_c D_c^-1 and S_c = E A_c^T with A_c = [-I; [d0]x]: the products by A_c's zeros
@@ -1386,9 +1388,10 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
           for (int r = 0; r < 6; r++) M[3 * i + j] += a_entry(d0, r, i) * a_entry(d0, r, j);
         for (int r = 0; r < 6; r++) b[i] -= a_entry(d0, r, i) * a[r];
       }
-      ok = chol_n<3>(M, kFastPivotGuard);
+      real rl[3];
+      ok = chol_n<3>(M, kFastPivotGuard, rl);
       if (ok) {
-        chol_solve_n<3>(M, b);
+        chol_solve_n<3>(M, rl, b);
         for (int i = 0; i < 3; i++) sv.y[i] = b[i];
       }
       fl.ok[0] = ok;
@@ -1401,7 +1404,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       for (int r = 0; r < 3; r++) { u[r] = f0[r] - f1[r]; un += u[r] * u[r]; }
       un = sqrt(un);
       ok = un > real(1e-12);
-      real nv[6], M[36], b[6];
+      real nv[6], M[36], b[6], rl[6];
       if (ok) {
         for (int r = 0; r < 3; r++) { nv[r] = u[r] / un / sqrt(real(2)); nv[3 + r] = -nv[r]; }
         for (int i = 0; i < 6; i++) {
@@ -1416,10 +1419,10 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
           for (int r = 0; r < 6; r++) s += a_entry(di, r, i % 3) * a[r];
           b[i] = -s;
         }
-        ok = chol_n<6>(M, kFastPivotGuard);
+        ok = chol_n<6>(M, kFastPivotGuard, rl);
       }
       if (ok) {
-        chol_solve_n<6>(M, b);
+        chol_solve_n<6>(M, rl, b);
         real nDn = 0, nr = 0;
         for (int c = 0; c < 2; c++)
           for (int i = 0; i < 3; i++) {
@@ -1451,17 +1454,17 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
 #pragma unroll
         for (int j = 0; j < 6; j++) Sm[6 * i + j] = (j <= i) ? fl.sc.Ssum[sch_lower(i, j)] : real(0);  // upper: unread
       for (int i = 0; i < 6; i++) h[i] = fl.sc.Ssum[SCH_H + i];
-      real lam[6];
+      real lam[6], rl[6];
       for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
 #ifdef HS_EXP_NO_SCHUR  // timing experiment only: no 6x6 factorization
       ok = 1;
       (void)Sm;
 #else
-      ok = chol_n<6>(Sm, kFastPivotGuard);
+      ok = chol_n<6>(Sm, kFastPivotGuard, rl);
 #endif
       if (ok) {
 #ifndef HS_EXP_NO_SCHUR
-        chol_solve_n<6>(Sm, lam);
+        chol_solve_n<6>(Sm, rl, lam);
 #endif
         for (int r = 0; r < 6; r++) fl.sc.lam[r] = lam[r];
       }
