@@ -451,15 +451,24 @@ __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g
   target[2] = dz + st.pos0[j][2];
 }
 
+// sample times t_i = dt + dt + ... (i terms, periodic.cpp:171-181), stored once per rollout by the
+// gait-setup pass (the same additions in the same order) for i < HS_TTAB
+#define HS_TTAB 48
+__device__ inline real sample_time(const SetupL& st, const real* t_tab, int isample) {
+  if (t_tab && isample < HS_TTAB) return t_tab[isample];
+  real t = 0;
+  for (int i = 0; i < isample; i++) t += st.dt;
+  return t;
+}
+
 template <class W>
 __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, int isample, int L,
-                           bool ignore_reach, const W& w, int k) {
+                           bool ignore_reach, const W& w, int k, const real* t_tab) {
   const int j = T->limb_pergen[L];
   const int ysign = T->limb_ysign[L];
   const int clen = T->limb_chain_len[L];
   const int lv[3] = {T->limb_node[L][0], T->limb_node[L][1], T->limb_node[L][2]};
-  real t = 0;  // t accumulates dt (periodic.cpp:171-181)
-  for (int i = 0; i < isample; i++) t += st.dt;
+  const real t = sample_time(st, t_tab, isample);  // t accumulates dt (periodic.cpp:171-181)
   real o0[3], o1[3], target[3];
   bool turned;
   gait_record(g, st, t, j, o0, o1, turned, target);
@@ -1134,6 +1143,58 @@ __device__ inline void chol_solve_n(const real* L, const real* rl, real* b) {
   }
 }
 
+// LDL^T of an N x N SPD matrix in place (row-major; lower part: unit-lower L, diagonal: d), no
+// square roots: pivot d_j = a_jj - sum_k L_jk (L_jk d_k), the Cholesky pivot in exact arithmetic, so
+// the guard (d_j > guard * max diagonal) decides like chol_n's. rd: 1 / d_j. False: a pivot under it.
+template <int N>
+__device__ inline bool ldl_n(real* a, real guard, real* rd) {
+  real mx = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) mx = fmax(mx, a[i * N + i]);
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    real v[N];  // L_jk d_k
+#pragma unroll
+    for (int k = 0; k < j; k++) v[k] = a[j * N + k] * a[k * N + k];
+    real dj = a[j * N + j];
+#pragma unroll
+    for (int k = 0; k < j; k++) dj -= a[j * N + k] * v[k];
+    if (!(dj > guard * mx)) return false;
+    const real r = real(1) / dj;
+    a[j * N + j] = dj;
+    rd[j] = r;
+#pragma unroll
+    for (int i = j + 1; i < N; i++) {
+      real t = a[i * N + j];
+#pragma unroll
+      for (int k = 0; k < j; k++) t -= a[i * N + k] * v[k];
+      a[i * N + j] = t * r;
+    }
+  }
+  return true;
+}
+
+// solve L D L^T x = b in place with ldl_n's factors
+template <int N>
+__device__ inline void ldl_solve_n(const real* L, const real* rd, real* b) {
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    real s = b[i];
+#pragma unroll
+    for (int k = 0; k < i; k++) s -= L[i * N + k] * b[k];
+    b[i] = s;
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) b[i] *= rd[i];
+#pragma unroll
+  for (int i = N - 1; i >= 0; i--) {
+    real s = b[i];
+#pragma unroll
+    for (int k = i + 1; k < N; k++) s -= L[k * N + i] * b[k];
+    b[i] = s;
+  }
+}
+
 __device__ inline void cross_rows(const real* d, real v[3][3]) {
   v[0][0] = 0;     v[0][1] = -d[2]; v[0][2] = d[1];
   v[1][0] = d[2];  v[1][1] = 0;     v[1][2] = -d[0];
@@ -1323,13 +1384,13 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       real L[9];
       for (int i = 0; i < 9; i++) L[i] = D[i];
       real rl[3];
-      ok = chol_n<3>(L, kFastPivotGuard, rl);
+      ok = ldl_n<3>(L, kFastPivotGuard, rl);
       if (ok) {
         real Dinv[9];
         for (int j = 0; j < 3; j++) {
           real e[3] = {0, 0, 0};
           e[j] = 1;
-          chol_solve_n<3>(L, rl, e);
+          ldl_solve_n<3>(L, rl, e);
           for (int i = 0; i < 3; i++) Dinv[3 * i + j] = e[i];
         }
         // E = A_c D_c^-1 and S_c = E A_c^T with A_c = [-I; [d0]x]: the products by A_c's zeros
@@ -1460,11 +1521,11 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       ok = 1;
       (void)Sm;
 #else
-      ok = chol_n<6>(Sm, kFastPivotGuard, rl);
+      ok = ldl_n<6>(Sm, kFastPivotGuard, rl);
 #endif
       if (ok) {
 #ifndef HS_EXP_NO_SCHUR
-        chol_solve_n<6>(Sm, rl, lam);
+        ldl_solve_n<6>(Sm, rl, lam);
 #endif
         for (int r = 0; r < 6; r++) fl.sc.lam[r] = lam[r];
       }
@@ -1840,6 +1901,7 @@ __device__ __attribute__((always_inline)) inline void forces_step(const hs_topo*
 struct RolloutWS {
   GenWS gen;  // also the tier-2 AugL (aliased)
   SetupL st;
+  real t_tab[HS_TTAB];  // sample times (sample_time), with the setup cache
 };
 static_assert(sizeof(AugL) <= sizeof(GenWS), "the augmented system aliases the general workspace");
 static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
@@ -1895,8 +1957,10 @@ __global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FL
       wave_sync();
     } else {
       gait_setup(T, g, a.n_t, sm.st, lane);
-      if (mp.setup_io == hs::SETUP_STORE && live)
+      if (mp.setup_io == hs::SETUP_STORE && live) {
         for (int e = lane; e < NW; e += HALF) cache[e] = lds[e];
+        for (int j = lane; j < HS_TTAB; j += HALF) rws[bb].t_tab[j] = sample_time(sm.st, nullptr, j);
+      }
     }
   }
   if (mp.setup_only) return;
@@ -1909,7 +1973,9 @@ __global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FL
 #ifndef HS_EXP_KIN_FIRST
 #define HS_EXP_KIN_FIRST 0  // timing experiment only: samples below this offset are not computed
 #endif
-    if (sl < NS && sl >= HS_EXP_KIN_FIRST) kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2);
+    if (sl < NS && sl >= HS_EXP_KIN_FIRST)
+      kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
+                 mp.setup_io == hs::SETUP_LOAD ? rws[bb].t_tab : nullptr);
     wave_sync();
   }
   STAMP(2);

@@ -1437,6 +1437,40 @@ void chol_solve(const double* L, int n, double* b) {
   }
 }
 
+// LDL^T (the kernel's ldl_n): unit-lower L below the diagonal, d on it; pivot guard as chol's
+bool ldl(double* a, int n, double guard) {
+  double mx = 0;
+  for (int i = 0; i < n; i++) mx = std::max(mx, a[i * n + i]);
+  double v[18];
+  for (int j = 0; j < n; j++) {
+    for (int k = 0; k < j; k++) v[k] = a[j * n + k] * a[k * n + k];
+    double dj = a[j * n + j];
+    for (int k = 0; k < j; k++) dj -= a[j * n + k] * v[k];
+    if (!(dj > guard * mx)) return false;
+    const double r = 1.0 / dj;
+    a[j * n + j] = dj;
+    for (int i = j + 1; i < n; i++) {
+      double t = a[i * n + j];
+      for (int k = 0; k < j; k++) t -= a[i * n + k] * v[k];
+      a[i * n + j] = t * r;
+    }
+  }
+  return true;
+}
+void ldl_solve(const double* L, int n, double* b) {
+  for (int i = 0; i < n; i++) {
+    double s = b[i];
+    for (int k = 0; k < i; k++) s -= L[i * n + k] * b[k];
+    b[i] = s;
+  }
+  for (int i = 0; i < n; i++) b[i] *= 1.0 / L[i * n + i];
+  for (int i = n - 1; i >= 0; i--) {
+    double s = b[i];
+    for (int k = i + 1; k < n; k++) s -= L[k * n + i] * b[k];
+    b[i] = s;
+  }
+}
+
 // rows of [d]x: ([d]x w)_r = v_r . w
 inline void cross_rows(const double* d, double v[3][3]) {
   v[0][0] = 0;     v[0][1] = -d[2]; v[0][2] = d[1];
@@ -1588,11 +1622,11 @@ bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<d
   for (int c = 0; c < nc; c++) {
     double L[9];
     for (int i = 0; i < 9; i++) L[i] = D[9 * c + i];
-    if (!chol(L, 3, kFastPivotGuard)) return aug_solve(nc, A, D, g, a, y);
+    if (!ldl(L, 3, kFastPivotGuard)) return aug_solve(nc, A, D, g, a, y);
     for (int j = 0; j < 3; j++) {  // Dinv columns
       double e[3] = {0, 0, 0};
       e[j] = 1;
-      chol_solve(L, 3, e);
+      ldl_solve(L, 3, e);
       for (int i = 0; i < 3; i++) Dinv[9 * c + 3 * i + j] = e[i];
     }
     const double* Ac = &A[18 * c];
@@ -1616,8 +1650,8 @@ bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<d
   }
   double lam[6];
   for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
-  if (!chol(S, 6, kFastPivotGuard)) return aug_solve(nc, A, D, g, a, y);
-  chol_solve(S, 6, lam);
+  if (!ldl(S, 6, kFastPivotGuard)) return aug_solve(nc, A, D, g, a, y);
+  ldl_solve(S, 6, lam);
   for (int c = 0; c < nc; c++) {
     const double* Ac = &A[18 * c];
     double t[3];
