@@ -1,6 +1,7 @@
-set -o pipefail
-cd $GRAFT_REPO_ROOT; O=gpurun_out/t7; mkdir -p $O
-timeout -k 10 120 python tools/variant_dump.py $O/base.npz > $O/d1.log 2>&1 || { tail $O/d1.log; exit 1; }
-timeout -k 10 120 env HSLABS_VARIANT=new python tools/variant_dump.py $O/new.npz > $O/d2.log 2>&1 || { tail $O/d2.log; exit 1; }
-python tools/variant_dump.py --compare $O/base.npz $O/new.npz | head -8; rm -f $O/*.npz
-VARIANTS="base new" REPS=3 TAG=ab7 bash tools/gpu_ab.sh
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/pv2; mkdir -p $O
+for v in base straight; do
+  if [ $v = base ]; then unset HSLABS_VARIANT; else export HSLABS_VARIANT=$v; fi
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 --output-format csv -d $O/$v -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu > $O/$v.log 2>&1 || { echo "$v failed"; tail -3 $O/$v.log; exit 1; }
+done
+cd $R && VARIANTS="base straight" REPS=2 TAG=ab8 bash tools/gpu_ab.sh
