@@ -471,33 +471,32 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         comm = H.Comm(world, rank, uid[0])
 
-    def run_k(k, best):
-        batch.key_steps = k * Hh  # the key's work covers the k calls of this job
-        if fused:
-            batch.run_calls(k, call_horizon=Hh, stream=stream, best=best, accumulate=True)
-        else:
-            batch.run_steps(k, stream=stream, best=best, accumulate=True)
-
     def launcher_k(k, best):
-        """the timed job: the same native call as run_k, its arguments resolved before the clock starts"""
+        """a job of k steps (the native launches), its arguments resolved before the clock starts"""
         batch.key_steps = k * Hh
         if fused:
             return batch.calls_launcher(k, call_horizon=Hh, stream=stream, best=best, accumulate=True)
-        return lambda: batch.run_steps(k, stream=stream, best=best, accumulate=True)
 
-    # warmup (untimed): the same native launches as the timed region, and the collective once
+        def steps():
+            batch.key_steps = k * Hh
+            batch.run_steps(k, stream=stream, best=best, accumulate=True)
+        return steps
+
+    # warmup (untimed): the same native launches as the timed region, and the collective once. Every
+    # host-side preparation of the timed job happens before it, so the timed job follows the warmup
+    # with no more idle GPU time than the barrier and the synchronize (idle time lowers the clocks the
+    # next job starts at: tools/sync_probe.py)
     batch.k0 = 0
+    warm = launcher_k(args.warmup, best=True)
+    job = launcher_k(args.steps, best=True)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     batch.work_cot.zero_()
     batch.reset_best()
-    run_k(args.warmup, best=True)
+    warm()
     if comm is not None:
         comm.reduce_best(batch.best_key, stream)
-    torch.cuda.synchronize()
-    batch.work_cot.zero_()
+    batch.work_cot.zero_()  # queued behind the warmup on the same stream
     batch.reset_best()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    batch.k0 = 0
-    job = launcher_k(args.steps, best=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

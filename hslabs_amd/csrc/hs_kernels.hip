@@ -400,11 +400,7 @@ __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g
   real tv = t * st.v;
   turned = false;
   real psi = 0;
-#ifdef HS_EXP_STRAIGHT  // timing experiment only: straight gaits compiled alone
-  if (false) {
-#else
   if (g.curvature != 0) {
-#endif
     int s = (g.curvature > 0) ? 1 : -1;
     psi = s * tv / st.max_radius;
     turned = psi != 0;
@@ -435,11 +431,7 @@ __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g
   real dx = (t_int + st.xs[j] + sx) * g.step_length;
   real dy = 0;
   real dz = sz * g.step_height;
-#ifdef HS_EXP_STRAIGHT
-  if (false) {
-#else
   if (g.curvature != 0) {  // turn_position (pergen.cpp:160-183)
-#endif
     int s = (g.curvature > 0) ? 1 : -1;
     real x0 = st.pos0[j][0], y0 = st.pos0[j][1];
     real rc = real(1) / g.curvature;

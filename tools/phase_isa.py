@@ -27,6 +27,8 @@ CLASSES = [
     ("valu", r"^v_"),
     ("salu", r"^s_"),
     ("branch", r"^s_(cbranch|branch)"),
+    ("sgpr_spill", r"^v_(readlane|writelane)_b32"),
+    ("vgpr_spill", r"^scratch_"),
 ]
 
 
