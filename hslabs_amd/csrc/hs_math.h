@@ -181,15 +181,6 @@ __device__ inline void euler_from(const A34& A, real* ang) {
   ang[2] = atan2(r21 / ct1, r11 / ct1);
 }
 
-// mod_twopi (visualization.cpp:73-79); bounded loops
-__device__ inline void mod_twopi(real& a) {
-  if (a < -kPi) {
-    for (int i = 0; i < 64 && a < -kPi; i++) a += 2 * kPi;
-  } else if (a > kPi) {
-    for (int i = 0; i < 64 && a > kPi; i++) a -= 2 * kPi;
-  }
-}
-
 __device__ inline real norm3(const real* v) {
   real s = real(0);
   s = s + v[0] * v[0];
@@ -198,44 +189,41 @@ __device__ inline real norm3(const real* v) {
   return sqrt(s);
 }
 
-// limb_solver_yxx (lik.cpp:151-184) and limb_solver_zxx (lik.cpp:189-223), bend = true
+// limb_solver_yxx (lik.cpp:151-184) and limb_solver_zxx (lik.cpp:189-223), bend = true, as one
+// straight-line sequence (kind only picks constants, so the independent atan2 and acos chains share
+// a basic block the scheduler can interleave); every operation is the solvers' own:
+//   yxx: d = p - (0, 0, s0 l0), c = (p2 - s0 l0) / l, theta = acos c + (1 - s0) pi/2,
+//        beta = s0 acos(.), gamma = s0 acos(.)
+//   zxx: d = p + (0, 0, l0),    c = (p2 + l0) / l,    theta = acos c - s0 pi/2,
+//        beta = acos(.),    gamma = acos(.)
+// (x - (-l0) = x + l0 and the angle offsets are exact). mod_twopi (visualization.cpp:73-79): atan2
+// is already in [-pi, pi], and theta in [0, 2 pi] (yxx) or [-pi/2, 3 pi/2] (zxx) needs at most one
+// subtraction of 2 pi.
 __device__ inline void limb_ik(int kind, const real* ls, int ysign, const real* p, real* ja, bool ignore_reach,
                                bool& unreach, bool& fail) {
-  real l0 = ls[0], l1 = ls[1], l2 = ls[2];
-  int s0 = ysign;
-  int s1 = 1;
+  const real l0 = ls[0], l1 = ls[1], l2 = ls[2];
+  const int s0 = ysign;
+  const bool yxx = kind == HS_LIK_YXX;
+  const real z0 = yxx ? s0 * l0 : -l0;
   real d[3];
-  if (kind == HS_LIK_YXX) {
-    real z0 = s0 * l0;
-    d[0] = p[0] - real(0); d[1] = p[1] - real(0); d[2] = p[2] - z0;
-  } else {
-    d[0] = p[0] + real(0); d[1] = p[1] + real(0); d[2] = p[2] + l0;
-  }
+  d[0] = p[0] - real(0); d[1] = p[1] - real(0); d[2] = p[2] - z0;
   real l = norm3(d);
-  if (l1 + l2 - l < 0) {
-    if (ignore_reach) { l = l1 + l2; unreach = true; }
-    else { fail = true; }
+  const bool out = l1 + l2 - l < 0;
+  if (out) {
+    if (ignore_reach) unreach = true;
+    else fail = true;
   }
-  real c, theta, phi = atan2(p[0], p[1]);
-  if (kind == HS_LIK_YXX) {
-    c = (p[2] - s0 * l0) / l;
-    theta = acos(c) + (1 - s0) * kPi / 2;
-  } else {
-    c = (p[2] + l0) / l;
-    theta = acos(c) - s0 * kPi / 2;
-  }
-  mod_twopi(phi);
-  mod_twopi(theta);
-  real ll = l * l;
-  real del = l2 * l2 - l1 * l1;
-  real beta, gamma;
-  if (kind == HS_LIK_YXX) {
-    beta = s1 * s0 * acos((ll - del) / (2 * l1 * l));
-    gamma = s1 * s0 * acos((ll + del) / (2 * l2 * l));
-  } else {
-    beta = s1 * acos((ll - del) / (2 * l1 * l));
-    gamma = s1 * acos((ll + del) / (2 * l2 * l));
-  }
+  l = (out && ignore_reach) ? l1 + l2 : l;
+  const real phi = atan2(p[0], p[1]);
+  const real c = (p[2] - z0) / l;
+  const real toff = yxx ? (s0 > 0 ? real(0) : kPi) : (s0 > 0 ? -kPi / 2 : kPi / 2);
+  real theta = acos(c) + toff;
+  theta = (theta > kPi) ? theta - 2 * kPi : theta;
+  const real ll = l * l;
+  const real del = l2 * l2 - l1 * l1;
+  const real sb = yxx ? real(s0) : real(1);  // s1 s0 (yxx) or s1 (zxx), s1 = 1 (bend)
+  const real beta = sb * acos((ll - del) / (2 * l1 * l));
+  const real gamma = sb * acos((ll + del) / (2 * l2 * l));
   ja[0] = -phi;
   ja[1] = -theta + beta;
   ja[2] = -(beta + gamma);
