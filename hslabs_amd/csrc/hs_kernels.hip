@@ -393,6 +393,9 @@ __device__ __attribute__((always_inline)) inline void node_features(const hs_top
 // pergensetup::set_rec at time t for lik limb L (pergen.cpp:225-239): torso position o0 and Euler
 // angles o1 (turn_torso, pergen.cpp:386-397; `turned` when the torso frame was rotated), and the
 // limb's foot target (limb_positions of its pergen index, pergen.cpp:82-94, 160-183)
+// STRAIGHT: the caller knows curvature == 0 (a wave of straight gaits), so the turning code is left
+// out and the record is one basic block the scheduler can interleave with the torso FK
+template <bool STRAIGHT = false>
 __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g, const SetupL& st, real t, int j,
                                                                   real* o0, real* o1, bool& turned, real* target) {
   o0[0] = g.torso_pos[0]; o0[1] = g.torso_pos[1]; o0[2] = g.torso_pos[2];
@@ -400,7 +403,7 @@ __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g
   real tv = t * st.v;
   turned = false;
   real psi = 0;
-  if (g.curvature != 0) {
+  if (!STRAIGHT && g.curvature != 0) {
     int s = (g.curvature > 0) ? 1 : -1;
     psi = s * tv / st.max_radius;
     turned = psi != 0;
@@ -431,7 +434,7 @@ __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g
   real dx = (t_int + st.xs[j] + sx) * g.step_length;
   real dy = 0;
   real dz = sz * g.step_height;
-  if (g.curvature != 0) {  // turn_position (pergen.cpp:160-183)
+  if (!STRAIGHT && g.curvature != 0) {  // turn_position (pergen.cpp:160-183)
     int s = (g.curvature > 0) ? 1 : -1;
     real x0 = st.pos0[j][0], y0 = st.pos0[j][1];
     real rc = real(1) / g.curvature;
@@ -461,7 +464,7 @@ __device__ inline real sample_time(const SetupL& st, const real* t_tab, int isam
   return t;
 }
 
-template <class W>
+template <bool STRAIGHT, class W>
 __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, int isample, int L,
                            bool ignore_reach, const W& w, int k, const real* t_tab) {
   const int j = T->limb_pergen[L];
@@ -471,11 +474,11 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
   const real t = sample_time(st, t_tab, isample);  // t accumulates dt (periodic.cpp:171-181)
   real o0[3], o1[3], target[3];
   bool turned;
-  gait_record(g, st, t, j, o0, o1, turned, target);
+  gait_record<STRAIGHT>(g, st, t, j, o0, o1, turned, target);
   STAMP(20);
   // set_jvalues_with_lik: torso + body chain FK, then limb IK (model.cpp:354-359, lik.cpp:89-99)
   real q6[6] = {o0[0], o0[1], o0[2], o1[0], o1[1], o1[2]};
-  const A34 F = turned ? free_joint(q6) : free_joint_sc(q6, st.tsc);  // straight gait: torso angles fixed
+  const A34 F = (!STRAIGHT && turned) ? free_joint(q6) : free_joint_sc(q6, st.tsc);  // straight: angles fixed
   const NodeK n0 = load_nodek(T, 0);  // the torso
   A34 A0 = mul(mul(n0.Jp, F), n0.pj);
   const bool wq = w.want_q(k);
@@ -1973,9 +1976,15 @@ __global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FL
 #ifndef HS_EXP_KIN_FIRST
 #define HS_EXP_KIN_FIRST 0  // timing experiment only: samples below this offset are not computed
 #endif
-    if (sl < NS && sl >= HS_EXP_KIN_FIRST)
-      kin_sample(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
-                 mp.setup_io == hs::SETUP_LOAD ? rws[bb].t_tab : nullptr);
+    const real* t_tab = mp.setup_io == hs::SETUP_LOAD ? rws[bb].t_tab : nullptr;
+    // both rollouts of the wave straight (the common case): the specialization without turning code
+    if (__ballot(g.curvature != 0) == 0) {
+      if (sl < NS && sl >= HS_EXP_KIN_FIRST)
+        kin_sample<true>(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2, t_tab);
+    } else {
+      if (sl < NS && sl >= HS_EXP_KIN_FIRST)
+        kin_sample<false>(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2, t_tab);
+    }
     wave_sync();
   }
   STAMP(2);
@@ -2026,7 +2035,7 @@ __global__ __launch_bounds__(WAVE) void hs_pergen_rec_kernel(const hs_topo* __re
   if (live && lane < nl) {
     real o0[3], o1[3], target[3];
     bool turned;
-    gait_record(g, st[sub], (real)times[ti], T->limb_pergen[lane], o0, o1, turned, target);
+    gait_record<false>(g, st[sub], (real)times[ti], T->limb_pergen[lane], o0, o1, turned, target);
     double* r = rec + it * (6 + 3 * nl);
     if (lane == 0)
       for (int i = 0; i < 3; i++) { r[i] = o0[i]; r[3 + i] = o1[i]; }
