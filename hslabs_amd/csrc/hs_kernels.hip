@@ -2131,8 +2131,9 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
 
 __global__ void hs_fused_reduce_kernel(hs_run_args a, real total_mass, const double* __restrict__ rollout_mass,
                                        const real* __restrict__ ws, int n_steps) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= a.n_rollouts) return;
+  const int b0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = b0 < a.n_rollouts;
+  const int b = live ? b0 : a.n_rollouts - 1;  // dead lanes load a valid row and store nothing
   if (rollout_mass) total_mass = (real)rollout_mass[b];  // a mixed plan: the rollout's model
   real w = a.accumulate ? outp(a.work_cot)[2 * (size_t)b] : real(0);
   const real dt = (real)a.params[b].period / a.n_t;  // gait_setup's st.dt
@@ -2148,11 +2149,19 @@ __global__ void hs_fused_reduce_kernel(hs_run_args a, real total_mass, const dou
   for (; s < n_steps; s++) w = fma(ws[(size_t)s * a.n_rollouts + b], dt, w);
   const real L = (real)a.params[b].step_length;
   const real cot = w / (total_mass * L);
-  outp(a.work_cot)[2 * (size_t)b] = w;
-  outp(a.work_cot)[2 * (size_t)b + 1] = cot;
-  if (a.best_key) {
+  if (live) {
+    outp(a.work_cot)[2 * (size_t)b] = w;
+    outp(a.work_cot)[2 * (size_t)b + 1] = cot;
+  }
+  if (a.best_key) {  // the wave's minimum first: one atomic per wave, not one per rollout on one address
     const real kc = key_cot(w, total_mass, L, a.n_t, a.key_steps);
-    atomicMin((unsigned long long*)a.best_key, (unsigned long long)best_key(kc, a.rollout_id_base + b));
+    unsigned long long k = live ? (unsigned long long)best_key(kc, a.rollout_id_base + b) : ~0ull;
+#pragma unroll
+    for (int off = WAVE / 2; off >= 1; off >>= 1) {
+      const unsigned long long o = __shfl_xor(k, off);
+      k = o < k ? o : k;
+    }
+    if (threadIdx.x == 0) atomicMin((unsigned long long*)a.best_key, k);
   }
 }
 
