@@ -1909,6 +1909,37 @@ struct RolloutWS {
 static_assert(sizeof(AugL) <= sizeof(GenWS), "the augmented system aliases the general workspace");
 static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 
+// The fused path's setup pass (hs_run_calls: gait setup once per rollout, stored for every step):
+// the rollout kernel's prologue and setup store alone, as its own small kernel (2 x 320 B of LDS, few
+// registers) so the pass does not carry the step kernel's code, registers and LDS
+__global__ __launch_bounds__(WAVE) void hs_setup_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
+                                                        RolloutWS* __restrict__ rws, hs::launch_map mp) {
+  __shared__ SetupL sst[2];
+  const int sub = threadIdx.x / HALF, lane = threadIdx.x % HALF;
+  const int wid = (int)blockIdx.x;
+  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
+  int b;
+  bool live;
+  if (mp.wave_rollouts) {
+    b = mp.wave_rollouts[2 * wid + sub];
+    live = b >= 0;
+    if (!live) b = mp.wave_rollouts[2 * wid];
+  } else {
+    b = wid * 2 + sub;
+    live = b < a.n_rollouts;
+    if (!live) b = a.n_rollouts - 1;
+  }
+  const GaitR g = load_gait(a.params[b]);
+  gait_setup(T, g, a.n_t, sst[sub], lane);  // every lane of the wave takes part (wave_sync inside)
+  if (live) {
+    constexpr int NW = sizeof(SetupL) / sizeof(real);
+    real* cache = reinterpret_cast<real*>(&rws[b].st);
+    const real* lds = reinterpret_cast<const real*>(&sst[sub]);
+    for (int e = lane; e < NW; e += HALF) cache[e] = lds[e];
+    for (int j = lane; j < HS_TTAB; j += HALF) rws[b].t_tab[j] = sample_time(sst[sub], nullptr, j);
+  }
+}
+
 template <int NM, bool FORCES>
 __global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FLOAT ? HS_MIN_WAVES_F32 : HS_MIN_WAVES)) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
                                                                                  hs_run_args a, RolloutWS* __restrict__ rws,
@@ -2120,6 +2151,13 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   if (a.n_rollouts <= 0 || mp.n_waves <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
   RolloutWS* ws = (RolloutWS*)workspace;
+#ifndef HS_SETUP_KERNEL
+#define HS_SETUP_KERNEL 1
+#endif
+  if (HS_SETUP_KERNEL && mp.setup_only) {
+    hipLaunchKernelGGL(hs_setup_kernel, dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
+    return (int)hipGetLastError();
+  }
   launch_map m = mp;
   m.fused_w = mp.setup_only ? 0 : mp.n_waves;
   m.n_waves = mp.setup_only ? mp.n_waves : mp.n_waves * mp.fused_n;  // the grid
