@@ -42,10 +42,11 @@ void free_on_device(int dev, void* p) {
 
 }  // namespace
 
-int ws_pool::get(void* stream, size_t n, void** out) {
+int ws_pool::get(void* stream, size_t n, void** out, bool* fresh) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return (int)e;
+  if (fresh) *fresh = false;
   for (slot& s : live) {
     if (s.dev != dev || s.stream != stream) continue;
     if (s.n < n) {
@@ -55,6 +56,7 @@ int ws_pool::get(void* stream, size_t n, void** out) {
       retired.emplace_back(dev, s.ptr);
       s.ptr = w;
       s.n = n;
+      if (fresh) *fresh = true;
     }
     *out = s.ptr;
     return 0;
@@ -64,6 +66,7 @@ int ws_pool::get(void* stream, size_t n, void** out) {
   if (e != hipSuccess) return (int)e;
   live.push_back({dev, stream, w, n});
   *out = w;
+  if (fresh) *fresh = true;
   return 0;
 }
 
@@ -176,7 +179,8 @@ int check_args(const hs_model_s* m, const hs_run_args* a) {
 // hs_run_calls / hs_run_mixed_calls: a setup-only pass, launches of CHUNK steps over (step, wavefront),
 // the in-order work reduce. Each step in flight in a launch has its own general-path scratch.
 int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map mp, ws_pool& gen_pool,
-              ws_pool& work_pool, std::mutex& mu, double total_mass, const double* rollout_mass, int32_t n_calls) {
+              ws_pool& work_pool, ws_pool& fix_pool, std::mutex& mu, double total_mass, const double* rollout_mass,
+              int32_t n_calls) {
   const int64_t S = (int64_t)n_calls * a.horizon;  // steps, one output row each
   if (S > (1 << 24)) return fail(HS_E_ARG, "too many steps");
   // steps per launch: the launch refills the SIMDs from its queue of wavefronts (the batch's last
@@ -195,8 +199,15 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
 #endif
   const int32_t B = a.n_rollouts;
   const int32_t CHUNK = std::max(1, std::min(HS_FUSED_MAX_STEPS, HS_FUSED_WAVES / std::max(1, mp.n_waves)));
+  const int32_t n_chunks = (int32_t)((S + CHUNK - 1) / CHUNK);
   const size_t gwb = hs::general_workspace_bytes();
-  void *gen = nullptr, *work = nullptr;
+  // steps the closed form declines (every step in HS_SOLVE_REFERENCE) are deferred to a fixup launch
+  // after each step launch, so the step kernel carries no call to the general path; one counter per
+  // launch, then the items
+  const bool defer = true;
+  const size_t fix_counts_bytes = ((size_t)n_chunks * sizeof(int32_t) + 255) / 256 * 256;
+  const size_t fix_bytes = fix_counts_bytes + (size_t)CHUNK * mp.n_waves * 2 * 2 * sizeof(int32_t);
+  void *gen = nullptr, *work = nullptr, *fix = nullptr;
   {
     std::lock_guard<std::mutex> lk(mu);
     hipError_t e = (hipError_t)gen_pool.get(a.stream, (size_t)CHUNK * (B + 1), &gen);
@@ -207,8 +218,14 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
     const size_t want =
         std::max(need, std::min((size_t)HS_FUSED_RESERVE_STEPS * B * sizeof(double), (size_t)512 << 20));
     if (e == hipSuccess) e = (hipError_t)work_pool.get(a.stream, (want + gwb - 1) / gwb, &work);
+    bool fresh = false;
+    if (e == hipSuccess && defer) e = (hipError_t)fix_pool.get(a.stream, (fix_bytes + gwb - 1) / gwb, &fix, &fresh);
+    // new counters start at zero; afterwards every call's work reduce leaves them zeroed
+    if (e == hipSuccess && fresh) e = hipMemsetAsync(fix, 0, fix_counts_bytes, (hipStream_t)a.stream);
     if (e != hipSuccess) return hip_fail(e, "hipMalloc(fused workspace)");
   }
+  int32_t* fix_counts = defer ? (int32_t*)fix : nullptr;
+  int32_t* fix_items = defer ? (int32_t*)((char*)fix + fix_counts_bytes) : nullptr;
   const bool f32 = a.precision == HS_PREC_F32;
   hs_run_args c = a;
   c.horizon = (int32_t)S;  // output rows per rollout
@@ -223,15 +240,28 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   mp.setup_only = 0;
   mp.setup_io = hs::SETUP_LOAD;
-  for (int64_t s0 = 0; le == 0 && s0 < S; s0 += CHUNK) {
+  mp.fix_items = fix_items;
+  for (int64_t s0 = 0, ci = 0; le == 0 && s0 < S; s0 += CHUNK, ci++) {
     mp.fused_s0 = (int32_t)s0;
     mp.fused_n = (int32_t)std::min<int64_t>(CHUNK, S - s0);
+    mp.fix_mode = defer ? hs::FIX_DEFER : hs::FIX_NONE;
+    mp.fix_count = defer ? fix_counts + ci : nullptr;
     le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+    if (le == 0 && defer) {  // the same steps' declined (step, rollout) items, with the general path
+      mp.fix_mode = hs::FIX_SOLVE;
+      le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+    }
   }
   if (le == 0)
-    le = f32 ? hs::launch_fused_reduce_f32(r, total_mass, rollout_mass, work, (int32_t)S)
-             : hs::launch_fused_reduce(r, total_mass, rollout_mass, work, (int32_t)S);
-  if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
+    le = f32 ? hs::launch_fused_reduce_f32(r, total_mass, rollout_mass, work, (int32_t)S, fix_counts,
+                                           defer ? n_chunks : 0)
+             : hs::launch_fused_reduce(r, total_mass, rollout_mass, work, (int32_t)S, fix_counts,
+                                       defer ? n_chunks : 0);
+  if (le != 0) {
+    if (defer)  // counters a failed call may have left behind
+      (void)hipMemsetAsync(fix_counts, 0, fix_counts_bytes, (hipStream_t)a.stream);
+    return hip_fail((hipError_t)le, "kernel launch");
+  }
   return HS_OK;
 }
 
@@ -263,7 +293,7 @@ struct hs_mixed_s {
   int32_t* d_wave_rollouts = nullptr;
   double* d_rollout_mass = nullptr;  // total mass of each rollout's model (the fused reduce's COT)
   ws_pool ws;
-  ws_pool fused_gen, fused_work;
+  ws_pool fused_gen, fused_work, fused_fix;
   std::mutex mu;
 };
 
@@ -301,6 +331,7 @@ void hs_model_free(hs_model_t m) {
   m->ws.release();
   m->fused_gen.release();
   m->fused_work.release();
+  m->fused_fix.release();
   delete m;
 }
 
@@ -375,8 +406,8 @@ int hs_run_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls) {
   void* ws = nullptr;
   rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);
   if (rc != HS_OK) return rc;
-  return run_fused(d, *a, ws, hs::single_model_map(m->host, a->n_rollouts), m->fused_gen, m->fused_work, m->mu,
-                   m->host.total_mass, nullptr, n_calls);
+  return run_fused(d, *a, ws, hs::single_model_map(m->host, a->n_rollouts), m->fused_gen, m->fused_work,
+                   m->fused_fix, m->mu, m->host.total_mass, nullptr, n_calls);
 }
 
 int hs_run_pd(hs_model_t m, const hs_run_args* a, const hs_pd_args* pd) {
@@ -489,6 +520,7 @@ void hs_mixed_free(hs_mixed_t p) {
   p->ws.release();
   p->fused_gen.release();
   p->fused_work.release();
+  p->fused_fix.release();
   delete p;
 }
 
@@ -555,7 +587,8 @@ int hs_run_mixed_calls(hs_mixed_t p, const hs_run_args* a, int32_t n_calls) {
     e = (hipError_t)p->ws.get(a->stream, (size_t)p->n_rollouts + 1, &ws);
   }
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
-  return run_fused(p->d_topos, *a, ws, mp, p->fused_gen, p->fused_work, p->mu, 0.0, p->d_rollout_mass, n_calls);
+  return run_fused(p->d_topos, *a, ws, mp, p->fused_gen, p->fused_work, p->fused_fix, p->mu, 0.0, p->d_rollout_mass,
+                   n_calls);
 }
 
 int hs_complete_traj(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n_t, int32_t ignore_reach,

@@ -23,6 +23,11 @@ int read_pgs_config(const char* path, int setup_id, hs_gait_params* out, std::st
 // Gait setup (pergensetup::setup_pergen, once per rollout in the reference) across the
 // launches of one call: the first launch computes and stores it per rollout, the rest load it.
 enum { SETUP_COMPUTE = 0, SETUP_STORE = 1, SETUP_LOAD = 2 };
+// Steps the closed form declines, in fused launches (hs_run_calls, HS_SOLVE_AUTO): the step launch
+// (FIX_DEFER) appends (local step, 2 * wavefront + half) items to fix_items and counts them in
+// *fix_count instead of calling the general path; the fixup launch after it (FIX_SOLVE, the
+// instantiation with the general path) recomputes those steps and stores their outputs and work.
+enum { FIX_NONE = 0, FIX_DEFER = 1, FIX_SOLVE = 2 };
 
 // Which rollouts a launch's wavefronts run and where their output rows go.
 struct launch_map {
@@ -48,6 +53,9 @@ struct launch_map {
   void* fused_work;
   void* fused_gen;
   int32_t setup_only;
+  int32_t fix_mode;     // FIX_*
+  int32_t* fix_count;   // items appended by the step launch (reset by the work reduce)
+  int32_t* fix_items;   // [2 * item]: local step, 2 * wavefront + half
 };
 
 // Kernel launcher (hs_kernels.hip). `workspace` holds general_workspace_bytes()
@@ -65,10 +73,11 @@ int launch_fused_f32(const hs_topo* d_topo, const hs_run_args& a, void* workspac
 // work_cot[b] = (w, w / (total_mass * step_length)) with w = (accumulate ? work_cot[b][0] : 0) + the steps'
 // work in step order, then the best key
 // (rollout_mass: per-rollout total mass of a mixed plan, else null and total_mass)
+// (fix_counts: the call's per-launch fixup counters, zeroed here for the next call)
 int launch_fused_reduce(const hs_run_args& a, double total_mass, const double* rollout_mass, const void* work_steps,
-                        int32_t n_steps);
+                        int32_t n_steps, int32_t* fix_counts, int32_t n_fix_counts);
 int launch_fused_reduce_f32(const hs_run_args& a, double total_mass, const double* rollout_mass,
-                            const void* work_steps, int32_t n_steps);
+                            const void* work_steps, int32_t n_steps, int32_t* fix_counts, int32_t n_fix_counts);
 
 // pergensetup::set_rec for n_rollouts x n_times items (hs_kernels.hip), rec [B][n_times][6 + 3 n_limbs]
 int launch_pergen_rec(const hs_topo* d_topo, const hs_gait_params* params, int32_t n_rollouts, const double* times,
@@ -102,7 +111,8 @@ struct ws_pool {
   std::vector<slot> live;
   std::vector<std::pair<int, void*>> retired;  // outgrown: kernels still queued may use them
   // workspace of >= n rollouts for (current device, stream); returns a hipError_t value
-  int get(void* stream, size_t n, void** out);
+  // (*fresh, if given: the slot was (re)allocated by this call)
+  int get(void* stream, size_t n, void** out, bool* fresh = nullptr);
   void release();
 };
 
@@ -114,5 +124,6 @@ struct hs_model_s {
   hs_simtopo_t<float>* sim_dev_f32[HS_MAX_DEVICES];  // rounded copy for the single-precision kernel
   ws_pool ws;
   ws_pool fused_gen, fused_work;  // hs_run_calls: general-path scratch per (step in a launch, rollout), step work
+  ws_pool fused_fix;              // hs_run_calls: fixup counters and items
   std::mutex mu;
 };

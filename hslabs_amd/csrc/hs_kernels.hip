@@ -1581,10 +1581,14 @@ __device__ inline uint64_t best_key(real cot, int64_t id) {
 // ---------------------------------------------------------------------------
 // One control-loop step at centre sample i (row = b * H + h of the outputs)
 // ---------------------------------------------------------------------------
-template <class W, class SV>
+// DEFER: a step the closed form declines is not solved here but handed to the fixup launch (the
+// step's half-wave stores nothing and `deferred` is set), so this instantiation has no call to the
+// out-of-line general path: the call alone costs the whole kernel SGPRs (spills in the hot solve
+// region) and 2.4 % of the step time
+template <bool DEFER, class W, class SV>
 __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st, SV& sv,
                      FastL& fl, WorkL& wk, const W& w, GenWS* G, int b, bool live, int h,
-                     real& work, int lane) {
+                     real& work, bool& deferred, bool may_general, int lane) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
   STAMP(3);
   dynamics(T, st, sv, w, lane);
@@ -1611,7 +1615,16 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
     if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
     if (nc == 1) flags |= HS_FLAG_FULL_RANK;
   } else {
-    flags = general_solve(T, sv, *G, w, k, lane) | HS_FLAG_GENERAL;
+#ifdef HS_EXP_NO_GENERAL  // timing experiment only: no general path (its steps keep y unset)
+    flags = HS_FLAG_GENERAL;
+#else
+    if constexpr (DEFER) {
+      deferred = true;  // uniform over the half-wave: its outputs come from the fixup launch
+      live = false;
+    } else if (may_general) {
+      flags = general_solve(T, sv, *G, w, k, lane) | HS_FLAG_GENERAL;
+    }
+#endif
   }
   STAMP(7);
 
@@ -1940,20 +1953,17 @@ __global__ __launch_bounds__(WAVE) void hs_setup_kernel(const hs_topo* __restric
   }
 }
 
-template <int NM, bool FORCES>
-__global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FLOAT ? HS_MIN_WAVES_F32 : HS_MIN_WAVES)) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
-                                                                                 hs_run_args a, RolloutWS* __restrict__ rws,
-                                                                                 hs::launch_map mp) {
-  __shared__ Smem<NM, FORCES> smem[2];
-  RSTAMP(16);
-  STAMP(15);
+// One wavefront's step: fused step fstep (0 outside fused launches) of batch wavefront wid. only_sub
+// >= 0 (the fixup launch): only that half stores, the other computes a copy and stores nothing.
+template <int NM, bool FORCES, bool DEFER>
+__device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo* __restrict__ T0, const hs_run_args& a,
+                                                                   RolloutWS* __restrict__ rws, const hs::launch_map& mp,
+                                                                   Smem<NM, FORCES>* smem, int fstep, int wid,
+                                                                   int only_sub) {
   const int sub = threadIdx.x / HALF;  // rollout slot within the wave
   const int lane = threadIdx.x % HALF; // lane within the rollout
   // one model per wavefront: the topology pointer stays wave-uniform (scalar loads)
   // (indexing the kernel argument keeps T a known-global pointer: global_load, not flat_load)
-  // fused steps: this wavefront's step and its wavefront within the batch
-  const int fstep = mp.fused_w ? (int)(blockIdx.x / mp.fused_w) : 0;
-  const int wid = mp.fused_w ? (int)(blockIdx.x % mp.fused_w) : (int)blockIdx.x;
   const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
   int b, bb;
   bool live;  // an idle half (odd group) computes a copy of its neighbour and stores nothing
@@ -1965,6 +1975,13 @@ __global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FL
     b = wid * 2 + sub;
     live = b < a.n_rollouts;
     bb = live ? b : a.n_rollouts - 1;
+  }
+  // fixup: the neighbour's step is already stored; that half runs along without storing and without
+  // the general path, whose workspace (the idle slot) the fixup's other wavefronts would share
+  const bool fix_idle = only_sub >= 0 && sub != only_sub;
+  if (fix_idle) {
+    bb = live ? b : bb;
+    live = false;
   }
   GenWS* G = mp.fused_gen
                  ? &((RolloutWS*)mp.fused_gen)[(size_t)fstep * (a.n_rollouts + 1) + (live ? b : a.n_rollouts)].gen
@@ -2023,8 +2040,17 @@ __global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FL
     forces_step(T, a, mp, sm.st, sm.sv, sm.d.fr, OneWin<NM, FORCES>{&sm.d}, b, live, h_row, lane);
     return;
   } else {
-    step(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.wk, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
-         lane);
+    bool deferred = false;
+    step<DEFER>(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.wk, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
+                deferred, !fix_idle, lane);
+    if (DEFER && deferred) {  // the fixup launch solves this (step, rollout) with the general path
+      if (lane == 0 && live) {
+        const int it = atomicAdd(mp.fix_count, 1);
+        mp.fix_items[2 * it] = fstep;
+        mp.fix_items[2 * it + 1] = 2 * wid + sub;
+      }
+      return;
+    }
   }
   if (mp.fused_w) {  // this step's joint sum of positive work, summed over the steps in order by the reduce
     if (lane == 0 && live)
@@ -2041,6 +2067,31 @@ __global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FL
       const real kc = key_cot(work, (real)T->total_mass, g.step_length, a.n_t, a.key_steps);
       atomicMin((unsigned long long*)a.best_key, (unsigned long long)best_key(kc, a.rollout_id_base + b));
     }
+  }
+}
+
+// MODE (hs::FIX_*): NONE, the step with the general path out of line; DEFER, the fused step launch
+// without it; SOLVE, the fixup launch over the deferred items (its own instantiation, so the loop
+// costs the other two nothing)
+template <int NM, bool FORCES, int MODE>
+__global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FLOAT ? HS_MIN_WAVES_F32 : HS_MIN_WAVES)) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
+                                                                                 hs_run_args a, RolloutWS* __restrict__ rws,
+                                                                                 hs::launch_map mp) {
+  __shared__ Smem<NM, FORCES> smem[2];
+  RSTAMP(16);
+  STAMP(15);
+  if constexpr (MODE == hs::FIX_SOLVE) {  // the deferred (step, rollout) items, one per wavefront
+    const int n = *mp.fix_count;           // written by the previous launch on this stream
+    for (int it = blockIdx.x; it < n; it += gridDim.x) {
+      const int fstep = mp.fix_items[2 * it], ws = mp.fix_items[2 * it + 1];
+      rollout_wave<NM, FORCES, false>(T0, a, rws, mp, smem, fstep, ws >> 1, ws & 1);
+      wave_sync();
+    }
+  } else {
+    // fused steps: this wavefront's step and its wavefront within the batch
+    const int fstep = mp.fused_w ? (int)(blockIdx.x / mp.fused_w) : 0;
+    const int wid = mp.fused_w ? (int)(blockIdx.x % mp.fused_w) : (int)blockIdx.x;
+    rollout_wave<NM, FORCES, MODE == hs::FIX_DEFER>(T0, a, rws, mp, smem, fstep, wid, -1);
   }
 }
 
@@ -2109,9 +2160,13 @@ int launch_pergen_rec(const hs_topo* d_topo, const hs_gait_params* params, int32
 template <int NM>
 void launch_nm(const hs_topo* d_topo, const hs_run_args& a, RolloutWS* ws, const launch_map& mp, hipStream_t st) {
   if (mp.tau_in)
-    hipLaunchKernelGGL((hs_rollout_kernel<NM, true>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
+    hipLaunchKernelGGL((hs_rollout_kernel<NM, true, FIX_NONE>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
+  else if (mp.fix_mode == FIX_DEFER)
+    hipLaunchKernelGGL((hs_rollout_kernel<NM, false, FIX_DEFER>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
+  else if (mp.fix_mode == FIX_SOLVE)
+    hipLaunchKernelGGL((hs_rollout_kernel<NM, false, FIX_SOLVE>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
   else
-    hipLaunchKernelGGL((hs_rollout_kernel<NM, false>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
+    hipLaunchKernelGGL((hs_rollout_kernel<NM, false, FIX_NONE>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
 }
 
 #if HS_REAL_IS_FLOAT
@@ -2161,6 +2216,9 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   launch_map m = mp;
   m.fused_w = mp.setup_only ? 0 : mp.n_waves;
   m.n_waves = mp.setup_only ? mp.n_waves : mp.n_waves * mp.fused_n;  // the grid
+  // the fixup launch: in HS_SOLVE_AUTO a few wavefronts loop over the deferred items (usually none:
+  // they exit at once); in HS_SOLVE_REFERENCE every step is an item, one wavefront each
+  if (mp.fix_mode == FIX_SOLVE) m.n_waves = a.solve_mode != HS_SOLVE_AUTO ? 2 * m.n_waves : (m.n_waves < 256 ? m.n_waves : 256);
   if (mp.max_parts <= 18) launch_nm<18>(d_topo, a, ws, m, st);
   else if (mp.max_parts <= 22) launch_nm<22>(d_topo, a, ws, m, st);
   else launch_nm<HS_NMAX>(d_topo, a, ws, m, st);
@@ -2168,7 +2226,10 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
 }
 
 __global__ void hs_fused_reduce_kernel(hs_run_args a, real total_mass, const double* __restrict__ rollout_mass,
-                                       const real* __restrict__ ws, int n_steps) {
+                                       const real* __restrict__ ws, int n_steps, int32_t* __restrict__ fix_counts,
+                                       int n_fix_counts) {
+  if (blockIdx.x == 0)  // the call's fixup launches have read their counters: zero them for the next call
+    for (int i = threadIdx.x; i < n_fix_counts; i += WAVE) fix_counts[i] = 0;
   const int b0 = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = b0 < a.n_rollouts;
   const int b = live ? b0 : a.n_rollouts - 1;  // dead lanes load a valid row and store nothing
@@ -2205,15 +2266,19 @@ __global__ void hs_fused_reduce_kernel(hs_run_args a, real total_mass, const dou
 
 #if HS_REAL_IS_FLOAT
 int launch_fused_reduce_f32(const hs_run_args& a, double total_mass, const double* rollout_mass,
-                            const void* work_steps, int32_t n_steps) {
+                            const void* work_steps, int32_t n_steps, int32_t* fix_counts, int32_t n_fix_counts) {
 #else
 int launch_fused_reduce(const hs_run_args& a, double total_mass, const double* rollout_mass, const void* work_steps,
-                        int32_t n_steps) {
+                        int32_t n_steps, int32_t* fix_counts, int32_t n_fix_counts) {
 #endif
-  if (a.n_rollouts <= 0 || !a.work_cot) return 0;
+  if (a.n_rollouts <= 0 || !a.work_cot) {  // nothing to sum: only the fixup counters to zero
+    if (n_fix_counts > 0)
+      return (int)hipMemsetAsync(fix_counts, 0, sizeof(int32_t) * n_fix_counts, (hipStream_t)a.stream);
+    return 0;
+  }
   // one wavefront per workgroup: B = 4096 spreads over 64 CUs instead of 16
   hipLaunchKernelGGL(hs_fused_reduce_kernel, dim3((a.n_rollouts + 63) / 64), dim3(64), 0, (hipStream_t)a.stream, a,
-                     (real)total_mass, rollout_mass, (const real*)work_steps, n_steps);
+                     (real)total_mass, rollout_mass, (const real*)work_steps, n_steps, fix_counts, n_fix_counts);
   return (int)hipGetLastError();
 }
 

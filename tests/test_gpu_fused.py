@@ -1,7 +1,9 @@
 """Fused control steps (hs_run_calls): the steps of hs_run_steps in few launches over
 (step, rollout), every step with its own output rows. Bitwise equality with the launch-per-step
 path is expected: the same kernel code per step, the gait setup stored by a setup-only pass
-(the same values the first launch of hs_run_steps stores), the work summed in step order.
+(the same values the first launch of hs_run_steps stores), the work summed in step order, and
+the steps the closed form declines (every step in HS_SOLVE_REFERENCE) recomputed by the fixup
+launch after each step launch with the general path the per-step kernel calls inline.
 """
 import os
 
@@ -245,3 +247,47 @@ def test_best_key_needs_work(gpu, hmodels):
     assert L.hs_run_calls(hmodels["hexapod"].handle, ctypes.byref(a), 2) != 0
     assert b"work_cot" in L.hs_last_error()
     assert L.hs_run_steps(hmodels["hexapod"].handle, ctypes.byref(a), 2, None) != 0
+
+
+def test_fused_reference_mode_fixups_over_two_launches(gpu, hmodels):
+    """HS_SOLVE_REFERENCE through hs_run_calls: every step is deferred by the step launch and solved
+    by the fixup launch that follows it (its items counted per launch), over S > CHUNK (two step
+    launches, each with its fixup) and an odd batch (an idle half-wave): rows, work and key equal
+    the launch-per-step loop, where the general path runs inline, bitwise."""
+    import torch
+
+    from hslabs_amd import synth
+
+    m = hmodels["myant"]
+    p = synth.gen_params(61, "myant", curved=True)
+    S = 270
+    outs = ("tau", "cf", "flags", "work_cot")
+    seq = gpu.DeviceBatch(m, p, n_t=20, horizon=1, outputs=outs)
+    seq.solve_mode = gpu.capi.HS_SOLVE_REFERENCE
+    seq.work_cot.zero_()
+    seq.reset_best()
+    rows = {k: [] for k in ("tau", "cf", "flags")}
+    for c in range(S):
+        seq.k0 = c % 20
+        seq.key_steps = S
+        seq.run(best=c == S - 1, accumulate=True)
+        for k in rows:
+            rows[k].append(npy(getattr(seq, k)))
+    fz = gpu.DeviceBatch(m, p, n_t=20, horizon=S, outputs=outs)
+    fz.solve_mode = gpu.capi.HS_SOLVE_REFERENCE
+    fz.work_cot.zero_()
+    fz.reset_best()
+    fz.run_calls(S, best=True, accumulate=True)
+    torch.cuda.synchronize()
+    for k in rows:
+        assert np.array_equal(np.concatenate(rows[k], axis=1), npy(getattr(fz, k)), equal_nan=True), k
+    assert (npy(fz.flags).astype(np.uint32) & 64).all()  # HS_FLAG_GENERAL: every step took the general path
+    assert np.array_equal(npy(seq.work_cot), npy(fz.work_cot))
+    assert np.array_equal(npy(seq.best_key), npy(fz.best_key))
+    # the fixup counters are left at zero: an AUTO call right after defers nothing stale
+    fz.solve_mode = gpu.capi.HS_SOLVE_AUTO
+    fz.work_cot.zero_()
+    fz.run_calls(20, accumulate=True)
+    torch.cuda.synchronize()
+    flat = npy(fz.flags).reshape(-1)[:61 * 20]  # rows packed with stride n_calls * call_horizon = 20
+    assert not (flat.astype(np.uint32) & 64).any()

@@ -130,8 +130,8 @@ def test_reference_solve_mode_pgs_setups(gpu, hmodels, oracle_mod, omodels, sid)
 def test_reference_solve_mode_synthetic(gpu, hmodels, oracle_mod, omodels, name, curved):
     """The Eigen-style path on synthetic batches: 4-6 contacts of a hexapod (k = 12..18), 1-4 of
     myant, rank retries where they occur (the rollout's global-memory workspace, an out-of-line
-    call from the 3-waves/SIMD kernel); the fused path's per-step scratch equals the
-    launch-per-call one bitwise."""
+    call from the 3-waves/SIMD kernel); the fused path (every step deferred by the step launch
+    and solved by its fixup launch) equals the launch-per-call one bitwise."""
     import torch
 
     from hslabs_amd import synth
