@@ -4,7 +4,7 @@ Compiles the HS_STAMPS build to assembly, slices the chosen kernel at its
 s_memtime stamps (slot = the store offset / 8) and counts instruction classes
 between consecutive stamps in code order.
 
-  python tools/phase_isa.py [--nm 22] [--forces] [-D NAME=VAL ...]
+  python tools/phase_isa.py [--nm 22] [--forces] [--mode 0|1|2] [-D NAME=VAL ...]
 """
 import argparse
 import collections
@@ -36,6 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nm", type=int, default=22)
     ap.add_argument("--forces", action="store_true")
+    ap.add_argument("--mode", type=int, default=1, help="hs::FIX_* instantiation (1: the fused step launch)")
     ap.add_argument("-D", action="append", default=[])
     ap.add_argument("--dump", help="write the kernel body here")
     a = ap.parse_args()
@@ -46,7 +47,7 @@ def main():
                         "--cuda-device-only", "-S", os.path.join(SRC, "hs_kernels.hip"), "-o", out],
                        check=True, stderr=subprocess.DEVNULL)
         text = open(out).read()
-    key = f"hs_rollout_kernelILi{a.nm}ELb{int(a.forces)}E"
+    key = f"hs_rollout_kernelILi{a.nm}ELb{int(a.forces)}ELi{0 if a.forces else a.mode}E"
     m = re.search(rf"^(_Z\S*{key}\S*):", text, re.M)
     body = text[m.end():text.index(".Lfunc_end", m.end())].splitlines()
     if a.dump:
