@@ -42,11 +42,10 @@ void free_on_device(int dev, void* p) {
 
 }  // namespace
 
-int ws_pool::get(void* stream, size_t n, void** out, bool* fresh) {
+int ws_pool::get(void* stream, size_t n, void** out) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return (int)e;
-  if (fresh) *fresh = false;
   for (slot& s : live) {
     if (s.dev != dev || s.stream != stream) continue;
     if (s.n < n) {
@@ -56,7 +55,6 @@ int ws_pool::get(void* stream, size_t n, void** out, bool* fresh) {
       retired.emplace_back(dev, s.ptr);
       s.ptr = w;
       s.n = n;
-      if (fresh) *fresh = true;
     }
     *out = s.ptr;
     return 0;
@@ -66,7 +64,6 @@ int ws_pool::get(void* stream, size_t n, void** out, bool* fresh) {
   if (e != hipSuccess) return (int)e;
   live.push_back({dev, stream, w, n});
   *out = w;
-  if (fresh) *fresh = true;
   return 0;
 }
 
@@ -203,8 +200,7 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   const size_t gwb = hs::general_workspace_bytes();
   // steps the closed form declines (every step in HS_SOLVE_REFERENCE) are deferred to a fixup launch
   // after each step launch, so the step kernel carries no call to the general path; one counter per
-  // launch, then the items
-  const bool defer = true;
+  // launch (zeroed by the setup pass), then the items
   const size_t fix_counts_bytes = ((size_t)n_chunks * sizeof(int32_t) + 255) / 256 * 256;
   const size_t fix_bytes = fix_counts_bytes + (size_t)CHUNK * mp.n_waves * 2 * 2 * sizeof(int32_t);
   void *gen = nullptr, *work = nullptr, *fix = nullptr;
@@ -218,14 +214,11 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
     const size_t want =
         std::max(need, std::min((size_t)HS_FUSED_RESERVE_STEPS * B * sizeof(double), (size_t)512 << 20));
     if (e == hipSuccess) e = (hipError_t)work_pool.get(a.stream, (want + gwb - 1) / gwb, &work);
-    bool fresh = false;
-    if (e == hipSuccess && defer) e = (hipError_t)fix_pool.get(a.stream, (fix_bytes + gwb - 1) / gwb, &fix, &fresh);
-    // new counters start at zero; afterwards every call's work reduce leaves them zeroed
-    if (e == hipSuccess && fresh) e = hipMemsetAsync(fix, 0, fix_counts_bytes, (hipStream_t)a.stream);
+    if (e == hipSuccess) e = (hipError_t)fix_pool.get(a.stream, (fix_bytes + gwb - 1) / gwb, &fix);
     if (e != hipSuccess) return hip_fail(e, "hipMalloc(fused workspace)");
   }
-  int32_t* fix_counts = defer ? (int32_t*)fix : nullptr;
-  int32_t* fix_items = defer ? (int32_t*)((char*)fix + fix_counts_bytes) : nullptr;
+  int32_t* fix_counts = (int32_t*)fix;
+  int32_t* fix_items = (int32_t*)((char*)fix + fix_counts_bytes);
   const bool f32 = a.precision == HS_PREC_F32;
   hs_run_args c = a;
   c.horizon = (int32_t)S;  // output rows per rollout
@@ -237,31 +230,39 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   mp.fused_gen = gen;
   mp.setup_only = 1;  // gait setup once per rollout, stored for every step
   mp.setup_io = hs::SETUP_STORE;
+  mp.fix_count = fix_counts;
+  mp.fix_n_counts = n_chunks;
   int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   mp.setup_only = 0;
   mp.setup_io = hs::SETUP_LOAD;
+  mp.fix_n_counts = 0;
   mp.fix_items = fix_items;
+  bool reduced = false;
   for (int64_t s0 = 0, ci = 0; le == 0 && s0 < S; s0 += CHUNK, ci++) {
     mp.fused_s0 = (int32_t)s0;
     mp.fused_n = (int32_t)std::min<int64_t>(CHUNK, S - s0);
-    mp.fix_mode = defer ? hs::FIX_DEFER : hs::FIX_NONE;
-    mp.fix_count = defer ? fix_counts + ci : nullptr;
+    mp.fix_mode = hs::FIX_DEFER;
+    mp.fix_count = fix_counts + ci;
     le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
-    if (le == 0 && defer) {  // the same steps' declined (step, rollout) items, with the general path
-      mp.fix_mode = hs::FIX_SOLVE;
-      le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+    if (le != 0) break;
+    // the same steps' declined (step, rollout) items, with the general path; after the last step
+    // launch of an HS_SOLVE_AUTO call (few items, if any) together with the work reduce
+    mp.fix_mode = hs::FIX_SOLVE;
+    mp.fix_reduce = s0 + CHUNK >= S && a.solve_mode == HS_SOLVE_AUTO && a.work_cot;
+    if (mp.fix_reduce) {
+      mp.red_total_mass = total_mass;
+      mp.red_rollout_mass = rollout_mass;
+      mp.red_n_steps = (int32_t)S;
+      mp.red_key_steps = r.key_steps;
+      mp.red_best_key = r.best_key;
+      reduced = true;
     }
+    le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   }
-  if (le == 0)
-    le = f32 ? hs::launch_fused_reduce_f32(r, total_mass, rollout_mass, work, (int32_t)S, fix_counts,
-                                           defer ? n_chunks : 0)
-             : hs::launch_fused_reduce(r, total_mass, rollout_mass, work, (int32_t)S, fix_counts,
-                                       defer ? n_chunks : 0);
-  if (le != 0) {
-    if (defer)  // counters a failed call may have left behind
-      (void)hipMemsetAsync(fix_counts, 0, fix_counts_bytes, (hipStream_t)a.stream);
-    return hip_fail((hipError_t)le, "kernel launch");
-  }
+  if (le == 0 && !reduced)
+    le = f32 ? hs::launch_fused_reduce_f32(r, total_mass, rollout_mass, work, (int32_t)S)
+             : hs::launch_fused_reduce(r, total_mass, rollout_mass, work, (int32_t)S);
+  if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
   return HS_OK;
 }
 

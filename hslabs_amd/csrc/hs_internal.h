@@ -26,7 +26,8 @@ enum { SETUP_COMPUTE = 0, SETUP_STORE = 1, SETUP_LOAD = 2 };
 // Steps the closed form declines, in fused launches (hs_run_calls, HS_SOLVE_AUTO): the step launch
 // (FIX_DEFER) appends (local step, 2 * wavefront + half) items to fix_items and counts them in
 // *fix_count instead of calling the general path; the fixup launch after it (FIX_SOLVE, the
-// instantiation with the general path) recomputes those steps and stores their outputs and work.
+// instantiation with the general path) recomputes those steps and stores their outputs and work
+// (after the call's last step launch, together with the work reduce).
 enum { FIX_NONE = 0, FIX_DEFER = 1, FIX_SOLVE = 2 };
 
 // Which rollouts a launch's wavefronts run and where their output rows go.
@@ -54,8 +55,15 @@ struct launch_map {
   void* fused_gen;
   int32_t setup_only;
   int32_t fix_mode;     // FIX_*
-  int32_t* fix_count;   // items appended by the step launch (reset by the work reduce)
+  int32_t* fix_count;   // items appended by the step launch (the setup pass zeroes the call's counters)
   int32_t* fix_items;   // [2 * item]: local step, 2 * wavefront + half
+  int32_t fix_n_counts; // setup pass: zero fix_count[0 .. fix_n_counts)
+  // FIX_SOLVE with fix_reduce: the call's last fixup and the work reduce in one launch (a workgroup per
+  // 64 rollouts fixes their items, then sums their work); red_*: the reduce's own arguments
+  int32_t fix_reduce, red_key_steps, red_n_steps;
+  double red_total_mass;
+  const double* red_rollout_mass;
+  uint64_t* red_best_key;
 };
 
 // Kernel launcher (hs_kernels.hip). `workspace` holds general_workspace_bytes()
@@ -73,11 +81,10 @@ int launch_fused_f32(const hs_topo* d_topo, const hs_run_args& a, void* workspac
 // work_cot[b] = (w, w / (total_mass * step_length)) with w = (accumulate ? work_cot[b][0] : 0) + the steps'
 // work in step order, then the best key
 // (rollout_mass: per-rollout total mass of a mixed plan, else null and total_mass)
-// (fix_counts: the call's per-launch fixup counters, zeroed here for the next call)
 int launch_fused_reduce(const hs_run_args& a, double total_mass, const double* rollout_mass, const void* work_steps,
-                        int32_t n_steps, int32_t* fix_counts, int32_t n_fix_counts);
+                        int32_t n_steps);
 int launch_fused_reduce_f32(const hs_run_args& a, double total_mass, const double* rollout_mass,
-                            const void* work_steps, int32_t n_steps, int32_t* fix_counts, int32_t n_fix_counts);
+                            const void* work_steps, int32_t n_steps);
 
 // pergensetup::set_rec for n_rollouts x n_times items (hs_kernels.hip), rec [B][n_times][6 + 3 n_limbs]
 int launch_pergen_rec(const hs_topo* d_topo, const hs_gait_params* params, int32_t n_rollouts, const double* times,
@@ -111,8 +118,7 @@ struct ws_pool {
   std::vector<slot> live;
   std::vector<std::pair<int, void*>> retired;  // outgrown: kernels still queued may use them
   // workspace of >= n rollouts for (current device, stream); returns a hipError_t value
-  // (*fresh, if given: the slot was (re)allocated by this call)
-  int get(void* stream, size_t n, void** out, bool* fresh = nullptr);
+  int get(void* stream, size_t n, void** out);
   void release();
 };
 

@@ -1335,7 +1335,9 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, AugL&
   return true;
 }
 
-template <class W, class SV>
+// TIER2: the augmented-system solve where a D_c or the Schur complement is singular; without it
+// (HS_DEFER_AUG builds of the fused step launch) such steps decline and go to the fixup launch
+template <bool TIER2 = true, class W, class SV>
 __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* T, SV& sv, FastL& fl, AugL& ag, const W& w,
                                                                  int nc, int lane) {
   const int n = T->n;
@@ -1441,7 +1443,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
   STAMP(18);
   const real a[6] = {sv.x[0], sv.x[1], sv.x[2], sv.x[3 * n], sv.x[3 * n + 1], sv.x[3 * n + 2]};
   for (int c = 0; c < nc; c++)
-    if (!fl.ok[c]) return aug_solve(fl, ag, sv, a, nc, lane);  // only nc >= 3 factors D_c
+    if (!fl.ok[c]) return TIER2 ? aug_solve(fl, ag, sv, a, nc, lane) : false;  // only nc >= 3 factors D_c
   int ok = 1;
   if (nc == 1) {  // unique least-squares solution (A^T A) w = -A^T a
     if (lane == 0) {
@@ -1536,7 +1538,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
     }
     wave_sync();
     STAMP(19);
-    if (!fl.ok[0]) return aug_solve(fl, ag, sv, a, nc, lane);
+    if (!fl.ok[0]) return TIER2 ? aug_solve(fl, ag, sv, a, nc, lane) : false;
     if (lane < nc) {
       const int c = lane;
       const real* d0 = fl.d0[c];
@@ -1578,6 +1580,46 @@ __device__ inline uint64_t best_key(real cot, int64_t id) {
   return ((uint64_t)ord << 32) | (uint32_t)id;
 }
 
+// The work reduce of a fused call for rollouts blockIdx.x * 64 + lane (one wavefront per workgroup):
+// work_cot[b] = (w, w / (total mass * step length)) with w = (accumulate ? work_cot[b][0] : 0) + the
+// steps' joint work sums times dt in step order, then the best key
+__device__ inline void reduce_rollouts(const hs_run_args& a, real total_mass, const double* __restrict__ rollout_mass,
+                                       const real* __restrict__ ws, int n_steps, uint64_t* best_key_out,
+                                       int key_steps) {
+  const int b0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = b0 < a.n_rollouts;
+  const int b = live ? b0 : a.n_rollouts - 1;  // dead lanes load a valid row and store nothing
+  if (rollout_mass) total_mass = (real)rollout_mass[b];  // a mixed plan: the rollout's model
+  real w = a.accumulate ? outp(a.work_cot)[2 * (size_t)b] : real(0);
+  const real dt = (real)a.params[b].period / a.n_t;  // gait_setup's st.dt
+  // periodic.cpp:302-303, in step order; the loads of 16 steps issue together ahead of their FMAs
+  int s = 0;
+  for (; s + 16 <= n_steps; s += 16) {
+    real v[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[j] = ws[(size_t)(s + j) * a.n_rollouts + b];
+#pragma unroll
+    for (int j = 0; j < 16; j++) w = fma(v[j], dt, w);
+  }
+  for (; s < n_steps; s++) w = fma(ws[(size_t)s * a.n_rollouts + b], dt, w);
+  const real L = (real)a.params[b].step_length;
+  const real cot = w / (total_mass * L);
+  if (live) {
+    outp(a.work_cot)[2 * (size_t)b] = w;
+    outp(a.work_cot)[2 * (size_t)b + 1] = cot;
+  }
+  if (best_key_out) {  // the wave's minimum first: one atomic per wave, not one per rollout on one address
+    const real kc = key_cot(w, total_mass, L, a.n_t, key_steps);
+    unsigned long long k = live ? (unsigned long long)best_key(kc, a.rollout_id_base + b) : ~0ull;
+#pragma unroll
+    for (int off = WAVE / 2; off >= 1; off >>= 1) {
+      const unsigned long long o = __shfl_xor(k, off);
+      k = o < k ? o : k;
+    }
+    if (threadIdx.x == 0) atomicMin((unsigned long long*)best_key_out, k);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // One control-loop step at centre sample i (row = b * H + h of the outputs)
 // ---------------------------------------------------------------------------
@@ -1610,7 +1652,11 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   wave_sync();
   if (true) {
 #else
-  if (a.solve_mode == HS_SOLVE_AUTO && fast_solve(T, sv, fl, *reinterpret_cast<AugL*>(G), w, nc, lane)) {
+#ifndef HS_DEFER_AUG
+#define HS_DEFER_AUG 0
+#endif
+  if (a.solve_mode == HS_SOLVE_AUTO &&
+      fast_solve<!(DEFER && HS_DEFER_AUG)>(T, sv, fl, *reinterpret_cast<AugL*>(G), w, nc, lane)) {
 #endif
     if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
     if (nc == 1) flags |= HS_FLAG_FULL_RANK;
@@ -1930,6 +1976,8 @@ __global__ __launch_bounds__(WAVE) void hs_setup_kernel(const hs_topo* __restric
   __shared__ SetupL sst[2];
   const int sub = threadIdx.x / HALF, lane = threadIdx.x % HALF;
   const int wid = (int)blockIdx.x;
+  if (wid == 0)  // the call's fixup counters, before its step launches append to them
+    for (int i = threadIdx.x; i < mp.fix_n_counts; i += WAVE) mp.fix_count[i] = 0;
   const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
   int b;
   bool live;
@@ -2080,9 +2128,23 @@ __global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FL
   __shared__ Smem<NM, FORCES> smem[2];
   RSTAMP(16);
   STAMP(15);
-  if constexpr (MODE == hs::FIX_SOLVE) {  // the deferred (step, rollout) items, one per wavefront
+  if constexpr (MODE == hs::FIX_SOLVE) {  // the deferred (step, rollout) items
     const int n = *mp.fix_count;           // written by the previous launch on this stream
-    for (int it = blockIdx.x; it < n; it += gridDim.x) {
+    if (mp.fix_reduce) {  // workgroup w: the items of rollouts 64 w .. 64 w + 63, then their work reduce
+      for (int it = 0; it < n; it++) {
+        const int fstep = mp.fix_items[2 * it], ws = mp.fix_items[2 * it + 1];
+        const int rb = mp.wave_rollouts ? mp.wave_rollouts[ws] : ws;
+        if (rb / WAVE != (int)blockIdx.x) continue;
+        rollout_wave<NM, FORCES, false>(T0, a, rws, mp, smem, fstep, ws >> 1, ws & 1);
+        wave_sync();
+      }
+      if (n > 0) __threadfence();  // the fixed steps' work terms, read back by the other lanes
+      __syncthreads();
+      reduce_rollouts(a, (real)mp.red_total_mass, mp.red_rollout_mass, reinterpret_cast<const real*>(mp.fused_work),
+                      mp.red_n_steps, mp.red_best_key, mp.red_key_steps);
+      return;
+    }
+    for (int it = blockIdx.x; it < n; it += gridDim.x) {  // one item per wavefront
       const int fstep = mp.fix_items[2 * it], ws = mp.fix_items[2 * it + 1];
       rollout_wave<NM, FORCES, false>(T0, a, rws, mp, smem, fstep, ws >> 1, ws & 1);
       wave_sync();
@@ -2206,10 +2268,7 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   if (a.n_rollouts <= 0 || mp.n_waves <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
   RolloutWS* ws = (RolloutWS*)workspace;
-#ifndef HS_SETUP_KERNEL
-#define HS_SETUP_KERNEL 1
-#endif
-  if (HS_SETUP_KERNEL && mp.setup_only) {
+  if (mp.setup_only) {
     hipLaunchKernelGGL(hs_setup_kernel, dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
     return (int)hipGetLastError();
   }
@@ -2219,6 +2278,7 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   // the fixup launch: in HS_SOLVE_AUTO a few wavefronts loop over the deferred items (usually none:
   // they exit at once); in HS_SOLVE_REFERENCE every step is an item, one wavefront each
   if (mp.fix_mode == FIX_SOLVE) m.n_waves = a.solve_mode != HS_SOLVE_AUTO ? 2 * m.n_waves : (m.n_waves < 256 ? m.n_waves : 256);
+  if (mp.fix_mode == FIX_SOLVE && mp.fix_reduce) m.n_waves = (a.n_rollouts + WAVE - 1) / WAVE;  // 64 rollouts each
   if (mp.max_parts <= 18) launch_nm<18>(d_topo, a, ws, m, st);
   else if (mp.max_parts <= 22) launch_nm<22>(d_topo, a, ws, m, st);
   else launch_nm<HS_NMAX>(d_topo, a, ws, m, st);
@@ -2226,59 +2286,21 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
 }
 
 __global__ void hs_fused_reduce_kernel(hs_run_args a, real total_mass, const double* __restrict__ rollout_mass,
-                                       const real* __restrict__ ws, int n_steps, int32_t* __restrict__ fix_counts,
-                                       int n_fix_counts) {
-  if (blockIdx.x == 0)  // the call's fixup launches have read their counters: zero them for the next call
-    for (int i = threadIdx.x; i < n_fix_counts; i += WAVE) fix_counts[i] = 0;
-  const int b0 = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = b0 < a.n_rollouts;
-  const int b = live ? b0 : a.n_rollouts - 1;  // dead lanes load a valid row and store nothing
-  if (rollout_mass) total_mass = (real)rollout_mass[b];  // a mixed plan: the rollout's model
-  real w = a.accumulate ? outp(a.work_cot)[2 * (size_t)b] : real(0);
-  const real dt = (real)a.params[b].period / a.n_t;  // gait_setup's st.dt
-  // periodic.cpp:302-303, in step order; the loads of 16 steps issue together ahead of their FMAs
-  int s = 0;
-  for (; s + 16 <= n_steps; s += 16) {
-    real v[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) v[j] = ws[(size_t)(s + j) * a.n_rollouts + b];
-#pragma unroll
-    for (int j = 0; j < 16; j++) w = fma(v[j], dt, w);
-  }
-  for (; s < n_steps; s++) w = fma(ws[(size_t)s * a.n_rollouts + b], dt, w);
-  const real L = (real)a.params[b].step_length;
-  const real cot = w / (total_mass * L);
-  if (live) {
-    outp(a.work_cot)[2 * (size_t)b] = w;
-    outp(a.work_cot)[2 * (size_t)b + 1] = cot;
-  }
-  if (a.best_key) {  // the wave's minimum first: one atomic per wave, not one per rollout on one address
-    const real kc = key_cot(w, total_mass, L, a.n_t, a.key_steps);
-    unsigned long long k = live ? (unsigned long long)best_key(kc, a.rollout_id_base + b) : ~0ull;
-#pragma unroll
-    for (int off = WAVE / 2; off >= 1; off >>= 1) {
-      const unsigned long long o = __shfl_xor(k, off);
-      k = o < k ? o : k;
-    }
-    if (threadIdx.x == 0) atomicMin((unsigned long long*)a.best_key, k);
-  }
+                                       const real* __restrict__ ws, int n_steps) {
+  reduce_rollouts(a, total_mass, rollout_mass, ws, n_steps, reinterpret_cast<uint64_t*>(a.best_key), a.key_steps);
 }
 
 #if HS_REAL_IS_FLOAT
 int launch_fused_reduce_f32(const hs_run_args& a, double total_mass, const double* rollout_mass,
-                            const void* work_steps, int32_t n_steps, int32_t* fix_counts, int32_t n_fix_counts) {
+                            const void* work_steps, int32_t n_steps) {
 #else
 int launch_fused_reduce(const hs_run_args& a, double total_mass, const double* rollout_mass, const void* work_steps,
-                        int32_t n_steps, int32_t* fix_counts, int32_t n_fix_counts) {
+                        int32_t n_steps) {
 #endif
-  if (a.n_rollouts <= 0 || !a.work_cot) {  // nothing to sum: only the fixup counters to zero
-    if (n_fix_counts > 0)
-      return (int)hipMemsetAsync(fix_counts, 0, sizeof(int32_t) * n_fix_counts, (hipStream_t)a.stream);
-    return 0;
-  }
+  if (a.n_rollouts <= 0 || !a.work_cot) return 0;
   // one wavefront per workgroup: B = 4096 spreads over 64 CUs instead of 16
   hipLaunchKernelGGL(hs_fused_reduce_kernel, dim3((a.n_rollouts + 63) / 64), dim3(64), 0, (hipStream_t)a.stream, a,
-                     (real)total_mass, rollout_mass, (const real*)work_steps, n_steps, fix_counts, n_fix_counts);
+                     (real)total_mass, rollout_mass, (const real*)work_steps, n_steps);
   return (int)hipGetLastError();
 }
 
