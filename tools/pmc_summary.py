@@ -1,7 +1,6 @@
 """Summarise tools/gpu_pmc.sh output (gpurun_out/<dir>/p*/run_counter_collection.csv) for
-hs_rollout_kernel: per-step medians of every counter over the fused dispatches (a dispatch's
-counts / the steps it ran = its wavefronts / the batch's wavefronts; the setup-only pass, one
-batch of wavefronts, is skipped), per-wave figures, and the HBM traffic per step of the batch
+hs_rollout_kernel's fused step launch: per-step medians of every counter over its dispatches (a
+dispatch's counts / the steps it ran = its wavefronts / the batch's wavefronts), per-wave figures, and the HBM traffic per step of the batch
 (MI355X_MICROARCH.md HBM/rocprofv3 section: FETCH_SIZE x2 on gfx950, sizes in KiB). The library
 hash the bench printed in the same passes goes into the JSON, and bench.py refuses the figures for
 any other library.
@@ -11,6 +10,7 @@ any other library.
 """
 import argparse
 import csv
+import re
 import glob
 import json
 import os
@@ -18,6 +18,7 @@ import statistics
 from collections import defaultdict
 
 KERNEL = "hs_rollout_kernel"
+STEP_LAUNCH = re.compile(r"hs_rollout_kernel<\d+, false, 1>")  # the fused step launch (hs::FIX_DEFER)
 
 
 def collect(root, n_waves):
@@ -25,12 +26,12 @@ def collect(root, n_waves):
     for path in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if KERNEL not in row["Kernel_Name"]:
-                    continue
+                if not STEP_LAUNCH.search(row["Kernel_Name"]):
+                    continue  # the setup pass and the fixup / reduce launch are separate kernels
                 grid = int(row.get("Grid_Size") or row.get("Grid_Size_X"))
                 steps = grid // 64 // n_waves
-                if grid // 64 == n_waves:
-                    continue  # the setup-only pass (or a one-step launch: same shape, skipped too)
+                if steps < 1:
+                    continue
                 key = (path, row["Dispatch_Id"])
                 d = vals[row["Counter_Name"]]
                 d[key] = d.get(key, 0.0) + float(row["Counter_Value"]) / steps
