@@ -69,3 +69,18 @@ def test_default_layout_is_configs3_over_ranks():
 def test_world_size_mismatch_is_an_error():
     r = run_bench("--gpus", "2", "--stub-cpu", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+def test_committed_pmc_summary_is_keyed_to_the_driver_workload():
+    """bench.py attaches the committed PMC traffic (profiles/pmc_traffic.json) only to the workload
+    key it was taken on and only for the library hash it records: the committed summary is the
+    driver's configs[1] run (bench.py --gpus 1 --steps 20 --warmup 5)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    j = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    assert j["workload"] == "hexapod B=4096 H=1"  # bench.py's traffic_key for configs[1]
+    assert len(j["lib_sha256"]) == 16 and j["hbm_bytes_per_step"] > 1_572_864  # >= the algorithmic bytes
+    got, why = bench.pmc_for("hexapod B=4096 H=1", j["lib_sha256"])
+    assert got is not None, why
+    assert bench.pmc_for("hexapod B=4096 H=1", "0" * 16)[0] is None  # another library: refused
