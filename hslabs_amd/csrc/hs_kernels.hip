@@ -608,6 +608,69 @@ __device__ __attribute__((always_inline)) inline void particular(const hs_topo* 
   }
 }
 
+// S1 as subtree sums (HS_S1_SUBTREE): the recursion above, unrolled. With the torso COM p0 as the
+// origin, x_i = (F_i, V_i - (J_i - p0) x F_i) (the root: (F_0, V_0)), where over i's subtree
+// F_i = sum f_k and V_i = sum (t_k + (P_k - p0) x f_k) -- the same equations (B0 x = f), summed in
+// another order. The node table is in preorder, so every subtree is the contiguous range
+// [i, i + size_i): a non-root node sums its range directly (a body segment's, the longest, is 7
+// parts on the hexapod), the root adds its children's sums; three wavefront syncs instead of one
+// per tree level.
+template <class W, class SV>
+__device__ __attribute__((always_inline)) inline void particular_sub(const hs_topo* T, SV& sv, const W& w, int lane) {
+  const int n = T->n;
+  const bool on = lane < n;
+  const hs_node& nd = T->node[on ? lane : 0];
+  const int sz = on ? nd.size : 0, parent = nd.parent, nk = nd.nkids;
+  int kids[HS_CMAX];
+#pragma unroll
+  for (int kk = 0; kk < HS_CMAX; kk++) kids[kk] = nd.kids[kk];
+  const real* P0 = w.pos(0, 0);
+  const real o[3] = {P0[0], P0[1], P0[2]};
+  if (on) {  // g_i = (f_i, t_i + (P_i - p0) x f_i), the torque part in place
+    const int i = lane;
+    const real* Pi = w.pos(0, i);
+    real f[3], t[3], d[3];
+    for (int j = 0; j < 3; j++) { f[j] = sv.f[3 * i + j]; t[j] = sv.f[3 * (n + i) + j]; d[j] = Pi[j] - o[j]; }
+    t[0] += d[1] * f[2] - d[2] * f[1];
+    t[1] += d[2] * f[0] - d[0] * f[2];
+    t[2] += d[0] * f[1] - d[1] * f[0];
+    for (int j = 0; j < 3; j++) sv.x[3 * (n + i) + j] = t[j];
+  }
+  wave_sync();
+  real F[3] = {0, 0, 0}, V[3] = {0, 0, 0};
+  const bool leafward = on && parent >= 0;
+  if (leafward) {  // the subtree's range, in preorder
+    for (int m = 0; m < sz; m++) {
+      const int kx = lane + m;
+      for (int j = 0; j < 3; j++) { F[j] += sv.x[3 * kx + j]; V[j] += sv.x[3 * (n + kx) + j]; }
+    }
+  }
+  if (leafward)  // every lane's reads above precede these writes (one wavefront, in order)
+    for (int j = 0; j < 3; j++) { sv.x[3 * lane + j] = F[j]; sv.x[3 * (n + lane) + j] = V[j]; }
+  wave_sync();
+  if (on && parent < 0) {  // the root: its own g plus its children's sums
+    for (int j = 0; j < 3; j++) { F[j] = sv.x[3 * lane + j]; V[j] = sv.x[3 * (n + lane) + j]; }
+#pragma unroll
+    for (int kk = 0; kk < HS_CMAX; kk++) {
+      if (kk >= nk) break;
+      const int c = kids[kk];
+      for (int j = 0; j < 3; j++) { F[j] += sv.x[3 * c + j]; V[j] += sv.x[3 * (n + c) + j]; }
+    }
+  }
+  if (on) {  // x_i; the root's reads above precede these writes
+    real d[3] = {0, 0, 0};
+    if (parent >= 0) {
+      const real* Ji = w.jpos(0, lane);
+      for (int j = 0; j < 3; j++) d[j] = Ji[j] - o[j];
+    }
+    V[0] -= d[1] * F[2] - d[2] * F[1];
+    V[1] -= d[2] * F[0] - d[0] * F[2];
+    V[2] -= d[0] * F[1] - d[1] * F[0];
+    for (int j = 0; j < 3; j++) { sv.x[3 * lane + j] = F[j]; sv.x[3 * (n + lane) + j] = V[j]; }
+  }
+  wave_sync();
+}
+
 // Tree-basis null-space entry for a torque row: (arm x e_jj)[row], arm = ref - fpos
 __device__ inline real cross_e(const real* d, int jj, int row) {
   // d x e0 = (0, d2, -d1); d x e1 = (-d2, 0, d0); d x e2 = (d1, -d0, 0)
@@ -1635,7 +1698,11 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   STAMP(3);
   dynamics(T, st, sv, w, lane);
   STAMP(4);
-  particular(T, sv, w, lane);
+#ifndef HS_S1_SUBTREE
+#define HS_S1_SUBTREE 1
+#endif
+  if constexpr (HS_S1_SUBTREE) particular_sub(T, sv, w, lane);
+  else particular(T, sv, w, lane);
   STAMP(5);
   // contact list in foot order (ftsolver contact columns)
   const uint32_t cmask = half_ballot(lane < nf && w.contact(0, lane));

@@ -513,6 +513,19 @@ int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& 
     if (nd.jtype == HS_J_HINGE) { nd.hinge = nh; t->hinge_ids[nh++] = i; }
   }
   t->nf = nf;
+  // subtree sizes; the table is in preorder (every subtree one contiguous range), which the
+  // rollout kernel's back-substitution relies on
+  for (int i = n - 1; i >= 0; i--) {
+    hs_node& nd = t->node[i];
+    nd.size = 1;
+    int next = i + 1;
+    for (int k = 0; k < nd.nkids; k++) {
+      if (nd.kids[k] != next) { err = "node table not in preorder"; return HS_E_TOPOLOGY; }
+      nd.size += t->node[nd.kids[k]].size;
+      next += t->node[nd.kids[k]].size;
+    }
+  }
+  if (n > 0 && t->node[0].size != n) { err = "node table not one tree"; return HS_E_TOPOLOGY; }
   // each hinge may carry at most one foot below it (keeps the 1st-order Gram block diagonal)
   for (int fi = 0; fi < nf; fi++)
     for (int a = t->footis[fi]; a >= 0; a = t->node[a].parent) {

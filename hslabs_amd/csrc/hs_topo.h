@@ -34,6 +34,7 @@ struct hs_node {
   int32_t hinge;        // motor index (0..nmj-1) or -1
   int32_t owner_limb;   // limb lane that computes this node's FK/features
   int32_t limb_below;   // limb whose foot is at/below this node, -1 if none or several
+  int32_t size;         // nodes in this node's subtree (preorder table: the subtree is [i, i + size))
 };
 
 struct hs_topo {
