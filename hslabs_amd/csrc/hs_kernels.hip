@@ -520,7 +520,8 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
 // ---------------------------------------------------------------------------
 // D: finite differences at the centre sample, lane = part (dynrec.cpp:175-224)
 // ---------------------------------------------------------------------------
-template <class W, class SV>
+// SYNC = false: the caller's next phase reads only this lane's rows (particular_sub's first stage)
+template <bool SYNC = true, class W, class SV>
 __device__ __attribute__((always_inline)) inline void dynamics(const hs_topo* T, const SetupL& st, SV& sv, const W& w, int lane) {
   const int n = T->n;
   if (lane < n) {
@@ -558,7 +559,7 @@ __device__ __attribute__((always_inline)) inline void dynamics(const hs_topo* T,
     }
     sv.f[3 * i + 2] += m * real(1);  // gravity, g = 1 (dynrec.cpp:291-295)
   }
-  wave_sync();
+  if (SYNC) wave_sync();
 }
 
 // ---------------------------------------------------------------------------
@@ -668,7 +669,7 @@ __device__ __attribute__((always_inline)) inline void particular_sub(const hs_to
     V[2] -= d[0] * F[1] - d[1] * F[0];
     for (int j = 0; j < 3; j++) { sv.x[3 * lane + j] = F[j]; sv.x[3 * (n + lane) + j] = V[j]; }
   }
-  wave_sync();
+  // no trailing sync: the caller's contact list ends with one before x is read across lanes
 }
 
 // Tree-basis null-space entry for a torque row: (arm x e_jj)[row], arm = ref - fpos
@@ -1696,11 +1697,12 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
                      real& work, bool& deferred, bool may_general, int lane) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
   STAMP(3);
-  dynamics(T, st, sv, w, lane);
-  STAMP(4);
 #ifndef HS_S1_SUBTREE
 #define HS_S1_SUBTREE 1
 #endif
+  // D writes, and S1's first stage reads, part i's rows on lane i only: no sync between them
+  dynamics<!HS_S1_SUBTREE>(T, st, sv, w, lane);
+  STAMP(4);
   if constexpr (HS_S1_SUBTREE) particular_sub(T, sv, w, lane);
   else particular(T, sv, w, lane);
   STAMP(5);
