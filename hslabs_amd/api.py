@@ -99,6 +99,18 @@ class KinematicModel:
     def get_config_dim(self) -> int:
         return self.config_dim
 
+    def switch_torso_penalty(self, force: bool, torque: bool):
+        """periodic::switch_torso_penalty (ftsolver.cpp:262-273) for every later solve on this model
+        (hs_model_set_torso_penalty); (False, False) raises HSError like the reference's exit."""
+        capi.check(capi.load().hs_model_set_torso_penalty(self.handle, int(bool(force)), int(bool(torque))),
+                   "hs_model_set_torso_penalty")
+
+    def torso_penalty(self) -> tuple:
+        f, t = ctypes.c_int32(), ctypes.c_int32()
+        capi.check(capi.load().hs_model_get_torso_penalty(self.handle, ctypes.byref(f), ctypes.byref(t)),
+                   "hs_model_get_torso_penalty")
+        return bool(f.value), bool(t.value)
+
     def number_of_motor_joints(self) -> int:
         return self.nmj
 
@@ -652,6 +664,27 @@ class Periodic:
     def get_total_mass(self) -> float:
         return self.model.total_mass
 
+    def switch_torso_penalty(self, force: bool, torque: bool) -> None:  # periodic.cpp:205-207
+        self.model.switch_torso_penalty(force, torque)
+        self._res = None
+
+
+class _Penalty11:
+    """measure_cot's own periodic solves with switch_torso_penalty(1,1) (player.cpp:263); the model's
+    setting (another periodic's, in the reference) is restored afterwards"""
+
+    def __init__(self, model: KinematicModel):
+        self.model = model
+
+    def __enter__(self):
+        self.saved = self.model.torso_penalty()
+        if self.saved != (True, True):
+            self.model.switch_torso_penalty(True, True)
+
+    def __exit__(self, *exc):
+        if self.saved != (True, True):
+            self.model.switch_torso_penalty(*self.saved)
+
 
 class ModelPlayer:
     """The hot-path-facing part of modelplayer (player.cpp:259-321)."""
@@ -660,7 +693,8 @@ class ModelPlayer:
         self.model = model
 
     def measure_cot(self, pgs: PgsConfigParams, n_t: int) -> float:  # player.cpp:269-285
-        r = run_host(self.model, [pgs], n_t=n_t, k0=0, horizon=n_t, want=("work_cot",))
+        with _Penalty11(self.model):
+            r = run_host(self.model, [pgs], n_t=n_t, k0=0, horizon=n_t, want=("work_cot",))
         return float(r["work_cot"][0, 1])
 
     @staticmethod
@@ -681,7 +715,8 @@ class ModelPlayer:
                           n_val: int):
         """All sweep values in one batched launch; returns [(val, cot)] (player.cpp:311-321)."""
         sw = self.sweep_params(pgs, param_name, val0, val1, n_val)
-        r = run_host(self.model, [p for _, p in sw], n_t=n_t, k0=0, horizon=n_t, want=("work_cot",))
+        with _Penalty11(self.model):
+            r = run_host(self.model, [p for _, p in sw], n_t=n_t, k0=0, horizon=n_t, want=("work_cot",))
         return [(v, float(r["work_cot"][i, 1])) for i, (v, _) in enumerate(sw)]
 
     def record_per_traj(self, pgs: PgsConfigParams, n_t: int, path: str = "traj.txt") -> np.ndarray:

@@ -12,7 +12,7 @@ import os
 
 from . import build as _build
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 HS_OK = 0
 HS_FLAG_RANK_RETRY = 1
@@ -40,7 +40,8 @@ EXPORTS = [
     "hs_sim_free", "hs_batch_create", "hs_batch_set_params", "hs_batch_run", "hs_batch_run_device", "hs_select_best",
     "hs_batch_best_key_device", "hs_batch_free", "hs_comm_unique_id", "hs_comm_init", "hs_comm_free", "hs_comm_size",
     "hs_comm_reduce_best", "hs_select_best_comm", "hs_pergen_rec", "hs_pergen_rec_host", "hs_model_lik",
-    "hs_model_lik_host", "hs_model_fk", "hs_model_fk_host", "hs_model_get_node",
+    "hs_model_lik_host", "hs_model_fk", "hs_model_fk_host", "hs_model_get_node", "hs_model_set_torso_penalty",
+    "hs_model_get_torso_penalty",
 ]
 HS_FLAG_LIK_FAILED = 128
 SIM_BODY_STRIDE = 13
@@ -171,6 +172,8 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_model_free.argtypes = [vp]
     L.hs_model_free.restype = None
     L.hs_model_get_dims.argtypes = [vp, ctypes.POINTER(ModelDimsC)]
+    L.hs_model_set_torso_penalty.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
+    L.hs_model_get_torso_penalty.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
     L.hs_pgs_config_read.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(GaitParamsC),
                                      ctypes.c_char_p, ctypes.c_int32]
     L.hs_run.argtypes = [vp, ctypes.POINTER(RunArgsC)]

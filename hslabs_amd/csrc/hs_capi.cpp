@@ -158,6 +158,14 @@ int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::lau
 }
 
 
+// switch_torso_penalty other than (1,1): the closed form solves the (1,1) problem, so every step of
+// the call takes the Eigen-style path (HS_SOLVE_REFERENCE routing, the launches sized for it)
+hs_run_args routed(const hs_run_args& a, int32_t torso_mask) {
+  hs_run_args c = a;
+  if (torso_mask != 3) c.solve_mode = HS_SOLVE_REFERENCE;
+  return c;
+}
+
 int check_args(const hs_model_s* m, const hs_run_args* a) {
   if (!m || !a) return fail(HS_E_ARG, "null model or args");
   if (a->n_rollouts < 0) return fail(HS_E_ARG, "n_rollouts < 0");
@@ -293,6 +301,7 @@ struct hs_mixed_s {
   int32_t* d_wave_model = nullptr;
   int32_t* d_wave_rollouts = nullptr;
   double* d_rollout_mass = nullptr;  // total mass of each rollout's model (the fused reduce's COT)
+  int32_t torso_mask = 3;            // 3 unless a model's switch_torso_penalty (at plan creation) differs
   ws_pool ws;
   ws_pool fused_gen, fused_work, fused_fix;
   std::mutex mu;
@@ -350,6 +359,38 @@ int hs_model_get_dims(hs_model_t m, hs_model_dims* o) {
   return HS_OK;
 }
 
+int hs_model_set_torso_penalty(hs_model_t m, int32_t force, int32_t torque) {
+  if (!m) return fail(HS_E_ARG, "null model");
+  if (!force && !torque) return fail(HS_E_ARG, "switch_torso_penalty(0,0): mask0 not set (ftsolver.cpp:245)");
+  const int32_t mask = (force ? 1 : 0) | (torque ? 2 : 0);
+  std::lock_guard<std::mutex> lk(m->mu);
+  m->host.torso_mask = mask;
+  bool uploaded = false;
+  for (int dev = 0; dev < HS_MAX_DEVICES; dev++) uploaded |= m->dev[dev] != nullptr;
+  if (!uploaded) return HS_OK;  // the first call uploads the host copy
+  int cur = 0;
+  hipError_t e = hipGetDevice(&cur);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  for (int dev = 0; dev < HS_MAX_DEVICES && e == hipSuccess; dev++) {
+    if (!m->dev[dev]) continue;
+    // later calls only: the device copy changes once the work queued before is done
+    e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess)
+      e = hipMemcpy(&m->dev[dev]->torso_mask, &mask, sizeof(mask), hipMemcpyHostToDevice);
+  }
+  (void)hipSetDevice(cur);
+  if (e != hipSuccess) return hip_fail(e, "hs_model_set_torso_penalty");
+  return HS_OK;
+}
+
+int hs_model_get_torso_penalty(hs_model_t m, int32_t* force, int32_t* torque) {
+  if (!m || !force || !torque) return fail(HS_E_ARG, "null argument");
+  *force = (m->host.torso_mask & 1) ? 1 : 0;
+  *torque = (m->host.torso_mask & 2) ? 1 : 0;
+  return HS_OK;
+}
+
 int hs_model_get_node(hs_model_t m, int32_t i, hs_node_info* o) {
   if (!m || !o) return fail(HS_E_ARG, "null argument");
   const hs_topo& t = m->host;
@@ -395,7 +436,8 @@ int hs_run_steps(hs_model_t m, const hs_run_args* a, int32_t n_calls, void* cons
   void* ws = nullptr;
   rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);  // + the idle half-wave of an odd batch
   if (rc != HS_OK) return rc;
-  return launch_steps(d, *a, ws, hs::single_model_map(m->host, a->n_rollouts), n_calls, kernel_events);
+  return launch_steps(d, routed(*a, m->host.torso_mask), ws, hs::single_model_map(m->host, a->n_rollouts), n_calls,
+                      kernel_events);
 }
 
 int hs_run_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls) {
@@ -407,7 +449,8 @@ int hs_run_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls) {
   void* ws = nullptr;
   rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);
   if (rc != HS_OK) return rc;
-  return run_fused(d, *a, ws, hs::single_model_map(m->host, a->n_rollouts), m->fused_gen, m->fused_work,
+  return run_fused(d, routed(*a, m->host.torso_mask), ws, hs::single_model_map(m->host, a->n_rollouts), m->fused_gen,
+                   m->fused_work,
                    m->fused_fix, m->mu, m->host.total_mass, nullptr, n_calls);
 }
 
@@ -430,7 +473,7 @@ int hs_run_pd(hs_model_t m, const hs_run_args* a, const hs_pd_args* pd) {
   mp.pd_tau = pd->tau_cmd;
   mp.pd_q0 = pd->q_target;
   mp.pd_dq0 = pd->dq_target;
-  return launch_steps(d, *a, ws, mp, 1, nullptr);
+  return launch_steps(d, routed(*a, m->host.torso_mask), ws, mp, 1, nullptr);
 }
 
 int hs_run_forces(hs_model_t m, const hs_run_args* a, const double* tau_in) {
@@ -470,6 +513,7 @@ int hs_mixed_create(const hs_model_t* models, int32_t n_models, const int32_t* m
     if (!models[k]) { delete p; return fail(HS_E_ARG, "null model"); }
     const hs_topo& t = models[k]->host;
     topos.push_back(t);
+    if (t.torso_mask != 3) p->torso_mask = t.torso_mask;  // routes the plan's calls (each wave reads its own)
     if (t.n > md.n_parts) {
       hs_model_get_dims(models[k], &md);  // the model with the most parts, maxima patched below
     }
@@ -559,7 +603,7 @@ int hs_run_mixed_steps(hs_mixed_t p, const hs_run_args* a, int32_t n_calls, void
     e = (hipError_t)p->ws.get(a->stream, (size_t)p->n_rollouts + 1, &ws);
   }
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
-  return launch_steps(p->d_topos, *a, ws, mp, n_calls, kernel_events);
+  return launch_steps(p->d_topos, routed(*a, p->torso_mask), ws, mp, n_calls, kernel_events);
 }
 
 int hs_run_mixed_calls(hs_mixed_t p, const hs_run_args* a, int32_t n_calls) {
@@ -588,7 +632,8 @@ int hs_run_mixed_calls(hs_mixed_t p, const hs_run_args* a, int32_t n_calls) {
     e = (hipError_t)p->ws.get(a->stream, (size_t)p->n_rollouts + 1, &ws);
   }
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
-  return run_fused(p->d_topos, *a, ws, mp, p->fused_gen, p->fused_work, p->fused_fix, p->mu, 0.0, p->d_rollout_mass,
+  return run_fused(p->d_topos, routed(*a, p->torso_mask), ws, mp, p->fused_gen, p->fused_work, p->fused_fix, p->mu, 0.0,
+                   p->d_rollout_mass,
                    n_calls);
 }
 

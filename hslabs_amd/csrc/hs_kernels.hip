@@ -104,6 +104,8 @@ struct GenMats {
   real ntn0[LD * LD], lu[LD * LD], Ny[LD * LD], qr[LD * LD];
   real n1[LD / 3][9];  // 3x3 diagonal blocks of the first-order Gram (column-major)
   real ntx0[LD], ntx1[LD], y0[LD], b[LD], z[LD], c[LD], hc[LD], nu[LD], nd[LD];
+  real u1[3][LD];  // torso rows of N in the first-order stage (switch_torso_penalty other than (1,1))
+  int coupled;     // u1 is set: the first-order Gram couples the contacts
   int8_t rowsT[LD], colsT[LD], q[LD], piv[LD], rycol[LD], cperm[LD];
 };
 using GenWS = GenMats<HS_KMAX, false>;
@@ -694,6 +696,11 @@ __device__ void build_grams(const hs_topo* T, const SV& sv, G& g, const W& w, in
   const int n = T->n;
   const int nc = k / 3;
   const real* P0 = w.pos(0, 0);
+  // switch_torso_penalty (ftsolver.cpp:262-273): the torso rows of mask0 (bit 0: force rows, bit 1:
+  // torque rows; the reference's (1,1) is 3). Rows outside mask0 belong to mask1 with weight 1, ahead
+  // of the joint torque rows in row order (set_penal_mask1, ftsolver.cpp:291-303)
+  const int tm = T->torso_mask;
+  const bool t_force0 = (tm & 1) != 0, t_torque0 = (tm & 2) != 0;
   // zeroth order: rows {0,1,2} = -I, rows {3n..3n+2} = (pos_0 - fpos) x e_jj, weight 1
   for (int e = lane; e < k * k; e += HALF) {
     int ci = e % k, cj = e / k;
@@ -703,11 +710,13 @@ __device__ void build_grams(const hs_topo* T, const SV& sv, G& g, const W& w, in
     real da[3], db[3];
     for (int r = 0; r < 3; r++) { da[r] = P0[r] - fa[r]; db[r] = P0[r] - fb[r]; }
     real s = real(0);
-    for (int r = 0; r < 3; r++) {
-      real na = (r == ja) ? real(-1) : real(0), nb = (r == jb) ? real(-1) : real(0);
-      s = s + na * nb;
-    }
-    for (int r = 0; r < 3; r++) s = s + cross_e(da, ja, r) * cross_e(db, jb, r);
+    if (t_force0)
+      for (int r = 0; r < 3; r++) {
+        real na = (r == ja) ? real(-1) : real(0), nb = (r == jb) ? real(-1) : real(0);
+        s = s + na * nb;
+      }
+    if (t_torque0)
+      for (int r = 0; r < 3; r++) s = s + cross_e(da, ja, r) * cross_e(db, jb, r);
     g.ntn0[ci + cj * LD] = s;
   }
   if (lane < k) {
@@ -716,12 +725,19 @@ __device__ void build_grams(const hs_topo* T, const SV& sv, G& g, const W& w, in
     real da[3];
     for (int r = 0; r < 3; r++) da[r] = P0[r] - fa[r];
     real s = real(0);
-    for (int r = 0; r < 3; r++) s = s + ((r == ja) ? real(-1) : real(0)) * (real(1) * sv.x[r]);
-    for (int r = 0; r < 3; r++) s = s + cross_e(da, ja, r) * (real(1) * sv.x[3 * n + r]);
+    if (t_force0)
+      for (int r = 0; r < 3; r++) s = s + ((r == ja) ? real(-1) : real(0)) * (real(1) * sv.x[r]);
+    if (t_torque0)
+      for (int r = 0; r < 3; r++) s = s + cross_e(da, ja, r) * (real(1) * sv.x[3 * n + r]);
     g.ntx0[ci] = s;
+    // the first-order torso rows (one group at most: mask0 is never empty), for the coupling terms
+    for (int r = 0; r < 3; r++)
+      g.u1[r][ci] = !t_force0 ? ((r == ja) ? real(-1) : real(0)) : (!t_torque0 ? cross_e(da, ja, r) : real(0));
   }
+  if (lane == 0) g.coupled = tm != 3;
   // first order: torque rows of the non-root ancestors of each contact foot,
-  // weighted by the joint-axis components (set_action_penalties, ftsolver.cpp:239-246)
+  // weighted by the joint-axis components (set_action_penalties, ftsolver.cpp:239-246),
+  // after the torso rows mask0 leaves out
   for (int e = lane; e < nc * 9 + k; e += HALF) {
     bool is_vec = e >= nc * 9;
     int cc = is_vec ? (e - nc * 9) / 3 : e / 9;
@@ -733,6 +749,21 @@ __device__ void build_grams(const hs_topo* T, const SV& sv, G& g, const W& w, in
     int chain[HS_NMAX], len = 0;
     for (int a = foot; a >= 0 && T->node[a].parent >= 0; a = T->node[a].parent) chain[len++] = a;
     real s = real(0);
+    if (!t_force0)  // torso force rows 0..2: N = -I per contact, x1 = x
+      for (int r = 0; r < 3; r++) {
+        real na = (r == a_col) ? real(-1) : real(0);
+        real nb = is_vec ? real(1) * sv.x[r] : ((r == b_col) ? real(-1) : real(0));
+        s = s + na * nb;
+      }
+    if (!t_torque0) {  // torso torque rows 3n..3n+2: N = [pos_0 - fpos]x
+      real d0[3];
+      for (int r = 0; r < 3; r++) d0[r] = P0[r] - fp[r];
+      for (int r = 0; r < 3; r++) {
+        real na = cross_e(d0, a_col, r);
+        real nb = is_vec ? real(1) * sv.x[3 * n + r] : cross_e(d0, b_col, r);
+        s = s + na * nb;
+      }
+    }
     for (int t = len - 1; t >= 0; t--) {
       int a = chain[t];
       const real* Ja = w.jpos(0, a);
@@ -756,6 +787,15 @@ __device__ void build_grams(const hs_topo* T, const SV& sv, G& g, const W& w, in
 template <class G>
 __device__ inline real ntn1_at(const G& g, int i, int j) {
   return (i / 3 == j / 3) ? g.n1[i / 3][(j % 3) * 3 + (i % 3)] : real(0);
+}
+// with torso rows in the first order (g.coupled): the off-block entries are their products, summed
+// in row order (the blocks already start with them)
+template <class G>
+__device__ inline real ntn1_full(const G& g, int i, int j) {
+  if (i / 3 == j / 3) return g.n1[i / 3][(j % 3) * 3 + (i % 3)];
+  real s = real(0);
+  for (int r = 0; r < 3; r++) s = s + g.u1[r][i] * g.u1[r][j];
+  return s;
 }
 
 // half-wave argmax with first-index tie break
@@ -937,8 +977,12 @@ __device__ inline real m_at(const G& g, int k, int dimker, int i, int j) {
   constexpr int LD = G::LD;
   real s = real(0);
   if (j < dimker) {
-    int b0 = (i / 3) * 3;
-    for (int kk = b0; kk < b0 + 3; kk++) s = s + ntn1_at(g, i, kk) * g.Ny[kk + j * LD];
+    if (g.coupled) {
+      for (int kk = 0; kk < k; kk++) s = s + ntn1_full(g, i, kk) * g.Ny[kk + j * LD];
+    } else {
+      int b0 = (i / 3) * 3;
+      for (int kk = b0; kk < b0 + 3; kk++) s = s + ntn1_at(g, i, kk) * g.Ny[kk + j * LD];
+    }
   } else {
     int col = g.rycol[j - dimker];
     for (int kk = 0; kk < k; kk++) s = s + g.ntn0[i + kk * LD] * g.ntn0[kk + col * LD];
@@ -1098,7 +1142,10 @@ __device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
     if (lane < k) {
       int i = lane, b0 = (i / 3) * 3;
       real t = real(0);
-      for (int kk = b0; kk < b0 + 3; kk++) t = t + ntn1_at(g, i, kk) * g.y0[kk];
+      if (g.coupled)
+        for (int kk = 0; kk < k; kk++) t = t + ntn1_full(g, i, kk) * g.y0[kk];
+      else
+        for (int kk = b0; kk < b0 + 3; kk++) t = t + ntn1_at(g, i, kk) * g.y0[kk];
       g.b[i] = -(g.ntx1[i] + t);
     }
     for (int e = lane; e < k * k; e += HALF) {  // m, built straight into the QR buffer

@@ -447,6 +447,7 @@ int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& 
   memcpy(t->ls, lik_variant == 2 ? ls_zxx : ls_yxx, sizeof(t->ls));
   int nl = (int)tops.size();
   t->n_limbs = nl;
+  t->torso_mask = 3;  // switch_torso_penalty(1,1), player.cpp:263
   static const int map4[4] = {0, 3, 1, 2}, map6[6] = {0, 3, 4, 1, 2, 5};  // pergen.cpp:243-262
   for (int L = 0; L < nl; L++) {
     int c = tops[L];

@@ -39,7 +39,8 @@ struct hs_node {
 
 struct hs_topo {
   int32_t n, nf, nmj, cfg;
-  int32_t n_limbs, lik_kind, max_depth, pad0;
+  int32_t n_limbs, lik_kind, max_depth;
+  int32_t torso_mask;      // switch_torso_penalty (ftsolver.cpp:262-273): bit 0 force, bit 1 torque rows in stage 0 (default 3)
   double ls[3];            // link lengths (lik.cpp:226-227)
   double rcap;             // foot capsule radius (lik.cpp:132-140)
   double total_mass;       // sum of part masses (periodic.cpp:320-325)

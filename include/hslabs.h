@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 9
+#define HSLABS_ABI_VERSION 10
 
 enum {
   HS_OK = 0,
@@ -81,6 +81,18 @@ int hs_model_load(const char* xml_path, hs_model_t* out);
 int hs_model_load_ex(const char* xml_path, int lik_variant, hs_model_t* out);
 void hs_model_free(hs_model_t model);
 int hs_model_get_dims(hs_model_t model, hs_model_dims* out);
+
+/* periodic::switch_torso_penalty -> forcetorquesolver::switch_torso_penalty (ftsolver.cpp:262-273):
+ * which torso rows form the zeroth-order stage of the contact solve (penal_mask0: the torso force
+ * rows with `force`, the torso torque rows with `torque`); the other torso rows join the first-order
+ * stage with weight 1 (set_penal_mask1, ftsolver.cpp:291-303; set_action_penalties 239-246). Applies
+ * to every later call on this model (hs_run*, hs_batch_*, and mixed plans created afterwards).
+ * The default is the reference's only call, (1,1) (player.cpp:263); with another mask every step
+ * takes the Eigen-style path (the closed form is the (1,1) problem's; flags carry HS_FLAG_GENERAL).
+ * (0,0) is HS_E_ARG: the reference exits with "mask0 not set" (ftsolver.cpp:245). Waits for the
+ * work queued on the devices that hold the model. */
+int hs_model_set_torso_penalty(hs_model_t model, int32_t force, int32_t torque);
+int hs_model_get_torso_penalty(hs_model_t model, int32_t* force, int32_t* torque);
 
 /* One model node (modelnode, model.h:64-86; kinematicmodel::get_mnode, model.h:108), nodes in XML
  * preorder (the order of mnodes, odeparts and dynparts). */

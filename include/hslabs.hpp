@@ -29,8 +29,9 @@
 //
 // Differences from the reference: errors throw hslabs::error instead of
 // exit(1); the whole cycle is computed on the GPU by compute_torques_over_period
-// (record_trajectory / compute_dynrecs / compute_dynrec_ders /
-// switch_torso_penalty only record their arguments); measure_cot_sweep runs all
+// (record_trajectory / compute_dynrecs / compute_dynrec_ders only record their
+// arguments; switch_torso_penalty sets the model's solver mask, as the reference's
+// ftsolver holds it); measure_cot_sweep runs all
 // sweep values in one batched launch.
 #ifndef HSLABS_HPP
 #define HSLABS_HPP
@@ -447,7 +448,6 @@ class periodic {
   const kinematicmodel* model_;
   const pergensetup* pgs_ = nullptr;
   int n_t_ = 0;
-  bool force_pen_ = true, torque_pen_ = true;
   std::vector<double> tau_, cf_, x_, wc_;
   std::vector<uint32_t> flags_;
   std::vector<double> rec_;  // get_complete_traj records
@@ -458,9 +458,10 @@ class periodic {
   void record_trajectory(const pergensetup* pgs, int n_t) { pgs_ = pgs; n_t_ = n_t; tau_.clear(); rec_.clear(); }
   void compute_dynrecs() {}
   void compute_dynrec_ders() {}
+  // ftsolver.cpp:262-273 through periodic.cpp:205-207: a setting of the model's solver, used by every
+  // later solve on it (hs_model_set_torso_penalty); (0,0) throws where the reference exits
   void switch_torso_penalty(bool force, bool torque) {
-    if (!force || !torque) throw error(HS_E_ARG, "only switch_torso_penalty(1,1) is on the GPU path");
-    force_pen_ = force; torque_pen_ = torque;
+    check(hs_model_set_torso_penalty(model_->handle(), force ? 1 : 0, torque ? 1 : 0), "switch_torso_penalty");
   }
   int get_nt() const { return n_t_; }
   int get_nfeet() const { return model_->number_of_feet(); }
@@ -653,8 +654,22 @@ class modelplayer {
     int n_limbs = (model_.get_config_dim() - 6) / 3;
     return new pergensetup(n_limbs, pcp, &model_);
   }
-  // player.cpp:269-285
+  // measure_cot's own periodic solves with switch_torso_penalty(1,1) (player.cpp:263); the model's
+  // setting (another periodic's, in the reference) is restored afterwards
+  struct penalty_11 {
+    hs_model_t m;
+    int32_t f = 1, t = 1;
+    explicit penalty_11(hs_model_t m_) : m(m_) {
+      check(hs_model_get_torso_penalty(m, &f, &t), "hs_model_get_torso_penalty");
+      if (!f || !t) check(hs_model_set_torso_penalty(m, 1, 1), "switch_torso_penalty");
+    }
+    ~penalty_11() {
+      if (!f || !t) (void)hs_model_set_torso_penalty(m, f, t);
+    }
+  };
+  // player.cpp:259-285
   double measure_cot(const pergensetup* pgs, int n_t) {
+    penalty_11 pen(model_.handle());
     periodic per(&model_);
     per.record_trajectory(pgs, n_t);
     per.compute_torques_over_period();
@@ -688,6 +703,7 @@ class modelplayer {
       vals.push_back(val);
     }
     std::vector<double> cot(params.size());
+    penalty_11 pen(model_.handle());
     batch b(model_, (int)params.size(), n_t, n_t, device_mask_);
     b.set_params(params);
     hs_batch_outputs o;

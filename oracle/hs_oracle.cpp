@@ -330,6 +330,10 @@ struct hso_model {
   std::vector<int> parentis, footis, hinge_ids;
   std::vector<double> masses;
   int n = 0, nf = 0, nmj = 0, cfg = 0;
+  // forcetorquesolver::switch_torso_penalty (ftsolver.cpp:262-273): bit 0 = torso force rows, bit 1 =
+  // torso torque rows in the zeroth-order stage (penal_mask0); the reference's only call is (1,1)
+  // (player.cpp:263), main.cpp:87 passes (1, 0+1)
+  int torso_mask = 3;
 };
 
 namespace {
@@ -1322,7 +1326,8 @@ Mat tree_null_basis(const hso_model* m, const DynRec& d) {
 }
 
 // forcetorquesolver::solve_contact_forces, ftsolver.cpp:185-236 (+ set_action_penalties 239-246,
-// masks 262-303: switch_torso_penalty(1,1) -> mask0 = {(0,3),(3n,3n+3)})
+// masks 262-303: switch_torso_penalty(f, t) -> mask0 = {(0,3) if f, (3n,3n+3) if t}, mask1 = the
+// complement in ascending row order, set_penal_mask1 291-303)
 void solve_contact_forces(const hso_model* m, const std::vector<double>& jz, const std::vector<double>& x,
                           const Mat& N, std::vector<double>& y, FTOut& out) {
   int n = m->n, k = N.c;
@@ -1330,9 +1335,11 @@ void solve_contact_forces(const hso_model* m, const std::vector<double>& jz, con
   for (int i = 3; i < 3 * n; i++) c[i] = 0;
   for (int i = 3; i < 3 * n; i++) c[3 * n + i] = jz[i];
   // rows of mask0 and mask1 (mask1 = complement)
-  std::vector<int> r0 = {0, 1, 2, 3 * n, 3 * n + 1, 3 * n + 2}, r1;
-  for (int i = 3; i < 3 * n; i++) r1.push_back(i);
-  for (int i = 3 * n + 3; i < 6 * n; i++) r1.push_back(i);
+  std::vector<int> r0, r1;
+  std::vector<char> in0(6 * n, 0);
+  if (m->torso_mask & 1) in0[0] = in0[1] = in0[2] = 1;
+  if (m->torso_mask & 2) in0[3 * n] = in0[3 * n + 1] = in0[3 * n + 2] = 1;
+  for (int i = 0; i < 6 * n; i++) (in0[i] ? r0 : r1).push_back(i);
   Mat N0((int)r0.size(), k), N1((int)r1.size(), k);
   std::vector<double> x0(r0.size()), x1(r1.size());
   for (size_t a = 0; a < r0.size(); a++) {
@@ -1783,7 +1790,8 @@ void solve_forcetorques(const hso_model* m, const DynRec& d, int basis, FTOut& o
     N = tree_null_basis(m, d);
   }
   std::vector<double> y;
-  if (basis == HSO_BASIS_FAST && fast_contact_solve(m, d, x, y)) {
+  // the closed form is the (1,1) penalty's; other masks take the Eigen-style path
+  if (basis == HSO_BASIS_FAST && m->torso_mask == 3 && fast_contact_solve(m, d, x, y)) {
     out.k = N.c;
     out.iters = 1;
     out.rank0 = -1;
@@ -2005,6 +2013,13 @@ int hso_model_load(const char* xml_path, hso_model** out) { return load_model(xm
 void hso_model_free(hso_model* m) { delete m; }
 void hso_model_dims(const hso_model* m, int* d) {
   d[0] = m->n; d[1] = m->nmj; d[2] = m->nf; d[3] = m->cfg; d[4] = m->lik_index; d[5] = (int)m->limbs.size();
+}
+
+int hso_model_set_torso_penalty(hso_model* m, int force, int torque) {
+  if (!m) return -1;
+  if (!force && !torque) return -2;  // mask_l0 == 0: the reference exits ("mask0 not set", ftsolver.cpp:245)
+  m->torso_mask = (force ? 1 : 0) | (torque ? 2 : 0);
+  return 0;
 }
 
 int hso_rollout(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, int basis, int ignore_reach,

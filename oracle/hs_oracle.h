@@ -56,6 +56,10 @@ int hso_model_load(const char* xml_path, hso_model** out);
 void hso_model_free(hso_model* m);
 /* n_parts, nmj, nfeet, config_dim, lik variant, n_limbs */
 void hso_model_dims(const hso_model* m, int* dims6);
+/* periodic::switch_torso_penalty -> forcetorquesolver::switch_torso_penalty (ftsolver.cpp:262-273):
+ * which torso rows (force, torque) form the zeroth-order stage of every later solve of this model
+ * (default (1,1), player.cpp:263). (0,0) returns -2: the reference exits (ftsolver.cpp:245). */
+int hso_model_set_torso_penalty(hso_model* m, int force, int torque);
 
 /*
  * One rollout, processing steps k = k0 .. k0+H-1, i.e. trajectory samples

@@ -153,6 +153,7 @@ def _bind(path):
     L.hso_model_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]
     L.hso_model_free.argtypes = [ctypes.c_void_p]
     L.hso_model_dims.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+    L.hso_model_set_torso_penalty.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     L.hso_rollout.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                               ctypes.c_int, ctypes.c_int, dp, dp, dp, dp,
                               ctypes.POINTER(ctypes.c_uint32), dp, dp]
@@ -213,6 +214,13 @@ class Model:
         d = (ctypes.c_int * 6)()
         self.L.hso_model_dims(h, d)
         self.n, self.nmj, self.nf, self.cfg, self.lik_index, self.n_limbs = list(d)
+
+    def switch_torso_penalty(self, force: bool, torque: bool):
+        """periodic::switch_torso_penalty (ftsolver.cpp:262-273) for every later solve of this model;
+        (False, False) raises: the reference exits (ftsolver.cpp:245)"""
+        rc = self.L.hso_model_set_torso_penalty(self.handle, int(bool(force)), int(bool(torque)))
+        if rc != 0:
+            raise ValueError(f"oracle: switch_torso_penalty({force}, {torque}) rejected (rc={rc})")
 
     def __del__(self):
         try:

@@ -44,6 +44,23 @@ def test_model_dims(product, omodels, name, n, nmj, nf, cfg):
     assert (o.n, o.nmj, o.nf, o.cfg) == (n, nmj, nf, cfg)
 
 
+def test_torso_penalty_setting(product):
+    """periodic::switch_torso_penalty (ftsolver.cpp:262-273): (1,1) by default (player.cpp:263), any
+    mask with at least one torso group, (0,0) refused where the reference exits (ftsolver.cpp:245)"""
+    m = product.KinematicModel(os.path.join(MODELS, "hexapod.xml"))
+    assert m.torso_penalty() == (True, True)
+    m.switch_torso_penalty(True, False)
+    assert m.torso_penalty() == (True, False)
+    m.switch_torso_penalty(False, True)
+    assert m.torso_penalty() == (False, True)
+    with pytest.raises(product.HSError, match="mask0 not set"):
+        m.switch_torso_penalty(False, False)
+    assert m.torso_penalty() == (False, True)  # unchanged by the refused call
+    per = product.Periodic(m)
+    per.switch_torso_penalty(True, True)
+    assert m.torso_penalty() == (True, True)
+
+
 def test_model_errors(product, tmp_path):
     with pytest.raises(product.HSError, match="cannot open"):
         product.KinematicModel(str(tmp_path / "nope.xml"))

@@ -148,7 +148,8 @@ def build_system(d, n):
     return B0, f, Bc
 
 
-def scipy_solve(d, n):
+def scipy_solve(d, n, force=True, torque=True):
+    """force / torque: switch_torso_penalty's zeroth-order torso rows (ftsolver.cpp:262-273)"""
     B0, f, Bc = build_system(d, n)
     k = Bc.shape[1]
     xp = np.linalg.solve(B0, f)
@@ -159,7 +160,8 @@ def scipy_solve(d, n):
     c[3:3 * n] = 0
     c[3 * n + 3:] = d["jz"].reshape(-1)[3:]
     m0 = np.zeros(6 * n, bool)
-    m0[[0, 1, 2, 3 * n, 3 * n + 1, 3 * n + 2]] = True
+    m0[[0, 1, 2]] = force
+    m0[[3 * n, 3 * n + 1, 3 * n + 2]] = torque
     A0, b0 = (c[:, None] * Nu)[m0], (c * xp)[m0]
     A1, b1 = (c[:, None] * Nu)[~m0], (c * xp)[~m0]
     y0 = -np.linalg.lstsq(A0, b0, rcond=1e-10)[0]
@@ -189,6 +191,41 @@ def test_independent_scipy_formulation(oracle_mod, omodels, sid):
         scale = max(1.0, np.abs(r["tau"][step]).max())
         assert np.abs(tau - r["tau"][step]).max() < 1e-8 * scale
         assert np.abs(cf - r["cf"][step]).max() < 1e-8 * max(1.0, np.abs(cf).max())
+
+
+# --- switch_torso_penalty(force, torque) other than (1,1) (ftsolver.cpp:262-273) ----------------
+@pytest.mark.parametrize("force,torque", [(1, 0), (0, 1)])
+@pytest.mark.parametrize("sid", [0, 8, 12, 24])
+def test_torso_penalty_masks(oracle_mod, sid, force, torque):
+    """mask0 = the chosen torso rows, mask1 = the rest (set_penal_mask1): both bases and the closed-form
+    mode (which declines to the Eigen-style path) agree, the independent scipy formulation with the same
+    masks agrees, and the zeroth-order rows come out exactly actuation-free"""
+    g = pgs(oracle_mod, sid)
+    m = oracle_mod.Model(os.path.join(MODELS, g.xml_file))  # not the shared fixture: the setting persists
+    m.switch_torso_penalty(force, torque)
+    ro = oracle_mod.rollout(m, g, 20, basis=oracle_mod.BASIS_ORTHO)
+    rt = oracle_mod.rollout(m, g, 20, basis=oracle_mod.BASIS_TREE)
+    rf = oracle_mod.rollout(m, g, 20, basis=oracle_mod.BASIS_FAST)
+    scale = max(1.0, np.abs(ro["tau"]).max())
+    assert np.abs(ro["tau"] - rt["tau"]).max() < 1e-9 * scale
+    assert np.array_equal(rt["tau"], rf["tau"])
+    contact = (rf["flags"] & oracle_mod.FLAG_NO_CONTACT) == 0
+    assert ((rf["flags"][contact] & oracle_mod.FLAG_GENERAL) != 0).all()
+    n = m.n
+    rows = [0, 1, 2] if force else [3 * n, 3 * n + 1, 3 * n + 2]
+    xs = ro["x"][contact][:, rows]
+    assert np.abs(xs).max() < 1e-9 * max(1.0, np.abs(ro["x"]).max())
+    for step in range(0, 20, 4):
+        d = oracle_mod.dynrec_dump(m, g, 20, step)
+        tau, cf = scipy_solve(d, n, bool(force), bool(torque))
+        assert np.abs(tau - ro["tau"][step]).max() < 1e-8 * scale
+        assert np.abs(cf - ro["cf"][step]).max() < 1e-8 * max(1.0, np.abs(cf).max())
+    # the setting matters: (1,1) gives other torques
+    m11 = oracle_mod.Model(os.path.join(MODELS, g.xml_file))
+    r11 = oracle_mod.rollout(m11, g, 20, basis=oracle_mod.BASIS_ORTHO)
+    assert np.abs(r11["tau"] - ro["tau"]).max() > 1e-6 * scale
+    with pytest.raises(ValueError):
+        m.switch_torso_penalty(False, False)  # the reference exits (ftsolver.cpp:245)
 
 
 # --- COT sweep shape (player.cpp:311-321, main.cpp:69) ------------------------------------------
