@@ -497,6 +497,13 @@ def main():
         comm.reduce_best(batch.best_key, stream)
     batch.work_cot.zero_()  # queued behind the warmup on the same stream
     batch.reset_best()
+    # wait for the warmup by polling an event instead of a blocking synchronize: a host thread that
+    # slept through the wait enqueues the timed job at ~half speed (tools/host_probe.py idle5 vs
+    # idle5spin: 30-35 -> 17-18 us before the first launch; profiles/r02_v9_host_probe.txt)
+    warm_done = torch.cuda.Event()
+    warm_done.record(stream)
+    while not warm_done.query():
+        pass
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -2087,12 +2087,20 @@ static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 // The fused path's setup pass (hs_run_calls: gait setup once per rollout, stored for every step):
 // the rollout kernel's prologue and setup store alone, as its own small kernel (2 x 320 B of LDS, few
 // registers) so the pass does not carry the step kernel's code, registers and LDS
-__global__ __launch_bounds__(WAVE) void hs_setup_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
+#ifndef HS_SETUP_WAVES
+#define HS_SETUP_WAVES 1  // wavefronts per workgroup of the setup pass
+#endif
+__global__ __launch_bounds__(WAVE * HS_SETUP_WAVES) void hs_setup_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
                                                         RolloutWS* __restrict__ rws, hs::launch_map mp) {
-  __shared__ SetupL sst[2];
-  const int sub = threadIdx.x / HALF, lane = threadIdx.x % HALF;
-  const int wid = (int)blockIdx.x;
-  if (wid == 0)  // the call's fixup counters, before its step launches append to them
+  __shared__ SetupL sst_all[2 * HS_SETUP_WAVES];
+  const int sub = (threadIdx.x % WAVE) / HALF, lane = threadIdx.x % HALF;
+  SetupL* sst = sst_all + 2 * (threadIdx.x / WAVE);
+  // past the batch's last wavefront: recompute the last one's setup and store nothing (the
+  // workgroup's barriers need every wavefront)
+  const int wid_raw = (int)blockIdx.x * HS_SETUP_WAVES + (int)(threadIdx.x / WAVE);
+  const bool wave_live = wid_raw < mp.n_waves;
+  const int wid = wave_live ? wid_raw : mp.n_waves - 1;
+  if (wid_raw == 0)  // the call's fixup counters, before its step launches append to them
     for (int i = threadIdx.x; i < mp.fix_n_counts; i += WAVE) mp.fix_count[i] = 0;
   const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
   int b;
@@ -2106,6 +2114,7 @@ __global__ __launch_bounds__(WAVE) void hs_setup_kernel(const hs_topo* __restric
     live = b < a.n_rollouts;
     if (!live) b = a.n_rollouts - 1;
   }
+  if (!wave_live) live = false;
   const GaitR g = load_gait(a.params[b]);
   gait_setup(T, g, a.n_t, sst[sub], lane);  // every lane of the wave takes part (wave_sync inside)
   if (live) {
@@ -2385,7 +2394,8 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   hipStream_t st = (hipStream_t)a.stream;
   RolloutWS* ws = (RolloutWS*)workspace;
   if (mp.setup_only) {
-    hipLaunchKernelGGL(hs_setup_kernel, dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
+    hipLaunchKernelGGL(hs_setup_kernel, dim3((mp.n_waves + HS_SETUP_WAVES - 1) / HS_SETUP_WAVES),
+                       dim3(WAVE * HS_SETUP_WAVES), 0, st, d_topo, a, ws, mp);
     return (int)hipGetLastError();
   }
   launch_map m = mp;

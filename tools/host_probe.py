@@ -3,7 +3,8 @@ wall time to a finished synchronize, and the HIP events around the kernels, for 
 and waiting. Tuning aid; one mode per process (device flags must precede the runtime's init).
   python tools/host_probe.py [plain|noevents|poll|graph|spin|idle|idle5]
 (idle: 1 s of GPU idle, then the job as warmup and the timed job; idle5: the same with bench.py's
-5-step warmup job)"""
+5-step warmup job; idle5spin: idle5 with the warmup's end polled on an event (the host thread kept
+awake) before the synchronize; idle5spin2: also the timed job's end polled)"""
 import ctypes
 import os
 import sys
@@ -37,7 +38,7 @@ def main():
         job()
     torch.cuda.synchronize()
     warm = job
-    if mode == "idle5":
+    if mode.startswith("idle5"):
         b.key_steps = 5
         warm = b.calls_launcher(5, stream=st, best=True)
         b.key_steps = K
@@ -63,6 +64,11 @@ def main():
         if mode.startswith("idle"):
             time.sleep(1.0)
         warm()  # the warmup right before, as in bench.py
+        if mode.startswith("idle5spin"):
+            ew = torch.cuda.Event()
+            ew.record(st)
+            while not ew.query():
+                pass
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         if mode != "noevents":
@@ -71,7 +77,7 @@ def main():
         if mode != "noevents":
             e1.record(st)
         t1 = time.perf_counter()
-        if mode == "poll":
+        if mode in ("poll", "idle5spin2"):
             while not e1.query():
                 pass
         torch.cuda.synchronize()
