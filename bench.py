@@ -123,7 +123,7 @@ def job_layout(args, world: int, rank: int) -> dict:
     if total < world:
         raise SystemExit(f"{total} rollouts cannot be sharded over {world} ranks")
     id0, count = shard(total, world, rank)
-    std = args.model == "hexapod" and args.horizon == 1 and not args.fp32 and not args.mixed
+    std = args.model == "hexapod" and args.horizon == 1 and not args.fp32 and not args.mixed and not args.curved
     if std and world == 1 and total == 4096:
         cfg = "configs[1]"
     elif std and total == CONFIG3_TOTAL and scaling == "strong":

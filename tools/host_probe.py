@@ -4,7 +4,7 @@ and waiting. Tuning aid; one mode per process (device flags must precede the run
   python tools/host_probe.py [plain|noevents|poll|graph|spin|idle|idle5]
 (idle: 1 s of GPU idle, then the job as warmup and the timed job; idle5: the same with bench.py's
 5-step warmup job; idle5spin: idle5 with the warmup's end polled on an event (the host thread kept
-awake) before the synchronize; idle5spin2: also the timed job's end polled)"""
+awake) before the synchronize; idle5spin2: also the timed job's end polled; idle5spin_noev: idle5spin without the events)"""
 import ctypes
 import os
 import sys
@@ -71,10 +71,10 @@ def main():
                 pass
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        if mode != "noevents":
+        if mode not in ("noevents", "idle5spin_noev"):
             e0.record(st)
         job()
-        if mode != "noevents":
+        if mode not in ("noevents", "idle5spin_noev"):
             e1.record(st)
         t1 = time.perf_counter()
         if mode in ("poll", "idle5spin2"):
@@ -84,7 +84,7 @@ def main():
         t2 = time.perf_counter()
         enq.append((t1 - t0) * 1e6)
         walls.append((t2 - t0) * 1e6)
-        evs.append(e0.elapsed_time(e1) * 1e3 if mode != "noevents" else float("nan"))
+        evs.append(e0.elapsed_time(e1) * 1e3 if mode not in ("noevents", "idle5spin_noev") else float("nan"))
     print(f"{mode}: enqueue {np.median(enq):.1f} us, wall {np.median(walls):.1f} us (min {np.min(walls):.1f}), "
           f"events {np.median(evs):.1f} us -> {4096 * 20 / np.median(walls):.1f} M steps/s")
 
