@@ -18,9 +18,13 @@ sys.path.insert(0, ROOT)
 
 def main():
     mode = sys.argv[1] if len(sys.argv) > 1 else "plain"
-    if mode == "spin":  # hipDeviceScheduleSpin before anything initializes the runtime
-        hip = ctypes.CDLL("libamdhip64.so")
+    label = mode
+    if mode == "spin" or mode.startswith("spinflag"):  # hipDeviceScheduleSpin before the runtime initializes
+        import importlib.util  # torch's own HIP runtime (same SONAME: the one every later library binds)
+        tlib = os.path.join(os.path.dirname(importlib.util.find_spec("torch").origin), "lib", "libamdhip64.so")
+        hip = ctypes.CDLL(tlib if os.path.exists(tlib) else "libamdhip64.so")
         print("hipSetDeviceFlags(spin) ->", hip.hipSetDeviceFlags(ctypes.c_uint(1)))
+        label, mode = mode, mode[len("spinflag_"):] if mode.startswith("spinflag_") else mode
     import torch
 
     import hslabs_amd as H
@@ -85,7 +89,7 @@ def main():
         enq.append((t1 - t0) * 1e6)
         walls.append((t2 - t0) * 1e6)
         evs.append(e0.elapsed_time(e1) * 1e3 if mode not in ("noevents", "idle5spin_noev") else float("nan"))
-    print(f"{mode}: enqueue {np.median(enq):.1f} us, wall {np.median(walls):.1f} us (min {np.min(walls):.1f}), "
+    print(f"{label}: enqueue {np.median(enq):.1f} us, wall {np.median(walls):.1f} us (min {np.min(walls):.1f}), "
           f"events {np.median(evs):.1f} us -> {4096 * 20 / np.median(walls):.1f} M steps/s")
 
 
