@@ -406,6 +406,21 @@ class DeviceBatch:
         capi.check(capi.load().hs_run_forces(self.model.handle, ctypes.byref(a), t.data_ptr()), "hs_run_forces")
         self._tau_in = t  # keep alive until the stream has consumed it
 
+    def run_forces_calls(self, tau_in, n_calls: int, call_horizon: int = 1, stream=None) -> None:
+        """n_calls calls of run_forces with call horizon ``call_horizon`` fused into few launches
+        (hs_run_forces_calls): tau_in is a device tensor [B][S][nmj] with S = n_calls *
+        call_horizon = this batch's horizon; every step writes its own row of cf (and q / flags)."""
+        S = n_calls * call_horizon
+        assert self.H == S, "the batch's horizon must equal n_calls * call_horizon (one row per step)"
+        t = tau_in.to(dtype=self.dtype, device=self.device).contiguous()
+        assert t.shape == (self.B, S, self.model.nmj)
+        a = self._args(stream, False, False)
+        a.tau = a.x = a.work_cot = None
+        a.horizon = call_horizon
+        capi.check(capi.load().hs_run_forces_calls(self.model.handle, ctypes.byref(a), n_calls, t.data_ptr()),
+                   "hs_run_forces_calls")
+        self._tau_in = t
+
     def run_steps(self, n_calls: int, stream=None, best: bool = False, accumulate: bool = True,
                   events=None) -> None:
         """n_calls launches marching k0 through the cycle (hs_run_steps); the launch loop is

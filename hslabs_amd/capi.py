@@ -12,7 +12,7 @@ import os
 
 from . import build as _build
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 HS_OK = 0
 HS_FLAG_RANK_RETRY = 1
@@ -32,7 +32,7 @@ COMM_ID_BYTES = 128
 # every symbol declared in include/hslabs.h
 EXPORTS = [
     "hs_model_load", "hs_model_load_ex", "hs_model_free", "hs_model_get_dims", "hs_pgs_config_read",
-    "hs_run", "hs_run_steps", "hs_run_calls", "hs_run_pd", "hs_run_forces", "hs_mixed_create", "hs_mixed_free",
+    "hs_run", "hs_run_steps", "hs_run_calls", "hs_run_pd", "hs_run_forces", "hs_run_forces_calls", "hs_mixed_create", "hs_mixed_free",
     "hs_mixed_get_dims", "hs_complete_traj", "hs_traj_save", "hs_run_forces_host",
     "hs_run_mixed", "hs_run_mixed_steps", "hs_run_mixed_calls", "hs_run_host", "hs_best_key_cot", "hs_best_key_encode",
     "hs_best_key_decode", "hs_last_error", "hs_abi_version",
@@ -181,6 +181,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_run_calls.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32]
     L.hs_run_mixed_calls.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32]
     L.hs_run_forces.argtypes = [vp, ctypes.POINTER(RunArgsC), vp]
+    L.hs_run_forces_calls.argtypes = [vp, ctypes.POINTER(RunArgsC), ctypes.c_int32, vp]
     L.hs_run_forces_host.argtypes = [vp, ctypes.POINTER(GaitParamsC), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                      ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]

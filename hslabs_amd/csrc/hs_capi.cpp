@@ -490,6 +490,43 @@ int hs_run_forces(hs_model_t m, const hs_run_args* a, const double* tau_in) {
   return launch_steps(d, *a, ws, mp, 1, nullptr);
 }
 
+int hs_run_forces_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls, const double* tau_in) {
+  int rc = check_args(m, a);
+  if (rc != HS_OK) return rc;
+  if (n_calls < 0) return fail(HS_E_ARG, "n_calls < 0");
+  if (a->n_rollouts > 0 && n_calls > 0 && !tau_in) return fail(HS_E_ARG, "tau_in is null");
+  if (a->n_rollouts == 0 || n_calls == 0) return HS_OK;
+  const int64_t S = (int64_t)n_calls * a->horizon;  // steps, one row each
+  if (S > (1 << 24)) return fail(HS_E_ARG, "too many steps");
+  const hs_topo* d = nullptr;
+  void* ws = nullptr;
+  rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);
+  if (rc != HS_OK) return rc;
+  hs::launch_map mp = hs::single_model_map(m->host, a->n_rollouts);
+  mp.tau_in = tau_in;
+  hs_run_args c = *a;
+  c.horizon = (int32_t)S;  // output (and tau_in) rows per rollout
+  c.tau = c.x = c.work_cot = nullptr;
+  c.best_key = nullptr;
+  // the run_fused scheme without the fixup and the work reduce: solve_forces has no declined steps
+  // to defer (its own solve covers every step) and no work. Its LDS layout runs 2 wavefronts / SIMD.
+  const int32_t CHUNK = std::max(1, std::min(HS_FUSED_MAX_STEPS, HS_FUSED_WAVES / std::max(1, mp.n_waves)));
+  const bool f32 = a->precision == HS_PREC_F32;
+  mp.fused_h = a->horizon;
+  mp.setup_only = 1;
+  mp.setup_io = hs::SETUP_STORE;
+  int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+  mp.setup_only = 0;
+  mp.setup_io = hs::SETUP_LOAD;
+  for (int64_t s0 = 0; le == 0 && s0 < S; s0 += CHUNK) {
+    mp.fused_s0 = (int32_t)s0;
+    mp.fused_n = (int32_t)std::min<int64_t>(CHUNK, S - s0);
+    le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+  }
+  if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
+  return HS_OK;
+}
+
 int hs_mixed_create(const hs_model_t* models, int32_t n_models, const int32_t* model_index, int32_t n_rollouts,
                     hs_mixed_t* out) {
   if (!models || !out || (n_rollouts > 0 && !model_index)) return fail(HS_E_ARG, "null argument");

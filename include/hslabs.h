@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 10
+#define HSLABS_ABI_VERSION 11
 
 enum {
   HS_OK = 0,
@@ -223,6 +223,14 @@ int hs_run_pd(hs_model_t model, const hs_run_args* args, const hs_pd_args* pd);
  * Tikhonov-regularized solution is returned). tau, x, work_cot and best_key are
  * not written. */
 int hs_run_forces(hs_model_t model, const hs_run_args* args, const double* tau_in);
+/* n_calls calls of hs_run_forces (call horizon args->horizon, k0 marching by it), fused like
+ * hs_run_calls: a setup pass stores each rollout's gait setup once, then launches of up to 512k
+ * wavefronts over (step, rollout); every step S = n_calls * horizon keeps its own row. tau_in is a
+ * DEVICE array [B][S][nmj], args->cf / q / flags have S rows per rollout. Outputs are bitwise those
+ * of hs_run_forces with horizon S. (periodic::solve_contforces_given_torques over a trajectory,
+ * periodic.cpp:368-374, as called per sample by modelplayer::test_dynamics,
+ * playerexperim.cpp:95-121.) */
+int hs_run_forces_calls(hs_model_t model, const hs_run_args* args, int32_t n_calls, const double* tau_in);
 /* Host-buffer, synchronous form: tau_in [B][H][nmj] -> cf [B][H][3*nfeet], flags [B][H] (may be NULL). */
 int hs_run_forces_host(hs_model_t model, const hs_gait_params* params, int32_t n_rollouts, int32_t n_t, int32_t k0,
                        int32_t horizon, int32_t ignore_reach, const double* tau_in, double* cf, uint32_t* flags);

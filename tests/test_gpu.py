@@ -358,6 +358,40 @@ def test_forces_given_torques_match_oracle(gpu, hmodels, oracle_mod, omodels, na
         assert np.abs(cf[b][ok] - fo["cf"][ok]).max() < 1e-9 * scale
 
 
+@pytest.mark.parametrize("name,B,n_calls,ch", [("hexapod", 12, 1, 20), ("hexapod", 97, 7, 3), ("myant", 300, 300, 1)])
+def test_forces_calls_bitwise_equal_run_forces(gpu, hmodels, name, B, n_calls, ch):
+    """hs_run_forces_calls (the fused form) writes exactly what n_calls calls of hs_run_forces
+    write (call horizon ch, k0 marching by ch through the cycle, hs_run_steps semantics): one call
+    of 20 steps, an odd batch (idle half-wavefront), and S = 300 > the launch's step chunk at small
+    B (two step launches)."""
+    import torch
+
+    from hslabs_amd import synth
+
+    m = hmodels[name]
+    S, k0 = n_calls * ch, 3
+    params = synth.gen_params(B, name, id0=97 + B)
+    full = gpu.DeviceBatch(m, params, n_t=20, k0=k0, horizon=S, outputs=("tau",))
+    full.run(best=False)
+    tau = full.tau + 0.1 * torch.sin(torch.arange(S, device=full.tau.device)[None, :, None]
+                                     + torch.arange(m.nmj, device=full.tau.device)[None, None, :])
+    fz = gpu.DeviceBatch(m, params, n_t=20, k0=k0, horizon=S, outputs=("cf", "q", "flags"))
+    fz.run_forces_calls(tau, n_calls, call_horizon=ch)
+    ref = gpu.DeviceBatch(m, params, n_t=20, k0=k0, horizon=ch, outputs=("cf", "q", "flags"))
+    cf, q, fl = [], [], []
+    for i in range(n_calls):
+        ref.k0 = (k0 + i * ch) % 20
+        ref.run_forces(tau[:, i * ch:(i + 1) * ch])
+        cf.append(ref.cf.clone())
+        q.append(ref.q.clone())
+        fl.append(ref.flags.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(fz.cf, torch.cat(cf, dim=1))
+    assert torch.equal(fz.q, torch.cat(q, dim=1))
+    assert torch.equal(fz.flags, torch.cat(fl, dim=1))
+    assert torch.isfinite(fz.cf).all()
+
+
 def test_position_control_matches_oracle(gpu, hmodels, oracle_mod, omodels):
     """hs_run_pd (player.cpp:388-432) against the oracle's control law, over the cycle
     incl. the wrap of tsi into [2, n_t + 1] (k0 = tsi - 2)."""
