@@ -1336,6 +1336,28 @@ __device__ inline void ws_sync() {
   else wave_sync();
 }
 
+// Lane-strided walks over matrix entries without integer divisions (a 32-bit division by a
+// runtime size is ~40 VALU instructions). TriWalk: the packed lower triangle row by row ((0,0),
+// (1,0), (1,1), (2,0), ...) with rows of r + 1 + extra entries, entries p = lane, lane + 32, ...
+template <int EXTRA = 0>
+struct TriWalk {
+  int r, c;
+  __device__ explicit TriWalk(int p) : r(0), c(p) { settle(); }
+  __device__ void settle() {
+    while (c > r + EXTRA) { c -= r + 1 + EXTRA; r++; }
+  }
+  __device__ void next() { c += HALF; settle(); }
+};
+// RectWalk: row-major entries of an (any) x ld rectangle
+struct RectWalk {
+  int r, c, ld;
+  __device__ RectWalk(int p, int ld_) : r(0), c(p), ld(ld_) { settle(); }
+  __device__ void settle() {
+    while (c >= ld) { c -= ld; r++; }
+  }
+  __device__ void next() { c += HALF; settle(); }
+};
+
 template <bool GLOBAL>
 __device__ __attribute__((always_inline)) inline bool chol_half(real* K, int k, real guard, int lane,
                                                                  real* rdiag = nullptr) {
@@ -1352,9 +1374,16 @@ __device__ __attribute__((always_inline)) inline bool chol_half(real* K, int k, 
     for (int i = j + 1 + lane; i < k; i += HALF) K[i * k + j] = K[i * k + j] * rl;
     ws_sync<GLOBAL>();
     const int m = k - 1 - j;
-    for (int e = lane; e < m * m; e += HALF) {
-      const int i = j + 1 + e / m, c2 = j + 1 + e % m;
-      if (c2 <= i) K[i * k + c2] -= K[i * k + j] * K[c2 * k + j];
+    if constexpr (GLOBAL) {  // the rollout kernels' tier 2 (aug_solve): its measured code kept
+      for (int e = lane; e < m * m; e += HALF) {
+        const int i = j + 1 + e / m, c2 = j + 1 + e % m;
+        if (c2 <= i) K[i * k + c2] -= K[i * k + j] * K[c2 * k + j];
+      }
+    } else {
+      for (TriWalk<> t(lane); t.r < m; t.next()) {  // the trailing lower triangle, entry by entry
+        const int i = j + 1 + t.r, c2 = j + 1 + t.c;
+        K[i * k + c2] -= K[i * k + j] * K[c2 * k + j];
+      }
     }
     ws_sync<GLOBAL>();
   }
@@ -1908,10 +1937,10 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
 // d = (torso part of x_part, z - jz . x_part). Rank-deficient normal matrix
 // (a straight leg): HS_FLAG_GENERAL, Tikhonov 1e-12 of its largest diagonal.
 // ---------------------------------------------------------------------------
+// i in the subtree of h: the node table is in preorder (the loader checks it), so the subtree is
+// [h, h + size) -- one load instead of a parent-pointer chase per test
 __device__ inline bool in_subtree(const hs_topo* T, int i, int h) {
-  for (int a = i; a >= 0; a = T->node[a].parent)
-    if (a == h) return true;
-  return false;
+  return i >= h && i < h + T->node[h].size;
 }
 
 __device__ inline void cross3(const real* a, const real* b, real* c) {
@@ -1924,9 +1953,10 @@ template <class W, class SV>
 __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_topo* T, const SV& sv, ForceL& fr, const W& w, const real* z, int lane) {
   const int n = T->n, nj = T->nmj, nf = T->nf, m = 6 + nj, nq = 3 * nf, ld = nq + 1;
   const real* P0 = w.pos(0, 0);
-  for (int e = lane; e < m * m; e += HALF) {  // I + G G^T, lower triangle
-    const int r = e / m, c = e % m;
-    if (c > r) continue;
+  // I + G G^T, lower triangle; packed row by row, so the torso block (rows < 6, the long sums over
+  // all parts) is the first 21 entries: one pass of the wavefront
+  for (TriWalk<> t(lane); t.r < m; t.next()) {
+    const int r = t.r, c = t.c;
     real s = real(0);
     if (r < 6) {
       for (int i = 1; i < n; i++) {
@@ -1947,8 +1977,13 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
       const real* Jh = w.jpos(0, h);
       const real* Zh = w.jz(0, h);
       const int h2 = (c >= 6) ? T->hinge_ids[c - 6] : -1;
-      for (int i = 1; i < n; i++) {
-        if (!in_subtree(T, i, h) || (h2 >= 0 && !in_subtree(T, i, h2))) continue;
+      // the parts in both subtrees, in increasing order: [max(h, h2), min of their ends) in preorder
+      int i0 = h, i1 = h + T->node[h].size;
+      if (h2 >= 0) {
+        i0 = max(i0, h2);
+        i1 = min(i1, h2 + T->node[h2].size);
+      }
+      for (int i = max(i0, 1); i < min(i1, n); i++) {
         const real* Pi = w.pos(0, i);
         real a3[3], u[3];
         for (int t = 0; t < 3; t++) a3[t] = Jh[t] - Pi[t];
@@ -1974,8 +2009,8 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     }
     fr.W[r * m + c] = ((r == c) ? real(1) : real(0)) + s;
   }
-  for (int e = lane; e < m * ld; e += HALF) {  // [C | d]
-    const int r = e / ld, q = e % ld;
+  for (RectWalk t(lane, ld); t.r < m; t.next()) {  // [C | d]
+    const int r = t.r, q = t.c;
     real v = real(0);
     if (q < nq) {
       const int fi = q / 3, jj = q % 3;
@@ -2030,9 +2065,8 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
       }
       eps *= real(1e-12);
     }
-    for (int e = lane; e < nq * ld; e += HALF) {
-      const int p = e / ld, q = e % ld;
-      if (q < nq && q > p) continue;
+    for (TriWalk<1> t(lane); t.r < nq; t.next()) {  // lower triangle of row p, then its rhs entry
+      const int p = t.r, q = (t.c == p + 1) ? nq : t.c;
       real s = 0;
       for (int i = 0; i < m; i++) s += fr.Ct[i * ld + p] * fr.Ct[i * ld + q];
       if (q < nq) fr.W[p * nq + q] = s + ((p == q) ? eps : real(0));
