@@ -124,8 +124,8 @@ struct CentreL {  // fields read after D
   int unreach[HS_LMAX];
 };
 
-struct ForceL {  // solve_forces: W = I + G G^T, later the normal matrix; L^-1 [C | d]
-  real W[(6 + HS_KMAX) * (6 + HS_KMAX)];
+struct ForceL {  // solve_forces: W = I + G G^T, later the normal matrix (packed lower triangles); L^-1 [C | d]
+  real W[(6 + HS_KMAX) * (7 + HS_KMAX) / 2];
   real Ct[(6 + HS_KMAX) * (HS_KMAX + 1)];
   real y[HS_KMAX];
 };
@@ -1374,18 +1374,36 @@ __device__ __attribute__((always_inline)) inline bool chol_half(real* K, int k, 
     for (int i = j + 1 + lane; i < k; i += HALF) K[i * k + j] = K[i * k + j] * rl;
     ws_sync<GLOBAL>();
     const int m = k - 1 - j;
-    if constexpr (GLOBAL) {  // the rollout kernels' tier 2 (aug_solve): its measured code kept
-      for (int e = lane; e < m * m; e += HALF) {
-        const int i = j + 1 + e / m, c2 = j + 1 + e % m;
-        if (c2 <= i) K[i * k + c2] -= K[i * k + j] * K[c2 * k + j];
-      }
-    } else {
-      for (TriWalk<> t(lane); t.r < m; t.next()) {  // the trailing lower triangle, entry by entry
-        const int i = j + 1 + t.r, c2 = j + 1 + t.c;
-        K[i * k + c2] -= K[i * k + j] * K[c2 * k + j];
-      }
+    for (int e = lane; e < m * m; e += HALF) {
+      const int i = j + 1 + e / m, c2 = j + 1 + e % m;
+      if (c2 <= i) K[i * k + c2] -= K[i * k + j] * K[c2 * k + j];
     }
     ws_sync<GLOBAL>();
+  }
+  return true;
+}
+
+// packed lower-triangle index (row-major: row r holds r + 1 entries)
+__device__ inline int pk(int r, int c) { return r * (r + 1) / 2 + c; }
+
+// chol_half's right-looking Cholesky on a packed lower triangle in LDS (solve_forces: its normal
+// matrices), the same operations per entry; the trailing update walks the packed entries
+__device__ __attribute__((always_inline)) inline bool chol_packed(real* K, int k, real guard, int lane) {
+  real mx = 0;
+  for (int i = 0; i < k; i++) mx = fmax(mx, K[pk(i, i)]);
+  for (int j = 0; j < k; j++) {
+    const real s = K[pk(j, j)];
+    if (!(s > guard * mx)) return false;
+    const real l = sqrt(s), rl = real(1) / l;
+    if (lane == 0) K[pk(j, j)] = l;
+    for (int i = j + 1 + lane; i < k; i += HALF) K[pk(i, j)] = K[pk(i, j)] * rl;
+    wave_sync();
+    const int m = k - 1 - j;
+    for (TriWalk<> t(lane); t.r < m; t.next()) {  // the trailing lower triangle, entry by entry
+      const int i = j + 1 + t.r, c2 = j + 1 + t.c;
+      K[pk(i, c2)] -= K[pk(i, j)] * K[pk(c2, j)];
+    }
+    wave_sync();
   }
   return true;
 }
@@ -2007,7 +2025,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
         }
       }
     }
-    fr.W[r * m + c] = ((r == c) ? real(1) : real(0)) + s;
+    fr.W[pk(r, c)] = ((r == c) ? real(1) : real(0)) + s;
   }
   for (RectWalk t(lane, ld); t.r < m; t.next()) {  // [C | d]
     const int r = t.r, q = t.c;
@@ -2045,12 +2063,12 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     fr.Ct[r * ld + q] = v;
   }
   wave_sync();
-  chol_half<false>(fr.W, m, real(0), lane);  // I + G G^T: eigenvalues >= 1
+  chol_packed(fr.W, m, real(0), lane);  // I + G G^T: eigenvalues >= 1
   if (lane < ld) {                // L^-1 [C | d], one column per lane
     for (int i = 0; i < m; i++) {
       real s = fr.Ct[i * ld + lane];
-      for (int t = 0; t < i; t++) s -= fr.W[i * m + t] * fr.Ct[t * ld + lane];
-      fr.Ct[i * ld + lane] = s / fr.W[i * m + i];
+      for (int t = 0; t < i; t++) s -= fr.W[pk(i, t)] * fr.Ct[t * ld + lane];
+      fr.Ct[i * ld + lane] = s / fr.W[pk(i, i)];
     }
   }
   wave_sync();
@@ -2069,23 +2087,23 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
       const int p = t.r, q = (t.c == p + 1) ? nq : t.c;
       real s = 0;
       for (int i = 0; i < m; i++) s += fr.Ct[i * ld + p] * fr.Ct[i * ld + q];
-      if (q < nq) fr.W[p * nq + q] = s + ((p == q) ? eps : real(0));
+      if (q < nq) fr.W[pk(p, q)] = s + ((p == q) ? eps : real(0));
       else fr.y[p] = s;
     }
     wave_sync();
-    if (chol_half<false>(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) break;
+    if (chol_packed(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) break;
     flags = HS_FLAG_GENERAL;  // least squares not unique
   }
   if (lane == 0) {
     for (int i = 0; i < nq; i++) {
       real s = fr.y[i];
-      for (int k = 0; k < i; k++) s -= fr.W[i * nq + k] * fr.y[k];
-      fr.y[i] = s / fr.W[i * nq + i];
+      for (int k = 0; k < i; k++) s -= fr.W[pk(i, k)] * fr.y[k];
+      fr.y[i] = s / fr.W[pk(i, i)];
     }
     for (int i = nq - 1; i >= 0; i--) {
       real s = fr.y[i];
-      for (int k = i + 1; k < nq; k++) s -= fr.W[k * nq + i] * fr.y[k];
-      fr.y[i] = s / fr.W[i * nq + i];
+      for (int k = i + 1; k < nq; k++) s -= fr.W[pk(k, i)] * fr.y[k];
+      fr.y[i] = s / fr.W[pk(i, i)];
     }
   }
   wave_sync();
