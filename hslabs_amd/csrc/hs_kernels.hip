@@ -1955,11 +1955,6 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
 // d = (torso part of x_part, z - jz . x_part). Rank-deficient normal matrix
 // (a straight leg): HS_FLAG_GENERAL, Tikhonov 1e-12 of its largest diagonal.
 // ---------------------------------------------------------------------------
-// i in the subtree of h: the node table is in preorder (the loader checks it), so the subtree is
-// [h, h + size) -- one load instead of a parent-pointer chase per test
-__device__ inline bool in_subtree(const hs_topo* T, int i, int h) {
-  return i >= h && i < h + T->node[h].size;
-}
 
 __device__ inline void cross3(const real* a, const real* b, real* c) {
   c[0] = a[1] * b[2] - a[2] * b[1];
@@ -1991,15 +1986,16 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
         s += v;
       }
     } else {
-      const int h = T->hinge_ids[r - 6];
+      // the node table is in preorder (the loader checks it): a motor's subtree is one range
+      // [h, end), and the parts in both subtrees, in increasing order, are their intersection
+      const int hr = T->hinge_range[r - 6], h = hr & 255;
       const real* Jh = w.jpos(0, h);
       const real* Zh = w.jz(0, h);
-      const int h2 = (c >= 6) ? T->hinge_ids[c - 6] : -1;
-      // the parts in both subtrees, in increasing order: [max(h, h2), min of their ends) in preorder
-      int i0 = h, i1 = h + T->node[h].size;
+      const int hr2 = (c >= 6) ? T->hinge_range[c - 6] : -1, h2 = (c >= 6) ? (hr2 & 255) : -1;
+      int i0 = h, i1 = hr >> 8;
       if (h2 >= 0) {
         i0 = max(i0, h2);
-        i1 = min(i1, h2 + T->node[h2].size);
+        i1 = min(i1, hr2 >> 8);
       }
       for (int i = max(i0, 1); i < min(i1, n); i++) {
         const real* Pi = w.pos(0, i);
@@ -2040,8 +2036,8 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
         for (int t = 0; t < 3; t++) d[t] = fp[t] - P0[t];
         v = cross_e(d, jj, r - 3);
       } else {
-        const int h = T->hinge_ids[r - 6];
-        if (in_subtree(T, T->footis[fi], h)) {
+        const int hr = T->hinge_range[r - 6], h = hr & 255, foot = T->footis[fi];
+        if (foot >= h && foot < (hr >> 8)) {  // the foot in motor r - 6's subtree
           const real* Jh = w.jpos(0, h);
           const real* Zh = w.jz(0, h);
           real d[3];

@@ -527,6 +527,10 @@ int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& 
     }
   }
   if (n > 0 && t->node[0].size != n) { err = "node table not one tree"; return HS_E_TOPOLOGY; }
+  for (int j = 0; j < t->nmj; j++) {  // motor j's subtree as one packed range [h, h + size)
+    const int h = t->hinge_ids[j];
+    t->hinge_range[j] = h | ((h + t->node[h].size) << 8);
+  }
   // each hinge may carry at most one foot below it (keeps the 1st-order Gram block diagonal)
   for (int fi = 0; fi < nf; fi++)
     for (int a = t->footis[fi]; a >= 0; a = t->node[a].parent) {

@@ -60,4 +60,7 @@ struct hs_topo {
   int32_t foot_chain[HS_LMAX][HS_NMAX];
   int32_t hinge_foot[HS_NMAX];          // node[hinge_ids[j]].limb_below by motor index j
   hs_node node[HS_NMAX];
+  // (after node[], so the fields above keep their offsets) motor j's subtree in the preorder
+  // table: hinge_ids[j] | (hinge_ids[j] + its size) << 8, one load for solve_forces' subtree tests
+  int32_t hinge_range[HS_NMAX];
 };
