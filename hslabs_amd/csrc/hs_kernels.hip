@@ -2060,12 +2060,23 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
   }
   wave_sync();
   chol_packed(fr.W, m, real(0), lane);  // I + G G^T: eigenvalues >= 1
-  if (lane < ld) {                // L^-1 [C | d], one column per lane
-    for (int i = 0; i < m; i++) {
-      real s = fr.Ct[i * ld + lane];
-      for (int t = 0; t < i; t++) s -= fr.W[pk(i, t)] * fr.Ct[t * ld + lane];
-      fr.Ct[i * ld + lane] = s / fr.W[pk(i, i)];
+  if (lane < ld) {  // L^-1 [C | d], one column per lane, the column in registers (m <= 6 + HS_KMAX)
+    constexpr int MM = 6 + HS_KMAX;
+    real col[MM];
+#pragma unroll
+    for (int i = 0; i < MM; i++) col[i] = (i < m) ? fr.Ct[i * ld + lane] : real(0);
+#pragma unroll
+    for (int i = 0; i < MM; i++) {
+      if (i < m) {
+        real s = col[i];
+#pragma unroll
+        for (int t = 0; t < i; t++) s -= fr.W[pk(i, t)] * col[t];
+        col[i] = s / fr.W[pk(i, i)];
+      }
     }
+#pragma unroll
+    for (int i = 0; i < MM; i++)
+      if (i < m) fr.Ct[i * ld + lane] = col[i];
   }
   wave_sync();
   uint32_t flags = 0;
@@ -2090,17 +2101,32 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     if (chol_packed(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) break;
     flags = HS_FLAG_GENERAL;  // least squares not unique
   }
-  if (lane == 0) {
-    for (int i = 0; i < nq; i++) {
-      real s = fr.y[i];
-      for (int k = 0; k < i; k++) s -= fr.W[pk(i, k)] * fr.y[k];
-      fr.y[i] = s / fr.W[pk(i, i)];
+  if (lane == 0) {  // the two triangular solves with y in registers (nq <= HS_KMAX)
+    real yv[HS_KMAX];
+#pragma unroll
+    for (int i = 0; i < HS_KMAX; i++) yv[i] = (i < nq) ? fr.y[i] : real(0);
+#pragma unroll
+    for (int i = 0; i < HS_KMAX; i++) {
+      if (i < nq) {
+        real s = yv[i];
+#pragma unroll
+        for (int k = 0; k < i; k++) s -= fr.W[pk(i, k)] * yv[k];
+        yv[i] = s / fr.W[pk(i, i)];
+      }
     }
-    for (int i = nq - 1; i >= 0; i--) {
-      real s = fr.y[i];
-      for (int k = i + 1; k < nq; k++) s -= fr.W[pk(k, i)] * fr.y[k];
-      fr.y[i] = s / fr.W[pk(i, i)];
+#pragma unroll
+    for (int i = HS_KMAX - 1; i >= 0; i--) {
+      if (i < nq) {
+        real s = yv[i];
+#pragma unroll
+        for (int k = i + 1; k < HS_KMAX; k++)
+          if (k < nq) s -= fr.W[pk(k, i)] * yv[k];
+        yv[i] = s / fr.W[pk(i, i)];
+      }
     }
+#pragma unroll
+    for (int i = 0; i < HS_KMAX; i++)
+      if (i < nq) fr.y[i] = yv[i];
   }
   wave_sync();
   return flags;
