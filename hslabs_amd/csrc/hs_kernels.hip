@@ -2023,6 +2023,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     }
     fr.W[pk(r, c)] = ((r == c) ? real(1) : real(0)) + s;
   }
+  STAMP(3);
   for (RectWalk t(lane, ld); t.r < m; t.next()) {  // [C | d]
     const int r = t.r, q = t.c;
     real v = real(0);
@@ -2059,7 +2060,9 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     fr.Ct[r * ld + q] = v;
   }
   wave_sync();
+  STAMP(4);
   chol_packed(fr.W, m, real(0), lane);  // I + G G^T: eigenvalues >= 1
+  STAMP(5);
   if (lane < ld) {  // L^-1 [C | d], one column per lane, the column in registers (m <= 6 + HS_KMAX)
     constexpr int MM = 6 + HS_KMAX;
     real col[MM];
@@ -2079,6 +2082,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
       if (i < m) fr.Ct[i * ld + lane] = col[i];
   }
   wave_sync();
+  STAMP(6);
   uint32_t flags = 0;
   for (int pass = 0; pass < 2; pass++) {  // normal equations; second pass regularized
     real eps = 0;
@@ -2098,9 +2102,11 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
       else fr.y[p] = s;
     }
     wave_sync();
+    STAMP(7);
     if (chol_packed(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) break;
     flags = HS_FLAG_GENERAL;  // least squares not unique
   }
+  STAMP(8);
   if (lane == 0) {  // the two triangular solves with y in registers (nq <= HS_KMAX)
     real yv[HS_KMAX];
 #pragma unroll
@@ -2129,6 +2135,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
       if (i < nq) fr.y[i] = yv[i];
   }
   wave_sync();
+  STAMP(9);
   return flags;
 }
 
@@ -2138,6 +2145,7 @@ __device__ __attribute__((always_inline)) inline void forces_step(const hs_topo*
   const int nf = T->nf, cfg = T->cfg, nl = T->n_limbs, nq = 3 * nf;
   dynamics(T, st, sv, w, lane);
   particular(T, sv, w, lane);
+  STAMP(10);
   const size_t row = (size_t)b * a.horizon + h;
   const real* z = inp(mp.tau_in) + (live ? row : 0) * mp.st_tau;
   uint32_t flags = forces_solve(T, sv, fr, w, z, lane);
@@ -2146,6 +2154,7 @@ __device__ __attribute__((always_inline)) inline void forces_step(const hs_topo*
   if (live && a.cf && lane < mp.st_cf) outp(a.cf)[row * mp.st_cf + lane] = (lane < nq) ? fr.y[lane] : real(0);
   if (live && a.q && lane < mp.st_q) outp(a.q)[row * mp.st_q + lane] = (lane < cfg) ? w.q(0)[lane] : real(0);
   if (live && a.flags && lane == 0) a.flags[row] = flags;
+  STAMP(11);
 }
 
 // Global per-rollout workspace: the general path's scratch and the gait-setup cache that
