@@ -1337,16 +1337,27 @@ __device__ inline void ws_sync() {
 }
 
 // Lane-strided walks over matrix entries without integer divisions (a 32-bit division by a
-// runtime size is ~40 VALU instructions). TriWalk: the packed lower triangle row by row ((0,0),
-// (1,0), (1,1), (2,0), ...) with rows of r + 1 + extra entries, entries p = lane, lane + 32, ...
+// runtime size is ~40 VALU instructions) or per-step loops. TriWalk: the packed lower triangle row
+// by row ((0,0), (1,0), (1,1), (2,0), ...) with rows of r + 1 + EXTRA entries, entries p = lane,
+// lane + 32, ...: the row from a single-precision square root (exact for p < 2^20), corrected by
+// one step either way
 template <int EXTRA = 0>
 struct TriWalk {
-  int r, c;
-  __device__ explicit TriWalk(int p) : r(0), c(p) { settle(); }
-  __device__ void settle() {
-    while (c > r + EXTRA) { c -= r + 1 + EXTRA; r++; }
+  int p, r, c;
+  __device__ explicit TriWalk(int p_) : p(p_) { locate(); }
+  // first index of row r: r (r + 1) / 2 + EXTRA r = r (r + 1 + 2 EXTRA) / 2
+  __device__ static int row0(int r) { return r * (r + 1 + 2 * EXTRA) / 2; }
+  __device__ void locate() {
+    const float b = 1.0f + 2.0f * EXTRA;  // r^2 + b r - 2 p = 0
+    r = (int)((sqrtf(b * b + 8.0f * (float)p) - b) * 0.5f);
+    if (row0(r + 1) <= p) r++;
+    if (row0(r) > p) r--;
+    c = p - row0(r);
   }
-  __device__ void next() { c += HALF; settle(); }
+  __device__ void next() {
+    p += HALF;
+    locate();
+  }
 };
 // RectWalk: row-major entries of an (any) x ld rectangle
 struct RectWalk {
