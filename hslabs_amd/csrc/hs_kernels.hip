@@ -1402,17 +1402,36 @@ __device__ inline int pk(int r, int c) { return r * (r + 1) / 2 + c; }
 __device__ __attribute__((always_inline)) inline bool chol_packed(real* K, int k, real guard, int lane) {
   real mx = 0;
   for (int i = 0; i < k; i++) mx = fmax(mx, K[pk(i, i)]);
-  for (int j = 0; j < k; j++) {
-    const real s = K[pk(j, j)];
-    if (!(s > guard * mx)) return false;
-    const real l = sqrt(s), rl = real(1) / l;
-    if (lane == 0) K[pk(j, j)] = l;
-    for (int i = j + 1 + lane; i < k; i += HALF) K[pk(i, j)] = K[pk(i, j)] * rl;
-    wave_sync();
-    const int m = k - 1 - j;
+  // two pivots per trailing pass: pivot j, column j + 1 updated by it, pivot j + 1, then every
+  // entry right of both takes pivot j's product and pivot j + 1's in that order -- each entry sees
+  // the operations of one pivot at a time, in pivot order, as in chol_half
+  for (int j = 0; j < k; j += 2) {
+    const bool two = j + 1 < k;
+    {
+      const real s = K[pk(j, j)];
+      if (!(s > guard * mx)) return false;
+      const real l = sqrt(s), rl = real(1) / l;
+      if (lane == 0) K[pk(j, j)] = l;
+      for (int i = j + 1 + lane; i < k; i += HALF) K[pk(i, j)] = K[pk(i, j)] * rl;
+      wave_sync();
+    }
+    if (two) {
+      for (int i = j + 1 + lane; i < k; i += HALF) K[pk(i, j + 1)] -= K[pk(i, j)] * K[pk(j + 1, j)];
+      wave_sync();
+      const real s = K[pk(j + 1, j + 1)];
+      if (!(s > guard * mx)) return false;
+      const real l = sqrt(s), rl = real(1) / l;
+      if (lane == 0) K[pk(j + 1, j + 1)] = l;
+      for (int i = j + 2 + lane; i < k; i += HALF) K[pk(i, j + 1)] = K[pk(i, j + 1)] * rl;
+      wave_sync();
+    }
+    const int j1 = two ? j + 2 : j + 1, m = k - j1;
     for (TriWalk<> t(lane); t.r < m; t.next()) {  // the trailing lower triangle, entry by entry
-      const int i = j + 1 + t.r, c2 = j + 1 + t.c;
-      K[pk(i, c2)] -= K[pk(i, j)] * K[pk(c2, j)];
+      const int i = j1 + t.r, c2 = j1 + t.c;
+      real v = K[pk(i, c2)];
+      v -= K[pk(i, j)] * K[pk(c2, j)];
+      if (two) v -= K[pk(i, j + 1)] * K[pk(c2, j + 1)];
+      K[pk(i, c2)] = v;
     }
     wave_sync();
   }
