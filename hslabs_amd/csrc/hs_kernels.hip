@@ -1996,10 +1996,8 @@ template <class W, class SV>
 __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_topo* T, const SV& sv, ForceL& fr, const W& w, const real* z, int lane) {
   const int n = T->n, nj = T->nmj, nf = T->nf, m = 6 + nj, nq = 3 * nf, ld = nq + 1;
   const real* P0 = w.pos(0, 0);
-  // I + G G^T, lower triangle; packed row by row, so the torso block (rows < 6, the long sums over
-  // all parts) is the first 21 entries: one pass of the wavefront
-  for (TriWalk<> t(lane); t.r < m; t.next()) {
-    const int r = t.r, c = t.c;
+  // I + G G^T, lower triangle, entry (r, c)
+  auto gram_entry = [&](const int r, const int c) {
     real s = real(0);
     if (r < 6) {
       for (int i = 1; i < n; i++) {
@@ -2052,7 +2050,17 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
       }
     }
     fr.W[pk(r, c)] = ((r == c) ? real(1) : real(0)) + s;
+  };
+  // by entry class, so the lanes of a pass take one branch: the torso block (rows < 6, the long
+  // sums over all parts; 21 entries, one pass), motor rows against the torso force and the torso
+  // torque columns, then the motor block
+  if (lane < 21) {
+    const TriWalk<> t(lane);
+    gram_entry(t.r, t.c);
   }
+  for (int p = lane; p < 3 * nj; p += HALF) gram_entry(6 + p / 3, p % 3);
+  for (int p = lane; p < 3 * nj; p += HALF) gram_entry(6 + p / 3, 3 + p % 3);
+  for (TriWalk<> t(lane); t.r < nj; t.next()) gram_entry(6 + t.r, 6 + t.c);
   STAMP(3);
   for (RectWalk t(lane, ld); t.r < m; t.next()) {  // [C | d]
     const int r = t.r, q = t.c;
