@@ -392,6 +392,32 @@ def test_forces_calls_bitwise_equal_run_forces(gpu, hmodels, name, B, n_calls, c
     assert torch.isfinite(fz.cf).all()
 
 
+def test_forces_calls_fp32(gpu, hmodels):
+    """The single-precision build of solve_forces: the fused form is bitwise the per-call form, and
+    both stay near the fp64 forces where the least squares is well posed (no HS_FLAG_GENERAL)."""
+    import torch
+
+    from hslabs_amd import synth
+
+    m = hmodels["hexapod"]
+    params = synth.gen_params(256, "hexapod", id0=2024)
+    full = gpu.DeviceBatch(m, params, n_t=20, k0=0, horizon=20, outputs=("tau",))
+    full.run_calls(20)
+    ref = gpu.DeviceBatch(m, params, n_t=20, k0=0, horizon=20, outputs=("cf", "flags"))
+    ref.run_forces(full.tau)
+    f32a = gpu.DeviceBatch(m, params, n_t=20, k0=0, horizon=20, outputs=("cf", "flags"), dtype=torch.float32)
+    f32a.run_forces(full.tau)
+    f32b = gpu.DeviceBatch(m, params, n_t=20, k0=0, horizon=20, outputs=("cf", "flags"), dtype=torch.float32)
+    f32b.run_forces_calls(full.tau, 20)
+    torch.cuda.synchronize()
+    assert torch.equal(f32a.cf, f32b.cf) and torch.equal(f32a.flags, f32b.flags)
+    c64, c32 = ref.cf.cpu().numpy(), f32b.cf.double().cpu().numpy()
+    ok = ((ref.flags.cpu().numpy() & 72) == 0) & ((f32b.flags.cpu().numpy() & 72) == 0)  # GENERAL | NAN
+    assert ok.mean() > 0.9
+    err = np.abs(c32 - c64).max(axis=-1) / np.maximum(1, np.abs(c64).max(axis=-1))
+    assert np.isfinite(c32[ok]).all() and np.median(err[ok]) < 1e-3
+
+
 def test_position_control_matches_oracle(gpu, hmodels, oracle_mod, omodels):
     """hs_run_pd (player.cpp:388-432) against the oracle's control law, over the cycle
     incl. the wrap of tsi into [2, n_t + 1] (k0 = tsi - 2)."""
