@@ -16,13 +16,14 @@ import numpy as np
 
 from . import capi
 
-# numpy view of hs_gait_params (128 bytes)
+# numpy view of hs_gait_params (192 bytes)
 GAIT_DTYPE = np.dtype([
     ("torso_pos", "<f8", (3,)), ("torso_angles", "<f8", (3,)), ("step_duration", "<f8"),
     ("period", "<f8"), ("step_length", "<f8"), ("step_height", "<f8"), ("curvature", "<f8"),
-    ("foot_shift", "<f8"), ("foot_shift_type", "<i4"), ("reserved0", "<i4"), ("reserved", "<f8", (3,)),
+    ("foot_shift", "<f8"), ("foot_shift_type", "<i4"), ("rec_transform_flag", "<i4"),
+    ("rec_transl", "<f8", (3,)), ("rec_eas", "<f8", (3,)), ("reserved", "<f8", (5,)),
 ])
-assert GAIT_DTYPE.itemsize == 128
+assert GAIT_DTYPE.itemsize == 192
 
 SWEEP_NAMES = ("step_duration", "period", "step_length", "step_height")  # pergen.cpp:423
 
@@ -40,6 +41,19 @@ class PgsConfigParams:
     step_height: float = 0.1
     curvature: float = 0.0
     foot_shift: tuple = (-1, 0.0)  # (type, value): -1 none, 0 lateral, 1 radial
+    # pergensetup's record transform (pergen.h:75-76; set_rec_transform, pergen.cpp:316-320):
+    # None, or (rec_transl, rec_eas) -- every record is then transformed (transform_rec, pergen.cpp:238)
+    rec_transform: tuple | None = None
+
+    def set_rec_rotation(self, rec_eas) -> None:
+        """pergensetup::set_rec_rotation (pergen.cpp:309-313): the rotation by Euler angles, the
+        transform's translation kept (zero unless set before)."""
+        transl = (0.0, 0.0, 0.0) if self.rec_transform is None else tuple(self.rec_transform[0])
+        self.rec_transform = (transl, tuple(float(v) for v in rec_eas))
+
+    def set_rec_transform(self, rec_transl, rec_eas) -> None:
+        """pergensetup::set_rec_transform (pergen.cpp:316-320)."""
+        self.rec_transform = (tuple(float(v) for v in rec_transl), tuple(float(v) for v in rec_eas))
 
     def to_record(self) -> np.ndarray:
         r = np.zeros((), GAIT_DTYPE)
@@ -52,6 +66,10 @@ class PgsConfigParams:
         r["curvature"] = self.curvature
         r["foot_shift_type"] = self.foot_shift[0]
         r["foot_shift"] = self.foot_shift[1]
+        if self.rec_transform is not None:
+            r["rec_transform_flag"] = 1
+            r["rec_transl"] = self.rec_transform[0]
+            r["rec_eas"] = self.rec_transform[1]
         return r
 
     @staticmethod
@@ -61,7 +79,9 @@ class PgsConfigParams:
             torso_angles=tuple(float(v) for v in r["torso_angles"]),
             step_duration=float(r["step_duration"]), period=float(r["period"]),
             step_length=float(r["step_length"]), step_height=float(r["step_height"]),
-            curvature=float(r["curvature"]), foot_shift=(int(r["foot_shift_type"]), float(r["foot_shift"])))
+            curvature=float(r["curvature"]), foot_shift=(int(r["foot_shift_type"]), float(r["foot_shift"])),
+            rec_transform=((tuple(float(v) for v in r["rec_transl"]), tuple(float(v) for v in r["rec_eas"]))
+                           if int(r["rec_transform_flag"]) else None))
 
 
 def read_pgs_config(path: str, setup_id: int) -> PgsConfigParams:
@@ -229,18 +249,39 @@ class ShardedBatch:
         capi.check(L.hs_batch_set_params(h, self.params.ctypes.data_as(ctypes.POINTER(capi.GaitParamsC))),
                    "hs_batch_set_params")
 
+    def _shapes(self) -> dict:
+        m, B, H = self.model, self.B, self.H
+        return {"q": (B, H, m.config_dim), "tau": (B, H, m.nmj), "cf": (B, H, 3 * m.nfeet),
+                "x": (B, H, 6 * m.n_parts), "flags": (B, H), "work": (B,), "cot": (B,)}
+
     def run(self, k0: int = 0, ignore_reach: bool = True, want=("tau", "cf", "flags", "work", "cot")) -> dict:
-        m, B, H, f = self.model, self.B, self.H, self.dtype
-        shapes = {"q": (B, H, m.config_dim), "tau": (B, H, m.nmj), "cf": (B, H, 3 * m.nfeet),
-                  "x": (B, H, 6 * m.n_parts), "flags": (B, H), "work": (B,), "cot": (B,)}
-        out = {k: np.zeros(shapes[k], np.uint32 if k == "flags" else f) for k in want}
+        shapes = self._shapes()
+        out = {k: np.zeros(shapes[k], np.uint32 if k == "flags" else self.dtype) for k in want}
         o = capi.BatchOutputsC(**{k: v.ctypes.data for k, v in out.items()})
         capi.check(capi.load().hs_batch_run(self.handle, k0, int(ignore_reach), ctypes.byref(o)), "hs_batch_run")
         return out
 
     def run_device(self, out: dict, k0: int = 0, ignore_reach: bool = True) -> None:
         """hs_batch_run_device: the requested outputs into caller-owned device tensors (any device of
-        the process; keys as in run(), whole-batch layouts)."""
+        the process; keys as in run(), whole-batch layouts). Every tensor is checked first: a known
+        key, the shape run() uses, the batch's float dtype (flags int32/uint32), contiguous and on a
+        GPU -- the native call copies raw bytes sized by the batch and cannot check any of that."""
+        import torch
+
+        shapes = self._shapes()
+        fdt = torch.float32 if self.dtype == np.float32 else torch.float64
+        for k, v in out.items():
+            if k not in shapes:
+                raise ValueError(f"run_device: unknown output {k!r} (expected one of {sorted(shapes)})")
+            if not isinstance(v, torch.Tensor) or not v.is_cuda:
+                raise ValueError(f"run_device: {k} must be a GPU tensor")
+            want = (torch.int32, torch.uint32) if k == "flags" else (fdt,)
+            if v.dtype not in want:
+                raise ValueError(f"run_device: {k} has dtype {v.dtype}, expected {' or '.join(map(str, want))}")
+            if tuple(v.shape) != shapes[k]:
+                raise ValueError(f"run_device: {k} has shape {tuple(v.shape)}, expected {shapes[k]}")
+            if not v.is_contiguous():
+                raise ValueError(f"run_device: {k} must be contiguous")
         o = capi.BatchOutputsC(**{k: v.data_ptr() for k, v in out.items()})
         capi.check(capi.load().hs_batch_run_device(self.handle, k0, int(ignore_reach), ctypes.byref(o)),
                    "hs_batch_run_device")

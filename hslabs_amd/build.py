@@ -84,10 +84,31 @@ def _compile(out: str, defines=(), verbose: bool = False, flags=()) -> str:
     return out
 
 
+def _isa_check(lib: str, fatal: bool) -> None:
+    """tools/isa_check.py on the built library: no vector instruction (a VGPR spill store, above all)
+    may sit where a divergent loop exits with EXEC == 0, the miscompile that broke the inlined
+    Eigen-style solve."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tools"))
+    try:
+        import isa_check
+    finally:
+        sys.path.pop(0)
+    if not os.path.exists(os.path.join(isa_check.LLVM, "llvm-objdump")):
+        print("isa_check skipped: llvm-objdump not found", file=sys.stderr)
+        return
+    bad = isa_check.check(lib)
+    if bad and fatal:
+        os.remove(lib)
+        raise RuntimeError(f"{lib}: {bad} device function(s) with vector instructions at EXEC == 0 after a "
+                           "divergent loop exit (tools/isa_check.py); the library was removed")
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
-    return _compile(LIB, verbose=verbose)
+    _compile(LIB, verbose=verbose)
+    _isa_check(LIB, fatal=True)
+    return LIB
 
 
 def build_variant(name: str, defines, verbose: bool = False, flags=()) -> str:
@@ -95,7 +116,9 @@ def build_variant(name: str, defines, verbose: bool = False, flags=()) -> str:
     sweep selects one by name with HSLABS_VARIANT=<name> (capi.load reports the library it loaded,
     and bench.py prints its path and hash). Delete them after the sweep."""
     os.makedirs(VARIANT_DIR, exist_ok=True)
-    return _compile(os.path.join(VARIANT_DIR, f"libhslabs_{name}.so"), defines, verbose, flags)
+    out = _compile(os.path.join(VARIANT_DIR, f"libhslabs_{name}.so"), defines, verbose, flags)
+    _isa_check(out, fatal=False)  # reported, not fatal: tuning builds may be inspected
+    return out
 
 
 if __name__ == "__main__":

@@ -12,7 +12,7 @@ import os
 
 from . import build as _build
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 HS_OK = 0
 HS_FLAG_RANK_RETRY = 1
@@ -48,7 +48,7 @@ SIM_BODY_STRIDE = 13
 
 
 class GaitParamsC(ctypes.Structure):
-    """hs_gait_params (128 bytes)."""
+    """hs_gait_params (192 bytes)."""
 
     _fields_ = [
         ("torso_pos", ctypes.c_double * 3),
@@ -60,12 +60,14 @@ class GaitParamsC(ctypes.Structure):
         ("curvature", ctypes.c_double),
         ("foot_shift", ctypes.c_double),
         ("foot_shift_type", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
-        ("reserved", ctypes.c_double * 3),
+        ("rec_transform_flag", ctypes.c_int32),
+        ("rec_transl", ctypes.c_double * 3),
+        ("rec_eas", ctypes.c_double * 3),
+        ("reserved", ctypes.c_double * 5),
     ]
 
 
-assert ctypes.sizeof(GaitParamsC) == 128
+assert ctypes.sizeof(GaitParamsC) == 192
 
 
 class BatchOutputsC(ctypes.Structure):

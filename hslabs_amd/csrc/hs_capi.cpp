@@ -1483,21 +1483,29 @@ int hs_select_best(hs_batch_t b, float* cot, int64_t* rollout_id) {
 
 int hs_select_best_comm(hs_batch_t b, hs_comm_t comm, float* cot, int64_t* rollout_id) {
   if (!comm) return fail(HS_E_ARG, "null comm");
+  // the local minimum, or the error that prevents it; either way this rank then takes part in the
+  // all-reduce (contributing UINT64_MAX on an error), so its peers are never left waiting in it
   uint64_t best = ~0ull;
-  int rc = local_best(b, &best);
-  if (rc != HS_OK) return rc;
-  for (auto& sh : b->shards)
-    if (sh.dev != hs::comm_device(comm)) return fail(HS_E_ARG, "the batch runs on a device the comm does not");
+  int rc = (cot && rollout_id) ? local_best(b, &best) : fail(HS_E_ARG, "null cot or rollout_id");
+  if (rc == HS_OK)
+    for (auto& sh : b->shards)
+      if (sh.dev != hs::comm_device(comm)) {
+        rc = fail(HS_E_ARG, "the batch runs on a device the comm does not");
+        best = ~0ull;
+      }
+  std::string err = rc != HS_OK ? std::string(hs_last_error()) : std::string();
   device_guard guard;
-  const hs_batch_s::shard& sh = b->shards[0];
-  hipError_t e = hipSetDevice(sh.dev);
-  if (e == hipSuccess) e = hipMemcpyAsync(sh.best_key, &best, sizeof(best), hipMemcpyHostToDevice, sh.stream);
+  hipStream_t st = nullptr;  // the comm device's null stream: the reduce does not use the batch's key
+  uint64_t* key = hs::comm_scratch(comm);
+  hipError_t e = hipSetDevice(hs::comm_device(comm));
+  if (e == hipSuccess) e = hipMemcpyAsync(key, &best, sizeof(best), hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return hip_fail(e, "hs_select_best_comm");
-  rc = hs::comm_reduce_min(comm, sh.best_key, sh.stream);
-  if (rc != HS_OK) return rc;
-  e = hipMemcpyAsync(&best, sh.best_key, sizeof(best), hipMemcpyDeviceToHost, sh.stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(sh.stream);
+  int rr = hs::comm_reduce_min(comm, key, st);
+  if (rr != HS_OK) return rr;
+  e = hipMemcpyAsync(&best, key, sizeof(best), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return hip_fail(e, "hs_select_best_comm");
+  if (rc != HS_OK) return fail(rc, err);
   hs_best_key_decode(best, cot, rollout_id);
   return HS_OK;
 }

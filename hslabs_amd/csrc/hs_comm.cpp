@@ -17,6 +17,7 @@ struct hs_comm_s {
   ncclComm_t comm = nullptr;
   int dev = 0;
   int32_t n_ranks = 0, rank = 0;
+  uint64_t* scratch = nullptr;  // 8 B on dev: hs_select_best_comm's reduce buffer (never a batch's own key)
 };
 
 namespace {
@@ -42,6 +43,8 @@ int comm_reduce_min(hs_comm_t c, uint64_t* key, void* stream) {
 }
 
 int comm_device(hs_comm_t c) { return c->dev; }
+
+uint64_t* comm_scratch(hs_comm_t c) { return c->scratch; }
 
 }  // namespace hs
 
@@ -75,6 +78,12 @@ int hs_comm_init(int32_t n_ranks, int32_t rank, const char id[HS_COMM_ID_BYTES],
   }
   c->n_ranks = n_ranks;
   c->rank = rank;
+  e = hipMalloc(&c->scratch, sizeof(uint64_t));
+  if (e != hipSuccess) {
+    (void)ncclCommDestroy(c->comm);
+    delete c;
+    return hs::set_error(HS_E_DEVICE, std::string("hipMalloc(comm scratch): ") + hipGetErrorString(e));
+  }
   *out = c;
   return HS_OK;
 }
@@ -82,6 +91,13 @@ int hs_comm_init(int32_t n_ranks, int32_t rank, const char id[HS_COMM_ID_BYTES],
 void hs_comm_free(hs_comm_t c) {
   if (!c) return;
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->scratch) {
+    int cur = 0;
+    if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(c->dev) == hipSuccess) {
+      (void)hipFree(c->scratch);
+      (void)hipSetDevice(cur);
+    }
+  }
   delete c;
 }
 

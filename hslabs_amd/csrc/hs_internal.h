@@ -16,6 +16,7 @@ int set_error(int code, const std::string& msg);
 // the best-key all-reduce of hs_comm.cpp (ncclMin over ncclUint64, in place, async on stream)
 int comm_reduce_min(hs_comm_t comm, uint64_t* key, void* stream);
 int comm_device(hs_comm_t comm);
+uint64_t* comm_scratch(hs_comm_t comm);  // 8 B on the comm's device
 
 int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& err, hs_simtopo* sim = nullptr);
 int read_pgs_config(const char* path, int setup_id, hs_gait_params* out, std::string& xml, std::string& err);

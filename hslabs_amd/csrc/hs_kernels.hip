@@ -109,6 +109,13 @@ struct GenMats {
   int8_t rowsT[LD], colsT[LD], q[LD], piv[LD], rycol[LD], cperm[LD];
 };
 using GenWS = GenMats<HS_KMAX, false>;
+// A rollout's global solve workspace: tier 2's augmented system (fast_solve) or the Eigen-style path's
+// matrices. Tier 2 runs first and the general path only after it declined; each writes every entry it
+// reads before reading it, so the members never carry values from one to the other.
+union SolveWS {
+  GenWS gen;
+  AugL aug;
+};
 
 template <int NM>
 struct StencilL {  // fields only the finite differences read
@@ -239,6 +246,7 @@ struct GaitR {
   real torso_pos[3], torso_angles[3];
   real step_duration, period, step_length, step_height, curvature, foot_shift;
   int foot_shift_type;
+  int rec_xf;  // rec_transform_flag: the transform itself is read where it applies (gait_record)
 };
 
 __device__ inline GaitR load_gait(const hs_gait_params& p) {
@@ -254,7 +262,23 @@ __device__ inline GaitR load_gait(const hs_gait_params& p) {
   g.curvature = (real)p.curvature;
   g.foot_shift = (real)p.foot_shift;
   g.foot_shift_type = p.foot_shift_type;
+  g.rec_xf = p.rec_transform_flag;
   return g;
+}
+
+// pergensetup::transform_rec (pergen.cpp:323-335) with rec_transform = affine_from_orientation(
+// {rec_transl, rec_eas}) (set_rec_transform, pergen.cpp:316-320): the torso by transform_orientation
+// (pergen.cpp:377-383: A1 = rec_transform A0, then its translation and Euler angles), the foot target
+// by rec_transform.mult with w = 1
+__device__ inline void transform_rec(const hs_gait_params& p, real* o0, real* o1, real* target) {
+  const real tr[3] = {(real)p.rec_transl[0], (real)p.rec_transl[1], (real)p.rec_transl[2]};
+  const A34 R = from_euler(tr, (real)p.rec_eas[0], (real)p.rec_eas[1], (real)p.rec_eas[2]);
+  const A34 A1 = mul(R, from_euler(o0, o1[0], o1[1], o1[2]));
+  o0[0] = A1(0, 3); o0[1] = A1(1, 3); o0[2] = A1(2, 3);
+  euler_from(A1, o1);
+  real t[3];
+  mulp(R, target, t);
+  target[0] = t[0]; target[1] = t[1]; target[2] = t[2];
 }
 
 // ---------------------------------------------------------------------------
@@ -398,8 +422,9 @@ __device__ __attribute__((always_inline)) inline void node_features(const hs_top
 // STRAIGHT: the caller knows curvature == 0 (a wave of straight gaits), so the turning code is left
 // out and the record is one basic block the scheduler can interleave with the torso FK
 template <bool STRAIGHT = false>
-__device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g, const SetupL& st, real t, int j,
-                                                                  real* o0, real* o1, bool& turned, real* target) {
+__device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g, const hs_gait_params& gp,
+                                                                  const SetupL& st, real t, int j, real* o0, real* o1,
+                                                                  bool& turned, real* target) {
   o0[0] = g.torso_pos[0]; o0[1] = g.torso_pos[1]; o0[2] = g.torso_pos[2];
   o1[0] = g.torso_angles[0]; o1[1] = g.torso_angles[1]; o1[2] = g.torso_angles[2];
   real tv = t * st.v;
@@ -454,6 +479,10 @@ __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g
   target[0] = dx + st.pos0[j][0];
   target[1] = dy + st.pos0[j][1];
   target[2] = dz + st.pos0[j][2];
+  if (!STRAIGHT && g.rec_xf) {  // set_rec's last step (pergen.cpp:238)
+    transform_rec(gp, o0, o1, target);
+    turned = true;  // the torso angles are no longer the configured ones
+  }
 }
 
 // sample times t_i = dt + dt + ... (i terms, periodic.cpp:171-181), stored once per rollout by the
@@ -467,8 +496,9 @@ __device__ inline real sample_time(const SetupL& st, const real* t_tab, int isam
 }
 
 template <bool STRAIGHT, class W>
-__device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* T, const GaitR& g, const SetupL& st, int isample, int L,
-                           bool ignore_reach, const W& w, int k, const real* t_tab) {
+__device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* T, const GaitR& g, const hs_gait_params& gp,
+                                                                 const SetupL& st, int isample, int L, bool ignore_reach,
+                                                                 const W& w, int k, const real* t_tab) {
   const int j = T->limb_pergen[L];
   const int ysign = T->limb_ysign[L];
   const int clen = T->limb_chain_len[L];
@@ -476,7 +506,7 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
   const real t = sample_time(st, t_tab, isample);  // t accumulates dt (periodic.cpp:171-181)
   real o0[3], o1[3], target[3];
   bool turned;
-  gait_record<STRAIGHT>(g, st, t, j, o0, o1, turned, target);
+  gait_record<STRAIGHT>(g, gp, st, t, j, o0, o1, turned, target);
   STAMP(20);
   // set_jvalues_with_lik: torso + body chain FK, then limb IK (model.cpp:354-359, lik.cpp:89-99)
   real q6[6] = {o0[0], o0[1], o0[2], o1[0], o1[1], o1[2]};
@@ -1182,15 +1212,17 @@ __device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
 }
 
 // The general path is an out-of-line call: it keeps its own register allocation apart from the
-// kernel body's 168-VGPR budget (3 waves/SIMD). Inlined at that budget the compiler spilled SGPRs
-// across it, and the Eigen-style path returned wrong forces on every step on the GPU (HS_SOLVE_
-// REFERENCE, tests/test_gpu_parity.py; correct with the 2-wave budget or out of line). The call
-// costs only the steps that take it (stack frame in scratch, 288 B per lane).
-#ifndef HS_GENERAL_INLINE
-#define HS_GENERAL_ATTR __attribute__((noinline))
-#else
-#define HS_GENERAL_ATTR __attribute__((always_inline)) inline
+// kernel body's 168-VGPR budget (3 waves/SIMD). Inlined at that budget (the former HS_GENERAL_INLINE
+// build) hipcc of ROCm 7.2 spills 7 VGPRs in the block that fullpiv_lu's lane-0 permutation loop
+// falls through to when its last lane leaves -- before that block restores EXEC, so the spill stores
+// run with EXEC == 0 and write nothing, and their reloads return stale scratch: wrong forces on every
+// HS_SOLVE_REFERENCE step. tools/isa_check.py finds the pattern in the built
+// library and hslabs_amd/build.py refuses a library that has it. The call costs only the steps that
+// take it (stack frame in scratch, 288 B per lane).
+#ifdef HS_GENERAL_INLINE
+#error "HS_GENERAL_INLINE: the inlined general path is miscompiled at 3 waves/SIMD (VGPR spills at EXEC == 0)"
 #endif
+#define HS_GENERAL_ATTR __attribute__((noinline))
 template <class W, class SV, class G>
 __device__ HS_GENERAL_ATTR uint32_t general_solve(const hs_topo* T, SV& sv, G& g, const W& w, int k, int lane) {
   build_grams(T, sv, g, w, k, lane);
@@ -1525,9 +1557,11 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, AugL&
 
 // TIER2: the augmented-system solve where a D_c or the Schur complement is singular; without it
 // (HS_DEFER_AUG builds of the fused step launch) such steps decline and go to the fixup launch
+// aug_ok = false (the fixup launch's idle half, which stores nothing): decline instead of using the
+// augmented system, whose global workspace is the idle slot every fixup wavefront shares
 template <bool TIER2 = true, class W, class SV>
 __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* T, SV& sv, FastL& fl, AugL& ag, const W& w,
-                                                                 int nc, int lane) {
+                                                                 int nc, bool aug_ok, int lane) {
   const int n = T->n;
   if (nc == 0) return true;
   const real* P0 = w.pos(0, 0);
@@ -1631,7 +1665,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
   STAMP(18);
   const real a[6] = {sv.x[0], sv.x[1], sv.x[2], sv.x[3 * n], sv.x[3 * n + 1], sv.x[3 * n + 2]};
   for (int c = 0; c < nc; c++)
-    if (!fl.ok[c]) return TIER2 ? aug_solve(fl, ag, sv, a, nc, lane) : false;  // only nc >= 3 factors D_c
+    if (!fl.ok[c]) return (TIER2 && aug_ok) ? aug_solve(fl, ag, sv, a, nc, lane) : false;  // only nc >= 3 factors D_c
   int ok = 1;
   if (nc == 1) {  // unique least-squares solution (A^T A) w = -A^T a
     if (lane == 0) {
@@ -1726,7 +1760,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
     }
     wave_sync();
     STAMP(19);
-    if (!fl.ok[0]) return TIER2 ? aug_solve(fl, ag, sv, a, nc, lane) : false;
+    if (!fl.ok[0]) return (TIER2 && aug_ok) ? aug_solve(fl, ag, sv, a, nc, lane) : false;
     if (lane < nc) {
       const int c = lane;
       const real* d0 = fl.d0[c];
@@ -1817,7 +1851,7 @@ __device__ inline void reduce_rollouts(const hs_run_args& a, real total_mass, co
 // region) and 2.4 % of the step time
 template <bool DEFER, class W, class SV>
 __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st, SV& sv,
-                     FastL& fl, WorkL& wk, const W& w, GenWS* G, int b, bool live, int h,
+                     FastL& fl, WorkL& wk, const W& w, SolveWS* G, int b, bool live, int h,
                      real& work, bool& deferred, bool may_general, int lane) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
   STAMP(3);
@@ -1838,8 +1872,8 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   int k = 3 * nc;
   uint32_t flags = 0;
   STAMP(6);
-  // tier 2 (aug_solve) and the general path share the rollout's global workspace: the general
-  // path runs only after tier 2 declined
+  // tier 2 (aug_solve) and the general path share the rollout's global workspace (SolveWS): the
+  // general path runs only after tier 2 declined. may_general = false (the fixup's idle half) skips both
 #ifdef HS_EXP_NO_SOLVE  // timing experiment only: no contact solve (y = 0)
   if (lane < k) sv.y[lane] = 0;
   wave_sync();
@@ -1849,7 +1883,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
 #define HS_DEFER_AUG 0
 #endif
   if (a.solve_mode == HS_SOLVE_AUTO &&
-      fast_solve<!(DEFER && HS_DEFER_AUG)>(T, sv, fl, *reinterpret_cast<AugL*>(G), w, nc, lane)) {
+      fast_solve<!(DEFER && HS_DEFER_AUG)>(T, sv, fl, G->aug, w, nc, may_general, lane)) {
 #endif
     if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
     if (nc == 1) flags |= HS_FLAG_FULL_RANK;
@@ -1861,7 +1895,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
       deferred = true;  // uniform over the half-wave: its outputs come from the fixup launch
       live = false;
     } else if (may_general) {
-      flags = general_solve(T, sv, *G, w, k, lane) | HS_FLAG_GENERAL;
+      flags = general_solve(T, sv, G->gen, w, k, lane) | HS_FLAG_GENERAL;
     }
 #endif
   }
@@ -2198,11 +2232,10 @@ __device__ __attribute__((always_inline)) inline void forces_step(const hs_topo*
 // Global per-rollout workspace: the general path's scratch and the gait-setup cache that
 // carries SetupL from the first launch of a call to the later ones (hs::SETUP_*).
 struct RolloutWS {
-  GenWS gen;  // also the tier-2 AugL (aliased)
+  SolveWS sol;
   SetupL st;
   real t_tab[HS_TTAB];  // sample times (sample_time), with the setup cache
 };
-static_assert(sizeof(AugL) <= sizeof(GenWS), "the augmented system aliases the general workspace");
 static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 
 // The fused path's setup pass (hs_run_calls: gait setup once per rollout, stored for every step):
@@ -2277,9 +2310,9 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
     bb = live ? b : bb;
     live = false;
   }
-  GenWS* G = mp.fused_gen
-                 ? &((RolloutWS*)mp.fused_gen)[(size_t)fstep * (a.n_rollouts + 1) + (live ? b : a.n_rollouts)].gen
-                 : &rws[live ? b : a.n_rollouts].gen;
+  SolveWS* G = mp.fused_gen
+                   ? &((RolloutWS*)mp.fused_gen)[(size_t)fstep * (a.n_rollouts + 1) + (live ? b : a.n_rollouts)].sol
+                   : &rws[live ? b : a.n_rollouts].sol;
   Smem<NM, FORCES>& sm = smem[sub];
   real work = (live && a.accumulate && a.work_cot && !mp.fused_w) ? outp(a.work_cot)[2 * (size_t)b] : real(0);
   int k0 = a.k0, h_row = mp.h_row;
@@ -2319,13 +2352,16 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
 #define HS_EXP_KIN_FIRST 0  // timing experiment only: samples below this offset are not computed
 #endif
     const real* t_tab = mp.setup_io == hs::SETUP_LOAD ? rws[bb].t_tab : nullptr;
-    // both rollouts of the wave straight (the common case): the specialization without turning code
-    if (__ballot(g.curvature != 0) == 0) {
+    // both rollouts of the wave straight and untransformed (the common case): the specialization
+    // without turning and record-transform code
+    if (__ballot(g.curvature != 0 || g.rec_xf) == 0) {
       if (sl < NS && sl >= HS_EXP_KIN_FIRST)
-        kin_sample<true>(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2, t_tab);
+        kin_sample<true>(T, g, a.params[bb], sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
+                         t_tab);
     } else {
       if (sl < NS && sl >= HS_EXP_KIN_FIRST)
-        kin_sample<false>(T, g, sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2, t_tab);
+        kin_sample<false>(T, g, a.params[bb], sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
+                          t_tab);
     }
     wave_sync();
   }
@@ -2425,7 +2461,7 @@ __global__ __launch_bounds__(WAVE) void hs_pergen_rec_kernel(const hs_topo* __re
   if (live && lane < nl) {
     real o0[3], o1[3], target[3];
     bool turned;
-    gait_record<false>(g, st[sub], (real)times[ti], T->limb_pergen[lane], o0, o1, turned, target);
+    gait_record<false>(g, params[b], st[sub], (real)times[ti], T->limb_pergen[lane], o0, o1, turned, target);
     double* r = rec + it * (6 + 3 * nl);
     if (lane == 0)
       for (int i = 0; i < 3; i++) { r[i] = o0[i]; r[3 + i] = o1[i]; }

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 11
+#define HSLABS_ABI_VERSION 12
 
 enum {
   HS_OK = 0,
@@ -43,8 +43,9 @@ enum {
                                     FullPivLU/ColPivQR path used (informational) */
 
 /* Gait setup of one rollout: the fields of pgsconfigparams (pergen.h:137-146),
- * same meaning and units as a pgs_config.txt line (player.cpp:170-208).
- * 128 bytes, so one wavefront reads a rollout's record in one coalesced load. */
+ * same meaning and units as a pgs_config.txt line (player.cpp:170-208), plus
+ * pergensetup's record transform (pergen.h:75-76). 192 bytes; the kernels read
+ * the first 104 and the transform only where rec_transform_flag is set. */
 typedef struct {
   double torso_pos[3];     /* "torso_pos" */
   double torso_angles[3];  /* "torso_angles" (Euler phi, theta, psi; model.cpp:45) */
@@ -55,8 +56,11 @@ typedef struct {
   double curvature;        /* 0 = straight (pergen.cpp:160-198) */
   double foot_shift;       /* lateral_foot_shift / radial_foot_shift value */
   int32_t foot_shift_type; /* -1 none, 0 lateral, 1 radial */
-  int32_t reserved0;
-  double reserved[3];
+  int32_t rec_transform_flag; /* pergensetup::rec_transform_flag (pergen.cpp:206, 319): 1 = every
+                                 record is transformed by rec_transform (set_rec, pergen.cpp:238) */
+  double rec_transl[3];    /* rec_transform = affine_from_orientation({rec_transl, rec_eas})   */
+  double rec_eas[3];       /* (set_rec_transform / set_rec_rotation, pergen.cpp:309-320)       */
+  double reserved[5];
 } hs_gait_params;
 
 typedef struct hs_model_s* hs_model_t;
@@ -90,7 +94,9 @@ int hs_model_get_dims(hs_model_t model, hs_model_dims* out);
  * The default is the reference's only call, (1,1) (player.cpp:263); with another mask every step
  * takes the Eigen-style path (the closed form is the (1,1) problem's; flags carry HS_FLAG_GENERAL).
  * (0,0) is HS_E_ARG: the reference exits with "mask0 not set" (ftsolver.cpp:245). Waits for the
- * work queued on the devices that hold the model. */
+ * work queued on the devices that hold the model. Not concurrent with hs_run* on the same model
+ * (like the reference's solver state, the setting belongs to the model): a launch issued by another
+ * thread while this call runs may see the old mask on the device and the new one on the host. */
 int hs_model_set_torso_penalty(hs_model_t model, int32_t force, int32_t torque);
 int hs_model_get_torso_penalty(hs_model_t model, int32_t* force, int32_t* torque);
 
@@ -401,7 +407,12 @@ int hs_comm_size(hs_comm_t comm, int32_t* n_ranks, int32_t* rank);
  * on stream (a hipStream_t, NULL = default stream) */
 int hs_comm_reduce_best(hs_comm_t comm, uint64_t* key, void* stream);
 /* hs_select_best across the ranks: this process's minimum over its batch's devices (the batch
- * must run on the comm's device only), all-reduced over the communicator, decoded on every rank */
+ * must run on the comm's device only), all-reduced over the communicator, decoded on every rank.
+ * The reduce runs in the comm's own 8-byte device buffer: the batch's per-device keys keep their
+ * local values (a later hs_select_best still returns this process's minimum). Collective: every
+ * rank must call it. A rank whose batch fails the checks (not run, another device, null outputs)
+ * still takes part, contributing the largest key, and then returns the error, so its peers complete
+ * (with the minimum over the other ranks); a null comm returns at once and leaves the peers waiting. */
 int hs_select_best_comm(hs_batch_t batch, hs_comm_t comm, float* cot, int64_t* rollout_id);
 
 /*

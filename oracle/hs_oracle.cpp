@@ -699,9 +699,13 @@ struct PGS {  // pergensetup, pergen.h:68-108
   std::vector<Vec> limb_poss;
   double v = 0;
   Vec torso_pos0, euler_angles;
+  Aff rec_transform;              // pergen.h:75, set_unity at construction (pergen.cpp:206)
+  bool rec_transform_flag = false;
 
   void init(int n_) {  // pergen.cpp:201-208, 243-262
     n = n_;
+    rec_transform.set_unity();
+    rec_transform_flag = false;
     pergen.init(n);
     limb_poss.assign(n, Vec());
     if (n == 4) likpergen = {0, 3, 1, 2};
@@ -731,6 +735,25 @@ struct PGS {  // pergensetup, pergen.h:68-108
       transform_orientation(A, o);
     }
   }
+  void set_rec_transform(const Vec& rec_transl, const Vec& rec_eas) {  // pergen.cpp:316-320
+    const Vec o[2] = {rec_transl, rec_eas};
+    affine_from_orientation(rec_transform, o);
+    rec_transform_flag = true;
+  }
+  void transform_rec(double* rec) const {  // pergen.cpp:323-335
+    Vec o[2];
+    o[0].set(rec);  // rec_to_orientation, pergen.cpp:365-368
+    o[1].set(rec + 3);
+    transform_orientation(rec_transform, o);
+    for (int i = 0; i < 3; i++) { rec[i] = o[0].v[i]; rec[3 + i] = o[1].v[i]; }  // orientation_to_rec
+    for (int i = 0; i < n; i++) {
+      Vec pos0, pos;
+      double* p = rec + 6 + i * 3;
+      pos0.set(p);
+      rec_transform.mult(pos0, pos);
+      for (int c = 0; c < 3; c++) p[c] = pos.v[c];
+    }
+  }
   void set_rec(double* rec, double t) {  // pergen.cpp:225-239
     Vec o[2] = {torso_pos0, euler_angles};
     turn_torso(t, o);
@@ -740,6 +763,7 @@ struct PGS {  // pergensetup, pergen.h:68-108
       int j = likpergen[i];
       for (int c = 0; c < 3; c++) rec[6 + i * 3 + c] = limb_poss[j].v[c];
     }
+    if (rec_transform_flag) transform_rec(rec);
   }
 };
 
@@ -790,6 +814,11 @@ void setup_pergen(hso_model* m, PGS& pgs, const hso_gait* g) {
   pgs.set_TLh(g->period, g->step_length, g->step_height);
   pgs.pergen.curvature = g->curvature;  // set_curvature
   pgs.pergen.compute_max_radius();
+  // the gait's record transform (set_rec_transform / set_rec_rotation, pergen.cpp:309-320; a sweep
+  // copies it from the swept setup, copy_rec_transform, pergen.cpp:338-342, 446)
+  if (g->rec_transform_flag)
+    pgs.set_rec_transform(Vec(g->rec_transl[0], g->rec_transl[1], g->rec_transl[2]),
+                          Vec(g->rec_eas[0], g->rec_eas[1], g->rec_eas[2]));
 }
 
 // ---------------------------------------------------------------------------

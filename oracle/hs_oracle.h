@@ -32,7 +32,8 @@ typedef struct {
   double curvature;
   double foot_shift;       /* value of lateral/radial foot shift */
   int32_t foot_shift_type; /* -1 none, 0 lateral, 1 radial (pergen.h:143) */
-  int32_t reserved;
+  int32_t rec_transform_flag; /* pergensetup::rec_transform_flag (pergen.h:76) */
+  double rec_transl[3], rec_eas[3]; /* set_rec_transform (pergen.cpp:316-320) */
 } hso_gait;
 
 /* null-space basis modes */

@@ -43,7 +43,9 @@ class Gait(ctypes.Structure):
         ("curvature", ctypes.c_double),
         ("foot_shift", ctypes.c_double),
         ("foot_shift_type", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("rec_transform_flag", ctypes.c_int32),
+        ("rec_transl", ctypes.c_double * 3),
+        ("rec_eas", ctypes.c_double * 3),
     ]
 
 
@@ -59,6 +61,7 @@ class GaitParams:
     curvature: float = 0.0
     foot_shift_type: int = -1
     foot_shift: float = 0.0
+    rec_transform: tuple | None = None  # (rec_transl, rec_eas): pergensetup::set_rec_transform
 
     def to_c(self) -> Gait:
         g = Gait()
@@ -72,6 +75,11 @@ class GaitParams:
         g.curvature = self.curvature
         g.foot_shift = self.foot_shift
         g.foot_shift_type = self.foot_shift_type
+        if self.rec_transform is not None:
+            g.rec_transform_flag = 1
+            for i in range(3):
+                g.rec_transl[i] = self.rec_transform[0][i]
+                g.rec_eas[i] = self.rec_transform[1][i]
         return g
 
 

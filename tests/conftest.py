@@ -48,7 +48,7 @@ def to_oracle_gait(O, p):
     return O.GaitParams(torso_pos=tuple(p.torso_pos), torso_angles=tuple(p.torso_angles),
                         step_duration=p.step_duration, period=p.period, step_length=p.step_length,
                         step_height=p.step_height, curvature=p.curvature, foot_shift_type=p.foot_shift[0],
-                        foot_shift=p.foot_shift[1])
+                        foot_shift=p.foot_shift[1], rec_transform=p.rec_transform)
 
 
 def record_to_oracle_gait(O, r):
@@ -58,4 +58,6 @@ def record_to_oracle_gait(O, r):
                         step_duration=float(r["step_duration"]), period=float(r["period"]),
                         step_length=float(r["step_length"]), step_height=float(r["step_height"]),
                         curvature=float(r["curvature"]), foot_shift_type=int(r["foot_shift_type"]),
-                        foot_shift=float(r["foot_shift"]))
+                        foot_shift=float(r["foot_shift"]),
+                        rec_transform=((tuple(float(v) for v in r["rec_transl"]), tuple(float(v) for v in r["rec_eas"]))
+                                       if int(r["rec_transform_flag"]) else None))

@@ -42,7 +42,7 @@ def main():
                          foot_shift=float(rec["foot_shift"]))
         r = O.rollout(m, g, N_T, basis=O.BASIS_ORTHO)
         taus.append(r["tau"]); cfs.append(r["cf"]); cots.append(r["cot"]); works.append(r["work"])
-    np.savez_compressed(os.path.join(HERE, "synth_hexapod16.npz"), params=arr.view(np.uint8).reshape(16, 128),
+    np.savez_compressed(os.path.join(HERE, "synth_hexapod16.npz"), params=arr.view(np.uint8).reshape(16, -1),
                         tau=np.array(taus), cf=np.array(cfs), cot=np.array(cots), work=np.array(works), n_t=N_T)
     print("golden written:", sorted(os.listdir(HERE)))
 

@@ -161,7 +161,7 @@ def test_run_argument_validation(product):
 def test_gait_record_layout(product):
     from hslabs_amd import GAIT_DTYPE, PgsConfigParams
 
-    assert GAIT_DTYPE.itemsize == 128 == ctypes.sizeof(product.capi.GaitParamsC)
+    assert GAIT_DTYPE.itemsize == 192 == ctypes.sizeof(product.capi.GaitParamsC)
     p = PgsConfigParams(torso_pos=(1, 2, 3), torso_angles=(4, 5, 6), step_duration=0.5, period=7, step_length=8,
                         step_height=9, curvature=10, foot_shift=(1, 11))
     rec = p.to_record()
@@ -170,6 +170,13 @@ def test_gait_record_layout(product):
     assert (c.step_duration, c.period, c.step_length, c.step_height, c.curvature, c.foot_shift,
             c.foot_shift_type) == (0.5, 7, 8, 9, 10, 11, 1)
     assert PgsConfigParams.from_record(rec) == p
+    assert c.rec_transform_flag == 0
+    p.set_rec_rotation((0, 0, -1.571))  # main.cpp:38
+    p.set_rec_transform((0.5, -0.25, 0.0), (0.1, 0.2, 0.3))
+    c = product.capi.GaitParamsC.from_buffer_copy(p.to_record().tobytes())
+    assert c.rec_transform_flag == 1 and list(c.rec_transl) == [0.5, -0.25, 0.0]
+    assert list(c.rec_eas) == [0.1, 0.2, 0.3]
+    assert PgsConfigParams.from_record(p.to_record()) == p
 
 
 def test_sweep_values_follow_pgssweeper(product):

@@ -71,11 +71,19 @@ def test_select_best_over_a_one_rank_comm(gpu, hexapod):
     sb = gpu.ShardedBatch(hexapod, params, horizon=20, n_t=20)
     sb.run(k0=0)
     comm = gpu.Comm(1, 0, gpu.Comm.unique_id())
-    assert sb.select_best(comm) == sb.select_best()
+    local = sb.select_best()
+    assert sb.select_best(comm) == local
+    assert sb.select_best() == local  # the reduce ran in the comm's own buffer, not the batch's key
     key = torch.tensor([0x0123456789ABCDEF], dtype=torch.int64, device="cuda")
     comm.reduce_best(key)
     torch.cuda.synchronize()
     assert int(key.item()) == 0x0123456789ABCDEF
+    # a rank whose batch has not run still completes the collective (contributing the largest key)
+    # and then returns the error
+    fresh = gpu.ShardedBatch(hexapod, params, horizon=20, n_t=20)
+    with pytest.raises(gpu.capi.HSError):
+        fresh.select_best(comm)
+    assert sb.select_best(comm) == local  # the communicator is still usable
     comm.free()
 
 
@@ -97,6 +105,31 @@ def test_batch_run_into_device_buffers(gpu, hexapod):
     for k, v in dev.items():
         got = v.cpu().numpy()
         assert np.array_equal(got.view(np.uint32) if k == "flags" else got, host[k]), k
+
+
+def test_batch_run_device_rejects_bad_tensors(gpu, hexapod):
+    """run_device checks every caller tensor before the native copy (which trusts the batch's sizes):
+    wrong dtype, too small, non-contiguous, on the host or an unknown key all raise, and nothing
+    is written."""
+    import torch
+
+    from hslabs_amd import synth
+
+    sb = gpu.ShardedBatch(hexapod, synth.gen_params(16, "hexapod"), horizon=20, n_t=20)
+    good = torch.zeros((16, 20, 18), dtype=torch.float64, device="cuda")
+    bad = {"dtype": {"tau": good.float()},
+           "shape": {"tau": good[:8]},
+           "contiguous": {"tau": torch.zeros((16, 18, 20), dtype=torch.float64, device="cuda").transpose(1, 2)},
+           "host": {"tau": good.cpu()},
+           "key": {"torques": good},
+           "flags dtype": {"flags": torch.zeros((16, 20), dtype=torch.float64, device="cuda")}}
+    for what, out in bad.items():
+        with pytest.raises(ValueError):
+            sb.run_device(out, k0=0)
+    assert not good.any().item(), "nothing may be written before the checks pass"
+    sb.run_device({"tau": good}, k0=0)
+    torch.cuda.synchronize()
+    assert good.abs().sum().item() > 0
 
 
 def test_batch_steps_and_fp32(gpu, hexapod):

@@ -91,6 +91,56 @@ def test_configs1_full_size_matches_oracle_tree(gpu, hmodels, oracle_mod, omodel
     np.testing.assert_allclose(g["work_cot"][:, 0], r["work"], rtol=1e-9, atol=1e-12)
 
 
+def test_configs3_last_rank_shard_matches_oracle(gpu, hmodels, oracle_mod, omodels):
+    """BASELINE configs[3]'s per-rank workload at full size, through the bench's exact path: the LAST
+    of 8 ranks' shard of the 262,144 rollouts (32,768 hexapod rollouts, global ids 229,376 ..
+    262,143, rollout_id_base 229,376), K = 20 fused control steps with the best key (the launcher
+    bench.py builds per rank: hs_run_calls, ~16k wavefronts per step, the fixup + reduce launch).
+    Every step against the oracle's tree mode (ftsolver.cpp:78-102); the accumulated work bitwise
+    equal to the per-step launches' (hs_run_steps, accumulate); the device best key equal to the
+    host encoding of the accumulated selection COTs with the global ids (hdist.best_key, the minimum
+    a caller of player.cpp:311-321 would take). The N > 1 RCCL reduce itself needs 8 GPUs: the
+    launcher's sharding and reduce are covered by tests/test_bench_launcher.py."""
+    import torch
+
+    from hslabs_amd import dist as hdist
+    from hslabs_amd import synth
+
+    world, total, K = 8, 262144, 20
+    id0, B = hdist.shard(total, world, world - 1)
+    assert (id0, B) == (229376, 32768)
+    model = hmodels["hexapod"]
+    params = synth.gen_params(B, "hexapod", id0=id0)
+    b = gpu.DeviceBatch(model, params, n_t=20, k0=0, horizon=K, outputs=("tau", "cf", "flags", "work_cot"),
+                        rollout_id_base=id0)
+    b.key_steps = K  # bench.py launcher_k
+    b.work_cot.zero_()
+    b.reset_best()
+    launch = b.calls_launcher(K, call_horizon=1, best=True, accumulate=True)
+    launch()
+    torch.cuda.synchronize()
+    g = {k: npy(getattr(b, k)) for k in ("tau", "cf", "flags", "work_cot")}
+    gaits = [record_to_oracle_gait(oracle_mod, r) for r in params]
+    r = oracle_mod.batch(omodels["hexapod"], gaits, 20, 0, K, basis=oracle_mod.BASIS_TREE, n_threads=threads())
+    check_tau(g["tau"], r["tau"], "configs[3] last rank vs tree")
+    check_cf(g["cf"], r["cf"], "configs[3] last rank vs tree")
+    assert np.array_equal(g["flags"].astype(np.uint32) & ~GEN, r["flags"])
+    np.testing.assert_allclose(g["work_cot"][:, 0], r["work"], rtol=1e-9, atol=1e-12)
+    # the per-step launches accumulate the same work in the same order
+    seq = gpu.DeviceBatch(model, params, n_t=20, k0=0, horizon=1, outputs=("work_cot",), rollout_id_base=id0)
+    seq.work_cot.zero_()
+    seq.run_steps(K, best=False, accumulate=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(npy(seq.work_cot), g["work_cot"])
+    # the shard's best key: the global id of the minimum selection COT
+    sel = hdist.select_cot(b.work_cot[:, 0], torch.from_numpy(np.ascontiguousarray(params["step_length"])).cuda(),
+                           model.total_mass, 20, K)
+    host_key = int(hdist.best_key(sel, id0).item()) ^ hdist._FLIP
+    assert int(b.best_key.item()) == host_key
+    cot, rid = hdist.decode(torch.tensor([host_key ^ hdist._FLIP]))
+    assert id0 <= rid < id0 + B and np.isfinite(cot)
+
+
 def test_configs1_sample_matches_oracle_ortho(gpu, hmodels, oracle_mod, omodels):
     """256 rollouts of the same batch against the reference-faithful orthonormal null basis (the
     Q of a QR of B^T that SparseQR spans, ftsolver.cpp:185-202): basis invariance on the GPU."""

@@ -1,0 +1,119 @@
+"""GPU parity of pergensetup's record transform (pergen.cpp:238, 309-342):
+set_rec's last step, transform_rec, applied on the device by gait_record (hs_pergen_rec and every
+rollout kernel), against the oracle's restatement (oracle/hs_oracle.cpp PGS::transform_rec, pinned
+by tests/test_oracle.py::test_rec_transform_*). The first case is the reference's own call,
+main.cpp:38: set_rec_rotation((0, 0, -1.571)) on pgs id 8.
+
+Tolerances as tests/test_gpu_parity.py: records 1e-12; per-joint torques < 1e-6 N*m on every step
+(north_star) and < 1e-9 * max(1, |tau|); contact forces < 1e-8 * max(1, |f|); flags identical."""
+import os
+from dataclasses import replace
+
+import numpy as np
+import pytest
+
+from conftest import MODELS, PGS_CONFIG, record_to_oracle_gait, to_oracle_gait
+from test_gpu_parity import GEN, check_cf, check_tau, fused_cycle, threads
+
+pytestmark = pytest.mark.gpu
+
+MAIN_CPP_38 = (0.0, 0.0, -1.571)
+
+
+@pytest.fixture(scope="module")
+def gpu(product):
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return product
+
+
+@pytest.fixture(scope="module")
+def hmodels(gpu):
+    return {n: gpu.KinematicModel(os.path.join(MODELS, f"{n}.xml")) for n in ("hexapod", "spider", "myant")}
+
+
+def transformed(params, rng, frac=0.5, tilt=0.05):
+    """a copy of the GAIT_DTYPE batch with a random record transform on about `frac` of its rollouts
+    (yaw anywhere, roll / pitch within +-tilt, translation within +-1 horizontally and +-0.02 up)"""
+    out = params.copy()
+    on = rng.random(len(out)) < frac
+    n = int(on.sum())
+    out["rec_transform_flag"][on] = 1
+    out["rec_transl"][on] = np.stack([rng.uniform(-1, 1, n), rng.uniform(-1, 1, n), rng.uniform(-0.02, 0.02, n)], 1)
+    out["rec_eas"][on] = np.stack([rng.uniform(-tilt, tilt, n), rng.uniform(-tilt, tilt, n),
+                                   rng.uniform(-np.pi, np.pi, n)], 1)
+    return out, on
+
+
+def test_pergen_rec_main_cpp_rotation(gpu, hmodels, omodels, oracle_mod):
+    O = oracle_mod
+    p = gpu.read_pgs_config(PGS_CONFIG, 8)
+    p.set_rec_rotation(MAIN_CPP_38)
+    times = np.linspace(0, 2 * p.period, 17)
+    rec = hmodels["hexapod"].pergen_rec([p], times)[0]
+    g = to_oracle_gait(O, p)
+    assert g.rec_transform is not None
+    plain = hmodels["hexapod"].pergen_rec([replace(p, rec_transform=None)], times)[0]
+    for k, t in enumerate(times):
+        ref = O.pergen_rec(omodels["hexapod"], g, t)
+        assert np.abs(rec[k] - ref).max() < 1e-12, t
+    assert np.abs(rec - plain).max() > 0.1  # the transform did move the records
+
+
+@pytest.mark.parametrize("name,curved", [("hexapod", False), ("hexapod", True), ("spider", True), ("myant", False)])
+def test_pergen_rec_random_transforms(gpu, hmodels, omodels, oracle_mod, name, curved):
+    from hslabs_amd import synth
+
+    O = oracle_mod
+    rng = np.random.default_rng(31)
+    params, _ = transformed(synth.gen_params(64, name, id0=500, curved=curved), rng, frac=0.7, tilt=0.5)
+    times = rng.uniform(0, 6, 5)
+    rec = hmodels[name].pergen_rec(params, times)
+    for b in range(64):
+        g = record_to_oracle_gait(O, params[b])
+        for k, t in enumerate(times):
+            assert np.abs(rec[b, k] - O.pergen_rec(omodels[name], g, t)).max() < 1e-12, (b, t)
+
+
+def test_rollout_main_cpp_rotation(gpu, hmodels, omodels, oracle_mod):
+    """pgs 8 with main.cpp:38's rotation through the full cycle (hs_run_host, launch per step) and the
+    fused path, against the oracle's orthonormal-basis and tree modes."""
+    O = oracle_mod
+    p = gpu.read_pgs_config(PGS_CONFIG, 8)
+    p.set_rec_rotation(MAIN_CPP_38)
+    res = gpu.run_host(hmodels["hexapod"], [p], n_t=20, k0=0, horizon=20)
+    for basis in (O.BASIS_ORTHO, O.BASIS_TREE):
+        r = O.rollout(omodels["hexapod"], to_oracle_gait(O, p), 20, basis=basis)
+        check_tau(res["tau"][0], r["tau"], "pgs 8 rotated")
+        check_cf(res["cf"][0], r["cf"], "pgs 8 rotated")
+        assert np.array_equal(res["flags"][0] & ~GEN, r["flags"])
+        assert float(res["work_cot"][0, 1]) == pytest.approx(r["cot"], rel=1e-9)
+    from hslabs_amd.api import params_array
+
+    g = fused_cycle(gpu, hmodels["hexapod"], params_array([p]))
+    assert np.array_equal(g["tau"][0], res["tau"][0]) and np.array_equal(g["cf"][0], res["cf"][0])
+
+
+@pytest.mark.parametrize("name,curved", [("hexapod", False), ("hexapod", True), ("spider", True), ("myant", False)])
+def test_rollout_random_transforms(gpu, hmodels, omodels, oracle_mod, name, curved):
+    """Synthetic batches, half of the rollouts transformed (so wavefronts mix transformed and plain
+    gaits and straight wavefronts lose the straight-only kinematics), the bench's fused path, every
+    step against the oracle's tree mode; the untransformed rollouts equal a run without any (to
+    1e-12: the same operations, in the kinematics variant with the turning code).""" 
+    from hslabs_amd import synth
+
+    O = oracle_mod
+    rng = np.random.default_rng(7 + curved)
+    base = synth.gen_params(256, name, id0=900, curved=curved)
+    params, on = transformed(base, rng)
+    g = fused_cycle(gpu, hmodels[name], params)
+    gaits = [record_to_oracle_gait(O, r) for r in params]
+    r = O.batch(omodels[name], gaits, 20, 0, 20, basis=O.BASIS_TREE, n_threads=threads())
+    check_tau(g["tau"], r["tau"], f"{name} transformed")
+    check_cf(g["cf"], r["cf"], f"{name} transformed")
+    assert np.array_equal(g["flags"].astype(np.uint32) & ~GEN, r["flags"])
+    np.testing.assert_allclose(g["work_cot"][:, 0], r["work"], rtol=1e-9, atol=1e-12)
+    plain = fused_cycle(gpu, hmodels[name], base)
+    scale = np.maximum(1, np.abs(plain["tau"][~on]))
+    assert (np.abs(plain["tau"][~on] - g["tau"][~on]) / scale).max() < 1e-12

@@ -389,3 +389,76 @@ def test_oracle_per_configuration_kinematics(oracle_mod, omodels):
             # the configuration is a fixed point: IK of the FK'd feet returns it
             q2, ok2, _ = O.set_jvalues_with_lik(m, rec, ignore_reach=True, config=q)
             assert ok2 and np.array_equal(q, q2)
+
+
+# --- pergensetup::transform_rec (pergen.cpp:238, 309-342): the record transform ------------------
+def _euler_R(a):
+    """dRFromEulerAngles in the affine's layout (model.cpp:45): Rz(psi) Ry(theta) Rx(phi)"""
+    phi, th, psi = a
+    cx, sx, cy, sy, cz, sz = np.cos(phi), np.sin(phi), np.cos(th), np.sin(th), np.cos(psi), np.sin(psi)
+    Rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    Rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    return Rz @ Ry @ Rx
+
+
+def _angles_from(R):
+    """euler_angles_from_affine (visualization.cpp:81-101)"""
+    th = -np.arcsin(R[2, 0])
+    c = np.cos(th)
+    return np.array([np.arctan2(R[2, 1] / c, R[2, 2] / c), th, np.arctan2(R[1, 0] / c, R[0, 0] / c)])
+
+
+def test_rec_transform_matches_rigid_motion(oracle_mod, omodels):
+    """Records of a gait with a record transform (translation t, Euler angles e) equal the
+    untransformed records moved rigidly: torso frame R(e) R0 with position R(e) p0 + t, every foot
+    target R(e) f + t (an independent numpy formulation); the identity transform changes nothing."""
+    from dataclasses import replace
+
+    O = oracle_mod
+    rng = np.random.default_rng(11)
+    for sid in (8, 10, 24, 0):
+        g = pgs(O, sid)
+        m = model_for(O, omodels, g)
+        n = m.n_limbs
+        ident = replace(g, rec_transform=((0.0, 0.0, 0.0), (0.0, 0.0, 0.0)))
+        for t in (0.0, 0.9, 2.7):
+            assert np.abs(O.pergen_rec(m, ident, t) - O.pergen_rec(m, g, t)).max() < 1e-15
+        for trial in range(6):
+            tr = rng.uniform(-1, 1, 3) if trial else np.zeros(3)
+            ea = np.array([0, 0, -1.571]) if trial == 0 else rng.uniform([-0.5, -0.5, -np.pi], [0.5, 0.5, np.pi])
+            gx = replace(g, rec_transform=(tuple(tr), tuple(ea)))
+            R = _euler_R(ea)
+            for t in (0.0, 1.3, 4.1):
+                r0 = O.pergen_rec(m, g, t)
+                r1 = O.pergen_rec(m, gx, t)
+                R1 = R @ _euler_R(r0[3:6])
+                assert np.abs(r1[0:3] - (R @ r0[0:3] + tr)).max() < 1e-12
+                assert np.abs(_euler_R(r1[3:6]) - R1).max() < 1e-12
+                assert np.abs(r1[3:6] - _angles_from(R1)).max() < 1e-12
+                feet0 = r0[6:].reshape(n, 3)
+                assert np.abs(r1[6:].reshape(n, 3) - (feet0 @ R.T + tr)).max() < 1e-12
+
+
+@pytest.mark.parametrize("sid", [8, 20, 23, 0])
+def test_rec_transform_translation_keeps_the_dynamics(oracle_mod, omodels, sid):
+    """A horizontal translation of the records is a symmetry of the path (gravity along z, the ground
+    plane z = 0, contacts by foot height, every force/torque row built from position differences):
+    joint values, motor torques, contact forces, work and COT equal the untransformed gait's. (A yaw
+    is not one: the angular velocity is the rate of the skew part of R, dynrec.cpp:142-145, 179,
+    which does not rotate with the frame.)"""
+    from dataclasses import replace
+
+    O = oracle_mod
+    g = pgs(O, sid)
+    m = model_for(O, omodels, g)
+    base = O.rollout(m, g, 20, basis=O.BASIS_TREE)
+    for tr in ((0.7, -0.4, 0.0), (-3.0, 5.0, 0.0)):
+        r = O.rollout(m, replace(g, rec_transform=(tr, (0.0, 0.0, 0.0))), 20, basis=O.BASIS_TREE)
+        scale = max(1.0, np.abs(base["tau"]).max())
+        assert np.abs(r["tau"] - base["tau"]).max() < 1e-9 * scale
+        assert np.array_equal(r["flags"], base["flags"])
+        assert r["cot"] == pytest.approx(base["cot"], rel=1e-9)
+        assert np.abs(r["cf"] - base["cf"]).max() < 1e-8 * max(1.0, np.abs(base["cf"]).max())
+        assert np.abs(r["q"][:, :2] - base["q"][:, :2] - np.array(tr[:2])).max() < 1e-12
+        assert np.abs(r["q"][:, 2:] - base["q"][:, 2:]).max() < 1e-12
