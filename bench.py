@@ -79,6 +79,10 @@ def parse(argv=None):
                          "(hs_run_steps, the online loop)")
     ap.add_argument("--sim", action="store_true",
                     help="closed-loop simulation (PD control + ODE QuickStep, 20 SOR iterations) steps/s")
+    ap.add_argument("--forces", action="store_true",
+                    help="solve_forces (contact forces given motor torques, ftsolver.cpp:331-378) steps/s: "
+                         "the K steps' torques from an untimed control-loop run, then K fused steps "
+                         "(hs_run_forces_calls)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=None, help="default: the host cores this process may use")
     ap.add_argument("--no-cpu", action="store_true")
@@ -320,6 +324,107 @@ def main_sim(args, torch, dist, world, rank, dev):
         dist.destroy_process_group()
 
 
+FORCES_METRIC = "solve_forces steps/sec: contact forces given motor torques (ftsolver.cpp:331-378)"
+
+
+def forces_cpu_baseline(name, params, tau, n_t, seconds):
+    """Oracle solve_forces (dense least squares of the reference's B with torque rows, Householder
+    QR; oracle/hs_oracle.cpp) on a bounded sample of the same batch and torques, one thread."""
+    from oracle import oracle as O
+
+    om = O.Model(os.path.join(ROOT, "models", f"{name}.xml"))
+    gaits = _oracle_gaits(O, params)
+    done, t0, b = 0, time.perf_counter(), 0
+    while True:
+        O.forces(om, gaits[b % len(gaits)], tau[b % len(gaits)], n_t=n_t)
+        done += tau.shape[1]
+        b += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(done / el, 1), "unit": "steps/s", "cores": 1, "kind": "port",
+            "sample": f"{done} solve_forces steps ({name}, {b} rollouts of the batch x {tau.shape[1]} steps, the "
+                      f"batch's own torques) in {el:.1f}s: oracle dense least squares (Householder QR of the "
+                      f"reference's B with the torque rows), g++ -O2, one thread"}
+
+
+def main_forces(args, torch, dist, world, rank, dev):
+    """solve_forces on the control loop's workload: B rollouts, K steps of the
+    motor torques the control loop computed for them (untimed), then the K steps of
+    forcetorquesolver::solve_forces fused (hs_run_forces_calls) in the timed region."""
+    import hslabs_amd as H
+    from hslabs_amd import capi, synth
+
+    lay = job_layout(args, world, rank)
+    B, K, n_t = lay["B"], args.steps, args.n_t
+    model = H.KinematicModel(os.path.join(ROOT, "models", f"{args.model}.xml"))
+    params = synth.gen_params(B, args.model, id0=lay["id0"], curved=args.curved)
+    rows = max(args.steps, args.warmup)
+    ctl = H.DeviceBatch(model, params, n_t=n_t, k0=0, horizon=rows, outputs=("tau", "cf"), device=dev,
+                        rollout_id_base=lay["id0"])
+    ctl.run_calls(rows, call_horizon=1)  # the torques (and, for the check, the contact forces)
+    stream = torch.cuda.current_stream(dev)
+    fb = H.DeviceBatch(model, params, n_t=n_t, k0=0, horizon=K, outputs=("cf", "flags"), device=dev,
+                       rollout_id_base=lay["id0"])
+    job = fb.forces_launcher(ctl.tau[:, :K], K, stream=stream)
+    warm_job = None
+    if args.warmup:
+        wb = H.DeviceBatch(model, params, n_t=n_t, k0=0, horizon=args.warmup, outputs=("cf",), device=dev)
+        warm_job = wb.forces_launcher(ctl.tau[:, :args.warmup], args.warmup, stream=stream)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if warm_job:
+        warm_job()
+    done_ev = torch.cuda.Event()
+    done_ev.record(stream)
+    while not done_ev.query():
+        pass
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    job()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / K
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+    # untimed check (playerexperim.cpp:95-121): the forces that realise the computed torques are the
+    # computed contact forces
+    cf, ref = fb.cf[:, :K].double(), ctl.cf[:, :K].double()
+    err = float(((cf - ref).abs().amax(dim=2) / ref.abs().amax(dim=2).clamp(min=1)).max().item())
+    general = int(((fb.flags[:, :K] & capi.HS_FLAG_GENERAL) != 0).sum().item())
+    if rank == 0:
+        nmj, nf = model.nmj, model.nfeet
+        step_bytes = 8 * (nmj + 3 * nf) + PARAM_BYTES  # torques in, forces of all feet out, the gait record
+        alg_bytes = B * step_bytes
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        out = {
+            "metric": FORCES_METRIC, "value": round(lay["total"] * K / elapsed, 1), "unit": "steps/s",
+            "n_gpus": world, "steps": K, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / K, 4),
+            "higher_is_better": True, "scaling": lay["scaling"], "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (splitmix64 gait parameters around pgs id 8; the torques the control loop computed)",
+            "config": {"workload": f"{args.model}.xml B={B}/GPU, {K} fused solve_forces steps (hs_run_forces_calls), "
+                                   f"n_t={n_t} fp64 (SURVEY.md 8f row 1)", "rollouts_per_gpu": B,
+                       "parallelism": f"rollout-sharded x{world}, no collective"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "hs_rollout_kernel<NM, true, 0>",
+                         "kernel_ms": round(kern_ms, 5), "alg_bytes_per_launch": alg_bytes,
+                         "alg_bytes_per_step": step_bytes},
+            "check": {"max_rel_cf_vs_control_loop": err, "general_steps": general},
+        }
+        out["cpu_baseline"] = None if (args.no_cpu or world > 1) else forces_cpu_baseline(
+            args.model, params[:64], ctl.tau[:64, :K].cpu().numpy(), n_t, min(args.cpu_seconds, 5.0))
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 # ---------------------------------------------------------------------------------------------
 # measurement files committed under profiles/ (never read from /root/reference)
 # ---------------------------------------------------------------------------------------------
@@ -425,6 +530,8 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     if args.sim:
         return main_sim(args, torch, dist, world, rank, dev)
+    if args.forces:
+        return main_forces(args, torch, dist, world, rank, dev)
 
     import hslabs_amd as H
     from hslabs_amd import capi, synth

@@ -462,6 +462,26 @@ class DeviceBatch:
                    "hs_run_forces_calls")
         self._tau_in = t
 
+    def forces_launcher(self, tau_in, n_calls: int, call_horizon: int = 1, stream=None):
+        """run_forces_calls(...) with its arguments resolved once: a no-argument callable that only
+        enqueues the fused launches (bench.py --forces' timed loop)."""
+        S = n_calls * call_horizon
+        assert self.H == S, "the batch's horizon must equal n_calls * call_horizon (one row per step)"
+        t = tau_in.to(dtype=self.dtype, device=self.device).contiguous()
+        assert t.shape == (self.B, S, self.model.nmj)
+        a = self._args(stream, False, False)
+        a.tau = a.x = a.work_cot = None
+        a.horizon = call_horizon
+        L = capi.load()
+        ref, h, ptr = ctypes.byref(a), self.model.handle, t.data_ptr()
+
+        def launch():
+            rc = L.hs_run_forces_calls(h, ref, n_calls, ptr)
+            if rc != capi.HS_OK:
+                capi.check(rc, "hs_run_forces_calls")
+        launch.args, launch.tau_in = a, t  # keep the struct and the torques alive with the callable
+        return launch
+
     def run_steps(self, n_calls: int, stream=None, best: bool = False, accumulate: bool = True,
                   events=None) -> None:
         """n_calls launches marching k0 through the cycle (hs_run_steps); the launch loop is

@@ -1555,6 +1555,122 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, AugL&
   return true;
 }
 
+// value of v on lane src of this half-wave (src the same on every lane: a loop constant): one
+// readlane per 32-bit word and half
+__device__ inline real half_bcast(real v, int src) {
+  const bool up = threadIdx.x >= HALF;
+#if HS_REAL_IS_FLOAT
+  const int w0 = __builtin_amdgcn_readlane(__float_as_int(v), src);
+  const int w1 = __builtin_amdgcn_readlane(__float_as_int(v), src + HALF);
+  return __int_as_float(up ? w1 : w0);
+#else
+  const long long u = __double_as_longlong(v);
+  const int lo = (int)u, hi = (int)(u >> 32);
+  const int l0 = __builtin_amdgcn_readlane(lo, src), h0 = __builtin_amdgcn_readlane(hi, src);
+  const int l1 = __builtin_amdgcn_readlane(lo, src + HALF), h1 = __builtin_amdgcn_readlane(hi, src + HALF);
+  const unsigned long long w = ((unsigned long long)(unsigned)(up ? h1 : h0) << 32) | (unsigned)(up ? l1 : l0);
+  return __longlong_as_double((long long)w);
+#endif
+}
+
+#ifndef HS_SCHUR_LANES
+#define HS_SCHUR_LANES 1
+#endif
+// The 6x6 Schur system S lam = a - h (ldl_n<6> + ldl_solve_n<6>, the oracle's fast mode) with the
+// factorization spread over lanes 0..5 of the half-wave: lane i holds row i of the packed sums and
+// applies pivot j's operations to it right-looking (L_ij = a_ij / d_j, then a_ic -= L_ij (L_cj d_j)
+// for j < c <= i: ldl_n's subtractions per entry, in the same pivot order, with the same products);
+// the pivots and the column just scaled come from their lanes by readlane, the reciprocal of each
+// pivot is formed on every lane. Every lane then gathers the factor and runs ldl_solve_n on it (the
+// forward / backward substitutions are one dependent chain either way). Returns the guard's verdict,
+// the same on every lane of the half; lane 0 stores lam.
+__device__ inline int schur_ldl6(FastL& fl, const real* a, int lane) {
+  const int i = lane < 6 ? lane : 5;  // lanes past row 5 repeat row 5 (their values are not read)
+  real row[6], mx = 0;
+#pragma unroll
+  for (int c = 0; c < 6; c++) {
+    row[c] = (c <= i) ? fl.sc.Ssum[sch_lower(i, c)] : real(0);
+    mx = fmax(mx, fl.sc.Ssum[sch_lower(c, c)]);
+  }
+  int ok = 1;
+  real rl[6];
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    const real dj = half_bcast(row[j], j);  // d_j: lane j's diagonal after pivots 0 .. j-1
+    if (!(dj > kFastPivotGuard * mx)) ok = 0;
+    const real r = real(1) / dj;
+    rl[j] = r;
+    if (i > j) row[j] = row[j] * r;
+#pragma unroll
+    for (int c = j + 1; c < 6; c++) {
+      const real v = half_bcast(row[j], c) * dj;  // L_cj d_j (ldl_n's v for row c)
+      if (c <= i) row[c] -= row[j] * v;
+    }
+  }
+  real Sm[36], lam[6];
+#pragma unroll
+  for (int c = 0; c < 6; c++) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) Sm[6 * c + k] = (k <= c) ? half_bcast(row[k], c) : real(0);  // upper: unread
+    lam[c] = a[c] - fl.sc.Ssum[SCH_H + c];
+  }
+#ifndef HS_EXP_NO_SCHUR
+  ldl_solve_n<6>(Sm, rl, lam);
+#endif
+  if (lane == 0) {
+    if (ok)
+      for (int r = 0; r < 6; r++) fl.sc.lam[r] = lam[r];
+    fl.ok[0] = ok;
+  }
+  return ok;
+}
+
+#ifndef HS_FORCES_REGS
+#define HS_FORCES_REGS 1
+#endif
+// chol_packed's factorization with the matrix in registers (solve_forces): lane i of the half-wave
+// holds row i of the packed lower triangle, pivot j comes from lane j and column j from the lanes
+// below it by readlane (half_bcast), so every entry takes the same operations in the same order
+// (right-looking: L_ij = K_ij / L_jj, then K_ic -= L_ij L_cj for j < c <= i) and L is bitwise
+// chol_packed's -- without its LDS round trips and wavefront syncs per pivot. rl[j] = 1 / L_jj (the
+// same on every lane); L is written back to K. False when a pivot falls to guard * max diagonal (the
+// failing half keeps going and its values are discarded by the caller).
+template <int NMAX>
+__device__ inline bool chol_regs(real* K, int k, real guard, real* rl, int lane) {
+  const int i = lane < k ? lane : k - 1;  // lanes past the last row repeat it (their values are not stored)
+  real row[NMAX], mx = 0;
+#pragma unroll
+  for (int c = 0; c < NMAX; c++) {
+    row[c] = (c <= i) ? K[pk(i, c)] : real(0);
+    if (c < k) mx = fmax(mx, K[pk(c, c)]);
+  }
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < NMAX; j++) {
+    if (j < k) {
+      const real d = half_bcast(row[j], j);
+      if (!(d > guard * mx)) ok = false;
+      const real l = sqrt(d), r = real(1) / l;
+      rl[j] = r;
+      if (i == j) row[j] = l;
+      else if (i > j) row[j] = row[j] * r;
+#pragma unroll
+      for (int c = j + 1; c < NMAX; c++) {
+        if (c < k) {
+          const real lc = half_bcast(row[j], c);
+          if (c <= i) row[c] -= row[j] * lc;
+        }
+      }
+    }
+  }
+  if (lane < k)
+#pragma unroll
+    for (int c = 0; c < NMAX; c++)
+      if (c <= i) K[pk(i, c)] = row[c];
+  wave_sync();
+  return ok;
+}
+
 // TIER2: the augmented-system solve where a D_c or the Schur complement is singular; without it
 // (HS_DEFER_AUG builds of the fused step launch) such steps decline and go to the fixup launch
 // aug_ok = false (the fixup launch's idle half, which stores nothing): decline instead of using the
@@ -1735,6 +1851,12 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       fl.sc.Ssum[lane] = s;
     }
     wave_sync();
+#if HS_SCHUR_LANES
+    // the 6x6 LDL^T right-looking over six lanes (lane i holds row i; pivots and columns broadcast by
+    // readlane), the solve on each lane with the factor gathered from them: every entry takes the
+    // operations ldl_n / ldl_solve_n apply to it, in the same order
+    ok = schur_ldl6(fl, a, lane);
+#else
     if (lane == 0) {
       real Sm[36], h[6];
 #pragma unroll
@@ -1758,6 +1880,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       }
       fl.ok[0] = ok;
     }
+#endif
     wave_sync();
     STAMP(19);
     if (!fl.ok[0]) return (TIER2 && aug_ok) ? aug_solve(fl, ag, sv, a, nc, lane) : false;
@@ -2133,10 +2256,17 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
   }
   wave_sync();
   STAMP(4);
-  chol_packed(fr.W, m, real(0), lane);  // I + G G^T: eigenvalues >= 1
+  constexpr int MM = 6 + HS_KMAX;
+  real rl[MM];  // 1 / L_ii of I + G G^T (the divisions of the substitutions, as multiplications)
+#if HS_FORCES_REGS
+  chol_regs<MM>(fr.W, m, real(0), rl, lane);  // I + G G^T: eigenvalues >= 1
+#else
+  chol_packed(fr.W, m, real(0), lane);
+#pragma unroll
+  for (int i = 0; i < MM; i++) rl[i] = (i < m) ? real(1) / fr.W[pk(i, i)] : real(0);
+#endif
   STAMP(5);
   if (lane < ld) {  // L^-1 [C | d], one column per lane, the column in registers (m <= 6 + HS_KMAX)
-    constexpr int MM = 6 + HS_KMAX;
     real col[MM];
 #pragma unroll
     for (int i = 0; i < MM; i++) col[i] = (i < m) ? fr.Ct[i * ld + lane] : real(0);
@@ -2146,7 +2276,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
         real s = col[i];
 #pragma unroll
         for (int t = 0; t < i; t++) s -= fr.W[pk(i, t)] * col[t];
-        col[i] = s / fr.W[pk(i, i)];
+        col[i] = s * rl[i];
       }
     }
 #pragma unroll
@@ -2156,6 +2286,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
   wave_sync();
   STAMP(6);
   uint32_t flags = 0;
+  real rn[HS_KMAX];  // 1 / M_ii of the normal matrix's factor
   for (int pass = 0; pass < 2; pass++) {  // normal equations; second pass regularized
     real eps = 0;
     if (pass == 1) {
@@ -2175,7 +2306,15 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     }
     wave_sync();
     STAMP(7);
-    if (chol_packed(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) break;
+#if HS_FORCES_REGS
+    if (chol_regs<HS_KMAX>(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), rn, lane)) break;
+#else
+    if (chol_packed(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) {
+#pragma unroll
+      for (int i = 0; i < HS_KMAX; i++) rn[i] = (i < nq) ? real(1) / fr.W[pk(i, i)] : real(0);
+      break;
+    }
+#endif
     flags = HS_FLAG_GENERAL;  // least squares not unique
   }
   STAMP(8);
@@ -2189,7 +2328,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
         real s = yv[i];
 #pragma unroll
         for (int k = 0; k < i; k++) s -= fr.W[pk(i, k)] * yv[k];
-        yv[i] = s / fr.W[pk(i, i)];
+        yv[i] = s * rn[i];
       }
     }
 #pragma unroll
@@ -2199,7 +2338,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
 #pragma unroll
         for (int k = i + 1; k < HS_KMAX; k++)
           if (k < nq) s -= fr.W[pk(k, i)] * yv[k];
-        yv[i] = s / fr.W[pk(i, i)];
+        yv[i] = s * rn[i];
       }
     }
 #pragma unroll

@@ -419,43 +419,180 @@ struct pgsconfigparams {
   }
 };
 
-// The gait of one rollout (pergensetup): its pgsconfigparams plus accessors.
+class pergensetup;
+
+// The periodicgenerator of a pergensetup (pergen.h:27-58), the accessors callers read through
+// pergensetup::get_pergen() (player.cpp:274 measure_cot: pgs->get_pergen()->get_step_length())
+class periodicgenerator {
+  const pgsconfigparams* pcp_;
+
+ public:
+  explicit periodicgenerator(const pgsconfigparams* pcp) : pcp_(pcp) {}
+  double get_period() const { return pcp_->TLh[0]; }
+  double get_step_length() const { return pcp_->TLh[1]; }
+  double get_step_duration() const { return pcp_->step_duration; }
+  double get_curvature() const { return pcp_->curvature; }
+  void get_TLh(double TLh[3]) const { std::copy(pcp_->TLh, pcp_->TLh + 3, TLh); }
+};
+
+// The gait of one rollout (pergensetup, pergen.h:68-108): its pgsconfigparams, the record
+// transform (pergen.h:75-76) and accessors.
 class pergensetup {
   pgsconfigparams pcp_;
   int n_;
   const kinematicmodel* model_;
+  periodicgenerator pergen_{&pcp_};
+  bool rec_transform_flag_ = false;  // pergen.cpp:207
+  double rec_transl_[3] = {0, 0, 0}, rec_eas_[3] = {0, 0, 0};
 
  public:
   pergensetup(int n_limbs, const pgsconfigparams& pcp, const kinematicmodel* model = nullptr)
       : pcp_(pcp), n_(n_limbs), model_(model) {}
-  // pergen.cpp:225-239: torso position and angles, then the feet in lik order, at time t
-  // (needs the model the gait was set up for: make_pergensu passes it)
+  pergensetup(const pergensetup& o)
+      : pcp_(o.pcp_), n_(o.n_), model_(o.model_), rec_transform_flag_(o.rec_transform_flag_) {
+    std::copy(o.rec_transl_, o.rec_transl_ + 3, rec_transl_);
+    std::copy(o.rec_eas_, o.rec_eas_ + 3, rec_eas_);
+  }
+  pergensetup& operator=(const pergensetup&) = delete;
+  // pergen.cpp:225-239: torso position and angles, then the feet in lik order, at time t, transformed
+  // by the record transform when set (needs the model the gait was set up for: make_pergensu passes it)
   void set_rec(double* rec, double t) const {
     if (!model_) throw error(HS_E_ARG, "pergensetup without a model");
-    hs_gait_params g = pcp_.to_c();
+    hs_gait_params g = to_c();
     check(hs_pergen_rec_host(model_->handle(), &g, 1, &t, 1, rec), "set_rec");
   }
   int get_limb_number() const { return n_; }
   int get_config_dim() const { return 6 + 3 * n_; }
   double get_period() const { return pcp_.TLh[0]; }
   double get_step_length() const { return pcp_.TLh[1]; }
+  const periodicgenerator* get_pergen() const { return &pergen_; }  // pergen.h:81
+  const kinematicmodel* get_model() const { return model_; }
   void get_config_params(pgsconfigparams* pcp) const { *pcp = pcp_; }
   const pgsconfigparams& params() const { return pcp_; }
   void set_TLh(double T, double L, double h) { pcp_.set_TLh(T, L, h); }
+  void set_TLh(const double TLh[3]) { pcp_.set_TLh(TLh[0], TLh[1], TLh[2]); }
+  // pergen.cpp:316-320: rec_transform = affine_from_orientation({rec_transl, rec_eas}), flag on
+  void set_rec_transform(const extvec& rec_transl, const extvec& rec_eas) {
+    rec_transl.get_components(rec_transl_);
+    rec_eas.get_components(rec_eas_);
+    rec_transform_flag_ = true;
+  }
+  // pergen.cpp:309-313: the rotation by Euler angles, the transform's translation kept
+  void set_rec_rotation(const extvec& rec_eas) {
+    extvec t(rec_transl_[0], rec_transl_[1], rec_transl_[2]);
+    set_rec_transform(t, rec_eas);
+  }
+  // pergen.cpp:338-342 (pgssweeper::next, pergen.cpp:446)
+  void copy_rec_transform(const pergensetup* pgs) {
+    rec_transform_flag_ = pgs->rec_transform_flag_;
+    std::copy(pgs->rec_transl_, pgs->rec_transl_ + 3, rec_transl_);
+    std::copy(pgs->rec_eas_, pgs->rec_eas_ + 3, rec_eas_);
+  }
+  bool get_rec_transform_flag() const { return rec_transform_flag_; }
+  // the ABI record of this gait: pgsconfigparams plus the record transform
+  hs_gait_params to_c() const {
+    hs_gait_params g = pcp_.to_c();
+    g.rec_transform_flag = rec_transform_flag_ ? 1 : 0;
+    for (int i = 0; i < 3; i++) { g.rec_transl[i] = rec_transl_[i]; g.rec_eas[i] = rec_eas_[i]; }
+    return g;
+  }
+};
+
+// pgssweeper (pergen.h:110-134; pergen.cpp:400-449): iterates over gaits made from pgs0 by
+// sweeping one parameter, each with pgs0's record transform (next, pergen.cpp:433-449)
+class pgssweeper {
+  const pergensetup* pgs0_;
+  pergensetup* pgs_ = nullptr;
+  int parami_ = -1, n_val_ = 0, vali_ = 0;
+  double val0_ = 0, delval_ = 0, val_ = 0;
+
+ public:
+  pgssweeper(const pergensetup* pgs, const kinematicmodel* /*model*/ = nullptr) : pgs0_(pgs) {}
+  ~pgssweeper() { delete pgs_; }
+  pgssweeper(const pgssweeper&) = delete;
+  pgssweeper& operator=(const pgssweeper&) = delete;
+  pergensetup* get_pgs() const { return pgs_; }
+  double get_val() const { return val_; }
+  // pergen.cpp:417-430; throws where the reference exits (unknown parameter)
+  void sweep(const std::string& param_name, double val0, double val1, int n_val) {
+    val0_ = val0;
+    n_val_ = n_val;
+    delval_ = (val1 - val0) / n_val;
+    vali_ = 0;
+    const char* names[] = {"step_duration", "period", "step_length", "step_height"};
+    parami_ = -1;
+    for (int i = 0; i < 4; i++)
+      if (param_name == names[i]) parami_ = i;
+    if (parami_ < 0) throw error(HS_E_ARG, "cannot sweep over " + param_name);
+    std::cout << "sweeping over " << param_name << ":" << std::endl;
+  }
+  // pergen.cpp:433-449
+  bool next() {
+    if (vali_ > n_val_) {
+      vali_ = 0;
+      return false;
+    }
+    val_ = val0_ + vali_ * delval_;
+    vali_++;
+    delete pgs_;
+    pgs_ = nullptr;
+    pgsconfigparams pcp;
+    pgs0_->get_config_params(&pcp);
+    if (parami_ == 0) pcp.step_duration = val_;
+    else if (parami_ > 0 && parami_ < 4) pcp.TLh[parami_ - 1] = val_;
+    pgs_ = new pergensetup(pgs0_->get_limb_number(), pcp, pgs0_->get_model());
+    pgs_->copy_rec_transform(pgs0_);
+    return true;
+  }
 };
 
 class periodic {
   const kinematicmodel* model_;
   const pergensetup* pgs_ = nullptr;
   int n_t_ = 0;
-  std::vector<double> tau_, cf_, x_, wc_;
+  mutable std::vector<double> tau_;  // computed_torques: row h = trajectory sample h + 2 (periodic.cpp:387)
+  std::vector<double> cf_, x_, wc_;
   std::vector<uint32_t> flags_;
-  std::vector<double> rec_;  // get_complete_traj records
+  std::vector<double> rec_;       // get_complete_traj records
+  std::vector<double> last_tau_;  // motor torques of the solver's last solve (get_motor_torques)
+  mutable std::vector<double> masses_;
+  mutable std::vector<int> parentis_, footis_;
   double min_cfz_ = 1e10, max_mu_ = -1e10;
 
+  hs_gait_params gait() const {
+    if (!pgs_) throw error(HS_E_ARG, "record_trajectory first");
+    return pgs_->to_c();
+  }
+  // dynrecs[i] exists with its derivatives for samples i = 2 .. n_t + 2 (traj_size = n_t + 5,
+  // periodic.cpp:79, 192-202); the reference reads out of bounds elsewhere, this throws
+  int step_of(int i) const {
+    if (!pgs_) throw error(HS_E_ARG, "record_trajectory first");
+    if (i < 2 || i > n_t_ + 2) throw error(HS_E_ARG, "trajectory sample " + std::to_string(i) + " has no dynamics record");
+    return i - 2;
+  }
+
  public:
-  explicit periodic(const kinematicmodel* model) : model_(model) {}
-  void record_trajectory(const pergensetup* pgs, int n_t) { pgs_ = pgs; n_t_ = n_t; tau_.clear(); rec_.clear(); }
+  // periodic.cpp:10-58 (set_dynparts): masses, parent ids and foot part ids in preorder
+  explicit periodic(const kinematicmodel* model) : model_(model) {
+    for (int i = 0; i < model->number_of_parts(); i++) {
+      const hs_node_info& nd = model->get_mnode(i)->info();
+      masses_.push_back(nd.mass);
+      parentis_.push_back(nd.parent);
+      if (nd.foot >= 0) footis_.push_back(i);
+    }
+  }
+  // periodic.h:43-48
+  int get_number_of_dynparts() const { return (int)masses_.size(); }
+  double* get_masses() const { return masses_.data(); }
+  int* get_parentis() const { return parentis_.data(); }
+  int* get_footis() const { return footis_.data(); }
+  void record_trajectory(const pergensetup* pgs, int n_t) {
+    pgs_ = pgs;
+    n_t_ = n_t;
+    tau_.clear();
+    rec_.clear();
+    last_tau_.clear();
+  }
   void compute_dynrecs() {}
   void compute_dynrec_ders() {}
   // ftsolver.cpp:262-273 through periodic.cpp:205-207: a setting of the model's solver, used by every
@@ -468,10 +605,9 @@ class periodic {
   double get_total_mass() const { return model_->total_mass(); }
   // periodic.cpp:377-391 (+ analyze_contforces 347-357)
   void compute_torques_over_period() {
-    if (!pgs_) throw error(HS_E_ARG, "record_trajectory first");
     const int nmj = model_->number_of_motor_joints(), nf = model_->number_of_feet();
     const int n = model_->number_of_parts(), cfg = model_->get_config_dim();
-    hs_gait_params g = pgs_->params().to_c();
+    hs_gait_params g = gait();
     tau_.assign((size_t)n_t_ * nmj, 0);
     cf_.assign((size_t)n_t_ * 3 * nf, 0);
     x_.assign((size_t)n_t_ * 6 * n, 0);
@@ -490,9 +626,11 @@ class periodic {
         double mu = std::sqrt(c[0] * c[0] + c[1] * c[1]) / c[2];
         if (mu > max_mu_) max_mu_ = mu;
       }
+    last_tau_.assign(tau_.end() - nmj, tau_.end());  // the loop's last solve: sample n_t + 1
   }
-  // computed_torques[i % n_t] holds the torques of trajectory sample i (periodic.cpp:387)
-  const double* get_computed_torques(int i) const {
+  // periodic.h:51: computed_torques[i % n_t] holds the torques of trajectory sample i
+  double* get_computed_torques(int i) const {
+    if (tau_.empty()) throw error(HS_E_ARG, "compute_torques_over_period first");
     int h = ((i - 2) % n_t_ + n_t_) % n_t_;
     return &tau_[(size_t)h * model_->number_of_motor_joints()];
   }
@@ -502,33 +640,49 @@ class periodic {
   }
   uint32_t get_flags(int i) const { return flags_[((i - 2) % n_t_ + n_t_) % n_t_]; }
   void get_contforce_stat(double* stat) const { stat[0] = min_cfz_; stat[1] = max_mu_; }
-  // periodic.cpp:368-374 (forcetorquesolver::solve_forces): forces of all feet for step i
+  // periodic.cpp:328-343: the motor torques of the force/torque solver's last solve (the last sample
+  // of compute_torques_over_period, or solve_torques_contforces' sample)
+  void get_motor_torques(double* motor_torques) const {
+    if (last_tau_.empty()) throw error(HS_E_ARG, "no force/torque solve yet");
+    std::copy(last_tau_.begin(), last_tau_.end(), motor_torques);
+  }
+  // periodic.cpp:361-366: motor torques and contact forces (3 nfeet, airborne feet 0) of sample i
+  void solve_torques_contforces(int i, double* torques, double* contforces) {
+    hs_gait_params g = gait();
+    const int k0 = step_of(i), nmj = model_->number_of_motor_joints();
+    std::vector<double> t((size_t)nmj);
+    check(hs_run_host(model_->handle(), &g, 1, n_t_, k0, 1, 1, nullptr, t.data(), contforces, nullptr, nullptr,
+                      nullptr),
+          "solve_torques_contforces");
+    std::copy(t.begin(), t.end(), torques);
+    last_tau_ = t;
+  }
+  // periodic.cpp:368-374 (forcetorquesolver::solve_forces): forces of all feet for sample i
   void solve_contforces_given_torques(int i, double* contforces, const double* torques) const {
-    if (!pgs_) throw error(HS_E_ARG, "record_trajectory first");
-    hs_gait_params g = pgs_->params().to_c();
-    int k0 = ((i - 2) % n_t_ + n_t_) % n_t_;
+    hs_gait_params g = gait();
+    const int k0 = step_of(i);
     check(hs_run_forces_host(model_->handle(), &g, 1, n_t_, k0, 1, 1, torques, contforces, nullptr),
           "solve_contforces_given_torques");
   }
   // periodic.cpp:406-426: n_t records of (q, dq, torques) = 2 config_dim + nmj
   void get_complete_traj(double** complete_traj) {
-    if (!pgs_) throw error(HS_E_ARG, "record_trajectory first");
     const int len = 2 * model_->get_config_dim() + model_->number_of_motor_joints();
-    if (rec_.empty()) {
-      hs_gait_params g = pgs_->params().to_c();
-      rec_.assign((size_t)n_t_ * len, 0);
-      check(hs_complete_traj(model_->handle(), &g, 1, n_t_, 1, rec_.data()), "get_complete_traj");
-    }
+    ensure_complete_traj();
     for (int i = 0; i < n_t_; i++) std::copy(&rec_[(size_t)i * len], &rec_[(size_t)i * len] + len, complete_traj[i]);
+  }
+  // periodic.cpp:408-417: the record of time step tsi < n_t (tsi < 2 read at tsi + n_t)
+  void get_complete_traj_rec(int tsi, double* rec) {
+    if (tsi >= n_t_) throw error(HS_E_ARG, "time step must be < n_t");  // the reference exits
+    if (tsi < 0) throw error(HS_E_ARG, "time step must be >= 0");
+    const int len = 2 * model_->get_config_dim() + model_->number_of_motor_joints();
+    ensure_complete_traj();
+    std::copy(&rec_[(size_t)tsi * len], &rec_[(size_t)tsi * len] + len, rec);
   }
   // periodic.cpp:394-404: motor angles and rates of trajectory sample tsi
   void get_motor_adas(int tsi, double* as, double* das) {
     const int cfg = model_->get_config_dim(), len = 2 * cfg + model_->number_of_motor_joints();
-    std::vector<double*> rows((size_t)n_t_);
-    std::vector<double> buf((size_t)n_t_ * len);
-    for (int i = 0; i < n_t_; i++) rows[i] = &buf[(size_t)i * len];
-    get_complete_traj(rows.data());
-    const double* r = rows[((tsi % n_t_) + n_t_) % n_t_];  // records are indexed by tsi mod n_t
+    ensure_complete_traj();
+    const double* r = &rec_[(size_t)(((tsi % n_t_) + n_t_) % n_t_) * len];  // records are indexed by tsi mod n_t
     std::copy(r + 6, r + cfg, as);
     std::copy(r + cfg + 6, r + 2 * cfg, das);
   }
@@ -536,6 +690,15 @@ class periodic {
   double work_over_period() {
     if (tau_.empty()) compute_torques_over_period();
     return wc_[0];
+  }
+
+ private:
+  void ensure_complete_traj() {
+    if (!rec_.empty()) return;
+    hs_gait_params g = gait();
+    const int len = 2 * model_->get_config_dim() + model_->number_of_motor_joints();
+    rec_.assign((size_t)n_t_ * len, 0);
+    check(hs_complete_traj(model_->handle(), &g, 1, n_t_, 1, rec_.data()), "get_complete_traj");
   }
 };
 
@@ -578,6 +741,7 @@ class modelplayer {
   uint32_t device_mask_ = 1u;  // devices a sweep is sharded over (hs_batch_create)
   hs_sim_t sim_ = nullptr;  // the ODE world of setup_per_controller (one rollout)
   double play_t_ = 0, play_dt_ = 0.01;
+  std::string traj_fname_ = "traj.txt";
   std::vector<double> last_tau_, last_q_;
 
  public:
@@ -589,7 +753,7 @@ class modelplayer {
   // world at the trajectory sample of t0, at rest; position control on (step_mode 6)
   void setup_per_controller(const pergensetup* pgs, double t0) {
     unset_per_controller();
-    hs_gait_params g = pgs->params().to_c();
+    hs_gait_params g = pgs->to_c();
     hs_sim_params sp;
     hs_sim_default_params(&sp);
     sp.dt = play_dt_;
@@ -674,7 +838,7 @@ class modelplayer {
     per.record_trajectory(pgs, n_t);
     per.compute_torques_over_period();
     double work = per.work_over_period();
-    double cot = work / (per.get_total_mass() * pgs->get_step_length());
+    double cot = work / (per.get_total_mass() * pgs->get_pergen()->get_step_length());
     if (contact_force_flag_) {
       double stat[2];
       per.get_contforce_stat(stat);
@@ -682,25 +846,27 @@ class modelplayer {
     }
     return cot;
   }
-  // player.cpp:311-321 with pgssweeper::sweep/next (pergen.cpp:417-449), one launch for all values
+  // player.cpp:311-321 with pgssweeper::sweep/next (pergen.cpp:417-449, each value with the swept
+  // gait's record transform), one launch for all values
   std::vector<std::pair<double, double>> measure_cot_sweep(const pergensetup* pgs, int n_t,
                                                            const std::string& param_name, double val0,
                                                            double val1, int n_val, bool print = true) {
-    const char* names[] = {"step_duration", "period", "step_length", "step_height"};
-    int parami = -1;
-    for (int i = 0; i < 4; i++)
-      if (param_name == names[i]) parami = i;
-    if (parami < 0) throw error(HS_E_ARG, "cannot sweep over " + param_name);
-    double delval = (val1 - val0) / n_val;
     std::vector<hs_gait_params> params;
     std::vector<double> vals;
-    for (int vali = 0; vali <= n_val; vali++) {
-      double val = val0 + vali * delval;
-      pgsconfigparams p = pgs->params();
-      if (parami == 0) p.step_duration = val;
-      else p.TLh[parami - 1] = val;
-      params.push_back(p.to_c());
-      vals.push_back(val);
+    {
+      pgssweeper sweeper(pgs, &model_);
+      std::streambuf* quiet = print ? nullptr : std::cout.rdbuf(nullptr);  // sweep() announces itself
+      try {
+        sweeper.sweep(param_name, val0, val1, n_val);
+      } catch (...) {
+        if (quiet) std::cout.rdbuf(quiet);
+        throw;
+      }
+      if (quiet) std::cout.rdbuf(quiet);
+      while (sweeper.next()) {
+        params.push_back(sweeper.get_pgs()->to_c());
+        vals.push_back(sweeper.get_val());
+      }
     }
     std::vector<double> cot(params.size());
     penalty_11 pen(model_.handle());
@@ -711,7 +877,6 @@ class modelplayer {
     o.cot = cot.data();
     b.run(0, o);
     std::vector<std::pair<double, double>> out;
-    if (print) std::cout << "sweeping over " << param_name << ":" << std::endl;
     for (size_t i = 0; i < vals.size(); i++) {
       out.emplace_back(vals[i], cot[i]);
       if (print) std::cout << "val = " << vals[i] << " COT = " << cot[i] << std::endl;
@@ -720,9 +885,10 @@ class modelplayer {
   }
   // devices measure_cot_sweep shards its rollouts over (bit d = HIP device d)
   void set_device_mask(uint32_t mask) { device_mask_ = mask; }
-  // player.cpp:617-629: one cycle's complete trajectory records to traj.txt
-  void record_per_traj(const pergensetup* pgs, int n_t, const std::string& fname = "traj.txt") {
+  // one cycle's complete trajectory records of n_t samples to fname (player.cpp:617-629 with n_t given)
+  void record_per_traj(const pergensetup* pgs, int n_t, const std::string& fname) {
     const int len = 2 * model_.get_config_dim() + model_.number_of_motor_joints();
+    penalty_11 pen(model_.handle());  // prepare_per_traj_dyn (player.cpp:263)
     double** traj = new_2d_array(n_t, len);
     periodic per(&model_);
     per.record_trajectory(pgs, n_t);
@@ -730,6 +896,32 @@ class modelplayer {
     save_2d_array(traj, n_t, len, fname, false);
     delete_2d_array(traj, n_t);
   }
+  // player.cpp:619-630: n_t = int(T / play_dt + .5) records of one cycle to traj.txt
+  void record_per_traj(const pergensetup* pgs) {
+    record_per_traj(pgs, int(pgs->get_period() / play_dt_ + .5), traj_fname_);
+  }
+  // player.cpp:634-655: every sweep value's cycle appended to traj.txt, n_t from the UNSWEPT period
+  // (the reference's), all values in one batched launch
+  void record_per_traj_sweep(const pergensetup* pgs, const std::string& param_name, double val0, double val1,
+                             int n_val) {
+    const int n_t = int(pgs->get_period() / play_dt_ + .5);
+    const int len = 2 * model_.get_config_dim() + model_.number_of_motor_joints();
+    std::vector<hs_gait_params> params;
+    pgssweeper sweeper(pgs, &model_);
+    sweeper.sweep(param_name, val0, val1, n_val);
+    while (sweeper.next()) params.push_back(sweeper.get_pgs()->to_c());
+    penalty_11 pen(model_.handle());
+    std::vector<double> rec(params.size() * (size_t)n_t * len);
+    check(hs_complete_traj(model_.handle(), params.data(), (int)params.size(), n_t, 1, rec.data()),
+          "record_per_traj_sweep");
+    std::vector<double*> rows((size_t)n_t);
+    for (size_t v = 0; v < params.size(); v++) {
+      for (int i = 0; i < n_t; i++) rows[(size_t)i] = &rec[(v * n_t + i) * (size_t)len];
+      save_2d_array(rows.data(), n_t, len, traj_fname_, v > 0);
+    }
+  }
+  // where record_per_traj[_sweep](pgs) write ("traj.txt" in the working directory, like the reference)
+  void set_traj_fname(const std::string& f) { traj_fname_ = f; }
   // playerexperim.cpp:95-121: contact forces recovered from the computed torques; returns the
   // distance s the reference prints
   double test_dynamics(const pergensetup* pgs, int n_t = 20, int tsi = 2) {

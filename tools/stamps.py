@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 
 from hslabs_amd import build as B  # noqa: E402
 
-LIB = os.path.join(B.OUT_DIR, "libhslabs_stamps.so")
+LIB = os.path.join(B.OUT_DIR, os.environ.get("STAMPS_LIB", "libhslabs_stamps.so"))
 PHASES = [("setup", 0, 1), ("kin(5 samples)", 1, 2), ("k:gait record", 1, 20), ("k:torso+body FK", 20, 21),
           ("k:limb IK", 21, 22), ("k:limb FK+features", 22, 2), ("dynamics", 3, 4), ("particular", 4, 5),
           ("contact list", 5, 6), ("contact solve", 6, 7), ("outputs", 7, 8), ("TOTAL", 0, 8)]
