@@ -1244,6 +1244,41 @@ __device__ HS_GENERAL_ATTR uint32_t general_solve(const hs_topo* T, SV& sv, G& g
 #endif
 constexpr real kFastPivotGuard = HS_REAL_IS_FLOAT ? real(HS_F32_GUARD) : real(1e-10);
 
+// Nearly collinear contact feet (nc >= 3): the zeroth-order Gram G = A A^T = sum_c A_c A_c^T is
+// close to rank 5. The reference's loop (ftsolver.cpp:205-232) then sees a rank-deficient first-order
+// system (its ntn0 * Ry columns carry G's conditioning squared), finds rel_error > 1e-6 and retries at
+// lower ranks, landing on a different answer from the closed form's exact minimizer. The closed form is
+// taken only when det(J) >= kZerothGuard * c2(J) * maxdiag(G): J = sum_c [e_c]x [e_c]x^T is the Schur
+// complement of G's translation block (e_c = d0_c - mean d0), det/c2 (c2 = sum of its principal 2x2
+// minors) its smallest eigenvalue to within a factor of 3, and the ratio tracks the reference's 6th
+// FullPivLU pivot ratio to within ~2x. Over the oracle's tree mode on 120k transformed steps (DESIGN.md
+// 3.4) every retry had the ratio below 2.5e-5; plain synthetic gaits stay above 2.9e-2. Steps under
+// the guard take the Eigen-style path, which restates the reference's loop.
+constexpr real kZerothGuard = real(1e-3);
+
+__device__ inline bool zeroth_well_posed(const real (*d0)[3], int nc) {
+  real mu[3] = {0, 0, 0};
+  for (int c = 0; c < nc; c++)
+    for (int r = 0; r < 3; r++) mu[r] += d0[c][r];
+  const real inv = real(1) / real(nc);
+  for (int r = 0; r < 3; r++) mu[r] *= inv;
+  real C[6] = {0, 0, 0, 0, 0, 0}, gd[3] = {0, 0, 0};  // C = sum e e^T (00 11 22 01 02 12); diag(G22)
+  for (int c = 0; c < nc; c++) {
+    real e[3];
+    for (int r = 0; r < 3; r++) e[r] = d0[c][r] - mu[r];
+    C[0] += e[0] * e[0]; C[1] += e[1] * e[1]; C[2] += e[2] * e[2];
+    C[3] += e[0] * e[1]; C[4] += e[0] * e[2]; C[5] += e[1] * e[2];
+    const real q0 = d0[c][0] * d0[c][0], q1 = d0[c][1] * d0[c][1], q2 = d0[c][2] * d0[c][2];
+    gd[0] += q1 + q2; gd[1] += q0 + q2; gd[2] += q0 + q1;
+  }
+  const real tr = C[0] + C[1] + C[2];
+  const real j00 = tr - C[0], j11 = tr - C[1], j22 = tr - C[2], j01 = -C[3], j02 = -C[4], j12 = -C[5];
+  const real det = j00 * (j11 * j22 - j12 * j12) - j01 * (j01 * j22 - j12 * j02) + j02 * (j01 * j12 - j11 * j02);
+  const real c2 = (j00 * j11 - j01 * j01) + (j00 * j22 - j02 * j02) + (j11 * j22 - j12 * j12);
+  const real md = fmax(real(nc), fmax(gd[0], fmax(gd[1], gd[2])));
+  return det >= kZerothGuard * c2 * md;  // false on NaN
+}
+
 // rl (N): receives 1 / L_jj, the reciprocal each pivot's column was scaled by, for chol_solve_n
 template <int N>
 __device__ inline bool chol_n(real* a, real guard, real* rl_out) {  // row-major, in place
@@ -1780,6 +1815,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
   wave_sync();
   STAMP(18);
   const real a[6] = {sv.x[0], sv.x[1], sv.x[2], sv.x[3 * n], sv.x[3 * n + 1], sv.x[3 * n + 2]};
+  if (nc >= 3 && !zeroth_well_posed(fl.d0, nc)) return false;  // uniform: every lane reads the same d0
   for (int c = 0; c < nc; c++)
     if (!fl.ok[c]) return (TIER2 && aug_ok) ? aug_solve(fl, ag, sv, a, nc, lane) : false;  // only nc >= 3 factors D_c
   int ok = 1;

@@ -61,3 +61,31 @@ def record_to_oracle_gait(O, r):
                         foot_shift=float(r["foot_shift"]),
                         rec_transform=((tuple(float(v) for v in r["rec_transl"]), tuple(float(v) for v in r["rec_eas"]))
                                        if int(r["rec_transform_flag"]) else None))
+
+
+def golden_params(raw):
+    """GAIT_DTYPE records from a fixture's raw bytes [B][record]: fixtures of ABI <= 11 hold 128-byte
+    records, whose first 104 bytes are the current record's (the record transform was added after)."""
+    import numpy as np
+
+    from hslabs_amd import GAIT_DTYPE
+
+    raw = np.asarray(raw, dtype=np.uint8).reshape(len(raw), -1)
+    out = np.zeros(raw.shape[0], GAIT_DTYPE)
+    out.view(np.uint8).reshape(raw.shape[0], -1)[:, :104] = raw[:, :104]
+    return out
+
+
+def transformed(params, rng, frac=0.5, tilt=0.05):
+    """a copy of the GAIT_DTYPE batch with a random record transform on about `frac` of its rollouts
+    (yaw anywhere, roll / pitch within +-tilt, translation within +-1 horizontally and +-0.02 up)"""
+    import numpy as np
+
+    out = params.copy()
+    on = rng.random(len(out)) < frac
+    n = int(on.sum())
+    out["rec_transform_flag"][on] = 1
+    out["rec_transl"][on] = np.stack([rng.uniform(-1, 1, n), rng.uniform(-1, 1, n), rng.uniform(-0.02, 0.02, n)], 1)
+    out["rec_eas"][on] = np.stack([rng.uniform(-tilt, tilt, n), rng.uniform(-tilt, tilt, n),
+                                   rng.uniform(-np.pi, np.pi, n)], 1)
+    return out, on

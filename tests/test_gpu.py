@@ -12,7 +12,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, MODELS, PGS_CONFIG, PGS_IDS, record_to_oracle_gait, to_oracle_gait
+from conftest import GOLDEN, MODELS, PGS_CONFIG, PGS_IDS, golden_params, record_to_oracle_gait, to_oracle_gait
 
 pytestmark = pytest.mark.gpu
 
@@ -66,10 +66,8 @@ def test_golden_vectors(gpu, hmodels, path):
 
 
 def test_golden_synthetic_batch(gpu, hmodels):
-    from hslabs_amd import GAIT_DTYPE
-
     z = np.load(os.path.join(GOLDEN, "synth_hexapod16.npz"))
-    params = z["params"].reshape(-1).view(GAIT_DTYPE)
+    params = golden_params(z["params"])
     g = gpu.run_host(hmodels["hexapod"], params, n_t=20, horizon=20)
     scale = np.maximum(1, np.abs(z["tau"]).max(axis=(1, 2)))
     assert (np.abs(g["tau"] - z["tau"]).max(axis=(1, 2)) < 1e-6 * scale).all()  # north_star bound

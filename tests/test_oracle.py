@@ -462,3 +462,25 @@ def test_rec_transform_translation_keeps_the_dynamics(oracle_mod, omodels, sid):
         assert np.abs(r["cf"] - base["cf"]).max() < 1e-8 * max(1.0, np.abs(base["cf"]).max())
         assert np.abs(r["q"][:, :2] - base["q"][:, :2] - np.array(tr[:2])).max() < 1e-12
         assert np.abs(r["q"][:, 2:] - base["q"][:, 2:]).max() < 1e-12
+
+
+def test_zeroth_guard_routes_collinear_contacts(oracle_mod, omodels):
+    """Tilted / lifted records can leave three same-side hexapod feet in contact, nearly on one line.
+    The reference's loop (ftsolver.cpp:205-232) then finds its first pass inconsistent and retries at
+    lower ranks (tree mode's RANK_RETRY), and its answer is not the closed form's exact minimizer (which
+    runs to kN forces there). Fast mode's zeroth_well_posed guard hands those steps to the Eigen-style
+    path (GENERAL), so fast mode equals tree mode on every step of the batch."""
+    from conftest import record_to_oracle_gait, transformed
+    from hslabs_amd import synth
+
+    O = oracle_mod
+    params, on = transformed(synth.gen_params(256, "hexapod", id0=900), np.random.default_rng(7))
+    gaits = [record_to_oracle_gait(O, r) for r in params]
+    rt = O.batch(omodels["hexapod"], gaits, 20, 0, 20, basis=O.BASIS_TREE, n_threads=8)
+    rf = O.batch(omodels["hexapod"], gaits, 20, 0, 20, basis=O.BASIS_FAST, n_threads=8)
+    retry = (rt["flags"] & O.FLAG_RANK_RETRY) != 0
+    assert retry.sum() >= 3 and on[np.nonzero(retry)[0]].all()
+    assert ((rf["flags"][retry] & O.FLAG_GENERAL) != 0).all()
+    scale = np.maximum(1, np.abs(rt["tau"]).max(axis=-1, keepdims=True))
+    assert (np.abs(rf["tau"] - rt["tau"]) / scale).max() < 1e-9
+    assert np.array_equal(rf["flags"] & ~np.uint32(O.FLAG_GENERAL), rt["flags"])
