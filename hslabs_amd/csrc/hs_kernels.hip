@@ -1247,36 +1247,49 @@ constexpr real kFastPivotGuard = HS_REAL_IS_FLOAT ? real(HS_F32_GUARD) : real(1e
 // Nearly collinear contact feet (nc >= 3): the zeroth-order Gram G = A A^T = sum_c A_c A_c^T is
 // close to rank 5. The reference's loop (ftsolver.cpp:205-232) then sees a rank-deficient first-order
 // system (its ntn0 * Ry columns carry G's conditioning squared), finds rel_error > 1e-6 and retries at
-// lower ranks, landing on a different answer from the closed form's exact minimizer. The closed form is
-// taken only when det(J) >= kZerothGuard * c2(J) * maxdiag(G): J = sum_c [e_c]x [e_c]x^T is the Schur
-// complement of G's translation block (e_c = d0_c - mean d0), det/c2 (c2 = sum of its principal 2x2
-// minors) its smallest eigenvalue to within a factor of 3, and the ratio tracks the reference's 6th
-// FullPivLU pivot ratio to within ~2x. Over the oracle's tree mode on 120k transformed steps (DESIGN.md
-// 3.4) every retry had the ratio below 2.5e-5; plain synthetic gaits stay above 2.9e-2. Steps under
-// the guard take the Eigen-style path, which restates the reference's loop.
-constexpr real kZerothGuard = real(1e-3);
+// lower ranks, landing on a different answer from the closed form's exact minimizer. G's smallest
+// eigenvalue is that of J = sum_c [e_c]x [e_c]x^T = tr(C) I - C (the Schur complement of its
+// translation block; e_c = d0_c - mean d0, C = sum_c e_c e_c^T), i.e. mu2 + mu3 for C's eigenvalues
+// mu1 >= mu2 >= mu3, which c2(C) / tr(C) gives to within a factor of 4 (c2 = the sum of C's principal
+// 2x2 minors). The closed form is taken only when c2(C) / (tr(C) maxdiag(G)) >= kZerothGuard; the
+// ratio follows the reference's 6th FullPivLU pivot ratio to within ~2x. Over the oracle's tree mode on
+// 120k transformed steps every retry had it below 2.5e-5; plain synthetic gaits stay
+// above 1e-2. Steps under the guard take the Eigen-style path, which restates the reference's loop.
+// No division: with s = sum d0_c and Q = sum d0_c d0_c^T, C' = nc Q - s s^T = nc C, so the test reads
+// c2(C') >= kZerothGuard * nc * tr(C') * maxdiag(G), maxdiag(G) = max(nc, tr Q - Q_ii). A heuristic
+// with a 40x margin on each side, so it runs in single precision: contact lane c holds d0_c, the nine
+// moments are summed over the 8-lane group by DPP (quad xor 1, xor 2, half-row mirror), and lanes past
+// nc add zeros. Every lane of the half-wave calls it; the verdict is the same on lanes 0 .. 7.
+constexpr float kZerothGuard = 1e-3f;
 
-__device__ inline bool zeroth_well_posed(const real (*d0)[3], int nc) {
-  real mu[3] = {0, 0, 0};
-  for (int c = 0; c < nc; c++)
-    for (int r = 0; r < 3; r++) mu[r] += d0[c][r];
-  const real inv = real(1) / real(nc);
-  for (int r = 0; r < 3; r++) mu[r] *= inv;
-  real C[6] = {0, 0, 0, 0, 0, 0}, gd[3] = {0, 0, 0};  // C = sum e e^T (00 11 22 01 02 12); diag(G22)
-  for (int c = 0; c < nc; c++) {
-    real e[3];
-    for (int r = 0; r < 3; r++) e[r] = d0[c][r] - mu[r];
-    C[0] += e[0] * e[0]; C[1] += e[1] * e[1]; C[2] += e[2] * e[2];
-    C[3] += e[0] * e[1]; C[4] += e[0] * e[2]; C[5] += e[1] * e[2];
-    const real q0 = d0[c][0] * d0[c][0], q1 = d0[c][1] * d0[c][1], q2 = d0[c][2] * d0[c][2];
-    gd[0] += q1 + q2; gd[1] += q0 + q2; gd[2] += q0 + q1;
+template <int CTRL>
+__device__ inline float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ inline float group8_sum(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_f<0x141>(v);  // row_half_mirror: lane i <- 7 - i, the other quad's sum
+  return v;
+}
+
+template <class W, class SV>
+__device__ inline bool zeroth_well_posed(const real* P0, const W& w, const SV& sv, int nc, int lane) {
+  float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+  if (lane < nc) {
+    const real* fp = w.fpos(0, sv.cfoot[lane]);
+    d0 = float(P0[0] - fp[0]); d1 = float(P0[1] - fp[1]); d2 = float(P0[2] - fp[2]);
   }
-  const real tr = C[0] + C[1] + C[2];
-  const real j00 = tr - C[0], j11 = tr - C[1], j22 = tr - C[2], j01 = -C[3], j02 = -C[4], j12 = -C[5];
-  const real det = j00 * (j11 * j22 - j12 * j12) - j01 * (j01 * j22 - j12 * j02) + j02 * (j01 * j12 - j11 * j02);
-  const real c2 = (j00 * j11 - j01 * j01) + (j00 * j22 - j02 * j02) + (j11 * j22 - j12 * j12);
-  const real md = fmax(real(nc), fmax(gd[0], fmax(gd[1], gd[2])));
-  return det >= kZerothGuard * c2 * md;  // false on NaN
+  const float s0 = group8_sum(d0), s1 = group8_sum(d1), s2 = group8_sum(d2);
+  const float q00 = group8_sum(d0 * d0), q11 = group8_sum(d1 * d1), q22 = group8_sum(d2 * d2);
+  const float q01 = group8_sum(d0 * d1), q02 = group8_sum(d0 * d2), q12 = group8_sum(d1 * d2);
+  const float k = float(nc);
+  const float c00 = k * q00 - s0 * s0, c11 = k * q11 - s1 * s1, c22 = k * q22 - s2 * s2;
+  const float c01 = k * q01 - s0 * s1, c02 = k * q02 - s0 * s2, c12 = k * q12 - s1 * s2;
+  const float c2 = (c00 * c11 - c01 * c01) + (c00 * c22 - c02 * c02) + (c11 * c22 - c12 * c12);
+  const float tq = q00 + q11 + q22;
+  const float md = fmaxf(k, fmaxf(tq - q00, fmaxf(tq - q11, tq - q22)));
+  return c2 >= kZerothGuard * k * (c00 + c11 + c22) * md;  // false on NaN
 }
 
 // rl (N): receives 1 / L_jj, the reciprocal each pivot's column was scaled by, for chol_solve_n
@@ -1590,122 +1603,6 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, AugL&
   return true;
 }
 
-// value of v on lane src of this half-wave (src the same on every lane: a loop constant): one
-// readlane per 32-bit word and half
-__device__ inline real half_bcast(real v, int src) {
-  const bool up = threadIdx.x >= HALF;
-#if HS_REAL_IS_FLOAT
-  const int w0 = __builtin_amdgcn_readlane(__float_as_int(v), src);
-  const int w1 = __builtin_amdgcn_readlane(__float_as_int(v), src + HALF);
-  return __int_as_float(up ? w1 : w0);
-#else
-  const long long u = __double_as_longlong(v);
-  const int lo = (int)u, hi = (int)(u >> 32);
-  const int l0 = __builtin_amdgcn_readlane(lo, src), h0 = __builtin_amdgcn_readlane(hi, src);
-  const int l1 = __builtin_amdgcn_readlane(lo, src + HALF), h1 = __builtin_amdgcn_readlane(hi, src + HALF);
-  const unsigned long long w = ((unsigned long long)(unsigned)(up ? h1 : h0) << 32) | (unsigned)(up ? l1 : l0);
-  return __longlong_as_double((long long)w);
-#endif
-}
-
-#ifndef HS_SCHUR_LANES
-#define HS_SCHUR_LANES 1
-#endif
-// The 6x6 Schur system S lam = a - h (ldl_n<6> + ldl_solve_n<6>, the oracle's fast mode) with the
-// factorization spread over lanes 0..5 of the half-wave: lane i holds row i of the packed sums and
-// applies pivot j's operations to it right-looking (L_ij = a_ij / d_j, then a_ic -= L_ij (L_cj d_j)
-// for j < c <= i: ldl_n's subtractions per entry, in the same pivot order, with the same products);
-// the pivots and the column just scaled come from their lanes by readlane, the reciprocal of each
-// pivot is formed on every lane. Every lane then gathers the factor and runs ldl_solve_n on it (the
-// forward / backward substitutions are one dependent chain either way). Returns the guard's verdict,
-// the same on every lane of the half; lane 0 stores lam.
-__device__ inline int schur_ldl6(FastL& fl, const real* a, int lane) {
-  const int i = lane < 6 ? lane : 5;  // lanes past row 5 repeat row 5 (their values are not read)
-  real row[6], mx = 0;
-#pragma unroll
-  for (int c = 0; c < 6; c++) {
-    row[c] = (c <= i) ? fl.sc.Ssum[sch_lower(i, c)] : real(0);
-    mx = fmax(mx, fl.sc.Ssum[sch_lower(c, c)]);
-  }
-  int ok = 1;
-  real rl[6];
-#pragma unroll
-  for (int j = 0; j < 6; j++) {
-    const real dj = half_bcast(row[j], j);  // d_j: lane j's diagonal after pivots 0 .. j-1
-    if (!(dj > kFastPivotGuard * mx)) ok = 0;
-    const real r = real(1) / dj;
-    rl[j] = r;
-    if (i > j) row[j] = row[j] * r;
-#pragma unroll
-    for (int c = j + 1; c < 6; c++) {
-      const real v = half_bcast(row[j], c) * dj;  // L_cj d_j (ldl_n's v for row c)
-      if (c <= i) row[c] -= row[j] * v;
-    }
-  }
-  real Sm[36], lam[6];
-#pragma unroll
-  for (int c = 0; c < 6; c++) {
-#pragma unroll
-    for (int k = 0; k < 6; k++) Sm[6 * c + k] = (k <= c) ? half_bcast(row[k], c) : real(0);  // upper: unread
-    lam[c] = a[c] - fl.sc.Ssum[SCH_H + c];
-  }
-#ifndef HS_EXP_NO_SCHUR
-  ldl_solve_n<6>(Sm, rl, lam);
-#endif
-  if (lane == 0) {
-    if (ok)
-      for (int r = 0; r < 6; r++) fl.sc.lam[r] = lam[r];
-    fl.ok[0] = ok;
-  }
-  return ok;
-}
-
-#ifndef HS_FORCES_REGS
-#define HS_FORCES_REGS 1
-#endif
-// chol_packed's factorization with the matrix in registers (solve_forces): lane i of the half-wave
-// holds row i of the packed lower triangle, pivot j comes from lane j and column j from the lanes
-// below it by readlane (half_bcast), so every entry takes the same operations in the same order
-// (right-looking: L_ij = K_ij / L_jj, then K_ic -= L_ij L_cj for j < c <= i) and L is bitwise
-// chol_packed's -- without its LDS round trips and wavefront syncs per pivot. rl[j] = 1 / L_jj (the
-// same on every lane); L is written back to K. False when a pivot falls to guard * max diagonal (the
-// failing half keeps going and its values are discarded by the caller).
-template <int NMAX>
-__device__ inline bool chol_regs(real* K, int k, real guard, real* rl, int lane) {
-  const int i = lane < k ? lane : k - 1;  // lanes past the last row repeat it (their values are not stored)
-  real row[NMAX], mx = 0;
-#pragma unroll
-  for (int c = 0; c < NMAX; c++) {
-    row[c] = (c <= i) ? K[pk(i, c)] : real(0);
-    if (c < k) mx = fmax(mx, K[pk(c, c)]);
-  }
-  bool ok = true;
-#pragma unroll
-  for (int j = 0; j < NMAX; j++) {
-    if (j < k) {
-      const real d = half_bcast(row[j], j);
-      if (!(d > guard * mx)) ok = false;
-      const real l = sqrt(d), r = real(1) / l;
-      rl[j] = r;
-      if (i == j) row[j] = l;
-      else if (i > j) row[j] = row[j] * r;
-#pragma unroll
-      for (int c = j + 1; c < NMAX; c++) {
-        if (c < k) {
-          const real lc = half_bcast(row[j], c);
-          if (c <= i) row[c] -= row[j] * lc;
-        }
-      }
-    }
-  }
-  if (lane < k)
-#pragma unroll
-    for (int c = 0; c < NMAX; c++)
-      if (c <= i) K[pk(i, c)] = row[c];
-  wave_sync();
-  return ok;
-}
-
 // TIER2: the augmented-system solve where a D_c or the Schur complement is singular; without it
 // (HS_DEFER_AUG builds of the fused step launch) such steps decline and go to the fixup launch
 // aug_ok = false (the fixup launch's idle half, which stores nothing): decline instead of using the
@@ -1716,6 +1613,11 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
   const int n = T->n;
   if (nc == 0) return true;
   const real* P0 = w.pos(0, 0);
+#ifndef HS_EXP_NO_ZEROTH_GUARD  // timing experiment only
+  const int coll = (nc >= 3 && !zeroth_well_posed(P0, w, sv, nc, lane)) ? 2 : 0;
+#else
+  const int coll = 0;
+#endif
   if (lane < nc) {  // A_c, D_c, g_c for contact c = lane
     const int c = lane, fi = sv.cfoot[c];
     const real* fp = w.fpos(0, fi);
@@ -1810,14 +1712,14 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
         for (int i = 0; i < 9; i++) fl.sc.Dinv[c][i] = Dinv[i];
       }
     }
-    fl.ok[c] = ok;
+    fl.ok[c] = ok | coll;
   }
   wave_sync();
   STAMP(18);
   const real a[6] = {sv.x[0], sv.x[1], sv.x[2], sv.x[3 * n], sv.x[3 * n + 1], sv.x[3 * n + 2]};
-  if (nc >= 3 && !zeroth_well_posed(fl.d0, nc)) return false;  // uniform: every lane reads the same d0
+  if (nc >= 3 && (fl.ok[0] & 2)) return false;  // nearly collinear contacts: the Eigen-style path
   for (int c = 0; c < nc; c++)
-    if (!fl.ok[c]) return (TIER2 && aug_ok) ? aug_solve(fl, ag, sv, a, nc, lane) : false;  // only nc >= 3 factors D_c
+    if (!(fl.ok[c] & 1)) return (TIER2 && aug_ok) ? aug_solve(fl, ag, sv, a, nc, lane) : false;  // only nc >= 3 factors D_c
   int ok = 1;
   if (nc == 1) {  // unique least-squares solution (A^T A) w = -A^T a
     if (lane == 0) {
@@ -1887,12 +1789,6 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       fl.sc.Ssum[lane] = s;
     }
     wave_sync();
-#if HS_SCHUR_LANES
-    // the 6x6 LDL^T right-looking over six lanes (lane i holds row i; pivots and columns broadcast by
-    // readlane), the solve on each lane with the factor gathered from them: every entry takes the
-    // operations ldl_n / ldl_solve_n apply to it, in the same order
-    ok = schur_ldl6(fl, a, lane);
-#else
     if (lane == 0) {
       real Sm[36], h[6];
 #pragma unroll
@@ -1916,7 +1812,6 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       }
       fl.ok[0] = ok;
     }
-#endif
     wave_sync();
     STAMP(19);
     if (!fl.ok[0]) return (TIER2 && aug_ok) ? aug_solve(fl, ag, sv, a, nc, lane) : false;
@@ -2292,17 +2187,10 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
   }
   wave_sync();
   STAMP(4);
-  constexpr int MM = 6 + HS_KMAX;
-  real rl[MM];  // 1 / L_ii of I + G G^T (the divisions of the substitutions, as multiplications)
-#if HS_FORCES_REGS
-  chol_regs<MM>(fr.W, m, real(0), rl, lane);  // I + G G^T: eigenvalues >= 1
-#else
-  chol_packed(fr.W, m, real(0), lane);
-#pragma unroll
-  for (int i = 0; i < MM; i++) rl[i] = (i < m) ? real(1) / fr.W[pk(i, i)] : real(0);
-#endif
+  chol_packed(fr.W, m, real(0), lane);  // I + G G^T: eigenvalues >= 1
   STAMP(5);
   if (lane < ld) {  // L^-1 [C | d], one column per lane, the column in registers (m <= 6 + HS_KMAX)
+    constexpr int MM = 6 + HS_KMAX;
     real col[MM];
 #pragma unroll
     for (int i = 0; i < MM; i++) col[i] = (i < m) ? fr.Ct[i * ld + lane] : real(0);
@@ -2312,7 +2200,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
         real s = col[i];
 #pragma unroll
         for (int t = 0; t < i; t++) s -= fr.W[pk(i, t)] * col[t];
-        col[i] = s * rl[i];
+        col[i] = s / fr.W[pk(i, i)];
       }
     }
 #pragma unroll
@@ -2322,7 +2210,6 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
   wave_sync();
   STAMP(6);
   uint32_t flags = 0;
-  real rn[HS_KMAX];  // 1 / M_ii of the normal matrix's factor
   for (int pass = 0; pass < 2; pass++) {  // normal equations; second pass regularized
     real eps = 0;
     if (pass == 1) {
@@ -2342,15 +2229,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     }
     wave_sync();
     STAMP(7);
-#if HS_FORCES_REGS
-    if (chol_regs<HS_KMAX>(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), rn, lane)) break;
-#else
-    if (chol_packed(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) {
-#pragma unroll
-      for (int i = 0; i < HS_KMAX; i++) rn[i] = (i < nq) ? real(1) / fr.W[pk(i, i)] : real(0);
-      break;
-    }
-#endif
+    if (chol_packed(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) break;
     flags = HS_FLAG_GENERAL;  // least squares not unique
   }
   STAMP(8);
@@ -2364,7 +2243,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
         real s = yv[i];
 #pragma unroll
         for (int k = 0; k < i; k++) s -= fr.W[pk(i, k)] * yv[k];
-        yv[i] = s * rn[i];
+        yv[i] = s / fr.W[pk(i, i)];
       }
     }
 #pragma unroll
@@ -2374,7 +2253,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
 #pragma unroll
         for (int k = i + 1; k < HS_KMAX; k++)
           if (k < nq) s -= fr.W[pk(k, i)] * yv[k];
-        yv[i] = s * rn[i];
+        yv[i] = s / fr.W[pk(i, i)];
       }
     }
 #pragma unroll

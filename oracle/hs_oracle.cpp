@@ -1575,36 +1575,30 @@ bool aug_solve(int nc, const std::vector<double>& A, const std::vector<double>& 
 // Nearly collinear contact feet (nc >= 3) make G = A A^T (zeroth-order rows) close to rank 5; the
 // reference's loop (ftsolver.cpp:205-232) then finds rel_error > 1e-6 on its first pass (ntn0 * Ry
 // carries G's conditioning squared) and retries at lower ranks, so the closed form's exact minimizer
-// is not its answer. Accepted when det(J) >= 1e-3 * c2(J) * maxdiag(G), J = sum_c [e_c]x [e_c]x^T,
-// e_c = d0_c - mean d0 (G's Schur complement on its translation block; det/c2 = its smallest
-// eigenvalue within 3x); the ratio follows the reference's 6th FullPivLU pivot ratio within ~2x, and
-// every retry measured in tree mode had it below 2.5e-5 (tests/test_oracle.py::test_zeroth_guard_*).
+// is not its answer. Accepted when c2(C) / (tr(C) maxdiag(G)) >= 1e-3, C = sum_c e_c e_c^T,
+// e_c = d0_c - mean d0 (c2(C) / tr(C) is G's smallest eigenvalue mu2 + mu3 within 4x); the ratio
+// follows the reference's 6th FullPivLU pivot ratio within ~2x, and every retry measured in tree mode
+// had it below 2.5e-5 (tests/test_oracle.py::test_zeroth_guard_*). The kernel's division-free form
+// (zeroth_well_posed in hs_kernels.hip): C' = nc Q - s s^T (s = sum d0_c, Q = sum d0_c d0_c^T),
+// c2(C') >= 1e-3 * nc * tr(C') * maxdiag(G).
 constexpr double kZerothGuard = 1e-3;
-bool zeroth_well_posed(const hso_model* m, const DynRec& d, const std::vector<int>& cf) {
+bool zeroth_well_posed(const DynRec& d, const std::vector<int>& cf) {
   const int nc = (int)cf.size();
-  (void)m;
-  double mu[3] = {0, 0, 0};
-  std::vector<double> d0(3 * nc);
-  for (int c = 0; c < nc; c++)
-    for (int r = 0; r < 3; r++) { d0[3 * c + r] = d.pos[0].v[r] - d.fpos[cf[c]].v[r]; mu[r] += d0[3 * c + r]; }
-  for (int r = 0; r < 3; r++) mu[r] *= 1.0 / nc;
-  double C[3][3] = {{0}}, gd[3] = {0, 0, 0};
+  double s0 = 0, s1 = 0, s2 = 0, q00 = 0, q11 = 0, q22 = 0, q01 = 0, q02 = 0, q12 = 0;
   for (int c = 0; c < nc; c++) {
-    double e[3];
-    for (int r = 0; r < 3; r++) e[r] = d0[3 * c + r] - mu[r];
-    for (int i = 0; i < 3; i++) for (int j = 0; j < 3; j++) C[i][j] += e[i] * e[j];
-    const double* dc = &d0[3 * c];
-    for (int i = 0; i < 3; i++) gd[i] += dc[0] * dc[0] + dc[1] * dc[1] + dc[2] * dc[2] - dc[i] * dc[i];
+    const Vec& fp = d.fpos[cf[c]];
+    const double d0 = d.pos[0].v[0] - fp.v[0], d1 = d.pos[0].v[1] - fp.v[1], d2 = d.pos[0].v[2] - fp.v[2];
+    s0 += d0; s1 += d1; s2 += d2;
+    q00 += d0 * d0; q11 += d1 * d1; q22 += d2 * d2;
+    q01 += d0 * d1; q02 += d0 * d2; q12 += d1 * d2;
   }
-  const double tr = C[0][0] + C[1][1] + C[2][2];
-  double J[3][3];
-  for (int i = 0; i < 3; i++) for (int j = 0; j < 3; j++) J[i][j] = (i == j ? tr : 0.0) - C[i][j];
-  const double det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) - J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
-                     J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
-  const double c2 = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) + (J[0][0] * J[2][2] - J[0][2] * J[2][0]) +
-                    (J[1][1] * J[2][2] - J[1][2] * J[2][1]);
-  const double md = std::max((double)nc, std::max(gd[0], std::max(gd[1], gd[2])));
-  return det >= kZerothGuard * c2 * md;
+  const double k = nc;
+  const double c00 = k * q00 - s0 * s0, c11 = k * q11 - s1 * s1, c22 = k * q22 - s2 * s2;
+  const double c01 = k * q01 - s0 * s1, c02 = k * q02 - s0 * s2, c12 = k * q12 - s1 * s2;
+  const double c2 = (c00 * c11 - c01 * c01) + (c00 * c22 - c02 * c02) + (c11 * c22 - c12 * c12);
+  const double tq = q00 + q11 + q22;
+  const double md = std::max(k, std::max(tq - q00, std::max(tq - q11, tq - q22)));
+  return c2 >= kZerothGuard * k * (c00 + c11 + c22) * md;
 }
 
 bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<double>& x, std::vector<double>& y) {
@@ -1688,7 +1682,7 @@ bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<d
     return true;
   }
   // nc >= 3: nearly collinear feet leave it to the Eigen-style path (the kernel's zeroth_well_posed)
-  if (!zeroth_well_posed(m, d, cf)) return false;
+  if (!zeroth_well_posed(d, cf)) return false;
   // Schur complement on the 6 zeroth-order constraints
   double S[36] = {0}, h[6] = {0};
   std::vector<double> Dinv(9 * nc);
