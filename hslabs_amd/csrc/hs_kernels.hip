@@ -55,7 +55,7 @@ static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a
 #define HS_MIN_WAVES 3  // fp64: 12 workgroups/CU at 13.0 KB LDS (hexapod), <= 168 VGPRs
 #endif
 #ifndef HS_MIN_WAVES_FORCES
-#define HS_MIN_WAVES_FORCES 2  // solve_forces mode (hs_run_forces): its LDS layout holds a 24 x 24 system
+#define HS_MIN_WAVES_FORCES 3  // solve_forces mode (hs_run_forces): the control step's LDS layout
 #endif
 #ifndef HS_MIN_WAVES_F32
 #define HS_MIN_WAVES_F32 4  // fp32: 9.9 KB LDS per hexapod workgroup; 128 VGPRs (216 B scratch)
@@ -131,10 +131,11 @@ struct CentreL {  // fields read after D
   int unreach[HS_LMAX];
 };
 
-struct ForceL {  // solve_forces: W = I + G G^T, later the normal matrix (packed lower triangles); L^-1 [C | d]
-  real W[(6 + HS_KMAX) * (7 + HS_KMAX) / 2];
-  real Ct[(6 + HS_KMAX) * (HS_KMAX + 1)];
-  real y[HS_KMAX];
+struct ForceL {  // solve_forces by limbs (forces_solve): per limb S_l and e_l (a), per foot K_f and q_f
+                 // (b); the dense fallback reuses the space from a[0][27] on (336 reals in all)
+  real a[HS_LMAX][27];
+  real b[HS_LMAX][27];
+  real spare[12];
 };
 
 template <int NM, bool FORCES>
@@ -479,10 +480,12 @@ __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g
   target[0] = dx + st.pos0[j][0];
   target[1] = dy + st.pos0[j][1];
   target[2] = dz + st.pos0[j][2];
+#ifndef HS_EXP_NO_RECXF  // timing experiment only
   if (!STRAIGHT && g.rec_xf) {  // set_rec's last step (pergen.cpp:238)
     transform_rec(gp, o0, o1, target);
     turned = true;  // the torso angles are no longer the configured ones
   }
+#endif
 }
 
 // sample times t_i = dt + dt + ... (i terms, periodic.cpp:171-181), stored once per rollout by the
@@ -2080,170 +2083,280 @@ __device__ inline void cross3(const real* a, const real* b, real* c) {
   c[2] = a[0] * b[1] - a[1] * b[0];
 }
 
+// Block elimination by limbs. Every hinge is a limb link and a limb's three links are its own
+// subtree (the loader's topology class), so W = I + G G^T couples motors of one limb only: ordered
+// (motors, torso) it is W = [[M, W_mt], [W_tm, W_tt]] with M = diag(M_l), 3 x 3 per limb, and C's motor
+// rows touch only their limb's foot. With S = W_tt - W_tm M^-1 W_mt (>= I), C~ = C_t - W_tm M^-1 C_m,
+// d~ = d_t - W_tm M^-1 d_m and, per foot, B_f = C_mf^T M_l^-1 C_mf, r_f = C_mf^T M_l^-1 d_m, the normal
+// equations are N y = r with N = diag(B_f) + C~^T S^-1 C~, r = r_b + C~^T S^-1 d~ (the same N as
+// (L^-1 C)^T (L^-1 C) for W = L L^T). When every B_f is well conditioned (LDL^T pivots above
+// kForcesBlockGuard of its diagonal), the Schur complement of diag(B_f) in the KKT system gives
+//   (S + sum_f C~_f B_f^-1 C~_f^T) lam = sum_f C~_f B_f^-1 r_f - d~,   y_f = B_f^-1 (r_f - C~_f^T lam),
+// a 6 x 6 system (>= I); otherwise (a straight leg: B_f singular) N is formed and factorized as a
+// dense 3 nf x 3 nf Cholesky, pivot guard kFastPivotGuard, HS_FLAG_GENERAL and the Tikhonov pass when
+// it trips. Lanes: one per limb for the limb's blocks (M_l = L D L^T: every product Y_a^T D^-1 Y_b,
+// Y = L^-1 [W_mt | C_m | d_m]), one per packed entry for the sums over limbs (in limb order).
+constexpr real kForcesBlockGuard = HS_REAL_IS_FLOAT ? real(1e-3) : real(1e-6);
+constexpr int FSUM = 27;  // packed 6 x 6 lower triangle (21) + a 6-vector
+
+// entry e < 21 of W_tt = I + sum_{i >= 1} T_i T_i^T from s = sum r_i, Q = sum r_i r_i^T (r_i = p_i - p_0;
+// T_i's torso block [[I, 0], [[r_i]x, I]]): n I; [s]x rows; (n + tr Q) I - Q
+__device__ inline real wtt_entry(int e, const real* ts, int n) {
+  const TriWalk<> t(e);
+  const int r = t.r, c = t.c;
+  if (r < 3) return (r == c) ? real(n) : real(0);
+  if (c < 3) return cross_e(ts, c, r - 3);
+  const int a = r - 3, b = c - 3;
+  const real* q = ts + 3;  // Q00 Q11 Q22 Q01 Q02 Q12
+  const real qab = (a == b) ? q[a] : q[a + b + 2];
+  return ((a == b) ? real(n) + q[0] + q[1] + q[2] : real(0)) - qab;
+}
+
 template <class W, class SV>
-__device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_topo* T, const SV& sv, ForceL& fr, const W& w, const real* z, int lane) {
-  const int n = T->n, nj = T->nmj, nf = T->nf, m = 6 + nj, nq = 3 * nf, ld = nq + 1;
+__device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_topo* T, SV& sv, ForceL& fr, const W& w,
+                                                                       const real* z, bool dense, int lane) {
+  const int n = T->n, nl = T->n_limbs, nq = 3 * T->nf;
   const real* P0 = w.pos(0, 0);
-  // I + G G^T, lower triangle, entry (r, c)
-  auto gram_entry = [&](const int r, const int c) {
-    real s = real(0);
-    if (r < 6) {
-      for (int i = 1; i < n; i++) {
-        const real* Pi = w.pos(0, i);
-        real ri[3], Sr[3] = {0, 0, 0}, Sc[3] = {0, 0, 0};
-        for (int t = 0; t < 3; t++) ri[t] = Pi[t] - P0[t];
-        // T_i row a = -(e_a, 0) for a < 3, -([r_i]x row a-3, e_{a-3}) for a >= 3
-        if (r >= 3) for (int t = 0; t < 3; t++) Sr[t] = cross_e(ri, t, r - 3);
-        if (c >= 3) for (int t = 0; t < 3; t++) Sc[t] = cross_e(ri, t, c - 3);
-        real v;
-        if (r < 3 && c < 3) v = (r == c) ? real(1) : real(0);
-        else if (c < 3) v = Sr[c];
-        else v = Sr[0] * Sc[0] + Sr[1] * Sc[1] + Sr[2] * Sc[2] + ((r == c) ? real(1) : real(0));
-        s += v;
+  real* ts = sv.y;  // the 9 part sums until y is written
+  if (lane < 9) {   // s (3), Q (6)
+    const int a = lane < 3 ? lane : (lane < 6 ? lane - 3 : (lane == 6 ? 0 : (lane == 7 ? 0 : 1)));
+    const int b = lane < 6 ? (lane < 3 ? -1 : lane - 3) : (lane == 6 ? 1 : 2);
+    real s = 0;
+    for (int i = 1; i < n; i++) {
+      const real* Pi = w.pos(0, i);
+      const real ra = Pi[a] - P0[a];
+      s += (b < 0) ? ra : ra * (Pi[b] - P0[b]);
+    }
+    ts[lane] = s;
+  }
+  // per limb: C~_f (6 x 3), B_f (raw and LDL^T), r_f stay in registers to the end
+  real Ct[18], Bd[6], Bl[9], rdB[3], rb[3];
+  int f = 0;
+  bool okB = true;
+  if (lane < nl) {
+    const int L = lane;
+    int p[3];
+    for (int k = 0; k < 3; k++) p[k] = T->limb_node[L][k];
+    f = T->node[p[2]].foot;
+    const real* fp = w.fpos(0, f);
+    real J[3][3], Z[3][3], P[3][3];
+    for (int k = 0; k < 3; k++)
+      for (int t = 0; t < 3; t++) {
+        J[k][t] = w.jpos(0, p[k])[t];
+        Z[k][t] = w.jz(0, p[k])[t];
+        P[k][t] = w.pos(0, p[k])[t];
       }
-    } else {
-      // the node table is in preorder (the loader checks it): a motor's subtree is one range
-      // [h, end), and the parts in both subtrees, in increasing order, are their intersection
-      const int hr = T->hinge_range[r - 6], h = hr & 255;
-      const real* Jh = w.jpos(0, h);
-      const real* Zh = w.jz(0, h);
-      const int hr2 = (c >= 6) ? T->hinge_range[c - 6] : -1, h2 = (c >= 6) ? (hr2 & 255) : -1;
-      int i0 = h, i1 = hr >> 8;
-      if (h2 >= 0) {
-        i0 = max(i0, h2);
-        i1 = min(i1, hr2 >> 8);
-      }
-      for (int i = max(i0, 1); i < min(i1, n); i++) {
-        const real* Pi = w.pos(0, i);
-        real a3[3], u[3];
-        for (int t = 0; t < 3; t++) a3[t] = Jh[t] - Pi[t];
-        cross3(a3, Zh, u);
-        if (c < 6) {  // T_i row c . (u, jz_h)
-          if (c < 3) {
-            s += -u[c];
-          } else {
-            real ri[3], ru[3];
-            for (int t = 0; t < 3; t++) ri[t] = Pi[t] - P0[t];
-            cross3(ri, u, ru);
-            s += -(ru[c - 3] + Zh[c - 3]);
-          }
-        } else {
-          const real* J2 = w.jpos(0, h2);
-          const real* Z2 = w.jz(0, h2);
-          real b3[3], u2[3];
-          for (int t = 0; t < 3; t++) b3[t] = J2[t] - Pi[t];
-          cross3(b3, Z2, u2);
-          s += u[0] * u2[0] + u[1] * u2[1] + u[2] * u2[2] + (Zh[0] * Z2[0] + Zh[1] * Z2[1] + Zh[2] * Z2[2]);
-        }
+    // raw rows of motor k: R[k] = (W_mt row (6), C_m row vs foot f (3), d_m (1)); M lower (k' <= k)
+    real R[3][10], M[9];
+    for (int k = 0; k < 3; k++) {
+      for (int c = 0; c < 10; c++) R[k][c] = 0;
+      for (int c = 0; c < 3; c++) M[3 * k + c] = (c == k) ? real(1) : real(0);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) {  // part p[i] lies in the subtrees of motors 0 .. i
+      real ri[3], u[3][3];
+      for (int t = 0; t < 3; t++) ri[t] = P[i][t] - P0[t];
+#pragma unroll
+      for (int k = 0; k <= i; k++) {
+        real a3[3], ru[3];
+        for (int t = 0; t < 3; t++) a3[t] = J[k][t] - P[i][t];
+        cross3(a3, Z[k], u[k]);
+        cross3(ri, u[k], ru);
+        for (int c = 0; c < 3; c++) R[k][c] += -u[k][c];
+        for (int c = 0; c < 3; c++) R[k][3 + c] += -(ru[c] + Z[k][c]);
+#pragma unroll
+        for (int k2 = 0; k2 <= k; k2++)
+          M[3 * k + k2] += (u[k][0] * u[k2][0] + u[k][1] * u[k2][1] + u[k][2] * u[k2][2]) +
+                           (Z[k][0] * Z[k2][0] + Z[k][1] * Z[k2][1] + Z[k][2] * Z[k2][2]);
       }
     }
-    fr.W[pk(r, c)] = ((r == c) ? real(1) : real(0)) + s;
-  };
-  // by entry class, so the lanes of a pass take one branch: the torso block (rows < 6, the long
-  // sums over all parts; 21 entries, one pass), motor rows against the torso force and the torso
-  // torque columns, then the motor block
-  if (lane < 21) {
-    const TriWalk<> t(lane);
-    gram_entry(t.r, t.c);
-  }
-  for (int p = lane; p < 3 * nj; p += HALF) gram_entry(6 + p / 3, p % 3);
-  for (int p = lane; p < 3 * nj; p += HALF) gram_entry(6 + p / 3, 3 + p % 3);
-  for (TriWalk<> t(lane); t.r < nj; t.next()) gram_entry(6 + t.r, 6 + t.c);
-  STAMP(3);
-  for (RectWalk t(lane, ld); t.r < m; t.next()) {  // [C | d]
-    const int r = t.r, q = t.c;
-    real v = real(0);
-    if (q < nq) {
-      const int fi = q / 3, jj = q % 3;
-      const real* fp = w.fpos(0, fi);
-      if (r < 3) {
-        v = (r == jj) ? real(1) : real(0);
-      } else if (r < 6) {
-        real d[3];
-        for (int t = 0; t < 3; t++) d[t] = fp[t] - P0[t];
-        v = cross_e(d, jj, r - 3);
-      } else {
-        const int hr = T->hinge_range[r - 6], h = hr & 255, foot = T->footis[fi];
-        if (foot >= h && foot < (hr >> 8)) {  // the foot in motor r - 6's subtree
-          const real* Jh = w.jpos(0, h);
-          const real* Zh = w.jz(0, h);
-          real d[3];
-          for (int t = 0; t < 3; t++) d[t] = Jh[t] - fp[t];
-          for (int t = 0; t < 3; t++) v += Zh[t] * cross_e(d, jj, t);
-        }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      real dd[3];
+      for (int t = 0; t < 3; t++) dd[t] = J[k][t] - fp[t];
+      for (int jj = 0; jj < 3; jj++) {
+        real v = 0;
+        for (int t = 0; t < 3; t++) v += Z[k][t] * cross_e(dd, jj, t);
+        R[k][6 + jj] = v;
       }
-    } else if (r < 3) {
-      v = sv.x[r];
-    } else if (r < 6) {
-      v = sv.x[3 * n + r - 3];
-    } else {
-      const int h = T->hinge_ids[r - 6];
-      const real* Zh = w.jz(0, h);
-      real t = 0;
-      for (int j = 0; j < 3; j++) t += Zh[j] * sv.x[3 * n + 3 * h + j];
-      v = z[r - 6] - t;
+      const int h = p[k], j = T->node[h].hinge;
+      real t0 = 0;
+      for (int t = 0; t < 3; t++) t0 += Z[k][t] * sv.x[3 * n + 3 * h + t];
+      R[k][9] = z[j] - t0;
     }
-    fr.Ct[r * ld + q] = v;
+    real rdM[3];
+    ldl_n<3>(M, real(0), rdM);  // M >= I
+#pragma unroll
+    for (int c = 0; c < 10; c++) {  // Y = L^-1 R
+      R[1][c] -= M[3] * R[0][c];
+      R[2][c] -= M[6] * R[0][c] + M[7] * R[1][c];
+    }
+    auto prod = [&](int a, int b) {  // (L^-1 R)_a^T D^-1 (L^-1 R)_b
+      return R[0][a] * rdM[0] * R[0][b] + R[1][a] * rdM[1] * R[1][b] + R[2][a] * rdM[2] * R[2][b];
+    };
+#pragma unroll
+    for (int e = 0; e < 21; e++) {  // S_l = W_tm M^-1 W_mt (packed lower)
+      const TriWalk<> t(e);
+      fr.a[L][e] = prod(t.r, t.c);
+    }
+#pragma unroll
+    for (int r = 0; r < 6; r++) fr.a[L][21 + r] = prod(r, 9);  // e_l = W_tm M^-1 d_m
+    real d[3];
+    for (int t = 0; t < 3; t++) d[t] = fp[t] - P0[t];
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+#pragma unroll
+      for (int jj = 0; jj < 3; jj++) {
+        const real ct = (r < 3) ? ((r == jj) ? real(1) : real(0)) : cross_e(d, jj, r - 3);
+        Ct[3 * r + jj] = ct - prod(r, 6 + jj);
+      }
+    Bd[0] = prod(6, 6); Bd[1] = prod(7, 6); Bd[2] = prod(7, 7);
+    Bd[3] = prod(8, 6); Bd[4] = prod(8, 7); Bd[5] = prod(8, 8);
+    for (int jj = 0; jj < 3; jj++) rb[jj] = prod(6 + jj, 9);
+    Bl[0] = Bd[0]; Bl[3] = Bd[1]; Bl[4] = Bd[2]; Bl[6] = Bd[3]; Bl[7] = Bd[4]; Bl[8] = Bd[5];
+    okB = ldl_n<3>(Bl, kForcesBlockGuard, rdB);
+    if (okB) {  // K_f = C~ B^-1 C~^T, q_f = C~ B^-1 r_f, through V = L_B^-1 [C~^T | r_f]
+      real V[3][7];
+      for (int c = 0; c < 6; c++)
+        for (int k = 0; k < 3; k++) V[k][c] = Ct[3 * c + k];
+      for (int k = 0; k < 3; k++) V[k][6] = rb[k];
+#pragma unroll
+      for (int c = 0; c < 7; c++) {
+        V[1][c] -= Bl[3] * V[0][c];
+        V[2][c] -= Bl[6] * V[0][c] + Bl[7] * V[1][c];
+      }
+      auto vp = [&](int a, int b) {
+        return V[0][a] * rdB[0] * V[0][b] + V[1][a] * rdB[1] * V[1][b] + V[2][a] * rdB[2] * V[2][b];
+      };
+#pragma unroll
+      for (int e = 0; e < 21; e++) {
+        const TriWalk<> t(e);
+        fr.b[L][e] = vp(t.r, t.c);
+      }
+#pragma unroll
+      for (int r = 0; r < 6; r++) fr.b[L][21 + r] = vp(r, 6);
+    }
   }
+  const bool fast = !dense && half_ballot(lane < nl && !okB) == 0;
   wave_sync();
   STAMP(4);
-  chol_packed(fr.W, m, real(0), lane);  // I + G G^T: eigenvalues >= 1
-  STAMP(5);
-  if (lane < ld) {  // L^-1 [C | d], one column per lane, the column in registers (m <= 6 + HS_KMAX)
-    constexpr int MM = 6 + HS_KMAX;
-    real col[MM];
-#pragma unroll
-    for (int i = 0; i < MM; i++) col[i] = (i < m) ? fr.Ct[i * ld + lane] : real(0);
-#pragma unroll
-    for (int i = 0; i < MM; i++) {
-      if (i < m) {
-        real s = col[i];
-#pragma unroll
-        for (int t = 0; t < i; t++) s -= fr.W[pk(i, t)] * col[t];
-        col[i] = s / fr.W[pk(i, i)];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < MM; i++)
-      if (i < m) fr.Ct[i * ld + lane] = col[i];
+  if (lane < FSUM) {  // sums over the limbs, in limb order; W_tt and the torso part of d added
+    real s = 0;
+    for (int L = 0; L < nl; L++) s += fast ? ((lane < 21) ? fr.b[L][lane] - fr.a[L][lane] : fr.b[L][lane] + fr.a[L][lane])
+                                          : fr.a[L][lane];
+    const real dt = (lane < 21) ? real(0) : (lane < 24 ? sv.x[lane - 21] : sv.x[3 * n + lane - 24]);
+    // fast: K = W_tt - sum S_l + sum K_f, rhs = sum (q_f + e_l) - d_t; else S = W_tt - sum S_l, d~ = d_t - sum e_l
+    const real v = (lane < 21) ? (fast ? wtt_entry(lane, ts, n) + s : wtt_entry(lane, ts, n) - s)
+                               : (fast ? s - dt : dt - s);
+    fr.a[0][lane] = v;  // lane reads column `lane` only, so slot 0 takes the sums in place
   }
   wave_sync();
-  STAMP(6);
+  STAMP(5);
   uint32_t flags = 0;
-  for (int pass = 0; pass < 2; pass++) {  // normal equations; second pass regularized
-    real eps = 0;
-    if (pass == 1) {
-      for (int p = 0; p < nq; p++) {
-        real s = 0;
-        for (int i = 0; i < m; i++) s += fr.Ct[i * ld + p] * fr.Ct[i * ld + p];
-        eps = fmax(eps, s);
-      }
-      eps *= real(1e-12);
+  if (fast) {
+    real K[36], rd[6], lam[6];
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+#pragma unroll
+      for (int c = 0; c < 6; c++) K[6 * r + c] = (c <= r) ? fr.a[0][pk(r, c)] : real(0);
+      lam[r] = fr.a[0][21 + r];
     }
-    for (TriWalk<1> t(lane); t.r < nq; t.next()) {  // lower triangle of row p, then its rhs entry
-      const int p = t.r, q = (t.c == p + 1) ? nq : t.c;
-      real s = 0;
-      for (int i = 0; i < m; i++) s += fr.Ct[i * ld + p] * fr.Ct[i * ld + q];
-      if (q < nq) fr.W[pk(p, q)] = s + ((p == q) ? eps : real(0));
-      else fr.y[p] = s;
+    ldl_n<6>(K, real(0), rd);  // >= I
+    ldl_solve_n<6>(K, rd, lam);
+    if (lane < nl) {  // y_f = B_f^-1 (r_f - C~_f^T lam)
+      real t[3];
+      for (int k = 0; k < 3; k++) {
+        real s = rb[k];
+        for (int r = 0; r < 6; r++) s -= Ct[3 * r + k] * lam[r];
+        t[k] = s;
+      }
+      ldl_solve_n<3>(Bl, rdB, t);
+      for (int k = 0; k < 3; k++) sv.y[3 * f + k] = t[k];
     }
     wave_sync();
-    STAMP(7);
-    if (chol_packed(fr.W, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) break;
+    STAMP(9);
+    return flags;
+  }
+  // dense normal equations over the feet (a B_f near singular): N = diag(B_f) + V^T D_S^-1 V with
+  // S = L_S D_S L_S^T, V = L_S^-1 C~, r = r_b + V^T D_S^-1 L_S^-1 d~
+  real* const base = &fr.a[0][0];
+  real* const Vm = base + FSUM;       // [6][HS_KMAX]
+  real* const vv = Vm + 6 * HS_KMAX;  // 6
+  real* const rdS = vv + 6;           // 6
+  real* const N = rdS + 6;            // packed lower, nq x nq
+  real* const rr = N + HS_KMAX * (HS_KMAX + 1) / 2;
+  {
+    real S[36], rd[6], v6[6];
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+#pragma unroll
+      for (int c = 0; c < 6; c++) S[6 * r + c] = (c <= r) ? base[pk(r, c)] : real(0);
+      v6[r] = base[21 + r];
+    }
+    ldl_n<6>(S, real(0), rd);  // >= I
+    for (int i = 0; i < 6; i++) {
+      real s = v6[i];
+      for (int k = 0; k < i; k++) s -= S[6 * i + k] * v6[k];
+      v6[i] = s;
+    }
+    if (lane < nl) {
+      for (int jj = 0; jj < 3; jj++) {
+        real col[6];
+        for (int i = 0; i < 6; i++) {
+          real s = Ct[3 * i + jj];
+          for (int k = 0; k < i; k++) s -= S[6 * i + k] * col[k];
+          col[i] = s;
+        }
+        for (int i = 0; i < 6; i++) Vm[i * HS_KMAX + 3 * f + jj] = col[i];
+      }
+    }
+    if (lane == 0)
+      for (int i = 0; i < 6; i++) {
+        vv[i] = v6[i];
+        rdS[i] = rd[i];
+      }
+  }
+  wave_sync();
+  real eps = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    for (TriWalk<1> t(lane); t.r < nq; t.next()) {  // V^T D^-1 V and its rhs, entry by entry
+      const int p = t.r, q = (t.c == p + 1) ? nq : t.c;
+      real s = 0;
+      for (int k = 0; k < 6; k++) s += Vm[k * HS_KMAX + p] * rdS[k] * ((q < nq) ? Vm[k * HS_KMAX + q] : vv[k]);
+      if (q < nq) N[pk(p, q)] = s + ((p == q) ? eps : real(0));
+      else rr[p] = s;
+    }
+    wave_sync();
+    if (lane < nl) {  // + the feet's own blocks
+      const int q0 = 3 * f;
+      N[pk(q0, q0)] += Bd[0];
+      N[pk(q0 + 1, q0)] += Bd[1];
+      N[pk(q0 + 1, q0 + 1)] += Bd[2];
+      N[pk(q0 + 2, q0)] += Bd[3];
+      N[pk(q0 + 2, q0 + 1)] += Bd[4];
+      N[pk(q0 + 2, q0 + 2)] += Bd[5];
+      for (int k = 0; k < 3; k++) rr[q0 + k] += rb[k];
+    }
+    wave_sync();
+    if (pass == 0) {
+      for (int p = 0; p < nq; p++) eps = fmax(eps, N[pk(p, p)]);
+      eps *= real(1e-12);
+    }
+    if (chol_packed(N, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) break;
     flags = HS_FLAG_GENERAL;  // least squares not unique
   }
   STAMP(8);
   if (lane == 0) {  // the two triangular solves with y in registers (nq <= HS_KMAX)
     real yv[HS_KMAX];
 #pragma unroll
-    for (int i = 0; i < HS_KMAX; i++) yv[i] = (i < nq) ? fr.y[i] : real(0);
+    for (int i = 0; i < HS_KMAX; i++) yv[i] = (i < nq) ? rr[i] : real(0);
 #pragma unroll
     for (int i = 0; i < HS_KMAX; i++) {
       if (i < nq) {
         real s = yv[i];
 #pragma unroll
-        for (int k = 0; k < i; k++) s -= fr.W[pk(i, k)] * yv[k];
-        yv[i] = s / fr.W[pk(i, i)];
+        for (int k = 0; k < i; k++) s -= N[pk(i, k)] * yv[k];
+        yv[i] = s / N[pk(i, i)];
       }
     }
 #pragma unroll
@@ -2252,13 +2365,13 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
         real s = yv[i];
 #pragma unroll
         for (int k = i + 1; k < HS_KMAX; k++)
-          if (k < nq) s -= fr.W[pk(k, i)] * yv[k];
-        yv[i] = s / fr.W[pk(i, i)];
+          if (k < nq) s -= N[pk(k, i)] * yv[k];
+        yv[i] = s / N[pk(i, i)];
       }
     }
 #pragma unroll
     for (int i = 0; i < HS_KMAX; i++)
-      if (i < nq) fr.y[i] = yv[i];
+      if (i < nq) sv.y[i] = yv[i];
   }
   wave_sync();
   STAMP(9);
@@ -2274,10 +2387,10 @@ __device__ __attribute__((always_inline)) inline void forces_step(const hs_topo*
   STAMP(10);
   const size_t row = (size_t)b * a.horizon + h;
   const real* z = inp(mp.tau_in) + (live ? row : 0) * mp.st_tau;
-  uint32_t flags = forces_solve(T, sv, fr, w, z, lane);
-  if (half_ballot(lane < nq && fr.y[lane] != fr.y[lane])) flags |= HS_FLAG_NAN;
+  uint32_t flags = forces_solve(T, sv, fr, w, z, a.solve_mode == HS_SOLVE_REFERENCE, lane);
+  if (half_ballot(lane < nq && sv.y[lane] != sv.y[lane])) flags |= HS_FLAG_NAN;
   if (half_ballot(lane < nl && w.unreach(0, lane))) flags |= HS_FLAG_UNREACH;
-  if (live && a.cf && lane < mp.st_cf) outp(a.cf)[row * mp.st_cf + lane] = (lane < nq) ? fr.y[lane] : real(0);
+  if (live && a.cf && lane < mp.st_cf) outp(a.cf)[row * mp.st_cf + lane] = (lane < nq) ? sv.y[lane] : real(0);
   if (live && a.q && lane < mp.st_q) outp(a.q)[row * mp.st_q + lane] = (lane < cfg) ? w.q(0)[lane] : real(0);
   if (live && a.flags && lane == 0) a.flags[row] = flags;
   STAMP(11);

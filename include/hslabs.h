@@ -166,7 +166,9 @@ typedef struct {
                              path only where the minimizer is not unique; HS_SOLVE_REFERENCE (1):
                              every step through the Eigen-style FullPivLU / ColPivHouseholderQR
                              adaptive-rank loop of ftsolver.cpp:185-236 (same results where the
-                             minimizer is unique; much slower; flags carry HS_FLAG_GENERAL) */
+                             minimizer is unique; much slower; flags carry HS_FLAG_GENERAL). In
+                             hs_run_forces[_calls]: every step through the dense normal equations
+                             over the feet instead of the 6 x 6 system (same results) */
   int32_t key_steps;      /* control steps whose work the best key covers (0: the steps of this
                              call, i.e. H for hs_run, n_calls * H for hs_run_steps / hs_run_calls);
                              callers that accumulate work over several calls pass the total */
