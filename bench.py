@@ -404,6 +404,9 @@ def main_forces(args, torch, dist, world, rank, dev):
         step_bytes = 8 * (nmj + 3 * nf) + PARAM_BYTES  # torques in, forces of all feet out, the gait record
         alg_bytes = B * step_bytes
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        lib = dict(capi.LOADED)
+        pmc, pmc_note = pmc_for(f"forces {args.model} B={B}", lib["sha256"], "pmc_traffic_forces.json")
+        traffic = None if pmc is None else int(round(pmc["hbm_bytes_per_step"] * B / pmc["rollouts"]))
         out = {
             "metric": FORCES_METRIC, "value": round(lay["total"] * K / elapsed, 1), "unit": "steps/s",
             "n_gpus": world, "steps": K, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / K, 4),
@@ -413,10 +416,13 @@ def main_forces(args, torch, dist, world, rank, dev):
                                    f"n_t={n_t} fp64 (SURVEY.md 8f row 1)", "rollouts_per_gpu": B,
                        "parallelism": f"rollout-sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "hs_rollout_kernel<NM, true, 0>",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_over_algorithmic": None if traffic is None else round(traffic / alg_bytes, 3),
+                         "traffic_note": pmc_note, "kernel": "hs_rollout_kernel<NM, true, 0>",
                          "kernel_ms": round(kern_ms, 5), "alg_bytes_per_launch": alg_bytes,
                          "alg_bytes_per_step": step_bytes},
             "check": {"max_rel_cf_vs_control_loop": err, "general_steps": general},
+            "lib": lib,
         }
         out["cpu_baseline"] = None if (args.no_cpu or world > 1) else forces_cpu_baseline(
             args.model, params[:64], ctl.tau[:64, :K].cpu().numpy(), n_t, min(args.cpu_seconds, 5.0))
@@ -438,11 +444,11 @@ def _profile_json(name):
         return None
 
 
-def pmc_for(traffic_key, lib_sha):
+def pmc_for(traffic_key, lib_sha, name="pmc_traffic.json"):
     """HBM bytes and issued FP64 lane ops per step of the batch from the committed PMC summary
     (tools/gpu_pmc.sh + tools/pmc_summary.py), only when it was taken on the library this process
     loaded (same sha256 prefix); else None and the reason."""
-    j = _profile_json("pmc_traffic.json")
+    j = _profile_json(name)
     if not j or j.get("workload") != traffic_key:
         return None, "no PMC summary for this workload"
     if j.get("lib_sha256") != lib_sha:

@@ -13,9 +13,10 @@ sys.path.insert(0, ROOT)
 from hslabs_amd import build as B  # noqa: E402
 
 LIB = os.path.join(B.OUT_DIR, "libhslabs_stamps.so")
-PHASES = [("kinematics", 1, 2), ("dynamics+particular", 2, 10), ("I+GG^T", 10, 3), ("[C|d]", 3, 4),
-          ("chol m", 4, 5), ("L^-1[C|d]", 5, 6), ("normal eq", 6, 7), ("chol nq", 7, 8), ("tri solves", 8, 9),
-          ("outputs", 9, 11), ("TOTAL", 1, 11)]
+# forces_solve's stamps: 10 after the particular solution, 4 after the limb blocks, 5 after the sums over
+# limbs, 9 after the 6 x 6 system and the feet's solves (or the dense route), 11 after the outputs
+PHASES = [("kinematics", 1, 2), ("dynamics+particular", 2, 10), ("limb blocks", 10, 4), ("sums over limbs", 4, 5),
+          ("6x6 + feet", 5, 9), ("outputs", 9, 11), ("TOTAL", 1, 11)]
 
 
 def main():

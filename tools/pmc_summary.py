@@ -19,14 +19,15 @@ from collections import defaultdict
 
 KERNEL = "hs_rollout_kernel"
 STEP_LAUNCH = re.compile(r"hs_rollout_kernel<\d+, false, 1>")  # the fused step launch (hs::FIX_DEFER)
+FORCES_LAUNCH = re.compile(r"hs_rollout_kernel<\d+, true, 0>")  # solve_forces' step launches (--forces)
 
 
-def collect(root, n_waves):
+def collect(root, n_waves, step_launch=STEP_LAUNCH):
     vals = defaultdict(dict)  # counter -> dispatch -> per-step value
     for path in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if not STEP_LAUNCH.search(row["Kernel_Name"]):
+                if not step_launch.search(row["Kernel_Name"]):
                     continue  # the setup pass and the fixup / reduce launch are separate kernels
                 grid = int(row.get("Grid_Size") or row.get("Grid_Size_X"))
                 steps = grid // 64 // n_waves
@@ -54,9 +55,10 @@ def main():
     ap.add_argument("--rollouts", type=int, required=True)
     ap.add_argument("--traffic-json")
     ap.add_argument("--cmd", default="bench.py --steps 20 --warmup 5 --no-cpu")
+    ap.add_argument("--forces", action="store_true", help="solve_forces' step launches (bench.py --forces)")
     a = ap.parse_args()
     n_waves = (a.rollouts + 1) // 2
-    v = collect(a.root, n_waves)
+    v = collect(a.root, n_waves, FORCES_LAUNCH if a.forces else STEP_LAUNCH)
     med = {c: statistics.median(x) for c, x in v.items()}
     sha = lib_of(a.root)
     lines = [f"{KERNEL}, {a.workload} ({a.cmd}), rocprofv3 --pmc, one group per pass, library {sha}",
