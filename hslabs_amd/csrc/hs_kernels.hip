@@ -1276,6 +1276,29 @@ __device__ inline float group8_sum(float v) {
   return v;
 }
 
+#ifndef HS_BLOCK_QUAD
+#define HS_BLOCK_QUAD 0
+#endif
+// sum over the 4-lane quad (DPP quad_perm xor 1, xor 2): every lane of the quad gets the same value
+// (each addition is commutative in its two operands)
+__device__ inline real quad_sum(real v) {
+#if HS_REAL_IS_FLOAT
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  return v;
+#else
+  auto dpp_d = [](double x, auto ctrl) {
+    const long long u = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_mov_dpp((int)u, decltype(ctrl)::value, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), decltype(ctrl)::value, 0xF, 0xF, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+  };
+  v += dpp_d(v, std::integral_constant<int, 0xB1>{});
+  v += dpp_d(v, std::integral_constant<int, 0x4E>{});
+  return v;
+#endif
+}
+
 template <class W, class SV>
 __device__ inline bool zeroth_well_posed(const real* P0, const W& w, const SV& sv, int nc, int lane) {
   float d0 = 0.f, d1 = 0.f, d2 = 0.f;
@@ -1343,6 +1366,23 @@ __device__ inline void chol_solve_n(const real* L, const real* rl, real* b) {
 // LDL^T of an N x N SPD matrix in place (row-major; lower part: unit-lower L, diagonal: d), no
 // square roots: pivot d_j = a_jj - sum_k L_jk (L_jk d_k), the Cholesky pivot in exact arithmetic, so
 // the guard (d_j > guard * max diagonal) decides like chol_n's. rd: 1 / d_j. False: a pivot under it.
+#ifndef HS_FAST_RCP
+#define HS_FAST_RCP 0
+#endif
+// 1 / x for a positive normal pivot: v_rcp_f64 refined by two Newton steps (within an ulp of the
+// correctly rounded quotient), five instructions instead of the IEEE division's scale / fixup sequence
+__device__ inline real pivot_rcp(real x) {
+#if HS_FAST_RCP && !HS_REAL_IS_FLOAT
+  real r = __builtin_amdgcn_rcp(x);
+  real e = fma(-x, r, real(1));
+  r = fma(r, e, r);
+  e = fma(-x, r, real(1));
+  return fma(r, e, r);
+#else
+  return real(1) / x;
+#endif
+}
+
 template <int N>
 __device__ inline bool ldl_n(real* a, real guard, real* rd) {
   real mx = 0;
@@ -1357,7 +1397,7 @@ __device__ inline bool ldl_n(real* a, real guard, real* rd) {
 #pragma unroll
     for (int k = 0; k < j; k++) dj -= a[j * N + k] * v[k];
     if (!(dj > guard * mx)) return false;
-    const real r = real(1) / dj;
+    const real r = pivot_rcp(dj);
     a[j * N + j] = dj;
     rd[j] = r;
 #pragma unroll
@@ -1621,6 +1661,104 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
 #else
   const int coll = 0;
 #endif
+#if HS_BLOCK_QUAD
+  // four lanes per contact (lane = 4 c + s): lane s sums the D_c / g_c terms of the foot chain's
+  // joints s, s + 4, the quad adds them (DPP), every lane of the quad factorizes D_c, and the Schur
+  // block's rows are split {s, 5 - s} (seven packed entries and two of h per lane; lane 3 repeats
+  // lane 2's rows and stores D_c, g_c, d0_c and D_c^-1 instead) -- one instruction stream, the lanes
+  // differing only in data
+  {
+    const int c = lane >> 2, s4 = lane & 3;
+    if (c < nc) {
+      const int fi = sv.cfoot[c];
+      const real* fp = w.fpos(0, fi);
+      real d0[3];
+      for (int r = 0; r < 3; r++) d0[r] = P0[r] - fp[r];
+      real Dp[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};  // packed lower 00 10 11 20 21 22
+      const int nch = T->foot_chain_len[fi];
+      for (int m = s4; m < nch; m += 4) {
+        const int p = T->foot_chain[fi][m];
+        const real* Jp = w.jpos(0, p);
+        const real* Jz = w.jz(0, p);
+        real da[3], va[3][3];
+        for (int r = 0; r < 3; r++) da[r] = Jp[r] - fp[r];
+        cross_rows(da, va);
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+          const real w2 = Jz[r] * Jz[r];
+#pragma unroll
+          for (int i = 0; i < 3; i++) {
+            if (i == r) continue;
+#pragma unroll
+            for (int j = 0; j <= i; j++)
+              if (j != r) Dp[i * (i + 1) / 2 + j] += w2 * va[r][i] * va[r][j];
+            g[i] += w2 * va[r][i] * sv.x[3 * n + 3 * p + r];
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 6; e++) Dp[e] = quad_sum(Dp[e]);
+#pragma unroll
+      for (int i = 0; i < 3; i++) g[i] = quad_sum(g[i]);
+      const real D[9] = {Dp[0], Dp[1], Dp[3], Dp[1], Dp[2], Dp[4], Dp[3], Dp[4], Dp[5]};
+      if (s4 == 3) {
+        for (int r = 0; r < 3; r++) fl.d0[c][r] = d0[r];
+        for (int i = 0; i < 9; i++) fl.D[c][i] = D[i];
+        for (int i = 0; i < 3; i++) fl.g[c][i] = g[i];
+      }
+      int ok = 1;
+      if (nc >= 3) {
+        real L[9];
+        for (int i = 0; i < 9; i++) L[i] = D[i];
+        real rl[3];
+        ok = ldl_n<3>(L, kFastPivotGuard, rl);
+        if (ok) {
+          real Dinv[9];
+          for (int j = 0; j < 3; j++) {
+            real e[3] = {0, 0, 0};
+            e[j] = 1;
+            ldl_solve_n<3>(L, rl, e);
+            for (int i = 0; i < 3; i++) Dinv[3 * i + j] = e[i];
+          }
+          if (s4 == 3)
+            for (int i = 0; i < 9; i++) fl.sc.Dinv[c][i] = Dinv[i];
+          const int sr = s4 < 3 ? s4 : 2, r0 = sr, r1 = 5 - sr;
+          real E0[3], E1[3];  // rows r0, r1 of E = A_c D_c^-1
+#pragma unroll
+          for (int j = 0; j < 3; j++) {
+            real a = 0, b = 0;
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+              a += a_entry(d0, r0, i) * Dinv[3 * i + j];
+              b += a_entry(d0, r1, i) * Dinv[3 * i + j];
+            }
+            E0[j] = a;
+            E1[j] = b;
+          }
+#pragma unroll
+          for (int t = 0; t < 7; t++) {  // row r0's r0 + 1 entries, then row r1's
+            const bool first = t <= r0;
+            const int r = first ? r0 : r1, q = first ? t : t - r0 - 1;
+            real v = 0;
+#pragma unroll
+            for (int j = 0; j < 3; j++) v += (first ? E0[j] : E1[j]) * a_entry(d0, q, j);
+            if (s4 < 3) fl.sc.S[c][sch_lower(r, q)] = v;
+          }
+          real h0 = 0, h1 = 0;
+          for (int j = 0; j < 3; j++) {
+            h0 += E0[j] * g[j];
+            h1 += E1[j] * g[j];
+          }
+          if (s4 < 3) {
+            fl.sc.S[c][SCH_H + r0] = h0;
+            fl.sc.S[c][SCH_H + r1] = h1;
+          }
+        }
+      }
+      if (s4 == 0) fl.ok[c] = ok | coll;
+    }
+  }
+#else
   if (lane < nc) {  // A_c, D_c, g_c for contact c = lane
     const int c = lane, fi = sv.cfoot[c];
     const real* fp = w.fpos(0, fi);
@@ -1717,6 +1855,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
     }
     fl.ok[c] = ok | coll;
   }
+#endif
   wave_sync();
   STAMP(18);
   const real a[6] = {sv.x[0], sv.x[1], sv.x[2], sv.x[3 * n], sv.x[3 * n + 1], sv.x[3 * n + 2]};

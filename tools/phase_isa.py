@@ -29,6 +29,10 @@ CLASSES = [
     ("branch", r"^s_(cbranch|branch)"),
     ("sgpr_spill", r"^v_(readlane|writelane)_b32"),
     ("vgpr_spill", r"^scratch_"),
+    ("cndmask", r"^v_cndmask"),
+    ("mov", r"^v_mov_b(32|64)"),
+    ("div_f64", r"^v_div_fixup_f64"),
+    ("sqrt_f64", r"^v_rsq_f64"),
 ]
 
 
