@@ -214,7 +214,9 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   void *gen = nullptr, *work = nullptr, *fix = nullptr;
   {
     std::lock_guard<std::mutex> lk(mu);
-    hipError_t e = (hipError_t)gen_pool.get(a.stream, (size_t)CHUNK * (B + 1), &gen);
+    // the general-path scratch of every step in flight: [CHUNK][B + 1] SolveWS (in workspace units)
+    hipError_t e = (hipError_t)gen_pool.get(
+        a.stream, ((size_t)CHUNK * (B + 1) * hs::solve_workspace_bytes() + gwb - 1) / gwb, &gen);
     // the [step][rollout] work buffer is reserved for at least HS_FUSED_RESERVE_STEPS steps (at most
     // 512 MB) on first use, so a caller growing its call length (a short warmup, then the real run)
     // does not hit a hipMalloc between its launches
@@ -240,6 +242,7 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   mp.setup_io = hs::SETUP_STORE;
   mp.fix_count = fix_counts;
   mp.fix_n_counts = n_chunks;
+  mp.ktab_n = hs::ktab_samples(a.n_t, a.horizon, S);  // the straight gaits' IK table, built by the setup pass
   int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   mp.setup_only = 0;
   mp.setup_io = hs::SETUP_LOAD;
@@ -515,6 +518,7 @@ int hs_run_forces_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls, con
   mp.fused_h = a->horizon;
   mp.setup_only = 1;
   mp.setup_io = hs::SETUP_STORE;
+  mp.ktab_n = hs::ktab_samples(a->n_t, a->horizon, S);
   int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   mp.setup_only = 0;
   mp.setup_io = hs::SETUP_LOAD;

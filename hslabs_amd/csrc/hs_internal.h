@@ -65,12 +65,20 @@ struct launch_map {
   double red_total_mass;
   const double* red_rollout_mass;
   uint64_t* red_best_key;
+  // fused calls of straight gaits: > 0 = the setup pass also tabulates the limb IK of samples
+  // [0, ktab_n) per rollout (ktab_samples), and the step launches read it instead of solving it
+  int32_t ktab_n;
 };
 
 // Kernel launcher (hs_kernels.hip). `workspace` holds general_workspace_bytes()
 // per rollout + 1 (global-memory scratch of the conditioning fallback; the
 // extra slot serves idle half-waves). Returns a hipError_t value.
 size_t general_workspace_bytes();
+// one fused step's general-path scratch per rollout (fused_gen holds [steps in a launch][B + 1] of them)
+size_t solve_workspace_bytes();
+// samples the IK table of a fused call covers (0: none): n_t + horizon + 3 when that fits and the
+// call's steps would evaluate more samples than the table does
+int32_t ktab_samples(int32_t n_t, int32_t horizon, int64_t steps);
 int launch_rollouts(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
 // single precision build of the same kernels (hs_kernels_f32.hip): outputs are float
 size_t general_workspace_bytes_f32();

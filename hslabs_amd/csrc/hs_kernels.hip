@@ -156,6 +156,28 @@ struct SetupL {
   SC3 tsc;  // sin / cos of the configured torso angles (every sample of a straight gait)
 };
 
+// Straight, untransformed gaits (curvature 0, no record transform): the torso keeps its configured
+// angles and moves by tv = t v along x (pergen.cpp:386-397 without the turn), and every body above
+// the limbs is jointless (the loader's topology check), so the torso frame, the chain's body frames
+// and each limb's hip joint frame (poslimb, lik.cpp:341-347) are a constant rotation with a
+// translation affine in tv: A(t) = [R | c + tv u], u = column 0 of the torso's J_A_parent. The gait
+// setup keeps them at tv = 0 (the products kin_sample forms, once per rollout instead of per sample).
+// IK table entry (RolloutWS::ktab): the joint values of a limb at a sample, their sines and cosines,
+// then 1 if unreachable or failed
+#ifndef HS_KT_SINCOS
+#define HS_KT_SINCOS 0  // the table also holds sin / cos of the joint values (measured slower: the
+                        // table kernel's cost outweighs the step's three sincos per lane)
+#endif
+constexpr int KT_W = HS_KT_SINCOS ? 10 : 4;
+#ifndef HS_KTAB_WAVES
+#define HS_KTAB_WAVES 1
+#endif
+struct KinFrames {
+  real A0[12];              // the torso (node 0)
+  real J0[HS_LMAX][12];     // each limb's hip joint frame
+  real Ab[HS_NMAX][12];     // body nodes of the limb chains, by node id (written by the owner limb)
+};
+
 template <int NM>
 struct SolveL {
   union {  // particular() overwrites each part's f with its x in place
@@ -282,10 +304,29 @@ __device__ inline void transform_rec(const hs_gait_params& p, real* o0, real* o1
   target[0] = t[0]; target[1] = t[1]; target[2] = t[2];
 }
 
+// the straight gait's frame at tv = t v: [R | c + tv u] (KinFrames)
+__device__ inline A34 frame_at(A34 A, const real* u, real tv) {
+#pragma unroll
+  for (int r = 0; r < 3; r++) A.at(r, 3) = fma(tv, u[r], A(r, 3));
+  return A;
+}
+__device__ inline A34 load34r(const real* m) {
+  A34 a;
+#pragma unroll
+  for (int i = 0; i < 12; i++) a.m[i] = m[i];
+  return a;
+}
+__device__ inline void store34r(const A34& a, real* m) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) m[i] = a.m[i];
+}
+
 // ---------------------------------------------------------------------------
 // S: gait setup, lanes L < n_limbs (pergen.cpp:453-507, 30-51, 143-153)
 // ---------------------------------------------------------------------------
-__device__ __attribute__((always_inline)) inline void gait_setup(const hs_topo* T, const GaitR& g, int n_t, SetupL& st, int lane) {
+// kf (optional): also store the straight gait's frames (KinFrames; the products straight_frames0 forms)
+__device__ __attribute__((always_inline)) inline void gait_setup(const hs_topo* T, const GaitR& g, int n_t, SetupL& st, int lane,
+                                                                 KinFrames* kf = nullptr) {
   const int nl = T->n_limbs;
   if (lane < nl) {
     const int L = lane;
@@ -295,9 +336,18 @@ __device__ __attribute__((always_inline)) inline void gait_setup(const hs_topo* 
     if (L == 0) st.tsc = tsc;
     A34 A0 = mul(mul(node_joint_parent(T, 0), free_joint_sc(q6, tsc)), node_pj(T, 0));  // orient_torso
     A34 A = A0;
-    for (int k = 1; k < T->limb_chain_len[L]; k++) A = mul(A, node_pj(T, T->limb_chain[L][k]));
+    for (int k = 1; k < T->limb_chain_len[L]; k++) {
+      const int v = T->limb_chain[L][k];
+      A = mul(A, node_pj(T, v));
+      if (kf && T->node[v].owner_limb == L) store34r(A, kf->Ab[v]);
+    }
     int c = T->limb_child[L];
-    A34 Ac = mul(mul(mul(A, node_joint_parent(T, c)), hinge_joint(real(0))), node_pj(T, c));
+    const A34 J0 = mul(A, node_joint_parent(T, c));  // the hip joint frame (poslimb)
+    if (kf) {
+      store34r(J0, kf->J0[L]);
+      if (L == 0) store34r(A0, kf->A0);
+    }
+    A34 Ac = mul(mul(J0, hinge_joint(real(0))), node_pj(T, c));
     real pos[3] = {Ac(0, 3), Ac(1, 3), Ac(2, 3)};  // get_limb_hip_pos
     if (g.foot_shift_type == 0) {                   // setup_foot_shift / shift_pos0
       real sh[3] = {real(0), g.foot_shift, real(0)}, ls[3];
@@ -498,6 +548,24 @@ __device__ inline real sample_time(const SetupL& st, const real* t_tab, int isam
   return t;
 }
 
+// limb FK with the new joint values (compute_dynrecs' recompute_modelnodes) from the hip joint frame
+// J; nk: the limb_child's node
+// (sq, cq: sin and cos of the joint values ja)
+template <class W>
+__device__ __attribute__((always_inline)) inline void limb_fk(const hs_topo* T, const int* lv, NodeK nk, const A34& J,
+                                                              const real* ja, const real* sq, const real* cq, bool wq,
+                                                              const W& w, int k) {
+  A34 A;
+#pragma unroll
+  for (int kk = 0; kk < 3; kk++) {  // limb_child, its first kid, that one's first kid
+    if (kk > 0) nk = load_nodek(T, lv[kk]);
+    A34 Jv = (kk == 0) ? J : mul(A, nk.Jp);
+    A = mul(mul_hinge(Jv, cq[kk], sq[kk]), nk.pj);
+    if (wq) w.q(k)[6 + nk.hinge] = ja[kk];
+    node_features(T, lv[kk], nk, A, &Jv, w, k);
+  }
+}
+
 template <bool STRAIGHT, class W>
 __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* T, const GaitR& g, const hs_gait_params& gp,
                                                                  const SetupL& st, int isample, int L, bool ignore_reach,
@@ -539,17 +607,111 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
   limb_ik(T->lik_kind, ls, ysign, pl, ja, ignore_reach, unreach, fail);
   if (w.want_centre(k)) w.unreach(k, L) = (unreach || fail) ? 1 : 0;
   STAMP(22);
-  // limb FK with the new joint values (compute_dynrecs' recompute_modelnodes)
+  real sq[3], cq[3];
 #pragma unroll
-  for (int kk = 0; kk < 3; kk++) {  // limb_child, its first kid, that one's first kid
-    if (kk > 0) nk = load_nodek(T, lv[kk]);
-    A34 Jv = (kk == 0) ? J : mul(A, nk.Jp);
-    real sq, cq;
-    sincos(ja[kk], &sq, &cq);
-    A = mul(mul_hinge(Jv, cq, sq), nk.pj);
-    if (wq) w.q(k)[6 + nk.hinge] = ja[kk];
-    node_features(T, lv[kk], nk, A, &Jv, w, k);
+  for (int kk = 0; kk < 3; kk++) sincos(ja[kk], &sq[kk], &cq[kk]);
+  limb_fk(T, lv, nk, J, ja, sq, cq, wq, w, k);
+}
+
+// A straight gait's frames at tv = 0 (KinFrames), the products of kin_sample with the torso at its
+// configured pose: torso A0 (orient_torso), the chain's body frames (body(v, A) for those limb L
+// owns) and the hip joint frame J0 of limb L
+template <class BODY>
+__device__ __attribute__((always_inline)) inline void straight_frames0(const hs_topo* T, const GaitR& g, const SC3& tsc,
+                                                                       int L, A34& A0, A34& J0, BODY&& body) {
+  const real q6[6] = {g.torso_pos[0], g.torso_pos[1], g.torso_pos[2], g.torso_angles[0], g.torso_angles[1],
+                      g.torso_angles[2]};
+  A0 = mul(mul(node_joint_parent(T, 0), free_joint_sc(q6, tsc)), node_pj(T, 0));
+  A34 A = A0;
+  const int clen = T->limb_chain_len[L];
+  for (int kk = 1; kk < clen; kk++) {
+    const int v = T->limb_chain[L][kk];
+    A = mul(A, node_pj(T, v));
+    if (T->node[v].owner_limb == L) body(v, A);
   }
+  J0 = mul(A, node_joint_parent(T, T->limb_node[L][0]));
+}
+
+// set_rec's foot target of limb L at time t and the limb IK from the hip frame J (kin_sample's
+// sequence from the gait record on); bad = unreachable (ignore_reach) or failed
+__device__ __attribute__((always_inline)) inline void straight_ik(const hs_topo* T, const GaitR& g,
+                                                                  const hs_gait_params& gp, const SetupL& st, real t,
+                                                                  int L, const A34& J, bool ignore_reach, real* ja,
+                                                                  bool& bad) {
+  real o0[3], o1[3], target[3];
+  bool turned;
+  gait_record<true>(g, gp, st, t, T->limb_pergen[L], o0, o1, turned, target);
+  const A34 Jinv = invert(J);
+  real pl[3];
+  mulp(Jinv, target, pl);
+  bool unreach = false, fail = false;
+  const real ls[3] = {(real)T->ls[0], (real)T->ls[1], (real)T->ls[2]};
+  limb_ik(T->lik_kind, ls, T->limb_ysign[L], pl, ja, ignore_reach, unreach, fail);
+  bad = unreach || fail;
+}
+
+// kin_sample for a straight, untransformed gait: the frames from kf (null: formed here), the joint
+// values and their sines and cosines from the IK table kt (null: solved here). The same products,
+// IK and sincos either way, so every path gives the same bits.
+template <class W>
+__device__ __attribute__((always_inline)) inline void kin_sample_straight(
+    const hs_topo* T, const GaitR& g, const hs_gait_params& gp, const SetupL& st, int isample, int L,
+    bool ignore_reach, const W& w, int k, const real* t_tab, const KinFrames* kf, const real* kt) {
+  const int lv[3] = {T->limb_node[L][0], T->limb_node[L][1], T->limb_node[L][2]};
+  const real t = sample_time(st, t_tab, isample);
+  const real tv = t * st.v;  // gait_record's torso advance
+  const bool wq = w.want_q(k);
+  const NodeK n0 = load_nodek(T, 0);
+  const real u[3] = {n0.Jp(0, 0), n0.Jp(1, 0), n0.Jp(2, 0)};
+  A34 A0, J;
+  if (kf) {
+    if (L == 0) A0 = load34r(kf->A0);
+    const int clen = T->limb_chain_len[L];
+    for (int kk = 1; kk < clen; kk++) {
+      const int v = T->limb_chain[L][kk];
+      const NodeK nc = load_nodek(T, v);
+      if (nc.owner == L) node_features(T, v, nc, frame_at(load34r(kf->Ab[v]), u, tv), nullptr, w, k);
+    }
+    J = load34r(kf->J0[L]);
+  } else {
+    straight_frames0(T, g, st.tsc, L, A0, J, [&](int v, const A34& Ab) {
+      node_features(T, v, load_nodek(T, v), frame_at(Ab, u, tv), nullptr, w, k);
+    });
+  }
+  if (L == 0) {
+    if (wq) {
+      real* q = w.q(k);
+      q[0] = g.torso_pos[0] + tv;
+      q[1] = g.torso_pos[1];
+      q[2] = g.torso_pos[2];
+      for (int i = 0; i < 3; i++) q[3 + i] = g.torso_angles[i];
+    }
+    node_features(T, 0, n0, frame_at(A0, u, tv), &n0.Jp, w, k);  // torso joint frame J = I * J_A_parent
+  }
+  J = frame_at(J, u, tv);
+  real ja[3], sq[3], cq[3];
+  bool bad;
+  if (kt) {
+    const real* e = kt + ((size_t)isample * HS_LMAX + L) * KT_W;
+#pragma unroll
+    for (int kk = 0; kk < 3; kk++) {
+      ja[kk] = e[kk];
+#if HS_KT_SINCOS
+      sq[kk] = e[3 + kk];
+      cq[kk] = e[6 + kk];
+#else
+      sincos(ja[kk], &sq[kk], &cq[kk]);
+#endif
+    }
+    bad = e[KT_W - 1] != 0;
+  } else {
+    straight_ik(T, g, gp, st, t, L, J, ignore_reach, ja, bad);
+#pragma unroll
+    for (int kk = 0; kk < 3; kk++) sincos(ja[kk], &sq[kk], &cq[kk]);
+  }
+  if (w.want_centre(k)) w.unreach(k, L) = bad ? 1 : 0;
+  NodeK nk = load_nodek(T, lv[0]);
+  limb_fk(T, lv, nk, J, ja, sq, cq, wq, w, k);
 }
 
 // ---------------------------------------------------------------------------
@@ -1277,7 +1439,7 @@ __device__ inline float group8_sum(float v) {
 }
 
 #ifndef HS_BLOCK_QUAD
-#define HS_BLOCK_QUAD 0
+#define HS_BLOCK_QUAD 1
 #endif
 // sum over the 4-lane quad (DPP quad_perm xor 1, xor 2): every lane of the quad gets the same value
 // (each addition is commutative in its two operands)
@@ -1367,7 +1529,7 @@ __device__ inline void chol_solve_n(const real* L, const real* rl, real* b) {
 // square roots: pivot d_j = a_jj - sum_k L_jk (L_jk d_k), the Cholesky pivot in exact arithmetic, so
 // the guard (d_j > guard * max diagonal) decides like chol_n's. rd: 1 / d_j. False: a pivot under it.
 #ifndef HS_FAST_RCP
-#define HS_FAST_RCP 0
+#define HS_FAST_RCP 1
 #endif
 // 1 / x for a positive normal pivot: v_rcp_f64 refined by two Newton steps (within an ulp of the
 // correctly rounded quotient), five instructions instead of the IEEE division's scale / fixup sequence
@@ -2537,10 +2699,16 @@ __device__ __attribute__((always_inline)) inline void forces_step(const hs_topo*
 
 // Global per-rollout workspace: the general path's scratch and the gait-setup cache that
 // carries SetupL from the first launch of a call to the later ones (hs::SETUP_*).
+#ifndef HS_KTAB
+#define HS_KTAB 64  // samples the IK table can hold: n_t + horizon + 3 of a fused call
+#endif
 struct RolloutWS {
   SolveWS sol;
   SetupL st;
   real t_tab[HS_TTAB];  // sample times (sample_time), with the setup cache
+  KinFrames kf;         // a straight gait's frames (with the setup cache)
+  real ktab[HS_KTAB][HS_LMAX][KT_W];  // fused calls of straight gaits: limb L at sample i (straight_ik,
+                                      // hs_ktab_kernel)
 };
 static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 
@@ -2576,7 +2744,8 @@ __global__ __launch_bounds__(WAVE * HS_SETUP_WAVES) void hs_setup_kernel(const h
   }
   if (!wave_live) live = false;
   const GaitR g = load_gait(a.params[b]);
-  gait_setup(T, g, a.n_t, sst[sub], lane);  // every lane of the wave takes part (wave_sync inside)
+  // every lane of the wave takes part (wave_sync inside); the frames too
+  gait_setup(T, g, a.n_t, sst[sub], lane, live ? &rws[b].kf : nullptr);
   if (live) {
     constexpr int NW = sizeof(SetupL) / sizeof(real);
     real* cache = reinterpret_cast<real*>(&rws[b].st);
@@ -2584,6 +2753,47 @@ __global__ __launch_bounds__(WAVE * HS_SETUP_WAVES) void hs_setup_kernel(const h
     for (int e = lane; e < NW; e += HALF) cache[e] = lds[e];
     for (int j = lane; j < HS_TTAB; j += HALF) rws[b].t_tab[j] = sample_time(sst[sub], nullptr, j);
   }
+}
+
+// The IK table of a fused call (hs::ktab_samples): one lane per (rollout slot, sample, limb), the
+// straight_ik of kin_sample_straight at sample s from the frames the setup pass stored
+__global__ __launch_bounds__(WAVE, HS_KTAB_WAVES) void hs_ktab_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
+                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
+  const int nt = mp.ktab_n;
+  const int64_t item = (int64_t)blockIdx.x * WAVE + threadIdx.x;  // ((2 wavefront + half) nt + sample) LMAX + limb
+  const int L = (int)(item % HS_LMAX);
+  const int64_t r = item / HS_LMAX;
+  const int s = (int)(r % nt);
+  const int64_t slot = r / nt;
+  if (slot >= 2 * (int64_t)mp.n_waves) return;
+  const int wid = (int)(slot >> 1), sub = (int)(slot & 1);
+  const int b = mp.wave_rollouts ? mp.wave_rollouts[2 * wid + sub] : 2 * wid + sub;
+  if (b < 0 || b >= a.n_rollouts) return;
+  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
+  if (L >= T->n_limbs) return;
+  const GaitR g = load_gait(a.params[b]);
+  if (g.curvature != 0 || g.rec_xf) return;  // kin_sample's turning / record-transform path
+  const RolloutWS& w = rws[b];
+  const real t = sample_time(w.st, w.t_tab, s);
+  const real tv = t * w.st.v;
+  const hs_aff34& Jp0 = T->node[0].J_A_parent;
+  const real u[3] = {(real)Jp0.m[0], (real)Jp0.m[1], (real)Jp0.m[2]};
+  const A34 J = frame_at(load34r(w.kf.J0[L]), u, tv);
+  real ja[3];
+  bool bad;
+  straight_ik(T, g, a.params[b], w.st, t, L, J, a.ignore_reach != 0, ja, bad);
+  real* e = rws[b].ktab[s][L];
+#pragma unroll
+  for (int kk = 0; kk < 3; kk++) {
+    e[kk] = ja[kk];
+#if HS_KT_SINCOS
+    real sq, cq;
+    sincos(ja[kk], &sq, &cq);
+    e[3 + kk] = sq;
+    e[6 + kk] = cq;
+#endif
+  }
+  e[KT_W - 1] = bad ? real(1) : real(0);
 }
 
 // One wavefront's step: fused step fstep (0 outside fused launches) of batch wavefront wid. only_sub
@@ -2616,9 +2826,8 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
     bb = live ? b : bb;
     live = false;
   }
-  SolveWS* G = mp.fused_gen
-                   ? &((RolloutWS*)mp.fused_gen)[(size_t)fstep * (a.n_rollouts + 1) + (live ? b : a.n_rollouts)].sol
-                   : &rws[live ? b : a.n_rollouts].sol;
+  SolveWS* G = mp.fused_gen ? &((SolveWS*)mp.fused_gen)[(size_t)fstep * (a.n_rollouts + 1) + (live ? b : a.n_rollouts)]
+                            : &rws[live ? b : a.n_rollouts].sol;
   Smem<NM, FORCES>& sm = smem[sub];
   real work = (live && a.accumulate && a.work_cot && !mp.fused_w) ? outp(a.work_cot)[2 * (size_t)b] : real(0);
   int k0 = a.k0, h_row = mp.h_row;
@@ -2640,7 +2849,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
       for (int e = lane; e < NW; e += HALF) lds[e] = cache[e];
       wave_sync();
     } else {
-      gait_setup(T, g, a.n_t, sm.st, lane);
+      gait_setup(T, g, a.n_t, sm.st, lane, mp.setup_io == hs::SETUP_STORE && live ? &rws[bb].kf : nullptr);
       if (mp.setup_io == hs::SETUP_STORE && live) {
         for (int e = lane; e < NW; e += HALF) cache[e] = lds[e];
         for (int j = lane; j < HS_TTAB; j += HALF) rws[bb].t_tab[j] = sample_time(sm.st, nullptr, j);
@@ -2654,20 +2863,19 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   const int i = k0 + 2;  // centre sample of this launch's step
   {
     const int sl = lane / nl, L = lane % nl;
-#ifndef HS_EXP_KIN_FIRST
-#define HS_EXP_KIN_FIRST 0  // timing experiment only: samples below this offset are not computed
-#endif
     const real* t_tab = mp.setup_io == hs::SETUP_LOAD ? rws[bb].t_tab : nullptr;
-    // both rollouts of the wave straight and untransformed (the common case): the specialization
-    // without turning and record-transform code
-    if (__ballot(g.curvature != 0 || g.rec_xf) == 0) {
-      if (sl < NS && sl >= HS_EXP_KIN_FIRST)
-        kin_sample<true>(T, g, a.params[bb], sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
-                         t_tab);
-    } else {
-      if (sl < NS && sl >= HS_EXP_KIN_FIRST)
+    // a straight, untransformed gait (the common case): its frames from the setup cache, its joint
+    // values from the call's IK table when there is one (kin_sample_straight)
+    if (sl < NS) {
+      if (g.curvature == 0 && !g.rec_xf) {
+        const KinFrames* kf = mp.setup_io == hs::SETUP_LOAD ? &rws[bb].kf : nullptr;
+        const real* kt = mp.ktab_n > 0 ? &rws[bb].ktab[0][0][0] : nullptr;
+        kin_sample_straight(T, g, a.params[bb], sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
+                            t_tab, kf, kt);
+      } else {
         kin_sample<false>(T, g, a.params[bb], sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
                           t_tab);
+      }
     }
     wave_sync();
   }
@@ -2796,6 +3004,12 @@ namespace hs {
 size_t general_workspace_bytes_f32() { return sizeof(RolloutWS); }
 #else
 size_t general_workspace_bytes() { return sizeof(RolloutWS); }
+size_t solve_workspace_bytes() { return sizeof(SolveWS); }  // >= the fp32 build's
+
+int32_t ktab_samples(int32_t n_t, int32_t horizon, int64_t steps) {
+  const int64_t nt = (int64_t)n_t + horizon + 3;  // fused sample indices: k0 < n_t + horizon - 1, + NS - 1
+  return (nt <= HS_KTAB && steps * NS > nt) ? (int32_t)nt : 0;
+}
 
 int launch_pergen_rec(const hs_topo* d_topo, const hs_gait_params* params, int32_t n_rollouts, const double* times,
                       int32_t n_times, double* rec, void* stream) {
@@ -2859,6 +3073,11 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   if (mp.setup_only) {
     hipLaunchKernelGGL(hs_setup_kernel, dim3((mp.n_waves + HS_SETUP_WAVES - 1) / HS_SETUP_WAVES),
                        dim3(WAVE * HS_SETUP_WAVES), 0, st, d_topo, a, ws, mp);
+    if (mp.ktab_n > 0) {  // the call's IK table, from the frames the setup pass stored
+      const int64_t items = 2 * (int64_t)mp.n_waves * mp.ktab_n * HS_LMAX;
+      hipLaunchKernelGGL(hs_ktab_kernel, dim3((unsigned)((items + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, d_topo, a, ws,
+                         mp);
+    }
     return (int)hipGetLastError();
   }
   launch_map m = mp;
