@@ -191,7 +191,6 @@ struct SolveL {
 template <int NM, bool FORCES>
 struct Smem {
   OneStore<NM, FORCES> d;
-  SetupL st;
   SolveL<NM> sv;
 };
 
@@ -324,7 +323,8 @@ __device__ inline void store34r(const A34& a, real* m) {
 // ---------------------------------------------------------------------------
 // S: gait setup, lanes L < n_limbs (pergen.cpp:453-507, 30-51, 143-153)
 // ---------------------------------------------------------------------------
-// kf (optional): also store the straight gait's frames (KinFrames; the products straight_frames0 forms)
+// kf (optional): also store the straight gait's frames (KinFrames: the torso frame, the chain's body
+// frames and the hip joint frames at the configured pose, products this setup forms anyway)
 __device__ __attribute__((always_inline)) inline void gait_setup(const hs_topo* T, const GaitR& g, int n_t, SetupL& st, int lane,
                                                                  KinFrames* kf = nullptr) {
   const int nl = T->n_limbs;
@@ -613,25 +613,6 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
   limb_fk(T, lv, nk, J, ja, sq, cq, wq, w, k);
 }
 
-// A straight gait's frames at tv = 0 (KinFrames), the products of kin_sample with the torso at its
-// configured pose: torso A0 (orient_torso), the chain's body frames (body(v, A) for those limb L
-// owns) and the hip joint frame J0 of limb L
-template <class BODY>
-__device__ __attribute__((always_inline)) inline void straight_frames0(const hs_topo* T, const GaitR& g, const SC3& tsc,
-                                                                       int L, A34& A0, A34& J0, BODY&& body) {
-  const real q6[6] = {g.torso_pos[0], g.torso_pos[1], g.torso_pos[2], g.torso_angles[0], g.torso_angles[1],
-                      g.torso_angles[2]};
-  A0 = mul(mul(node_joint_parent(T, 0), free_joint_sc(q6, tsc)), node_pj(T, 0));
-  A34 A = A0;
-  const int clen = T->limb_chain_len[L];
-  for (int kk = 1; kk < clen; kk++) {
-    const int v = T->limb_chain[L][kk];
-    A = mul(A, node_pj(T, v));
-    if (T->node[v].owner_limb == L) body(v, A);
-  }
-  J0 = mul(A, node_joint_parent(T, T->limb_node[L][0]));
-}
-
 // set_rec's foot target of limb L at time t and the limb IK from the hip frame J (kin_sample's
 // sequence from the gait record on); bad = unreachable (ignore_reach) or failed
 __device__ __attribute__((always_inline)) inline void straight_ik(const hs_topo* T, const GaitR& g,
@@ -650,13 +631,12 @@ __device__ __attribute__((always_inline)) inline void straight_ik(const hs_topo*
   bad = unreach || fail;
 }
 
-// kin_sample for a straight, untransformed gait: the frames from kf (null: formed here), the joint
-// values and their sines and cosines from the IK table kt (null: solved here). The same products,
-// IK and sincos either way, so every path gives the same bits.
+// kin_sample for a straight, untransformed gait: the frames from kf (the gait setup's), the joint
+// values from the IK table kt (null: solved here, with the table kernel's straight_ik).
 template <class W>
 __device__ __attribute__((always_inline)) inline void kin_sample_straight(
     const hs_topo* T, const GaitR& g, const hs_gait_params& gp, const SetupL& st, int isample, int L,
-    bool ignore_reach, const W& w, int k, const real* t_tab, const KinFrames* kf, const real* kt) {
+    bool ignore_reach, const W& w, int k, const real* t_tab, const KinFrames& kf, const real* kt) {
   const int lv[3] = {T->limb_node[L][0], T->limb_node[L][1], T->limb_node[L][2]};
   const real t = sample_time(st, t_tab, isample);
   const real tv = t * st.v;  // gait_record's torso advance
@@ -664,19 +644,19 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
   const NodeK n0 = load_nodek(T, 0);
   const real u[3] = {n0.Jp(0, 0), n0.Jp(1, 0), n0.Jp(2, 0)};
   A34 A0, J;
-  if (kf) {
-    if (L == 0) A0 = load34r(kf->A0);
-    const int clen = T->limb_chain_len[L];
-    for (int kk = 1; kk < clen; kk++) {
-      const int v = T->limb_chain[L][kk];
-      const NodeK nc = load_nodek(T, v);
-      if (nc.owner == L) node_features(T, v, nc, frame_at(load34r(kf->Ab[v]), u, tv), nullptr, w, k);
-    }
-    J = load34r(kf->J0[L]);
-  } else {
-    straight_frames0(T, g, st.tsc, L, A0, J, [&](int v, const A34& Ab) {
-      node_features(T, v, load_nodek(T, v), frame_at(Ab, u, tv), nullptr, w, k);
-    });
+  real kte[KT_W];
+  if (kt) {  // the IK table row first: no other value feeds its address
+    const real* e = kt + ((size_t)isample * HS_LMAX + L) * KT_W;
+#pragma unroll
+    for (int i = 0; i < KT_W; i++) kte[i] = e[i];
+  }
+  J = load34r(kf.J0[L]);
+  if (L == 0) A0 = load34r(kf.A0);
+  const int clen = T->limb_chain_len[L];
+  for (int kk = 1; kk < clen; kk++) {
+    const int v = T->limb_chain[L][kk];
+    const NodeK nc = load_nodek(T, v);
+    if (nc.owner == L) node_features(T, v, nc, frame_at(load34r(kf.Ab[v]), u, tv), nullptr, w, k);
   }
   if (L == 0) {
     if (wq) {
@@ -688,28 +668,30 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
     }
     node_features(T, 0, n0, frame_at(A0, u, tv), &n0.Jp, w, k);  // torso joint frame J = I * J_A_parent
   }
+  STAMP(20);
   J = frame_at(J, u, tv);
   real ja[3], sq[3], cq[3];
   bool bad;
   if (kt) {
-    const real* e = kt + ((size_t)isample * HS_LMAX + L) * KT_W;
 #pragma unroll
     for (int kk = 0; kk < 3; kk++) {
-      ja[kk] = e[kk];
+      ja[kk] = kte[kk];
 #if HS_KT_SINCOS
-      sq[kk] = e[3 + kk];
-      cq[kk] = e[6 + kk];
+      sq[kk] = kte[3 + kk];
+      cq[kk] = kte[6 + kk];
 #else
       sincos(ja[kk], &sq[kk], &cq[kk]);
 #endif
     }
-    bad = e[KT_W - 1] != 0;
+    bad = kte[KT_W - 1] != 0;
+    STAMP(21);
   } else {
     straight_ik(T, g, gp, st, t, L, J, ignore_reach, ja, bad);
 #pragma unroll
     for (int kk = 0; kk < 3; kk++) sincos(ja[kk], &sq[kk], &cq[kk]);
   }
   if (w.want_centre(k)) w.unreach(k, L) = bad ? 1 : 0;
+  STAMP(22);
   NodeK nk = load_nodek(T, lv[0]);
   limb_fk(T, lv, nk, J, ja, sq, cq, wq, w, k);
 }
@@ -2718,14 +2700,13 @@ static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 #ifndef HS_SETUP_WAVES
 #define HS_SETUP_WAVES 1  // wavefronts per workgroup of the setup pass
 #endif
-__global__ __launch_bounds__(WAVE * HS_SETUP_WAVES) void hs_setup_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
-                                                        RolloutWS* __restrict__ rws, hs::launch_map mp) {
-  __shared__ SetupL sst_all[2 * HS_SETUP_WAVES];
+// One wavefront's gait setup (wavefront wid_raw of the batch; sst: two SetupL in LDS)
+__device__ __attribute__((always_inline)) inline void setup_wave(const hs_topo* __restrict__ T0, const hs_run_args& a,
+                                                                 RolloutWS* __restrict__ rws, const hs::launch_map& mp,
+                                                                 int wid_raw, SetupL* sst) {
   const int sub = (threadIdx.x % WAVE) / HALF, lane = threadIdx.x % HALF;
-  SetupL* sst = sst_all + 2 * (threadIdx.x / WAVE);
   // past the batch's last wavefront: recompute the last one's setup and store nothing (the
   // workgroup's barriers need every wavefront)
-  const int wid_raw = (int)blockIdx.x * HS_SETUP_WAVES + (int)(threadIdx.x / WAVE);
   const bool wave_live = wid_raw < mp.n_waves;
   const int wid = wave_live ? wid_raw : mp.n_waves - 1;
   if (wid_raw == 0)  // the call's fixup counters, before its step launches append to them
@@ -2755,24 +2736,37 @@ __global__ __launch_bounds__(WAVE * HS_SETUP_WAVES) void hs_setup_kernel(const h
   }
 }
 
+__global__ __launch_bounds__(WAVE * HS_SETUP_WAVES) void hs_setup_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
+                                                                        RolloutWS* __restrict__ rws, hs::launch_map mp) {
+  __shared__ SetupL sst_all[2 * HS_SETUP_WAVES];
+  setup_wave(T0, a, rws, mp, (int)blockIdx.x * HS_SETUP_WAVES + (int)(threadIdx.x / WAVE),
+             sst_all + 2 * (threadIdx.x / WAVE));
+}
+
 // The IK table of a fused call (hs::ktab_samples): one lane per (rollout slot, sample, limb), the
-// straight_ik of kin_sample_straight at sample s from the frames the setup pass stored
-__global__ __launch_bounds__(WAVE, HS_KTAB_WAVES) void hs_ktab_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
-                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
-  const int nt = mp.ktab_n;
-  const int64_t item = (int64_t)blockIdx.x * WAVE + threadIdx.x;  // ((2 wavefront + half) nt + sample) LMAX + limb
-  const int L = (int)(item % HS_LMAX);
-  const int64_t r = item / HS_LMAX;
-  const int s = (int)(r % nt);
-  const int64_t slot = r / nt;
-  if (slot >= 2 * (int64_t)mp.n_waves) return;
+// straight_ik of kin_sample_straight at sample s from the frames the setup pass stored. Item
+// ((2 wavefront + half) nt + sample) LMAX + limb; its wavefront, or -1 when it has nothing to do.
+__device__ inline int ktab_item_wave(const hs_topo* __restrict__ T0, const hs_run_args& a, const hs::launch_map& mp,
+                                     int64_t item) {
+  const int64_t slot = item / HS_LMAX / mp.ktab_n;
+  if (slot >= 2 * (int64_t)mp.n_waves) return -1;
   const int wid = (int)(slot >> 1), sub = (int)(slot & 1);
   const int b = mp.wave_rollouts ? mp.wave_rollouts[2 * wid + sub] : 2 * wid + sub;
-  if (b < 0 || b >= a.n_rollouts) return;
+  if (b < 0 || b >= a.n_rollouts) return -1;
   const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
-  if (L >= T->n_limbs) return;
+  if ((int)(item % HS_LMAX) >= T->n_limbs) return -1;
+  // kin_sample's turning / record-transform path (the step kernel's test, in the working precision)
+  if ((real)a.params[b].curvature != 0 || a.params[b].rec_transform_flag) return -1;
+  return wid;
+}
+__device__ inline void ktab_item(const hs_topo* __restrict__ T0, const hs_run_args& a, RolloutWS* __restrict__ rws,
+                                 const hs::launch_map& mp, int64_t item, int wid) {
+  const int L = (int)(item % HS_LMAX);
+  const int64_t slot = item / HS_LMAX / mp.ktab_n;
+  const int s = (int)(item / HS_LMAX % mp.ktab_n);
+  const int b = mp.wave_rollouts ? mp.wave_rollouts[slot] : (int)slot;
+  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
   const GaitR g = load_gait(a.params[b]);
-  if (g.curvature != 0 || g.rec_xf) return;  // kin_sample's turning / record-transform path
   const RolloutWS& w = rws[b];
   const real t = sample_time(w.st, w.t_tab, s);
   const real tv = t * w.st.v;
@@ -2794,6 +2788,77 @@ __global__ __launch_bounds__(WAVE, HS_KTAB_WAVES) void hs_ktab_kernel(const hs_t
 #endif
   }
   e[KT_W - 1] = bad ? real(1) : real(0);
+}
+
+__global__ __launch_bounds__(WAVE, HS_KTAB_WAVES) void hs_ktab_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
+                                                                      RolloutWS* __restrict__ rws, hs::launch_map mp) {
+  const int64_t item = (int64_t)blockIdx.x * WAVE + threadIdx.x;
+  const int wid = ktab_item_wave(T0, a, mp, item);
+  if (wid >= 0) ktab_item(T0, a, rws, mp, item, wid);
+}
+
+// The setup pass and the IK table in one launch (hs_run_calls): blocks take tickets in the order
+// they start (an atomic counter, as in a decoupled look-back); the first n_waves tickets run the gait
+// setup of a wavefront and then publish it (prep_ready[wid] = prep_epoch, a release at agent scope),
+// the rest run table items, each lane waiting (acquire) for its rollout's setup. A table block waits
+// only on setup blocks that already hold a ticket, hence run, so the wait ends; the table's work
+// overlaps the setup pass's latency instead of following it.
+#ifndef HS_PREP_WAVES
+#define HS_PREP_WAVES 1
+#endif
+#ifndef HS_PREP_SLEEP
+#define HS_PREP_SLEEP 16  // s_sleep units (64 clocks) between polls
+#endif
+#ifndef HS_PREP
+#define HS_PREP 0  // 1: the setup pass and the IK table in one launch; measured far slower (the table
+                   // blocks' polls: 206 us against 13 + 18 us for the two launches), so off
+#endif
+#ifndef HS_PREP_RMW
+#define HS_PREP_RMW 0  // poll with an atomic read-modify-write (performed at the memory side) instead of a load
+#endif
+__global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
+                                                                      RolloutWS* __restrict__ rws, hs::launch_map mp) {
+  __shared__ SetupL sst[2];
+  __shared__ uint32_t tk_s;
+  if (threadIdx.x == 0) {
+    const uint32_t tk = atomicAdd(mp.prep_ctr, 1u);
+    if (tk + 1 == gridDim.x) atomicExch(mp.prep_ctr, 0u);  // every block holds its ticket: zero for the next call
+    tk_s = tk;
+  }
+  __syncthreads();
+  const uint32_t tk = tk_s;
+  if (tk < (uint32_t)mp.n_waves) {
+    setup_wave(T0, a, rws, mp, (int)tk, sst);
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(mp.prep_ready + tk, mp.prep_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const int64_t item = (int64_t)(tk - (uint32_t)mp.n_waves) * WAVE + threadIdx.x;
+  const int wid = ktab_item_wave(T0, a, mp, item);
+  if (wid < 0) return;
+  // bounded (~0.3 s): a setup that never published would leave NaN joint values, not a hung GPU
+  // (relaxed polls, then one acquire: an acquire per poll invalidates the caches the setup waves use)
+  auto poll = [&]() {
+#if HS_PREP_RMW
+    return __hip_atomic_fetch_or(mp.prep_ready + wid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    return __hip_atomic_load(mp.prep_ready + wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+  };
+  for (int spin = 0; poll() != mp.prep_epoch; spin++) {
+    if (spin >= (1 << 20)) {
+      const int64_t slot = item / HS_LMAX / mp.ktab_n;
+      const int b = mp.wave_rollouts ? mp.wave_rollouts[slot] : (int)slot;
+      real* e = rws[b].ktab[item / HS_LMAX % mp.ktab_n][item % HS_LMAX];
+      for (int i = 0; i < KT_W; i++) e[i] = __builtin_nan("");
+      return;
+    }
+    __builtin_amdgcn_s_sleep(HS_PREP_SLEEP);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  ktab_item(T0, a, rws, mp, item, wid);
 }
 
 // One wavefront's step: fused step fstep (0 outside fused launches) of batch wavefront wid. only_sub
@@ -2841,39 +2906,25 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   const bool ignore_reach = a.ignore_reach != 0;
 
   STAMP(0);
-  {
-    constexpr int NW = sizeof(SetupL) / sizeof(real);
-    real* cache = reinterpret_cast<real*>(&rws[bb].st);  // the idle half reads its neighbour's
-    real* lds = reinterpret_cast<real*>(&sm.st);
-    if (mp.setup_io == hs::SETUP_LOAD) {
-      for (int e = lane; e < NW; e += HALF) lds[e] = cache[e];
-      wave_sync();
-    } else {
-      gait_setup(T, g, a.n_t, sm.st, lane, mp.setup_io == hs::SETUP_STORE && live ? &rws[bb].kf : nullptr);
-      if (mp.setup_io == hs::SETUP_STORE && live) {
-        for (int e = lane; e < NW; e += HALF) cache[e] = lds[e];
-        for (int j = lane; j < HS_TTAB; j += HALF) rws[bb].t_tab[j] = sample_time(sm.st, nullptr, j);
-      }
-    }
-  }
-  if (mp.setup_only) return;
+  // the gait setup of the rollout, stored by the call's setup pass (hs_setup_kernel / hs_prep_kernel;
+  // the idle half reads its neighbour's): read from global memory where it is used
+  const SetupL& st = rws[bb].st;
   STAMP(1);
 
   // K: the five-sample window, lane = (sample, limb)
   const int i = k0 + 2;  // centre sample of this launch's step
   {
     const int sl = lane / nl, L = lane % nl;
-    const real* t_tab = mp.setup_io == hs::SETUP_LOAD ? rws[bb].t_tab : nullptr;
-    // a straight, untransformed gait (the common case): its frames from the setup cache, its joint
+    const real* t_tab = rws[bb].t_tab;
+    // a straight, untransformed gait (the common case): its frames from the setup pass, its joint
     // values from the call's IK table when there is one (kin_sample_straight)
     if (sl < NS) {
       if (g.curvature == 0 && !g.rec_xf) {
-        const KinFrames* kf = mp.setup_io == hs::SETUP_LOAD ? &rws[bb].kf : nullptr;
         const real* kt = mp.ktab_n > 0 ? &rws[bb].ktab[0][0][0] : nullptr;
-        kin_sample_straight(T, g, a.params[bb], sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
-                            t_tab, kf, kt);
+        kin_sample_straight(T, g, a.params[bb], st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
+                            t_tab, rws[bb].kf, kt);
       } else {
-        kin_sample<false>(T, g, a.params[bb], sm.st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
+        kin_sample<false>(T, g, a.params[bb], st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
                           t_tab);
       }
     }
@@ -2881,11 +2932,11 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   }
   STAMP(2);
   if constexpr (FORCES) {
-    forces_step(T, a, mp, sm.st, sm.sv, sm.d.fr, OneWin<NM, FORCES>{&sm.d}, b, live, h_row, lane);
+    forces_step(T, a, mp, st, sm.sv, sm.d.fr, OneWin<NM, FORCES>{&sm.d}, b, live, h_row, lane);
     return;
   } else {
     bool deferred = false;
-    step<DEFER>(T, a, mp, sm.st, sm.sv, sm.d.fl, sm.d.wk, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
+    step<DEFER>(T, a, mp, st, sm.sv, sm.d.fl, sm.d.wk, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
                 deferred, !fix_idle, lane);
     if (DEFER && deferred) {  // the fixup launch solves this (step, rollout) with the general path
       if (lane == 0 && live) {
@@ -3071,6 +3122,12 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   hipStream_t st = (hipStream_t)a.stream;
   RolloutWS* ws = (RolloutWS*)workspace;
   if (mp.setup_only) {
+    if (HS_PREP && mp.ktab_n > 0 && mp.prep_ctr) {  // the setup pass and the IK table in one launch
+      const int64_t items = 2 * (int64_t)mp.n_waves * mp.ktab_n * HS_LMAX;
+      hipLaunchKernelGGL(hs_prep_kernel, dim3((unsigned)(mp.n_waves + (items + WAVE - 1) / WAVE)), dim3(WAVE), 0, st,
+                         d_topo, a, ws, mp);
+      return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(hs_setup_kernel, dim3((mp.n_waves + HS_SETUP_WAVES - 1) / HS_SETUP_WAVES),
                        dim3(WAVE * HS_SETUP_WAVES), 0, st, d_topo, a, ws, mp);
     if (mp.ktab_n > 0) {  // the call's IK table, from the frames the setup pass stored

@@ -291,3 +291,31 @@ def test_fused_reference_mode_fixups_over_two_launches(gpu, hmodels):
     torch.cuda.synchronize()
     flat = npy(fz.flags).reshape(-1)[:61 * 20]  # rows packed with stride n_calls * call_horizon = 20
     assert not (flat.astype(np.uint32) & 64).any()
+
+
+@pytest.mark.parametrize("n_t,pattern", [(20, "alternate"), (20, "pairs"), (70, "alternate")])
+def test_fused_straight_and_curved_rollouts(gpu, hmodels, n_t, pattern):
+    """Straight gaits take the frame / IK-table kinematics (kin_sample_straight, the table built by
+    the fused call's setup pass when n_t + H + 3 <= HS_KTAB; n_t = 70 has none), curved ones the
+    turning path. Waves holding one of each ("alternate") run both; "pairs" keeps each wave uniform.
+    The fused call equals the launch-per-step horizon run (IK solved inline) bitwise."""
+    import torch
+    from hslabs_amd import synth
+
+    m = hmodels["hexapod"]
+    B = 130
+    p = synth.gen_params(B, "hexapod")
+    pc = synth.gen_params(B, "hexapod", curved=True)
+    sel = (np.arange(B) % 2 == 1) if pattern == "alternate" else ((np.arange(B) // 2) % 2 == 1)
+    p[sel] = pc[sel]
+    assert (p["curvature"] != 0).sum() == sel.sum()
+    H = 20  # <= n_t: hs_run's horizon rows do not wrap k0, the fused calls' do
+    ref = gpu.DeviceBatch(m, p, n_t=n_t, horizon=H, outputs=OUTS)
+    ref.run(best=True)
+    fz = gpu.DeviceBatch(m, p, n_t=n_t, horizon=H, outputs=OUTS)
+    fz.work_cot.zero_()
+    fz.run_calls(H, call_horizon=1, best=True, accumulate=False)
+    torch.cuda.synchronize()
+    for k in ("q", "dq", "tau", "cf", "x", "flags", "work_cot", "best_key"):
+        assert np.array_equal(npy(getattr(ref, k)), npy(getattr(fz, k)), equal_nan=True), k
+    assert np.isfinite(npy(fz.tau)).all()
