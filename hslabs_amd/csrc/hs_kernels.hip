@@ -47,6 +47,14 @@ namespace {
 
 using namespace hsd;
 
+// timing experiments (tuning builds only)
+#ifndef HS_EXP_HINGE0
+#define HS_EXP_HINGE0 1  // Rz(0) as mul_hinge(J0, 1, 0): the same values, no sincos in the setup chain
+#endif
+#ifndef HS_EXP_FENCE
+#define HS_EXP_FENCE 0
+#endif
+
 constexpr int WAVE = 64;
 constexpr int HALF = 32;     // lanes per rollout: two rollouts per wavefront
 constexpr int NS = 5;        // samples in the derivative stencil (periodic.cpp:192-202)
@@ -347,7 +355,11 @@ __device__ __attribute__((always_inline)) inline void gait_setup(const hs_topo* 
       store34r(J0, kf->J0[L]);
       if (L == 0) store34r(A0, kf->A0);
     }
+#if HS_EXP_HINGE0
+    A34 Ac = mul(mul_hinge(J0, real(1), real(0)), node_pj(T, c));  // timing experiment: Rz(0) without the sincos
+#else
     A34 Ac = mul(mul(J0, hinge_joint(real(0))), node_pj(T, c));
+#endif
     real pos[3] = {Ac(0, 3), Ac(1, 3), Ac(2, 3)};  // get_limb_hip_pos
     if (g.foot_shift_type == 0) {                   // setup_foot_shift / shift_pos0
       real sh[3] = {real(0), g.foot_shift, real(0)}, ls[3];
@@ -2950,6 +2962,12 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   if (mp.fused_w) {  // this step's joint sum of positive work, summed over the steps in order by the reduce
     if (lane == 0 && live)
       reinterpret_cast<real*>(mp.fused_work)[(size_t)(mp.fused_s0 + fstep) * a.n_rollouts + b] = work;
+#if HS_EXP_FENCE  // timing experiment: the agent-scope release and ticket a last-wave reduce would need
+    if (DEFER) {
+      __threadfence();
+      if (threadIdx.x == 0) atomicAdd(mp.fix_count, 0);
+    }
+#endif
     return;
   }
   if (lane == 0 && live) {

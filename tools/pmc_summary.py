@@ -39,6 +39,22 @@ def collect(root, n_waves, step_launch=STEP_LAUNCH):
     return {c: sorted(d.values()) for c, d in vals.items()}
 
 
+def collect_job_kernels(root):
+    """The call's other kernels (setup pass, IK table pass, fixup + work reduce): counter -> kernel ->
+    per-dispatch values (one dispatch of each per job)."""
+    vals = defaultdict(lambda: defaultdict(list))
+    for path in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
+        per = defaultdict(float)
+        for row in csv.DictReader(open(path)):
+            name = row["Kernel_Name"]
+            for k in ("hs_setup_kernel", "hs_ktab_kernel", "hs_prep_kernel", "hs_rollout_kernel<22, false, 2>"):
+                if k in name:
+                    per[(row["Counter_Name"], k, row["Dispatch_Id"])] += float(row["Counter_Value"])
+        for (c, k, _), v in per.items():
+            vals[c][k].append(v)
+    return vals
+
+
 def lib_of(root):
     for log in sorted(glob.glob(os.path.join(root, "p*.log"))):
         for ln in open(log):
@@ -56,6 +72,7 @@ def main():
     ap.add_argument("--traffic-json")
     ap.add_argument("--cmd", default="bench.py --steps 20 --warmup 5 --no-cpu")
     ap.add_argument("--forces", action="store_true", help="solve_forces' step launches (bench.py --forces)")
+    ap.add_argument("--job-steps", type=int, default=20, help="steps per job: the per-job kernels' share")
     a = ap.parse_args()
     n_waves = (a.rollouts + 1) // 2
     v = collect(a.root, n_waves, FORCES_LAUNCH if a.forces else STEP_LAUNCH)
@@ -77,11 +94,25 @@ def main():
         if "SQ_WAVE_CYCLES" in med and "SQ_WAIT_ANY" in med:
             lines.append(f"  wait fraction (SQ_WAIT_ANY / SQ_WAVE_CYCLES) {med['SQ_WAIT_ANY'] / med['SQ_WAVE_CYCLES']:.3f}")
     traffic = fp64 = None
+    job_steps = a.job_steps
     if "FETCH_SIZE" in med and "WRITE_SIZE" in med:
         traffic = int(round((2 * med["FETCH_SIZE"] + med["WRITE_SIZE"]) * 1024))
-        lines.append(f"HBM traffic per step of the batch (FETCH_SIZE x2 + WRITE_SIZE): {traffic} bytes "
+        lines.append(f"HBM traffic per step of the batch, step launch (FETCH_SIZE x2 + WRITE_SIZE): {traffic} bytes "
                      f"(FETCH_SIZE alone x1: {int(med['FETCH_SIZE'] * 1024)} B; the x2 is calibrated for 16-B/lane "
                      f"streaming loads, these are narrower, so the figure is an upper bound)")
+        if not a.forces:
+            jk = collect_job_kernels(a.root)
+            extra = 0.0
+            for k in sorted(set(jk.get("FETCH_SIZE", {})) | set(jk.get("WRITE_SIZE", {}))):
+                f_ = statistics.median(jk["FETCH_SIZE"].get(k, [0.0]))
+                w_ = statistics.median(jk["WRITE_SIZE"].get(k, [0.0]))
+                b_ = (2 * f_ + w_) * 1024
+                extra += b_
+                lines.append(f"  once per job: {k:32s} FETCH_SIZE {f_:.1f} KiB, WRITE_SIZE {w_:.1f} KiB -> {int(b_)} B")
+            if extra:
+                traffic += int(round(extra / job_steps))
+                lines.append(f"HBM traffic per step of the batch at {job_steps} steps per job, those kernels included: "
+                             f"{traffic} bytes")
     if all(c in med for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64")):
         fp64 = int(64 * (med["SQ_INSTS_VALU_ADD_F64"] + med["SQ_INSTS_VALU_MUL_F64"] +
                          2 * med["SQ_INSTS_VALU_FMA_F64"]))

@@ -15,8 +15,8 @@ sys.path.insert(0, ROOT)
 from hslabs_amd import build as B  # noqa: E402
 
 LIB = os.path.join(B.OUT_DIR, os.environ.get("STAMPS_LIB", "libhslabs_stamps.so"))
-PHASES = [("setup", 0, 1), ("kin(5 samples)", 1, 2), ("k:frames", 1, 20), ("k:IK / table", 20, 21),
-          ("k:sincos", 21, 22), ("k:limb FK+features", 22, 2), ("dynamics", 3, 4), ("particular", 4, 5),
+PHASES = [("setup", 0, 1), ("kin(5 samples)", 1, 2), ("k:frames", 1, 20), ("k:table+sincos", 20, 21),
+          ("k:(inline IK)", 21, 22), ("k:limb FK+features", 22, 2), ("dynamics", 3, 4), ("particular", 4, 5),
           ("contact list", 5, 6), ("contact solve", 6, 7), ("outputs", 7, 8), ("TOTAL", 0, 8)]
 # general path (waves where it ran): grams, LU, LU solve + kernel, m, QR, QR solve
 GENERAL = [("g:grams", 6, 9), ("g:LU", 9, 10), ("g:solve+kernel", 10, 11), ("g:m", 11, 12), ("g:QR", 12, 13),
