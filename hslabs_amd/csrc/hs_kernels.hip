@@ -643,26 +643,44 @@ __device__ __attribute__((always_inline)) inline void straight_ik(const hs_topo*
   bad = unreach || fail;
 }
 
+// What kin_sample_straight loads that no computed value feeds (the sample time, the torso speed, the
+// hip frame, the IK table row): loaded at the wave's start, before the gait record decides the path,
+// so these latencies overlap the gait parameters' instead of following them
+struct StraightPre {
+  real t, v;
+  A34 J0;
+  real kte[KT_W];
+};
+__device__ __attribute__((always_inline)) inline StraightPre straight_preload(const SetupL& st, const real* t_tab,
+                                                                             const KinFrames& kf, const real* kt,
+                                                                             int isample, int L) {
+  StraightPre p;
+  p.t = sample_time(st, t_tab, isample);
+  p.v = st.v;
+  p.J0 = load34r(kf.J0[L]);
+  if (kt) {
+    const real* e = kt + ((size_t)isample * HS_LMAX + L) * KT_W;
+#pragma unroll
+    for (int i = 0; i < KT_W; i++) p.kte[i] = e[i];
+  }
+  return p;
+}
+
 // kin_sample for a straight, untransformed gait: the frames from kf (the gait setup's), the joint
-// values from the IK table kt (null: solved here, with the table kernel's straight_ik).
+// values from the IK table kt (null: solved here, with the table kernel's straight_ik); pre: the
+// preloaded values (straight_preload)
 template <class W>
 __device__ __attribute__((always_inline)) inline void kin_sample_straight(
     const hs_topo* T, const GaitR& g, const hs_gait_params& gp, const SetupL& st, int isample, int L,
-    bool ignore_reach, const W& w, int k, const real* t_tab, const KinFrames& kf, const real* kt) {
+    bool ignore_reach, const W& w, int k, const StraightPre& pre, const KinFrames& kf, const real* kt) {
   const int lv[3] = {T->limb_node[L][0], T->limb_node[L][1], T->limb_node[L][2]};
-  const real t = sample_time(st, t_tab, isample);
-  const real tv = t * st.v;  // gait_record's torso advance
+  const real t = pre.t;
+  const real tv = t * pre.v;  // gait_record's torso advance
   const bool wq = w.want_q(k);
   const NodeK n0 = load_nodek(T, 0);
   const real u[3] = {n0.Jp(0, 0), n0.Jp(1, 0), n0.Jp(2, 0)};
-  A34 A0, J;
-  real kte[KT_W];
-  if (kt) {  // the IK table row first: no other value feeds its address
-    const real* e = kt + ((size_t)isample * HS_LMAX + L) * KT_W;
-#pragma unroll
-    for (int i = 0; i < KT_W; i++) kte[i] = e[i];
-  }
-  J = load34r(kf.J0[L]);
+  A34 A0, J = pre.J0;
+  const real* kte = pre.kte;
   if (L == 0) A0 = load34r(kf.A0);
   const int clen = T->limb_chain_len[L];
   for (int kk = 1; kk < clen; kk++) {
@@ -2802,9 +2820,19 @@ __device__ inline void ktab_item(const hs_topo* __restrict__ T0, const hs_run_ar
   e[KT_W - 1] = bad ? real(1) : real(0);
 }
 
+// XCD-aware: blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), and
+// the setup pass and the step launches run batch wavefront wid on the XCD of block wid (fused steps:
+// when the batch's wavefront count is a multiple of 8), so block t = 8 q + x takes the items of
+// wavefront 8 (q / bpw) + x: its table rows are written on the XCD whose L2 the steps read them from
+__host__ __device__ inline int ktab_blocks_per_wave(int nt) { return (2 * nt * HS_LMAX + WAVE - 1) / WAVE; }
 __global__ __launch_bounds__(WAVE, HS_KTAB_WAVES) void hs_ktab_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
                                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
-  const int64_t item = (int64_t)blockIdx.x * WAVE + threadIdx.x;
+  const int bpw = ktab_blocks_per_wave(mp.ktab_n);
+  const int x = (int)(blockIdx.x % 8), q = (int)(blockIdx.x / 8);
+  const int w = 8 * (q / bpw) + x;
+  const int local = (q % bpw) * WAVE + (int)threadIdx.x;
+  if (w >= mp.n_waves || local >= 2 * mp.ktab_n * HS_LMAX) return;
+  const int64_t item = (int64_t)w * 2 * mp.ktab_n * HS_LMAX + local;
   const int wid = ktab_item_wave(T0, a, mp, item);
   if (wid >= 0) ktab_item(T0, a, rws, mp, item, wid);
 }
@@ -2913,28 +2941,29 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
     k0 = (int)(((int64_t)a.k0 + (int64_t)c * mp.fused_h) % a.n_t) + s % mp.fused_h;
     h_row = s;
   }
-  const GaitR g = load_gait(a.params[bb]);
   const int nl = T->n_limbs;
-  const bool ignore_reach = a.ignore_reach != 0;
-
-  STAMP(0);
   // the gait setup of the rollout, stored by the call's setup pass (hs_setup_kernel / hs_prep_kernel;
   // the idle half reads its neighbour's): read from global memory where it is used
   const SetupL& st = rws[bb].st;
+  const int i = k0 + 2;  // centre sample of this launch's step
+  const int sl = lane / nl, L = lane % nl;
+  const real* kt = mp.ktab_n > 0 ? &rws[bb].ktab[0][0][0] : nullptr;
+  const StraightPre pre = straight_preload(st, rws[bb].t_tab, rws[bb].kf, kt, i - 2 + (sl < NS ? sl : 0), L);
+  const GaitR g = load_gait(a.params[bb]);
+  const bool ignore_reach = a.ignore_reach != 0;
+
+  STAMP(0);
   STAMP(1);
 
   // K: the five-sample window, lane = (sample, limb)
-  const int i = k0 + 2;  // centre sample of this launch's step
   {
-    const int sl = lane / nl, L = lane % nl;
     const real* t_tab = rws[bb].t_tab;
     // a straight, untransformed gait (the common case): its frames from the setup pass, its joint
     // values from the call's IK table when there is one (kin_sample_straight)
     if (sl < NS) {
       if (g.curvature == 0 && !g.rec_xf) {
-        const real* kt = mp.ktab_n > 0 ? &rws[bb].ktab[0][0][0] : nullptr;
         kin_sample_straight(T, g, a.params[bb], st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
-                            t_tab, rws[bb].kf, kt);
+                            pre, rws[bb].kf, kt);
       } else {
         kin_sample<false>(T, g, a.params[bb], st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
                           t_tab);
@@ -3149,9 +3178,8 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
     hipLaunchKernelGGL(hs_setup_kernel, dim3((mp.n_waves + HS_SETUP_WAVES - 1) / HS_SETUP_WAVES),
                        dim3(WAVE * HS_SETUP_WAVES), 0, st, d_topo, a, ws, mp);
     if (mp.ktab_n > 0) {  // the call's IK table, from the frames the setup pass stored
-      const int64_t items = 2 * (int64_t)mp.n_waves * mp.ktab_n * HS_LMAX;
-      hipLaunchKernelGGL(hs_ktab_kernel, dim3((unsigned)((items + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, d_topo, a, ws,
-                         mp);
+      const int64_t blocks = 8 * (int64_t)ktab_blocks_per_wave(mp.ktab_n) * ((mp.n_waves + 7) / 8);
+      hipLaunchKernelGGL(hs_ktab_kernel, dim3((unsigned)blocks), dim3(WAVE), 0, st, d_topo, a, ws, mp);
     }
     return (int)hipGetLastError();
   }
