@@ -153,7 +153,7 @@ int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::lau
   base.setup_io = hs::SETUP_STORE;
   base.fix_n_counts = 0;
   base.prep_ctr = nullptr;  // two launches (the prep kernel's counter lives in the fused path's pools)
-  base.ktab_n = hs::ktab_samples(a.n_t, a.horizon, S);
+  hs::ktab_range(a.k0, a.n_t, a.horizon, n_calls, &base.ktab_lo, &base.ktab_n);
   const int le0 = (a.precision == HS_PREC_F32) ? hs::launch_fused_f32(d, c, ws, base) : hs::launch_fused(d, c, ws, base);
   if (le0 != 0) return hip_fail((hipError_t)le0, "kernel launch (setup pass)");
   base.setup_only = 0;
@@ -271,7 +271,7 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   mp.setup_io = hs::SETUP_STORE;
   mp.fix_count = fix_counts;
   mp.fix_n_counts = n_chunks;
-  mp.ktab_n = hs::ktab_samples(a.n_t, a.horizon, S);  // the straight gaits' IK table, built by the setup pass
+  hs::ktab_range(a.k0, a.n_t, a.horizon, n_calls, &mp.ktab_lo, &mp.ktab_n);  // straight gaits' IK table (setup pass)
   mp.prep_ctr = (uint32_t*)prep;
   mp.prep_ready = (uint32_t*)prep + 64;
   mp.prep_epoch = next_epoch();
@@ -317,6 +317,7 @@ launch_map single_model_map(const hs_topo& t, int32_t n_rollouts) {
   launch_map mp{};
   mp.n_waves = (n_rollouts + 1) / 2;  // two rollouts per wavefront
   mp.max_parts = t.n;
+  mp.ktab_nl = t.n_limbs;
   mp.st_tau = t.nmj;
   mp.st_cf = 3 * t.nf;
   mp.st_q = t.cfg;
@@ -551,7 +552,7 @@ int hs_run_forces_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls, con
   mp.fused_h = a->horizon;
   mp.setup_only = 1;
   mp.setup_io = hs::SETUP_STORE;
-  mp.ktab_n = hs::ktab_samples(a->n_t, a->horizon, S);
+  hs::ktab_range(a->k0, a->n_t, a->horizon, n_calls, &mp.ktab_lo, &mp.ktab_n);
   int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   mp.setup_only = 0;
   mp.setup_io = hs::SETUP_LOAD;

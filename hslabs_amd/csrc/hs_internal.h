@@ -65,9 +65,10 @@ struct launch_map {
   double red_total_mass;
   const double* red_rollout_mass;
   uint64_t* red_best_key;
-  // fused calls of straight gaits: > 0 = the setup pass also tabulates the limb IK of samples
-  // [0, ktab_n) per rollout (ktab_samples), and the step launches read it instead of solving it
-  int32_t ktab_n;
+  // calls of straight gaits: > 0 = the setup pass also tabulates the limb IK of samples
+  // [ktab_lo, ktab_lo + ktab_n) per rollout (ktab_range), and the step launches read it instead of
+  // solving it; ktab_nl: limbs per sample the table kernel enumerates (the launch's largest model)
+  int32_t ktab_n, ktab_lo, ktab_nl;
   // with ktab_n: the setup pass and the table in one launch (hs_prep_kernel): its block ticket counter
   // (zero between launches) and per-wavefront setup flags (= prep_epoch once published)
   uint32_t* prep_ctr;
@@ -81,9 +82,10 @@ struct launch_map {
 size_t general_workspace_bytes();
 // one fused step's general-path scratch per rollout (fused_gen holds [steps in a launch][B + 1] of them)
 size_t solve_workspace_bytes();
-// samples the IK table of a fused call covers (0: none): n_t + horizon + 3 when that fits and the
-// call's steps would evaluate more samples than the table does
-int32_t ktab_samples(int32_t n_t, int32_t horizon, int64_t steps);
+// the samples an IK table for n_calls calls of `horizon` steps from k0 covers: [lo, lo + n), every
+// sample a step of those calls reads; n = 0 (no table) when that exceeds the table or the steps
+// would evaluate no more samples than the table does
+void ktab_range(int32_t k0, int32_t n_t, int32_t horizon, int64_t n_calls, int32_t* lo, int32_t* n);
 int launch_rollouts(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
 // single precision build of the same kernels (hs_kernels_f32.hip): outputs are float
 size_t general_workspace_bytes_f32();

@@ -47,6 +47,18 @@ namespace {
 
 using namespace hsd;
 
+#ifndef HS_ST_LDS
+#define HS_ST_LDS 0  // 1: copy the setup record to LDS per step (round 2's layout) instead of global reads
+#endif
+#ifndef HS_KTE_PRELOAD
+// the IK table row loaded at wave start, before the gait is known to be straight (fp64: +1.3 % at
+// K = 200 on hexapod); in the fp32 build inside the straight branch (spider, whose synthetic gaits are
+// curved, 346 -> 370 M steps/s: the row's registers stay out of the turning path)
+#define HS_KTE_PRELOAD (!HS_REAL_IS_FLOAT)
+#endif
+#ifndef HS_KTAB_GRID
+#define HS_KTAB_GRID 0  // > 0: the IK table kernel's grid cap (a grid-stride loop over its blocks)
+#endif
 // timing experiments (tuning builds only)
 #ifndef HS_EXP_HINGE0
 #define HS_EXP_HINGE0 1  // Rz(0) as mul_hinge(J0, 1, 0): the same values, no sincos in the setup chain
@@ -200,6 +212,9 @@ template <int NM, bool FORCES>
 struct Smem {
   OneStore<NM, FORCES> d;
   SolveL<NM> sv;
+#if HS_ST_LDS
+  SetupL st;  // the setup pass's record, copied per step
+#endif
 };
 
 // Cross-lane exchange through LDS inside the single wave of a workgroup: an
@@ -651,15 +666,16 @@ struct StraightPre {
   A34 J0;
   real kte[KT_W];
 };
+// (kt: the table, whose row r holds sample lo + r)
 __device__ __attribute__((always_inline)) inline StraightPre straight_preload(const SetupL& st, const real* t_tab,
                                                                              const KinFrames& kf, const real* kt,
-                                                                             int isample, int L) {
+                                                                             int isample, int lo, int L) {
   StraightPre p;
   p.t = sample_time(st, t_tab, isample);
   p.v = st.v;
   p.J0 = load34r(kf.J0[L]);
   if (kt) {
-    const real* e = kt + ((size_t)isample * HS_LMAX + L) * KT_W;
+    const real* e = kt + ((size_t)(isample - lo) * HS_LMAX + L) * KT_W;
 #pragma unroll
     for (int i = 0; i < KT_W; i++) p.kte[i] = e[i];
   }
@@ -672,7 +688,7 @@ __device__ __attribute__((always_inline)) inline StraightPre straight_preload(co
 template <class W>
 __device__ __attribute__((always_inline)) inline void kin_sample_straight(
     const hs_topo* T, const GaitR& g, const hs_gait_params& gp, const SetupL& st, int isample, int L,
-    bool ignore_reach, const W& w, int k, const StraightPre& pre, const KinFrames& kf, const real* kt) {
+    bool ignore_reach, const W& w, int k, const StraightPre& pre, const KinFrames& kf, const real* kt, int ktab_lo) {
   const int lv[3] = {T->limb_node[L][0], T->limb_node[L][1], T->limb_node[L][2]};
   const real t = pre.t;
   const real tv = t * pre.v;  // gait_record's torso advance
@@ -680,7 +696,16 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
   const NodeK n0 = load_nodek(T, 0);
   const real u[3] = {n0.Jp(0, 0), n0.Jp(1, 0), n0.Jp(2, 0)};
   A34 A0, J = pre.J0;
+#if HS_KTE_PRELOAD
   const real* kte = pre.kte;
+#else
+  real kte[KT_W];  // the table row, loaded once the gait is known to be straight
+  if (kt) {
+    const real* e = kt + ((size_t)(isample - ktab_lo) * HS_LMAX + L) * KT_W;
+#pragma unroll
+    for (int i = 0; i < KT_W; i++) kte[i] = e[i];
+  }
+#endif
   if (L == 0) A0 = load34r(kf.A0);
   const int clen = T->limb_chain_len[L];
   for (int kk = 1; kk < clen; kk++) {
@@ -2184,16 +2209,16 @@ __device__ inline void reduce_rollouts(const hs_run_args& a, real total_mass, co
   if (rollout_mass) total_mass = (real)rollout_mass[b];  // a mixed plan: the rollout's model
   real w = a.accumulate ? outp(a.work_cot)[2 * (size_t)b] : real(0);
   const real dt = (real)a.params[b].period / a.n_t;  // gait_setup's st.dt
-  // periodic.cpp:302-303, in step order; the loads of 16 steps issue together ahead of their FMAs
-  int s = 0;
-  for (; s + 16 <= n_steps; s += 16) {
-    real v[16];
+  // periodic.cpp:302-303, in step order; the loads of up to 32 steps issue together ahead of their
+  // FMAs (a 20-step job: one round trip)
+  for (int s = 0; s < n_steps; s += 32) {
+    real v[32];
 #pragma unroll
-    for (int j = 0; j < 16; j++) v[j] = ws[(size_t)(s + j) * a.n_rollouts + b];
+    for (int j = 0; j < 32; j++) v[j] = s + j < n_steps ? ws[(size_t)(s + j) * a.n_rollouts + b] : real(0);
 #pragma unroll
-    for (int j = 0; j < 16; j++) w = fma(v[j], dt, w);
+    for (int j = 0; j < 32; j++)
+      if (s + j < n_steps) w = fma(v[j], dt, w);
   }
-  for (; s < n_steps; s++) w = fma(ws[(size_t)s * a.n_rollouts + b], dt, w);
   const real L = (real)a.params[b].step_length;
   const real cot = w / (total_mass * L);
   if (live) {
@@ -2773,32 +2798,35 @@ __global__ __launch_bounds__(WAVE * HS_SETUP_WAVES) void hs_setup_kernel(const h
              sst_all + 2 * (threadIdx.x / WAVE));
 }
 
-// The IK table of a fused call (hs::ktab_samples): one lane per (rollout slot, sample, limb), the
+// The IK table of a call (hs::ktab_range): one lane per (rollout slot, sample, limb), the
 // straight_ik of kin_sample_straight at sample s from the frames the setup pass stored. Item
 // ((2 wavefront + half) nt + sample) LMAX + limb; its wavefront, or -1 when it has nothing to do.
+__device__ inline int ktab_lanes(const hs::launch_map& mp) { return mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX; }
 __device__ inline int ktab_item_wave(const hs_topo* __restrict__ T0, const hs_run_args& a, const hs::launch_map& mp,
                                      int64_t item) {
-  const int64_t slot = item / HS_LMAX / mp.ktab_n;
+  const int nli = ktab_lanes(mp);
+  const int64_t slot = item / nli / mp.ktab_n;
   if (slot >= 2 * (int64_t)mp.n_waves) return -1;
   const int wid = (int)(slot >> 1), sub = (int)(slot & 1);
   const int b = mp.wave_rollouts ? mp.wave_rollouts[2 * wid + sub] : 2 * wid + sub;
   if (b < 0 || b >= a.n_rollouts) return -1;
   const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
-  if ((int)(item % HS_LMAX) >= T->n_limbs) return -1;
+  if ((int)(item % nli) >= T->n_limbs) return -1;
   // kin_sample's turning / record-transform path (the step kernel's test, in the working precision)
   if ((real)a.params[b].curvature != 0 || a.params[b].rec_transform_flag) return -1;
   return wid;
 }
 __device__ inline void ktab_item(const hs_topo* __restrict__ T0, const hs_run_args& a, RolloutWS* __restrict__ rws,
                                  const hs::launch_map& mp, int64_t item, int wid) {
-  const int L = (int)(item % HS_LMAX);
-  const int64_t slot = item / HS_LMAX / mp.ktab_n;
-  const int s = (int)(item / HS_LMAX % mp.ktab_n);
+  const int nli = ktab_lanes(mp);
+  const int L = (int)(item % nli);
+  const int64_t slot = item / nli / mp.ktab_n;
+  const int s = (int)(item / nli % mp.ktab_n);  // table row s: sample ktab_lo + s
   const int b = mp.wave_rollouts ? mp.wave_rollouts[slot] : (int)slot;
   const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
   const GaitR g = load_gait(a.params[b]);
   const RolloutWS& w = rws[b];
-  const real t = sample_time(w.st, w.t_tab, s);
+  const real t = sample_time(w.st, w.t_tab, mp.ktab_lo + s);
   const real tv = t * w.st.v;
   const hs_aff34& Jp0 = T->node[0].J_A_parent;
   const real u[3] = {(real)Jp0.m[0], (real)Jp0.m[1], (real)Jp0.m[2]};
@@ -2824,17 +2852,23 @@ __device__ inline void ktab_item(const hs_topo* __restrict__ T0, const hs_run_ar
 // the setup pass and the step launches run batch wavefront wid on the XCD of block wid (fused steps:
 // when the batch's wavefront count is a multiple of 8), so block t = 8 q + x takes the items of
 // wavefront 8 (q / bpw) + x: its table rows are written on the XCD whose L2 the steps read them from
-__host__ __device__ inline int ktab_blocks_per_wave(int nt) { return (2 * nt * HS_LMAX + WAVE - 1) / WAVE; }
+__host__ __device__ inline int ktab_blocks_per_wave(int nt, int nli) { return (2 * nt * nli + WAVE - 1) / WAVE; }
 __global__ __launch_bounds__(WAVE, HS_KTAB_WAVES) void hs_ktab_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
                                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
-  const int bpw = ktab_blocks_per_wave(mp.ktab_n);
-  const int x = (int)(blockIdx.x % 8), q = (int)(blockIdx.x / 8);
-  const int w = 8 * (q / bpw) + x;
-  const int local = (q % bpw) * WAVE + (int)threadIdx.x;
-  if (w >= mp.n_waves || local >= 2 * mp.ktab_n * HS_LMAX) return;
-  const int64_t item = (int64_t)w * 2 * mp.ktab_n * HS_LMAX + local;
-  const int wid = ktab_item_wave(T0, a, mp, item);
-  if (wid >= 0) ktab_item(T0, a, rws, mp, item, wid);
+  const int nli = ktab_lanes(mp);
+  const int bpw = ktab_blocks_per_wave(mp.ktab_n, nli);
+  const int64_t n_blocks = 8 * (int64_t)bpw * ((mp.n_waves + 7) / 8);
+  // logical block lb = 8 q + x (a grid of a multiple of 8 keeps its XCD)
+  for (int64_t lb = blockIdx.x; lb < n_blocks; lb += gridDim.x) {
+    const int x = (int)(lb % 8);
+    const int64_t q = lb / 8;
+    const int w = (int)(8 * (q / bpw) + x);
+    const int local = (int)(q % bpw) * WAVE + (int)threadIdx.x;
+    if (w >= mp.n_waves || local >= 2 * mp.ktab_n * nli) continue;
+    const int64_t item = (int64_t)w * 2 * mp.ktab_n * nli + local;
+    const int wid = ktab_item_wave(T0, a, mp, item);
+    if (wid >= 0) ktab_item(T0, a, rws, mp, item, wid);
+  }
 }
 
 // The setup pass and the IK table in one launch (hs_run_calls): blocks take tickets in the order
@@ -2889,9 +2923,10 @@ __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_t
   };
   for (int spin = 0; poll() != mp.prep_epoch; spin++) {
     if (spin >= (1 << 20)) {
-      const int64_t slot = item / HS_LMAX / mp.ktab_n;
+      const int nli = ktab_lanes(mp);
+      const int64_t slot = item / nli / mp.ktab_n;
       const int b = mp.wave_rollouts ? mp.wave_rollouts[slot] : (int)slot;
-      real* e = rws[b].ktab[item / HS_LMAX % mp.ktab_n][item % HS_LMAX];
+      real* e = rws[b].ktab[item / nli % mp.ktab_n][item % nli];
       for (int i = 0; i < KT_W; i++) e[i] = __builtin_nan("");
       return;
     }
@@ -2944,11 +2979,23 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   const int nl = T->n_limbs;
   // the gait setup of the rollout, stored by the call's setup pass (hs_setup_kernel / hs_prep_kernel;
   // the idle half reads its neighbour's): read from global memory where it is used
+#if HS_ST_LDS
+  {
+    constexpr int NW = sizeof(SetupL) / sizeof(real);
+    const real* cache = reinterpret_cast<const real*>(&rws[bb].st);
+    real* lds = reinterpret_cast<real*>(&smem[sub].st);
+    for (int e = lane; e < NW; e += HALF) lds[e] = cache[e];
+    wave_sync();
+  }
+  const SetupL& st = smem[sub].st;
+#else
   const SetupL& st = rws[bb].st;
+#endif
   const int i = k0 + 2;  // centre sample of this launch's step
   const int sl = lane / nl, L = lane % nl;
   const real* kt = mp.ktab_n > 0 ? &rws[bb].ktab[0][0][0] : nullptr;
-  const StraightPre pre = straight_preload(st, rws[bb].t_tab, rws[bb].kf, kt, i - 2 + (sl < NS ? sl : 0), L);
+  const StraightPre pre = straight_preload(st, rws[bb].t_tab, rws[bb].kf, HS_KTE_PRELOAD ? kt : nullptr,
+                                           i - 2 + (sl < NS ? sl : 0), mp.ktab_lo, L);
   const GaitR g = load_gait(a.params[bb]);
   const bool ignore_reach = a.ignore_reach != 0;
 
@@ -2963,7 +3010,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
     if (sl < NS) {
       if (g.curvature == 0 && !g.rec_xf) {
         kin_sample_straight(T, g, a.params[bb], st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
-                            pre, rws[bb].kf, kt);
+                            pre, rws[bb].kf, kt, mp.ktab_lo);
       } else {
         kin_sample<false>(T, g, a.params[bb], st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
                           t_tab);
@@ -3104,9 +3151,21 @@ size_t general_workspace_bytes_f32() { return sizeof(RolloutWS); }
 size_t general_workspace_bytes() { return sizeof(RolloutWS); }
 size_t solve_workspace_bytes() { return sizeof(SolveWS); }  // >= the fp32 build's
 
-int32_t ktab_samples(int32_t n_t, int32_t horizon, int64_t steps) {
-  const int64_t nt = (int64_t)n_t + horizon + 3;  // fused sample indices: k0 < n_t + horizon - 1, + NS - 1
-  return (nt <= HS_KTAB && steps * NS > nt) ? (int32_t)nt : 0;
+void ktab_range(int32_t k0, int32_t n_t, int32_t horizon, int64_t n_calls, int32_t* lo_out, int32_t* n_out) {
+  // call c starts at centre sample (k0 + c horizon) % n_t + 2 (the fused and the per-step paths
+  // alike) and its steps read that first k0 + [0, horizon + NS - 1); the first k0s repeat with a
+  // period dividing n_t
+  int64_t lo = INT64_MAX, hi = 0;
+  const int64_t nc = n_calls < n_t ? n_calls : n_t;
+  for (int64_t c = 0; c < nc; c++) {
+    const int64_t f = ((int64_t)k0 + c * horizon) % n_t;
+    lo = f < lo ? f : lo;
+    hi = f + horizon + NS - 1 > hi ? f + horizon + NS - 1 : hi;
+  }
+  const int64_t n = hi - lo;
+  const bool use = nc > 0 && n <= HS_KTAB && n_calls * horizon * NS > n;
+  *lo_out = use ? (int32_t)lo : 0;
+  *n_out = use ? (int32_t)n : 0;
 }
 
 int launch_pergen_rec(const hs_topo* d_topo, const hs_gait_params* params, int32_t n_rollouts, const double* times,
@@ -3170,7 +3229,7 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   RolloutWS* ws = (RolloutWS*)workspace;
   if (mp.setup_only) {
     if (HS_PREP && mp.ktab_n > 0 && mp.prep_ctr) {  // the setup pass and the IK table in one launch
-      const int64_t items = 2 * (int64_t)mp.n_waves * mp.ktab_n * HS_LMAX;
+      const int64_t items = 2 * (int64_t)mp.n_waves * mp.ktab_n * (mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX);
       hipLaunchKernelGGL(hs_prep_kernel, dim3((unsigned)(mp.n_waves + (items + WAVE - 1) / WAVE)), dim3(WAVE), 0, st,
                          d_topo, a, ws, mp);
       return (int)hipGetLastError();
@@ -3178,7 +3237,9 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
     hipLaunchKernelGGL(hs_setup_kernel, dim3((mp.n_waves + HS_SETUP_WAVES - 1) / HS_SETUP_WAVES),
                        dim3(WAVE * HS_SETUP_WAVES), 0, st, d_topo, a, ws, mp);
     if (mp.ktab_n > 0) {  // the call's IK table, from the frames the setup pass stored
-      const int64_t blocks = 8 * (int64_t)ktab_blocks_per_wave(mp.ktab_n) * ((mp.n_waves + 7) / 8);
+      int64_t blocks =
+          8 * (int64_t)ktab_blocks_per_wave(mp.ktab_n, mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX) * ((mp.n_waves + 7) / 8);
+      if (HS_KTAB_GRID > 0 && blocks > HS_KTAB_GRID) blocks = HS_KTAB_GRID / 8 * 8;
       hipLaunchKernelGGL(hs_ktab_kernel, dim3((unsigned)blocks), dim3(WAVE), 0, st, d_topo, a, ws, mp);
     }
     return (int)hipGetLastError();

@@ -20,6 +20,10 @@ for i in 1 2; do
 done
 timeout -k 10 300 python bench.py --forces --steps 20 --warmup 5 > $OUT/bench_forces.json 2> $OUT/bench_forces.err || { echo forces failed; tail -20 $OUT/bench_forces.err; exit 1; }
 python -c "import json;d=json.load(open('$OUT/bench_forces.json'));print('forces', round(d['value']/1e6,2), 'M; kernel us/step', round(d['roofline']['kernel_ms']*1e3,3))"
+for w in "--model spider --rollouts 16384 --horizon 32 --fp32" "--model spider --rollouts 16384 --horizon 32" "--mixed" "--model myant" "--rollouts 32768" "--curved" "--sim" "--sim --fp32 --model spider --rollouts 16384"; do
+  timeout -k 10 180 python -u bench.py --no-cpu $w >> $OUT/other_workloads.jsonl 2>>$OUT/other.err || { echo "other workload failed: $w"; tail -5 $OUT/other.err; exit 1; }
+  tail -1 $OUT/other_workloads.jsonl | python -c "import json,sys;d=json.loads(sys.stdin.read());print('$w', round(d['value']/1e6,3), 'M', d['unit'])"
+done
 FUSED=1 timeout -k 10 120 python tools/stamps.py > $OUT/stamps_fused.txt 2>&1 || { echo stamps failed; tail -5 $OUT/stamps_fused.txt; exit 1; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu > $OUT/prof.log 2>&1 || { echo prof failed; tail -20 $OUT/prof.log; exit 1; }
