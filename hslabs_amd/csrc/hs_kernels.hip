@@ -56,9 +56,6 @@ using namespace hsd;
 // curved, 346 -> 370 M steps/s: the row's registers stay out of the turning path)
 #define HS_KTE_PRELOAD (!HS_REAL_IS_FLOAT)
 #endif
-#ifndef HS_KTAB_GRID
-#define HS_KTAB_GRID 0  // > 0: the IK table kernel's grid cap (a grid-stride loop over its blocks)
-#endif
 // timing experiments (tuning builds only)
 #ifndef HS_EXP_HINGE0
 #define HS_EXP_HINGE0 1  // Rz(0) as mul_hinge(J0, 1, 0): the same values, no sincos in the setup chain
@@ -2802,38 +2799,37 @@ __global__ __launch_bounds__(WAVE * HS_SETUP_WAVES) void hs_setup_kernel(const h
 // straight_ik of kin_sample_straight at sample s from the frames the setup pass stored. Item
 // ((2 wavefront + half) nt + sample) LMAX + limb; its wavefront, or -1 when it has nothing to do.
 __device__ inline int ktab_lanes(const hs::launch_map& mp) { return mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX; }
-__device__ inline int ktab_item_wave(const hs_topo* __restrict__ T0, const hs_run_args& a, const hs::launch_map& mp,
-                                     int64_t item) {
+// Item `local` of batch wavefront w (local < 2 nt nli: half, table row, limb; 32-bit arithmetic):
+// its rollout, or -1 when it has nothing to do (an idle half, a limb the model lacks, a curved gait)
+__device__ inline int ktab_item_rollout(const hs_topo* __restrict__ T0, const hs_run_args& a, const hs::launch_map& mp,
+                                       int w, int local, int& s, int& L) {
   const int nli = ktab_lanes(mp);
-  const int64_t slot = item / nli / mp.ktab_n;
-  if (slot >= 2 * (int64_t)mp.n_waves) return -1;
-  const int wid = (int)(slot >> 1), sub = (int)(slot & 1);
-  const int b = mp.wave_rollouts ? mp.wave_rollouts[2 * wid + sub] : 2 * wid + sub;
+  L = local % nli;
+  const int r = local / nli;
+  s = r % mp.ktab_n;
+  const int sub = r / mp.ktab_n;
+  if (w >= mp.n_waves || sub > 1) return -1;
+  const int b = mp.wave_rollouts ? mp.wave_rollouts[2 * w + sub] : 2 * w + sub;
   if (b < 0 || b >= a.n_rollouts) return -1;
-  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
-  if ((int)(item % nli) >= T->n_limbs) return -1;
+  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[w] : T0;
+  if (L >= T->n_limbs) return -1;
   // kin_sample's turning / record-transform path (the step kernel's test, in the working precision)
   if ((real)a.params[b].curvature != 0 || a.params[b].rec_transform_flag) return -1;
-  return wid;
+  return b;
 }
 __device__ inline void ktab_item(const hs_topo* __restrict__ T0, const hs_run_args& a, RolloutWS* __restrict__ rws,
-                                 const hs::launch_map& mp, int64_t item, int wid) {
-  const int nli = ktab_lanes(mp);
-  const int L = (int)(item % nli);
-  const int64_t slot = item / nli / mp.ktab_n;
-  const int s = (int)(item / nli % mp.ktab_n);  // table row s: sample ktab_lo + s
-  const int b = mp.wave_rollouts ? mp.wave_rollouts[slot] : (int)slot;
-  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
+                                 const hs::launch_map& mp, int w, int b, int s, int L) {
+  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[w] : T0;
   const GaitR g = load_gait(a.params[b]);
-  const RolloutWS& w = rws[b];
-  const real t = sample_time(w.st, w.t_tab, mp.ktab_lo + s);
-  const real tv = t * w.st.v;
+  const RolloutWS& ws = rws[b];
+  const real t = sample_time(ws.st, ws.t_tab, mp.ktab_lo + s);  // table row s: sample ktab_lo + s
+  const real tv = t * ws.st.v;
   const hs_aff34& Jp0 = T->node[0].J_A_parent;
   const real u[3] = {(real)Jp0.m[0], (real)Jp0.m[1], (real)Jp0.m[2]};
-  const A34 J = frame_at(load34r(w.kf.J0[L]), u, tv);
+  const A34 J = frame_at(load34r(ws.kf.J0[L]), u, tv);
   real ja[3];
   bool bad;
-  straight_ik(T, g, a.params[b], w.st, t, L, J, a.ignore_reach != 0, ja, bad);
+  straight_ik(T, g, a.params[b], ws.st, t, L, J, a.ignore_reach != 0, ja, bad);
   real* e = rws[b].ktab[s][L];
 #pragma unroll
   for (int kk = 0; kk < 3; kk++) {
@@ -2857,18 +2853,12 @@ __global__ __launch_bounds__(WAVE, HS_KTAB_WAVES) void hs_ktab_kernel(const hs_t
                                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
   const int nli = ktab_lanes(mp);
   const int bpw = ktab_blocks_per_wave(mp.ktab_n, nli);
-  const int64_t n_blocks = 8 * (int64_t)bpw * ((mp.n_waves + 7) / 8);
-  // logical block lb = 8 q + x (a grid of a multiple of 8 keeps its XCD)
-  for (int64_t lb = blockIdx.x; lb < n_blocks; lb += gridDim.x) {
-    const int x = (int)(lb % 8);
-    const int64_t q = lb / 8;
-    const int w = (int)(8 * (q / bpw) + x);
-    const int local = (int)(q % bpw) * WAVE + (int)threadIdx.x;
-    if (w >= mp.n_waves || local >= 2 * mp.ktab_n * nli) continue;
-    const int64_t item = (int64_t)w * 2 * mp.ktab_n * nli + local;
-    const int wid = ktab_item_wave(T0, a, mp, item);
-    if (wid >= 0) ktab_item(T0, a, rws, mp, item, wid);
-  }
+  const int x = (int)(blockIdx.x % 8), q = (int)(blockIdx.x / 8);
+  const int w = 8 * (q / bpw) + x;
+  const int local = (q % bpw) * WAVE + (int)threadIdx.x;
+  int s, L;
+  const int b = ktab_item_rollout(T0, a, mp, w, local, s, L);
+  if (b >= 0) ktab_item(T0, a, rws, mp, w, b, s, L);
 }
 
 // The setup pass and the IK table in one launch (hs_run_calls): blocks take tickets in the order
@@ -2910,8 +2900,11 @@ __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_t
     return;
   }
   const int64_t item = (int64_t)(tk - (uint32_t)mp.n_waves) * WAVE + threadIdx.x;
-  const int wid = ktab_item_wave(T0, a, mp, item);
-  if (wid < 0) return;
+  const int per_wave = 2 * mp.ktab_n * ktab_lanes(mp);
+  const int wid = (int)(item / per_wave);
+  int s, L;
+  const int b = ktab_item_rollout(T0, a, mp, wid, (int)(item % per_wave), s, L);
+  if (b < 0) return;
   // bounded (~0.3 s): a setup that never published would leave NaN joint values, not a hung GPU
   // (relaxed polls, then one acquire: an acquire per poll invalidates the caches the setup waves use)
   auto poll = [&]() {
@@ -2923,17 +2916,14 @@ __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_t
   };
   for (int spin = 0; poll() != mp.prep_epoch; spin++) {
     if (spin >= (1 << 20)) {
-      const int nli = ktab_lanes(mp);
-      const int64_t slot = item / nli / mp.ktab_n;
-      const int b = mp.wave_rollouts ? mp.wave_rollouts[slot] : (int)slot;
-      real* e = rws[b].ktab[item / nli % mp.ktab_n][item % nli];
+      real* e = rws[b].ktab[s][L];
       for (int i = 0; i < KT_W; i++) e[i] = __builtin_nan("");
       return;
     }
     __builtin_amdgcn_s_sleep(HS_PREP_SLEEP);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  ktab_item(T0, a, rws, mp, item, wid);
+  ktab_item(T0, a, rws, mp, wid, b, s, L);
 }
 
 // One wavefront's step: fused step fstep (0 outside fused launches) of batch wavefront wid. only_sub
@@ -3237,9 +3227,8 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
     hipLaunchKernelGGL(hs_setup_kernel, dim3((mp.n_waves + HS_SETUP_WAVES - 1) / HS_SETUP_WAVES),
                        dim3(WAVE * HS_SETUP_WAVES), 0, st, d_topo, a, ws, mp);
     if (mp.ktab_n > 0) {  // the call's IK table, from the frames the setup pass stored
-      int64_t blocks =
+      const int64_t blocks =
           8 * (int64_t)ktab_blocks_per_wave(mp.ktab_n, mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX) * ((mp.n_waves + 7) / 8);
-      if (HS_KTAB_GRID > 0 && blocks > HS_KTAB_GRID) blocks = HS_KTAB_GRID / 8 * 8;
       hipLaunchKernelGGL(hs_ktab_kernel, dim3((unsigned)blocks), dim3(WAVE), 0, st, d_topo, a, ws, mp);
     }
     return (int)hipGetLastError();
