@@ -669,13 +669,9 @@ def main():
         if flop is not None and not args.fp32:
             alg_flops = flop["flops_per_step"] * B * Hh
             tf = alg_flops / (kern_ms * 1e-3) / 1e12
-            win = (flop.get("kernel_window") or {}).get("flops_per_step")
             fp64 = {"bound": "fp64 valu", "algorithmic_flops_per_step": flop["flops_per_step"],
                     "achieved_tflops": round(tf, 3), "peak_tflops": FP64_PEAK_TFLOPS, "frac": tf / FP64_PEAK_TFLOPS,
                     "source": "profiles/flops.json: " + str(flop.get("source"))}
-            if win:  # what the kernel issues: the 5-sample stencil window recomputed for every step
-                fp64["kernel_window_flops_per_step"] = win
-                fp64["kernel_window_tflops"] = round(win * B * Hh / (kern_ms * 1e-3) / 1e12, 3)
             if pmc is not None and pmc.get("fp64_lane_flops_per_step"):
                 issued = pmc["fp64_lane_flops_per_step"] * B / pmc["rollouts"]
                 fp64["issued_lane_flops_per_step_of_batch"] = int(issued)
