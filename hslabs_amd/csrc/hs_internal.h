@@ -121,9 +121,9 @@ int launch_sim_steps(const hs_topo* d_topo, const hs_simtopo* d_sim, const hs_si
 
 constexpr int HS_MAX_DEVICES = 64;
 
-// Per-rollout device workspaces (general-path scratch + the setup cache), one per
-// (device, stream): launches on one stream run in order, so a call's launches may pass
-// the setup cache from one to the next, and calls on different streams never share one.
+// Per-rollout device workspaces (general-path scratch, the setup record, the IK table), one per
+// (device, stream): launches on one stream run in order, so a call's setup pass hands the record
+// to its step launches, and calls on different streams never share one.
 struct ws_pool {
   struct slot {
     int dev;

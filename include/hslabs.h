@@ -189,7 +189,10 @@ int hs_run(hs_model_t model, const hs_run_args* args);
  * args->best_key) is taken once, after the last call, over the accumulated work
  * (key_steps 0 = n_calls * horizon steps). kernel_events, if not
  * NULL, holds 2 * n_calls caller-created hipEvent_t recorded immediately before
- * and after each launch (per-launch kernel timing on the launch stream). */
+ * and after each launch (per-launch kernel timing on the launch stream). Every call
+ * (hs_run, hs_run_steps, hs_run_calls, the forces and PD forms) first runs the setup
+ * pass: each rollout's gait setup, a straight gait's frames and, when the steps read
+ * more samples than it holds, the limb IK of those samples (before the events). */
 int hs_run_steps(hs_model_t model, const hs_run_args* args, int32_t n_calls, void* const* kernel_events);
 
 /* Position control (modelplayer::set_position_control_torques +

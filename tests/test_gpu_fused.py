@@ -319,3 +319,34 @@ def test_fused_straight_and_curved_rollouts(gpu, hmodels, n_t, pattern):
     for k in ("q", "dq", "tau", "cf", "x", "flags", "work_cot", "best_key"):
         assert np.array_equal(npy(getattr(ref, k)), npy(getattr(fz, k)), equal_nan=True), k
     assert np.isfinite(npy(fz.tau)).all()
+
+
+@pytest.mark.parametrize("name,k0,H,n_calls", [("hexapod", 7, 5, 3), ("myant", 13, 2, 9), ("hexapod", 18, 1, 6)])
+def test_ik_table_rows_match_single_steps(gpu, hmodels, name, k0, H, n_calls):
+    """The IK table covers the samples [lo, lo + n) a call reads (hs::ktab_range; here lo > 0 and,
+    for k0 = 18, calls that wrap mod n_t). Every step of the fused call equals the same step run on
+    its own (one launch, one step: no table, the IK solved inline by the step kernel) to rounding:
+    a table row off by one sample would move the torques by O(1)."""
+    import torch
+    from hslabs_amd import synth
+
+    m = hmodels[name]
+    B, n_t = 64, 20
+    p = synth.gen_params(B, name, id0=555)
+    fz = gpu.DeviceBatch(m, p, n_t=n_t, k0=k0, horizon=n_calls * H, outputs=("tau", "cf", "q"))
+    fz.run_calls(n_calls, call_horizon=H)
+    torch.cuda.synchronize()
+    tau = npy(fz.tau)
+    q = npy(fz.q)
+    for c in range(n_calls):
+        for h in range(H):
+            kk = (k0 + c * H) % n_t + h
+            if kk >= n_t:  # a single call from kk would start at kk mod n_t
+                continue
+            one = gpu.DeviceBatch(m, p, n_t=n_t, k0=kk, horizon=1, outputs=("tau", "cf", "q"))
+            one.run()
+            torch.cuda.synchronize()
+            row = c * H + h
+            ref_tau, ref_q = npy(one.tau)[:, 0], npy(one.q)[:, 0]
+            assert np.allclose(q[:, row], ref_q, rtol=0, atol=1e-12), (c, h)
+            assert np.allclose(tau[:, row], ref_tau, rtol=1e-9, atol=1e-9), (c, h)
