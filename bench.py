@@ -327,25 +327,41 @@ def main_sim(args, torch, dist, world, rank, dev):
 FORCES_METRIC = "solve_forces steps/sec: contact forces given motor torques (ftsolver.cpp:331-378)"
 
 
-def forces_cpu_baseline(name, params, tau, n_t, seconds):
-    """Oracle solve_forces (dense least squares of the reference's B with torque rows, Householder
-    QR; oracle/hs_oracle.cpp) on a bounded sample of the same batch and torques, one thread."""
+def forces_cpu_baseline(name, params, tau, n_t, seconds, threads=None):
+    """Oracle solve_forces (the reference's B with the torque rows, torso columns out, a column-by-
+    column Householder QR with the kernel's rank rule; oracle/hs_oracle.cpp) on a bounded sample of
+    the same batch and torques, built and threaded like the control loop's baseline (cpu_baseline):
+    g++ -O3 -march=native for this host's CPU, std::thread over the rollouts."""
     from oracle import oracle as O
 
-    om = O.Model(os.path.join(ROOT, "models", f"{name}.xml"))
+    cpus = host_cpus()
+    threads = max(1, threads or cpus["usable"])
+    build = "g++ -O3 -march=native"
+    try:
+        L, _ = O.perf_lib(cpus["model"])
+    except Exception as e:
+        L, build = O.lib(), f"g++ -O2 -ffp-contract=off (native build failed: {type(e).__name__})"
+    om = O.Model(os.path.join(ROOT, "models", f"{name}.xml"), L=L)
     gaits = _oracle_gaits(O, params)
-    done, t0, b = 0, time.perf_counter(), 0
-    while True:
-        O.forces(om, gaits[b % len(gaits)], tau[b % len(gaits)], n_t=n_t)
-        done += tau.shape[1]
-        b += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": round(done / el, 1), "unit": "steps/s", "cores": 1, "kind": "port",
-            "sample": f"{done} solve_forces steps ({name}, {b} rollouts of the batch x {tau.shape[1]} steps, the "
-                      f"batch's own torques) in {el:.1f}s: oracle dense least squares (Householder QR of the "
-                      f"reference's B with the torque rows), g++ -O2, one thread"}
+    tau = np.ascontiguousarray(tau, dtype=np.float64)
+
+    def timed(nthr, budget):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            O.forces_batch(om, gaits, tau, n_t=n_t, n_threads=nthr, L=L)
+            done += tau.shape[0] * tau.shape[1]
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return done / el, done, el
+
+    single, _, _ = timed(1, min(2.0, seconds / 4))
+    rate, done, el = timed(threads, seconds)
+    return {"value": round(rate, 1), "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"{done} solve_forces steps ({name}, {tau.shape[0]} rollouts of the batch x {tau.shape[1]} steps, "
+                      f"the batch's own torques) in {el:.1f}s: oracle least squares (Householder QR of the reference's "
+                      f"B with the torque rows), {build}, std::thread x{threads}; single-thread {single:.1f} steps/s",
+            "single_thread": round(single, 1),
+            "host": {"cpu_model": cpus["model"], "threads_used": threads}}
 
 
 def main_forces(args, torch, dist, world, rank, dev):
@@ -424,8 +440,9 @@ def main_forces(args, torch, dist, world, rank, dev):
             "check": {"max_rel_cf_vs_control_loop": err, "general_steps": general},
             "lib": lib,
         }
+        nb = min(B, 256)
         out["cpu_baseline"] = None if (args.no_cpu or world > 1) else forces_cpu_baseline(
-            args.model, params[:64], ctl.tau[:64, :K].cpu().numpy(), n_t, min(args.cpu_seconds, 5.0))
+            args.model, params[:nb], ctl.tau[:nb, :K].cpu().numpy(), n_t, args.cpu_seconds, args.cpu_threads)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -25,6 +25,12 @@ GAIT_DTYPE = np.dtype([
 ])
 assert GAIT_DTYPE.itemsize == 192
 
+
+def _require(ok: bool, msg: str) -> None:
+    """argument check that survives python -O (the native call would read past a short tensor)"""
+    if not ok:
+        raise ValueError(msg)
+
 SWEEP_NAMES = ("step_duration", "period", "step_length", "step_height")  # pergen.cpp:423
 
 
@@ -311,7 +317,7 @@ class Comm:
     constructs a Comm with its device current."""
 
     def __init__(self, n_ranks: int, rank: int, uid: bytes):
-        assert len(uid) == capi.COMM_ID_BYTES
+        _require(len(uid) == capi.COMM_ID_BYTES, f"a comm id is {capi.COMM_ID_BYTES} bytes")
         h = ctypes.c_void_p()
         capi.check(capi.load().hs_comm_init(n_ranks, rank, uid, ctypes.byref(h)), "hs_comm_init")
         self.handle, self.n_ranks, self.rank = h, n_ranks, rank
@@ -425,7 +431,7 @@ class DeviceBatch:
         q = q_meas.to(**f64).contiguous()
         dq = dq_meas.to(**f64).contiguous()
         shape = (self.B, self.H, self.model.nmj)
-        assert q.shape == shape and dq.shape == shape
+        _require(q.shape == shape and dq.shape == shape, f"q_meas / dq_meas must be {shape}")
         out = torch.empty(shape, **f64)
         q0 = torch.empty(shape, **f64) if targets else None
         dq0 = torch.empty(shape, **f64) if targets else None
@@ -441,7 +447,7 @@ class DeviceBatch:
         forcetorquesolver::solve_forces): tau_in is a device tensor [B][H][nmj]; writes
         self.cf (and q / flags if allocated)."""
         t = tau_in.to(dtype=self.dtype, device=self.device).contiguous()
-        assert t.shape == (self.B, self.H, self.model.nmj)
+        _require(t.shape == (self.B, self.H, self.model.nmj), f"tau_in must be {(self.B, self.H, self.model.nmj)}")
         a = self._args(stream, False, False)
         a.tau = a.x = a.work_cot = None
         capi.check(capi.load().hs_run_forces(self.model.handle, ctypes.byref(a), t.data_ptr()), "hs_run_forces")
@@ -452,9 +458,9 @@ class DeviceBatch:
         (hs_run_forces_calls): tau_in is a device tensor [B][S][nmj] with S = n_calls *
         call_horizon = this batch's horizon; every step writes its own row of cf (and q / flags)."""
         S = n_calls * call_horizon
-        assert self.H == S, "the batch's horizon must equal n_calls * call_horizon (one row per step)"
+        _require(self.H == S, "the batch's horizon must equal n_calls * call_horizon (one row per step)")
         t = tau_in.to(dtype=self.dtype, device=self.device).contiguous()
-        assert t.shape == (self.B, S, self.model.nmj)
+        _require(t.shape == (self.B, S, self.model.nmj), f"tau_in must be {(self.B, S, self.model.nmj)}")
         a = self._args(stream, False, False)
         a.tau = a.x = a.work_cot = None
         a.horizon = call_horizon
@@ -466,9 +472,9 @@ class DeviceBatch:
         """run_forces_calls(...) with its arguments resolved once: a no-argument callable that only
         enqueues the fused launches (bench.py --forces' timed loop)."""
         S = n_calls * call_horizon
-        assert self.H == S, "the batch's horizon must equal n_calls * call_horizon (one row per step)"
+        _require(self.H == S, "the batch's horizon must equal n_calls * call_horizon (one row per step)")
         t = tau_in.to(dtype=self.dtype, device=self.device).contiguous()
-        assert t.shape == (self.B, S, self.model.nmj)
+        _require(t.shape == (self.B, S, self.model.nmj), f"tau_in must be {(self.B, S, self.model.nmj)}")
         a = self._args(stream, False, False)
         a.tau = a.x = a.work_cot = None
         a.horizon = call_horizon
@@ -490,7 +496,7 @@ class DeviceBatch:
         a = self._args(stream, best, accumulate)
         ev = None
         if events is not None:
-            assert len(events) == 2 * n_calls
+            _require(len(events) == 2 * n_calls, "events must hold 2 * n_calls events")
             st = stream if stream is not None else self.torch.cuda.current_stream(self.device)
             for e in events:  # torch creates the HIP event on first record
                 if not e.cuda_event:
@@ -503,7 +509,7 @@ class DeviceBatch:
                        accumulate: bool = True):
         """run_calls(...) with its arguments resolved once: returns a no-argument callable that only
         enqueues the fused launches (for timed loops: no per-call pointer lookups in Python)."""
-        assert self.H >= n_calls * call_horizon, "outputs need one row per fused step"
+        _require(self.H >= n_calls * call_horizon, "outputs need one row per fused step")
         a = self._args(stream, best, accumulate)
         a.horizon = call_horizon
         L = capi.load()
@@ -526,7 +532,7 @@ class DeviceBatch:
         fused into few launches (hs_run_calls): every step keeps its own output row, rows packed
         per rollout with stride n_calls * call_horizon, so this batch's horizon must be at least
         that (equal: the [B][H] views hold the steps in order)."""
-        assert self.H >= n_calls * call_horizon, "outputs need one row per fused step"
+        _require(self.H >= n_calls * call_horizon, "outputs need one row per fused step")
         a = self._args(stream, best, accumulate)
         a.horizon = call_horizon
         L = capi.load()
@@ -663,7 +669,7 @@ class MixedBatch(DeviceBatch):
         capi.check(L.hs_mixed_get_dims(plan, ctypes.byref(d)), "hs_mixed_get_dims")
         self.dims = d
         self.model = self.models[0]
-        assert len(params_array(params)) == len(self.model_index)
+        _require(len(params_array(params)) == len(self.model_index), "one parameter record per rollout of the plan")
         self._alloc(d, params, n_t, k0, horizon, ignore_reach, outputs, device, rollout_id_base, dtype)
 
     def _launch(self, a, n_calls, ev):

@@ -43,7 +43,7 @@ void free_on_device(int dev, void* p) {
 
 }  // namespace
 
-int ws_pool::get(void* stream, size_t n, void** out, bool zero) {
+int ws_pool::get(void* stream, size_t n, void** out) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return (int)e;
@@ -52,8 +52,6 @@ int ws_pool::get(void* stream, size_t n, void** out, bool zero) {
     if (s.n < n) {
       void* w = nullptr;
       e = hipMalloc(&w, n * hs::general_workspace_bytes());  // fp64 slot >= fp32 slot
-      if (e != hipSuccess) return (int)e;
-      if (zero) e = hipMemsetAsync(w, 0, n * hs::general_workspace_bytes(), (hipStream_t)stream);
       if (e != hipSuccess) return (int)e;
       retired.emplace_back(dev, s.ptr);
       s.ptr = w;
@@ -64,8 +62,6 @@ int ws_pool::get(void* stream, size_t n, void** out, bool zero) {
   }
   void* w = nullptr;
   e = hipMalloc(&w, n * hs::general_workspace_bytes());
-  if (e != hipSuccess) return (int)e;
-  if (zero) e = hipMemsetAsync(w, 0, n * hs::general_workspace_bytes(), (hipStream_t)stream);
   if (e != hipSuccess) return (int)e;
   live.push_back({dev, stream, w, n});
   *out = w;
@@ -147,12 +143,10 @@ int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::lau
   // one gait setup per rollout per call: the setup pass of the fused path (hs_setup_kernel, with the
   // straight gaits' IK table when it pays, hs_ktab_kernel) stores it and every launch loads it, so the
   // kinematics of these launches and of hs_run_calls' fused launches come from the same kernels
-  const int64_t S = (int64_t)n_calls * a.horizon;
   hs::launch_map base = mp;
   base.setup_only = 1;
   base.setup_io = hs::SETUP_STORE;
   base.fix_n_counts = 0;
-  base.prep_ctr = nullptr;  // two launches (the prep kernel's counter lives in the fused path's pools)
   hs::ktab_range(a.k0, a.n_t, a.horizon, n_calls, &base.ktab_lo, &base.ktab_n);
   const int le0 = (a.precision == HS_PREC_F32) ? hs::launch_fused_f32(d, c, ws, base) : hs::launch_fused(d, c, ws, base);
   if (le0 != 0) return hip_fail((hipError_t)le0, "kernel launch (setup pass)");
@@ -197,18 +191,10 @@ int check_args(const hs_model_s* m, const hs_run_args* a) {
   return HS_OK;
 }
 
-// a fresh nonzero value per prep launch (hs_prep_kernel's setup flags; zeroed memory holds none)
-uint32_t next_epoch() {
-  static std::atomic<uint32_t> epoch{0};
-  uint32_t e;
-  do e = epoch.fetch_add(1) + 1; while (e == 0);
-  return e;
-}
-
 // hs_run_calls / hs_run_mixed_calls: a setup-only pass, launches of CHUNK steps over (step, wavefront),
 // the in-order work reduce. Each step in flight in a launch has its own general-path scratch.
 int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map mp, ws_pool& gen_pool,
-              ws_pool& work_pool, ws_pool& fix_pool, ws_pool& prep_pool, std::mutex& mu, double total_mass, const double* rollout_mass,
+              ws_pool& work_pool, ws_pool& fix_pool, std::mutex& mu, double total_mass, const double* rollout_mass,
               int32_t n_calls) {
   const int64_t S = (int64_t)n_calls * a.horizon;  // steps, one output row each
   if (S > (1 << 24)) return fail(HS_E_ARG, "too many steps");
@@ -235,11 +221,7 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   // launch (zeroed by the setup pass), then the items
   const size_t fix_counts_bytes = ((size_t)n_chunks * sizeof(int32_t) + 255) / 256 * 256;
   const size_t fix_bytes = fix_counts_bytes + (size_t)CHUNK * mp.n_waves * 2 * 2 * sizeof(int32_t);
-  // the prep launch's ticket counter and per-wavefront setup flags (hs_prep_kernel), in a pool of their
-  // own that holds nothing else: zeroed when allocated, the counter back at 0 after every launch, the
-  // flags at past epochs
-  const size_t prep_bytes = 256 + (size_t)mp.n_waves * sizeof(uint32_t);
-  void *gen = nullptr, *work = nullptr, *fix = nullptr, *prep = nullptr;
+  void *gen = nullptr, *work = nullptr, *fix = nullptr;
   {
     std::lock_guard<std::mutex> lk(mu);
     // the general-path scratch of every step in flight: [CHUNK][B + 1] SolveWS (in workspace units)
@@ -253,7 +235,6 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
         std::max(need, std::min((size_t)HS_FUSED_RESERVE_STEPS * B * sizeof(double), (size_t)512 << 20));
     if (e == hipSuccess) e = (hipError_t)work_pool.get(a.stream, (want + gwb - 1) / gwb, &work);
     if (e == hipSuccess) e = (hipError_t)fix_pool.get(a.stream, (fix_bytes + gwb - 1) / gwb, &fix);
-    if (e == hipSuccess) e = (hipError_t)prep_pool.get(a.stream, (prep_bytes + gwb - 1) / gwb, &prep, true);
     if (e != hipSuccess) return hip_fail(e, "hipMalloc(fused workspace)");
   }
   int32_t* fix_counts = (int32_t*)fix;
@@ -272,9 +253,6 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   mp.fix_count = fix_counts;
   mp.fix_n_counts = n_chunks;
   hs::ktab_range(a.k0, a.n_t, a.horizon, n_calls, &mp.ktab_lo, &mp.ktab_n);  // straight gaits' IK table (setup pass)
-  mp.prep_ctr = (uint32_t*)prep;
-  mp.prep_ready = (uint32_t*)prep + 64;
-  mp.prep_epoch = next_epoch();
   int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   mp.setup_only = 0;
   mp.setup_io = hs::SETUP_LOAD;
@@ -339,7 +317,7 @@ struct hs_mixed_s {
   double* d_rollout_mass = nullptr;  // total mass of each rollout's model (the fused reduce's COT)
   int32_t torso_mask = 3;            // 3 unless a model's switch_torso_penalty (at plan creation) differs
   ws_pool ws;
-  ws_pool fused_gen, fused_work, fused_fix, fused_prep;
+  ws_pool fused_gen, fused_work, fused_fix;
   std::mutex mu;
 };
 
@@ -378,7 +356,6 @@ void hs_model_free(hs_model_t m) {
   m->fused_gen.release();
   m->fused_work.release();
   m->fused_fix.release();
-  m->fused_prep.release();
   delete m;
 }
 
@@ -488,7 +465,7 @@ int hs_run_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls) {
   if (rc != HS_OK) return rc;
   return run_fused(d, routed(*a, m->host.torso_mask), ws, hs::single_model_map(m->host, a->n_rollouts), m->fused_gen,
                    m->fused_work,
-                   m->fused_fix, m->fused_prep, m->mu, m->host.total_mass, nullptr, n_calls);
+                   m->fused_fix, m->mu, m->host.total_mass, nullptr, n_calls);
 }
 
 int hs_run_pd(hs_model_t m, const hs_run_args* a, const hs_pd_args* pd) {
@@ -641,7 +618,6 @@ void hs_mixed_free(hs_mixed_t p) {
   p->fused_gen.release();
   p->fused_work.release();
   p->fused_fix.release();
-  p->fused_prep.release();
   delete p;
 }
 
@@ -708,7 +684,7 @@ int hs_run_mixed_calls(hs_mixed_t p, const hs_run_args* a, int32_t n_calls) {
     e = (hipError_t)p->ws.get(a->stream, (size_t)p->n_rollouts + 1, &ws);
   }
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
-  return run_fused(p->d_topos, routed(*a, p->torso_mask), ws, mp, p->fused_gen, p->fused_work, p->fused_fix, p->fused_prep, p->mu, 0.0,
+  return run_fused(p->d_topos, routed(*a, p->torso_mask), ws, mp, p->fused_gen, p->fused_work, p->fused_fix, p->mu, 0.0,
                    p->d_rollout_mass,
                    n_calls);
 }
@@ -1532,6 +1508,7 @@ int hs_select_best_comm(hs_batch_t b, hs_comm_t comm, float* cot, int64_t* rollo
         rc = fail(HS_E_ARG, "the batch runs on a device the comm does not");
         best = ~0ull;
       }
+  if (rc != HS_OK) best = ~0ull;  // local_best may have failed after a partial minimum
   std::string err = rc != HS_OK ? std::string(hs_last_error()) : std::string();
   device_guard guard;
   hipStream_t st = nullptr;  // the comm device's null stream: the reduce does not use the batch's key

@@ -69,11 +69,6 @@ struct launch_map {
   // [ktab_lo, ktab_lo + ktab_n) per rollout (ktab_range), and the step launches read it instead of
   // solving it; ktab_nl: limbs per sample the table kernel enumerates (the launch's largest model)
   int32_t ktab_n, ktab_lo, ktab_nl;
-  // with ktab_n: the setup pass and the table in one launch (hs_prep_kernel): its block ticket counter
-  // (zero between launches) and per-wavefront setup flags (= prep_epoch once published)
-  uint32_t* prep_ctr;
-  uint32_t* prep_ready;
-  uint32_t prep_epoch;
 };
 
 // Kernel launcher (hs_kernels.hip). `workspace` holds general_workspace_bytes()
@@ -133,9 +128,8 @@ struct ws_pool {
   };
   std::vector<slot> live;
   std::vector<std::pair<int, void*>> retired;  // outgrown: kernels still queued may use them
-  // workspace of >= n rollouts for (current device, stream); returns a hipError_t value. zero: a new
-  // allocation is zeroed (on the stream, before anything queued after this call)
-  int get(void* stream, size_t n, void** out, bool zero = false);
+  // workspace of >= n rollouts for (current device, stream); returns a hipError_t value
+  int get(void* stream, size_t n, void** out);
   void release();
 };
 
@@ -148,6 +142,5 @@ struct hs_model_s {
   ws_pool ws;
   ws_pool fused_gen, fused_work;  // hs_run_calls: general-path scratch per (step in a launch, rollout), step work
   ws_pool fused_fix;              // hs_run_calls: fixup counters and items
-  ws_pool fused_prep;             // hs_run_calls: the prep launch's ticket counter and setup flags
   std::mutex mu;
 };

@@ -56,21 +56,11 @@ using namespace hsd;
 #ifndef HS_PRELOAD
 #define HS_PRELOAD (!HS_REAL_IS_FLOAT)  // straight_preload at wave start (0: inside the straight branch)
 #endif
-#ifndef HS_ST_LDS
-#define HS_ST_LDS 0  // 1: copy the setup record to LDS per step (round 2's layout) instead of global reads
-#endif
 #ifndef HS_KTE_PRELOAD
 // the IK table row loaded at wave start, before the gait is known to be straight (fp64: +1.3 % at
 // K = 200 on hexapod); in the fp32 build inside the straight branch (spider, whose synthetic gaits are
 // curved, 346 -> 370 M steps/s: the row's registers stay out of the turning path)
 #define HS_KTE_PRELOAD (!HS_REAL_IS_FLOAT)
-#endif
-// timing experiments (tuning builds only)
-#ifndef HS_EXP_HINGE0
-#define HS_EXP_HINGE0 1  // Rz(0) as mul_hinge(J0, 1, 0): the same values, no sincos in the setup chain
-#endif
-#ifndef HS_EXP_FENCE
-#define HS_EXP_FENCE 0
 #endif
 
 constexpr int WAVE = 64;
@@ -190,14 +180,7 @@ struct SetupL {
 // setup keeps them at tv = 0 (the products kin_sample forms, once per rollout instead of per sample).
 // IK table entry (RolloutWS::ktab): the joint values of a limb at a sample, their sines and cosines,
 // then 1 if unreachable or failed
-#ifndef HS_KT_SINCOS
-#define HS_KT_SINCOS 0  // the table also holds sin / cos of the joint values (measured slower: the
-                        // table kernel's cost outweighs the step's three sincos per lane)
-#endif
-constexpr int KT_W = HS_KT_SINCOS ? 10 : 4;
-#ifndef HS_KTAB_WAVES
-#define HS_KTAB_WAVES 1
-#endif
+constexpr int KT_W = 4;
 struct KinFrames {
   real A0[12];              // the torso (node 0)
   real J0[HS_LMAX][12];     // each limb's hip joint frame
@@ -218,8 +201,8 @@ template <int NM, bool FORCES>
 struct Smem {
   OneStore<NM, FORCES> d;
   SolveL<NM> sv;
-#if HS_ST_LDS || HS_CURVED_LDS
-  SetupL st;  // the setup pass's record, copied per step (HS_CURVED_LDS: in waves with a curved gait)
+#if HS_CURVED_LDS
+  SetupL st;  // the setup pass's record, copied per step in waves with a curved gait
 #endif
 };
 
@@ -235,6 +218,12 @@ __device__ inline void wave_sync() {
 constexpr real kEps = HS_REAL_IS_FLOAT ? FLT_EPSILON : DBL_EPSILON;
 constexpr real kTiny = HS_REAL_IS_FLOAT ? FLT_MIN : DBL_MIN;
 constexpr real kRelTol = HS_REAL_IS_FLOAT ? real(1e-4) : real(1e-6);
+// HS_FLAG_NEAR_RANK bands (include/hslabs.h; oracle/hs_oracle.cpp NearTrack): a decision whose value lies
+// within kNearBand of its threshold (rel_error: within 10x of kRelTol; ColPivQR's squared column norms:
+// within kNearBand^2) is flagged, since another rounding may take it the other way
+constexpr real kNearBand = real(4);
+// v is within `band` of threshold t (both positive; a NaN is not)
+__device__ inline bool near_thr(real v, real t, real band) { return v >= t / band && v <= t * band; }
 
 // The ABI's arrays are double*; in the fp32 build they hold floats.
 __device__ inline real* outp(double* p) { return reinterpret_cast<real*>(p); }
@@ -376,11 +365,7 @@ __device__ __attribute__((always_inline)) inline void gait_setup(const hs_topo* 
       store34r(J0, kf->J0[L]);
       if (L == 0) store34r(A0, kf->A0);
     }
-#if HS_EXP_HINGE0
-    A34 Ac = mul(mul_hinge(J0, real(1), real(0)), node_pj(T, c));  // timing experiment: Rz(0) without the sincos
-#else
-    A34 Ac = mul(mul(J0, hinge_joint(real(0))), node_pj(T, c));
-#endif
+    A34 Ac = mul(mul_hinge(J0, real(1), real(0)), node_pj(T, c));  // Rz(0): cos 0 = 1, sin 0 = 0
     real pos[3] = {Ac(0, 3), Ac(1, 3), Ac(2, 3)};  // get_limb_hip_pos
     if (g.foot_shift_type == 0) {                   // setup_foot_shift / shift_pos0
       real sh[3] = {real(0), g.foot_shift, real(0)}, ls[3];
@@ -563,12 +548,10 @@ __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g
   target[0] = dx + st.pos0[j][0];
   target[1] = dy + st.pos0[j][1];
   target[2] = dz + st.pos0[j][2];
-#ifndef HS_EXP_NO_RECXF  // timing experiment only
   if (!STRAIGHT && g.rec_xf) {  // set_rec's last step (pergen.cpp:238)
     transform_rec(gp, o0, o1, target);
     turned = true;  // the torso angles are no longer the configured ones
   }
-#endif
 }
 
 // sample times t_i = dt + dt + ... (i terms, periodic.cpp:171-181), stored once per rollout by the
@@ -737,12 +720,7 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
 #pragma unroll
     for (int kk = 0; kk < 3; kk++) {
       ja[kk] = kte[kk];
-#if HS_KT_SINCOS
-      sq[kk] = kte[3 + kk];
-      cq[kk] = kte[6 + kk];
-#else
       sincos(ja[kk], &sq[kk], &cq[kk]);
-#endif
     }
     bad = kte[KT_W - 1] != 0;
     STAMP(21);
@@ -849,7 +827,7 @@ __device__ __attribute__((always_inline)) inline void particular(const hs_topo* 
   }
 }
 
-// S1 as subtree sums (HS_S1_SUBTREE): the recursion above, unrolled. With the torso COM p0 as the
+// S1 as subtree sums: the recursion above, unrolled. With the torso COM p0 as the
 // origin, x_i = (F_i, V_i - (J_i - p0) x F_i) (the root: (F_0, V_0)), where over i's subtree
 // F_i = sum f_k and V_i = sum (t_k + (P_k - p0) x f_k) -- the same equations (B0 x = f), summed in
 // another order. The node table is in preorder, so every subtree is the contiguous range
@@ -1109,6 +1087,16 @@ __device__ LUInfo fullpiv_lu(G& g, int k, int lane) {
   return info;
 }
 
+// any nonzero pivot within kNearBand of the rank threshold maxpivot * thr (the decisions lu_rank takes)
+template <class G>
+__device__ inline bool lu_near(const G& g, const LUInfo& info, real thr) {
+  constexpr int LD = G::LD;
+  const real pt = fabs(info.maxpivot) * thr;
+  bool nr = false;
+  for (int i = 0; i < info.nz; i++) nr |= near_thr(fabs(g.lu[i + i * LD]), pt, kNearBand);
+  return nr;
+}
+
 template <class G>
 __device__ inline int lu_rank(const G& g, const LUInfo& info, real thr) {
   constexpr int LD = G::LD;
@@ -1229,8 +1217,9 @@ __device__ inline real m_at(const G& g, int k, int dimker, int i, int j) {
 }
 
 // Eigen 3.3 ColPivHouseholderQR on g.qr (k x k, holding m); returns nonzero pivots
+// near: a nonzero-pivot decision (Eigen's |col|^2 < threshold_helper (k - p)) within kNearBand^2
 template <class G>
-__device__ int colpiv_qr(G& g, int k, int lane) {
+__device__ int colpiv_qr(G& g, int k, int lane, bool& near) {
   constexpr int LD = G::LD;
   if (lane < k) {
     real s = 0;
@@ -1250,6 +1239,7 @@ __device__ int colpiv_qr(G& g, int k, int lane) {
     real bv = g.nu[p];
     for (int j = p + 1; j < k; j++)
       if (g.nu[j] > bv) { bv = g.nu[j]; bi = j; }
+    if (np == k) near |= near_thr(bv * bv, threshold_helper * (real)(k - p), kNearBand * kNearBand);
     if (np == k && bv * bv < threshold_helper * (real)(k - p)) np = p;
     gsync<G>();
     if (lane == 0) g.cperm[p] = bi;
@@ -1369,7 +1359,9 @@ __device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
     for (int guard = 0; guard < 2100 && r > rank0; guard++) {  // setThreshold doubling
       thr = 2 * thr;
       r = lu_rank(g, info, thr);
+      flags |= HS_FLAG_NEAR_RANK;  // the threshold now sits within 2x of a pivot by construction
     }
+    if (lu_near(g, info, thr)) flags |= HS_FLAG_NEAR_RANK;
     lu_solve(g, info, k, r, lane);
     lu_kernel_image(g, info, k, r, thr, lane);
     STAMP(11);
@@ -1392,7 +1384,9 @@ __device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
     }
     gsync<G>();
     STAMP(12);
-    int np = colpiv_qr(g, k, lane);
+    bool qr_near = false;
+    int np = colpiv_qr(g, k, lane, qr_near);
+    if (qr_near) flags |= HS_FLAG_NEAR_RANK;
     STAMP(13);
     qr_solve(g, k, np, lane);
     STAMP(14);
@@ -1406,6 +1400,7 @@ __device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
     real rn = 0, bn = 0;
     for (int i = 0; i < k; i++) { rn += g.c[i] * g.c[i]; bn += g.b[i] * g.b[i]; }
     rel_error = sqrt(rn) / sqrt(bn);
+    if (near_thr(rel_error, kRelTol, real(10))) flags |= HS_FLAG_NEAR_RANK;
     rank0--;
     if (lane < k) {
       real s = real(0);
@@ -1447,10 +1442,7 @@ __device__ HS_GENERAL_ATTR uint32_t general_solve(const hs_topo* T, SV& sv, G& g
 // Cholesky pivot falls under the guard -> general path.
 // ---------------------------------------------------------------------------
 // conditioning guard of the closed-form Cholesky pivots (relative to the largest diagonal)
-#ifndef HS_F32_GUARD
-#define HS_F32_GUARD 1e-4
-#endif
-constexpr real kFastPivotGuard = HS_REAL_IS_FLOAT ? real(HS_F32_GUARD) : real(1e-10);
+constexpr real kFastPivotGuard = HS_REAL_IS_FLOAT ? real(1e-4) : real(1e-10);
 
 // Nearly collinear contact feet (nc >= 3): the zeroth-order Gram G = A A^T = sum_c A_c A_c^T is
 // close to rank 5. The reference's loop (ftsolver.cpp:205-232) then sees a rank-deficient first-order
@@ -1481,9 +1473,6 @@ __device__ inline float group8_sum(float v) {
   return v;
 }
 
-#ifndef HS_BLOCK_QUAD
-#define HS_BLOCK_QUAD 1
-#endif
 // sum over the 4-lane quad (DPP quad_perm xor 1, xor 2): every lane of the quad gets the same value
 // (each addition is commutative in its two operands)
 __device__ inline real quad_sum(real v) {
@@ -1504,8 +1493,10 @@ __device__ inline real quad_sum(real v) {
 #endif
 }
 
+// bit 0: well posed (take the closed form); bit 1: the ratio lies within kNearBand of the guard
+// (HS_FLAG_NEAR_RANK: another rounding may route the step the other way)
 template <class W, class SV>
-__device__ inline bool zeroth_well_posed(const real* P0, const W& w, const SV& sv, int nc, int lane) {
+__device__ inline int zeroth_well_posed(const real* P0, const W& w, const SV& sv, int nc, int lane) {
   float d0 = 0.f, d1 = 0.f, d2 = 0.f;
   if (lane < nc) {
     const real* fp = w.fpos(0, sv.cfoot[lane]);
@@ -1520,12 +1511,14 @@ __device__ inline bool zeroth_well_posed(const real* P0, const W& w, const SV& s
   const float c2 = (c00 * c11 - c01 * c01) + (c00 * c22 - c02 * c02) + (c11 * c22 - c12 * c12);
   const float tq = q00 + q11 + q22;
   const float md = fmaxf(k, fmaxf(tq - q00, fmaxf(tq - q11, tq - q22)));
-  return c2 >= kZerothGuard * k * (c00 + c11 + c22) * md;  // false on NaN
+  const float t = kZerothGuard * k * (c00 + c11 + c22) * md;
+  return (c2 >= t ? 1 : 0) | (c2 >= t / float(kNearBand) && c2 <= t * float(kNearBand) ? 2 : 0);  // 0 on NaN
 }
 
 // rl (N): receives 1 / L_jj, the reciprocal each pivot's column was scaled by, for chol_solve_n
+// near: set when a pivot lies within kNearBand of the guard (HS_FLAG_NEAR_RANK)
 template <int N>
-__device__ inline bool chol_n(real* a, real guard, real* rl_out) {  // row-major, in place
+__device__ inline bool chol_n(real* a, real guard, real* rl_out, bool& near) {  // row-major, in place
   real mx = 0;
 #pragma unroll
   for (int i = 0; i < N; i++) mx = fmax(mx, a[i * N + i]);
@@ -1534,6 +1527,7 @@ __device__ inline bool chol_n(real* a, real guard, real* rl_out) {  // row-major
     real s = a[j * N + j];
 #pragma unroll
     for (int k = 0; k < j; k++) s -= a[j * N + k] * a[j * N + k];
+    near |= near_thr(s, guard * mx, kNearBand);
     if (!(s > guard * mx)) return false;
     const real l = sqrt(s), rl = real(1) / l;  // one division per pivot (oracle chol)
     a[j * N + j] = l;
@@ -1571,13 +1565,10 @@ __device__ inline void chol_solve_n(const real* L, const real* rl, real* b) {
 // LDL^T of an N x N SPD matrix in place (row-major; lower part: unit-lower L, diagonal: d), no
 // square roots: pivot d_j = a_jj - sum_k L_jk (L_jk d_k), the Cholesky pivot in exact arithmetic, so
 // the guard (d_j > guard * max diagonal) decides like chol_n's. rd: 1 / d_j. False: a pivot under it.
-#ifndef HS_FAST_RCP
-#define HS_FAST_RCP 1
-#endif
 // 1 / x for a positive normal pivot: v_rcp_f64 refined by two Newton steps (within an ulp of the
 // correctly rounded quotient), five instructions instead of the IEEE division's scale / fixup sequence
 __device__ inline real pivot_rcp(real x) {
-#if HS_FAST_RCP && !HS_REAL_IS_FLOAT
+#if !HS_REAL_IS_FLOAT
   real r = __builtin_amdgcn_rcp(x);
   real e = fma(-x, r, real(1));
   r = fma(r, e, r);
@@ -1588,8 +1579,9 @@ __device__ inline real pivot_rcp(real x) {
 #endif
 }
 
+// near (guarded factorizations): set when a pivot lies within kNearBand of the guard
 template <int N>
-__device__ inline bool ldl_n(real* a, real guard, real* rd) {
+__device__ inline bool ldl_n(real* a, real guard, real* rd, bool& near) {
   real mx = 0;
 #pragma unroll
   for (int i = 0; i < N; i++) mx = fmax(mx, a[i * N + i]);
@@ -1601,6 +1593,7 @@ __device__ inline bool ldl_n(real* a, real guard, real* rd) {
     real dj = a[j * N + j];
 #pragma unroll
     for (int k = 0; k < j; k++) dj -= a[j * N + k] * v[k];
+    near |= near_thr(dj, guard * mx, kNearBand);
     if (!(dj > guard * mx)) return false;
     const real r = pivot_rcp(dj);
     a[j * N + j] = dj;
@@ -1614,6 +1607,13 @@ __device__ inline bool ldl_n(real* a, real guard, real* rd) {
     }
   }
   return true;
+}
+
+// unguarded (guard 0: SPD by construction, no decision taken)
+template <int N>
+__device__ inline bool ldl_n(real* a, real guard, real* rd) {
+  bool unused = false;
+  return ldl_n<N>(a, guard, rd, unused);
 }
 
 // solve L D L^T x = b in place with ldl_n's factors
@@ -1698,12 +1698,13 @@ struct RectWalk {
 };
 
 template <bool GLOBAL>
-__device__ __attribute__((always_inline)) inline bool chol_half(real* K, int k, real guard, int lane,
+__device__ __attribute__((always_inline)) inline bool chol_half(real* K, int k, real guard, int lane, bool& near,
                                                                  real* rdiag = nullptr) {
   real mx = 0;
   for (int i = 0; i < k; i++) mx = fmax(mx, K[i * k + i]);
   for (int j = 0; j < k; j++) {
     const real s = K[j * k + j];
+    near |= near_thr(s, guard * mx, kNearBand);
     if (!(s > guard * mx)) return false;
     const real l = sqrt(s), rl = real(1) / l;
     if (lane == 0) {
@@ -1726,32 +1727,37 @@ __device__ __attribute__((always_inline)) inline bool chol_half(real* K, int k, 
 __device__ inline int pk(int r, int c) { return r * (r + 1) / 2 + c; }
 
 // chol_half's right-looking Cholesky on a packed lower triangle in LDS (solve_forces: its normal
-// matrices), the same operations per entry; the trailing update walks the packed entries
-__device__ __attribute__((always_inline)) inline bool chol_packed(real* K, int k, real guard, int lane) {
+// matrix), the same operations per entry; the trailing update walks the packed entries. A pivot at or
+// under guard * (largest diagonal) drops its variable (returned in the mask): its column is zeroed, so
+// the later pivots are those of the system without it, and the caller's solves leave it at 0 -- the
+// basic solution of a rank-deficient least squares (SparseQR's, ftsolver.cpp:349-353, in the natural
+// column order). near: a pivot within kNearBand of the guard (HS_FLAG_NEAR_RANK).
+__device__ __attribute__((always_inline)) inline uint32_t chol_packed(real* K, int k, real guard, int lane,
+                                                                      bool& near) {
   real mx = 0;
   for (int i = 0; i < k; i++) mx = fmax(mx, K[pk(i, i)]);
+  uint32_t dropped = 0;
+  // one pivot's column: scaled by 1 / L_jj, or zeroed when the pivot is dropped (L_jj = 1 then)
+  auto pivot = [&](int j) {
+    const real s = K[pk(j, j)];
+    near |= near_thr(s, guard * mx, kNearBand);
+    const bool keep = s > guard * mx;  // false on NaN
+    const real l = keep ? sqrt(s) : real(1), rl = keep ? real(1) / l : real(0);
+    if (!keep) dropped |= 1u << j;
+    if (lane == 0) K[pk(j, j)] = l;
+    for (int i = j + 1 + lane; i < k; i += HALF) K[pk(i, j)] = K[pk(i, j)] * rl;
+    wave_sync();
+  };
   // two pivots per trailing pass: pivot j, column j + 1 updated by it, pivot j + 1, then every
   // entry right of both takes pivot j's product and pivot j + 1's in that order -- each entry sees
   // the operations of one pivot at a time, in pivot order, as in chol_half
   for (int j = 0; j < k; j += 2) {
     const bool two = j + 1 < k;
-    {
-      const real s = K[pk(j, j)];
-      if (!(s > guard * mx)) return false;
-      const real l = sqrt(s), rl = real(1) / l;
-      if (lane == 0) K[pk(j, j)] = l;
-      for (int i = j + 1 + lane; i < k; i += HALF) K[pk(i, j)] = K[pk(i, j)] * rl;
-      wave_sync();
-    }
+    pivot(j);
     if (two) {
       for (int i = j + 1 + lane; i < k; i += HALF) K[pk(i, j + 1)] -= K[pk(i, j)] * K[pk(j + 1, j)];
       wave_sync();
-      const real s = K[pk(j + 1, j + 1)];
-      if (!(s > guard * mx)) return false;
-      const real l = sqrt(s), rl = real(1) / l;
-      if (lane == 0) K[pk(j + 1, j + 1)] = l;
-      for (int i = j + 2 + lane; i < k; i += HALF) K[pk(i, j + 1)] = K[pk(i, j + 1)] * rl;
-      wave_sync();
+      pivot(j + 1);
     }
     const int j1 = two ? j + 2 : j + 1, m = k - j1;
     for (TriWalk<> t(lane); t.r < m; t.next()) {  // the trailing lower triangle, entry by entry
@@ -1763,7 +1769,7 @@ __device__ __attribute__((always_inline)) inline bool chol_packed(real* K, int k
     }
     wave_sync();
   }
-  return true;
+  return dropped;
 }
 
 // nc >= 3 with a singular D_c (straight, IK-clamped leg) or Schur complement:
@@ -1773,7 +1779,7 @@ __device__ __attribute__((always_inline)) inline bool chol_packed(real* K, int k
 // False when the minimizer is not unique (a pivot under the guard).
 template <class SV>
 __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, AugL& ag, SV& sv, const real* a, int nc,
-                                                                int lane) {
+                                                                int lane, bool& near) {
   const int k = 3 * nc;
   auto Aat = [&](int r, int i) { return a_entry(fl.d0[i / 3], r, i % 3); };  // A (6 x k)
   real md = 0, ma = 0;
@@ -1804,7 +1810,7 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, AugL&
     ag.X[i * 7 + q] = v;
   }
   __syncthreads();
-  if (!chol_half<true>(ag.K, k, kFastPivotGuard, lane, ag.rdiag)) return false;
+  if (!chol_half<true>(ag.K, k, kFastPivotGuard, lane, near, ag.rdiag)) return false;
   __syncthreads();
   if (lane < 7) {  // K X = [A^T | g~], one right-hand column per lane
     const int q = lane;
@@ -1833,7 +1839,7 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, AugL&
     for (int i = 0; i < 36; i++) St[i] = ag.St[i];
     for (int i = 0; i < 6; i++) lam[i] = ag.lam[i];
     real rl[6];
-    int ok = chol_n<6>(St, kFastPivotGuard, rl);
+    int ok = chol_n<6>(St, kFastPivotGuard, rl, near);
     if (ok) {
       chol_solve_n<6>(St, rl, lam);
       for (int i = 0; i < 6; i++) ag.lam[i] = lam[i];
@@ -1851,22 +1857,19 @@ __device__ __attribute__((always_inline)) inline bool aug_solve(FastL& fl, AugL&
   return true;
 }
 
-// TIER2: the augmented-system solve where a D_c or the Schur complement is singular; without it
-// (HS_DEFER_AUG builds of the fused step launch) such steps decline and go to the fixup launch
 // aug_ok = false (the fixup launch's idle half, which stores nothing): decline instead of using the
 // augmented system, whose global workspace is the idle slot every fixup wavefront shares
-template <bool TIER2 = true, class W, class SV>
-__device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* T, SV& sv, FastL& fl, AugL& ag, const W& w,
-                                                                 int nc, bool aug_ok, int lane) {
+// lnear: this lane saw a routing decision within kNearBand of its guard (fast_solve ballots it)
+template <class W, class SV>
+__device__ __attribute__((always_inline)) inline bool fast_solve_lanes(const hs_topo* T, SV& sv, FastL& fl, AugL& ag,
+                                                                       const W& w, int nc, bool aug_ok, int lane,
+                                                                       bool& lnear) {
   const int n = T->n;
   if (nc == 0) return true;
   const real* P0 = w.pos(0, 0);
-#ifndef HS_EXP_NO_ZEROTH_GUARD  // timing experiment only
-  const int coll = (nc >= 3 && !zeroth_well_posed(P0, w, sv, nc, lane)) ? 2 : 0;
-#else
-  const int coll = 0;
-#endif
-#if HS_BLOCK_QUAD
+  const int zw = nc >= 3 ? zeroth_well_posed(P0, w, sv, nc, lane) : 1;
+  const int coll = (zw & 1) ? 0 : 2;
+  lnear |= (zw & 2) != 0 && lane < 8;  // the group of lanes 0 .. 7 holds the contacts' sums
   // four lanes per contact (lane = 4 c + s): lane s sums the D_c / g_c terms of the foot chain's
   // joints s, s + 4, the quad adds them (DPP), every lane of the quad factorizes D_c, and the Schur
   // block's rows are split {s, 5 - s} (seven packed entries and two of h per lane; lane 3 repeats
@@ -1916,7 +1919,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
         real L[9];
         for (int i = 0; i < 9; i++) L[i] = D[i];
         real rl[3];
-        ok = ldl_n<3>(L, kFastPivotGuard, rl);
+        ok = ldl_n<3>(L, kFastPivotGuard, rl, lnear);
         if (ok) {
           real Dinv[9];
           for (int j = 0; j < 3; j++) {
@@ -1963,110 +1966,12 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       if (s4 == 0) fl.ok[c] = ok | coll;
     }
   }
-#else
-  if (lane < nc) {  // A_c, D_c, g_c for contact c = lane
-    const int c = lane, fi = sv.cfoot[c];
-    const real* fp = w.fpos(0, fi);
-    real d0[3], v[3][3];
-    for (int r = 0; r < 3; r++) d0[r] = P0[r] - fp[r];
-    cross_rows(d0, v);
-    real Ac[18];
-    for (int r = 0; r < 3; r++)
-      for (int j = 0; j < 3; j++) { Ac[r * 3 + j] = (r == j) ? real(-1) : real(0); Ac[(3 + r) * 3 + j] = v[r][j]; }
-    for (int r = 0; r < 3; r++) fl.d0[c][r] = d0[r];
-    real D[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-    const int nch = T->foot_chain_len[fi];
-    int chain[HS_CHAIN_MAX];  // independent loads instead of a parent-pointer chase
-#pragma unroll
-    for (int m = 0; m < HS_CHAIN_MAX; m++) chain[m] = T->foot_chain[fi][m];
-#pragma unroll
-    for (int m = 0; m < HS_CHAIN_MAX; m++) {
-      if (m >= nch) break;
-      const int p = chain[m];
-      const real* Jp = w.jpos(0, p);
-      const real* Jz = w.jz(0, p);
-      real da[3], va[3][3];
-      for (int r = 0; r < 3; r++) da[r] = Jp[r] - fp[r];
-      cross_rows(da, va);
-      // (va[r][r] = 0: the products it enters add exact zeros and are skipped)
-#pragma unroll
-      for (int r = 0; r < 3; r++) {
-        real w2 = Jz[r] * Jz[r];
-        if (w2 == 0) continue;
-#pragma unroll
-        for (int i = 0; i < 3; i++) {
-          if (i == r) continue;
-#pragma unroll
-          for (int j = 0; j < 3; j++)
-            if (j != r) D[3 * i + j] += w2 * va[r][i] * va[r][j];
-          g[i] += w2 * va[r][i] * sv.x[3 * n + 3 * p + r];
-        }
-      }
-    }
-    for (int i = 0; i < 9; i++) fl.D[c][i] = D[i];
-    for (int i = 0; i < 3; i++) fl.g[c][i] = g[i];
-    int ok = 1;
-    if (nc >= 3) {
-      real L[9];
-      for (int i = 0; i < 9; i++) L[i] = D[i];
-      real rl[3];
-      ok = ldl_n<3>(L, kFastPivotGuard, rl);
-      if (ok) {
-        real Dinv[9];
-        for (int j = 0; j < 3; j++) {
-          real e[3] = {0, 0, 0};
-          e[j] = 1;
-          ldl_solve_n<3>(L, rl, e);
-          for (int i = 0; i < 3; i++) Dinv[3 * i + j] = e[i];
-        }
-        // E = A_c D_c^-1 and S_c = E A_c^T with A_c = [-I; [d0]x]: the products by A_c's zeros
-        // (identity off-diagonal, cross-matrix diagonal) add exact zeros and are skipped, the
-        // remaining terms are summed in the same order
-        real E[18];
-#pragma unroll
-        for (int r = 0; r < 6; r++)
-#pragma unroll
-          for (int j = 0; j < 3; j++) {
-            real s = 0;
-            if (r < 3) {
-              s += real(-1) * Dinv[3 * r + j];
-            } else {
-#pragma unroll
-              for (int i = 0; i < 3; i++)
-                if (i != r - 3) s += Ac[r * 3 + i] * Dinv[3 * i + j];
-            }
-            E[r * 3 + j] = s;
-          }
-#pragma unroll
-        for (int r = 0; r < 6; r++) {
-#pragma unroll
-          for (int q = 0; q <= r; q++) {  // lower triangle: all the Cholesky below reads
-            real s = 0;
-            if (q < 3) {
-              s += E[r * 3 + q] * real(-1);
-            } else {
-#pragma unroll
-              for (int j = 0; j < 3; j++)
-                if (j != q - 3) s += E[r * 3 + j] * Ac[q * 3 + j];
-            }
-            fl.sc.S[c][sch_lower(r, q)] = s;
-          }
-          real s = 0;
-          for (int j = 0; j < 3; j++) s += E[r * 3 + j] * g[j];
-          fl.sc.S[c][SCH_H + r] = s;
-        }
-        for (int i = 0; i < 9; i++) fl.sc.Dinv[c][i] = Dinv[i];
-      }
-    }
-    fl.ok[c] = ok | coll;
-  }
-#endif
   wave_sync();
   STAMP(18);
   const real a[6] = {sv.x[0], sv.x[1], sv.x[2], sv.x[3 * n], sv.x[3 * n + 1], sv.x[3 * n + 2]};
   if (nc >= 3 && (fl.ok[0] & 2)) return false;  // nearly collinear contacts: the Eigen-style path
   for (int c = 0; c < nc; c++)
-    if (!(fl.ok[c] & 1)) return (TIER2 && aug_ok) ? aug_solve(fl, ag, sv, a, nc, lane) : false;  // only nc >= 3 factors D_c
+    if (!(fl.ok[c] & 1)) return aug_ok ? aug_solve(fl, ag, sv, a, nc, lane, lnear) : false;  // only nc >= 3 factors D_c
   int ok = 1;
   if (nc == 1) {  // unique least-squares solution (A^T A) w = -A^T a
     if (lane == 0) {
@@ -2078,7 +1983,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
         for (int r = 0; r < 6; r++) b[i] -= a_entry(d0, r, i) * a[r];
       }
       real rl[3];
-      ok = chol_n<3>(M, kFastPivotGuard, rl);
+      ok = chol_n<3>(M, kFastPivotGuard, rl, lnear);
       if (ok) {
         chol_solve_n<3>(M, rl, b);
         for (int i = 0; i < 3; i++) sv.y[i] = b[i];
@@ -2108,7 +2013,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
           for (int r = 0; r < 6; r++) s += a_entry(di, r, i % 3) * a[r];
           b[i] = -s;
         }
-        ok = chol_n<6>(M, kFastPivotGuard, rl);
+        ok = chol_n<6>(M, kFastPivotGuard, rl, lnear);
       }
       if (ok) {
         chol_solve_n<6>(M, rl, b);
@@ -2145,23 +2050,16 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
       for (int i = 0; i < 6; i++) h[i] = fl.sc.Ssum[SCH_H + i];
       real lam[6], rl[6];
       for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
-#ifdef HS_EXP_NO_SCHUR  // timing experiment only: no 6x6 factorization
-      ok = 1;
-      (void)Sm;
-#else
-      ok = ldl_n<6>(Sm, kFastPivotGuard, rl);
-#endif
+      ok = ldl_n<6>(Sm, kFastPivotGuard, rl, lnear);
       if (ok) {
-#ifndef HS_EXP_NO_SCHUR
         ldl_solve_n<6>(Sm, rl, lam);
-#endif
         for (int r = 0; r < 6; r++) fl.sc.lam[r] = lam[r];
       }
       fl.ok[0] = ok;
     }
     wave_sync();
     STAMP(19);
-    if (!fl.ok[0]) return (TIER2 && aug_ok) ? aug_solve(fl, ag, sv, a, nc, lane) : false;
+    if (!fl.ok[0]) return aug_ok ? aug_solve(fl, ag, sv, a, nc, lane, lnear) : false;
     if (lane < nc) {
       const int c = lane;
       const real* d0 = fl.d0[c];
@@ -2186,6 +2084,17 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
   }
   wave_sync();
   return fl.ok[0] != 0;
+}
+
+// near (uniform over the half-wave): a routing decision of the closed form lay within kNearBand of its
+// guard on some lane (HS_FLAG_NEAR_RANK)
+template <class W, class SV>
+__device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* T, SV& sv, FastL& fl, AugL& ag, const W& w,
+                                                                 int nc, bool aug_ok, int lane, bool& near) {
+  bool lnear = false;
+  const bool ok = fast_solve_lanes(T, sv, fl, ag, w, nc, aug_ok, lane, lnear);
+  near = half_ballot(lnear) != 0;
+  return ok;
 }
 
 // selection COT of the best-rollout key (hs_best_key_cot, include/hslabs.h): one cycle's work over
@@ -2256,14 +2165,10 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
                      real& work, bool& deferred, bool may_general, int lane) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
   STAMP(3);
-#ifndef HS_S1_SUBTREE
-#define HS_S1_SUBTREE 1
-#endif
   // D writes, and S1's first stage reads, part i's rows on lane i only: no sync between them
-  dynamics<!HS_S1_SUBTREE>(T, st, sv, w, lane);
+  dynamics<false>(T, st, sv, w, lane);
   STAMP(4);
-  if constexpr (HS_S1_SUBTREE) particular_sub(T, sv, w, lane);
-  else particular(T, sv, w, lane);
+  particular_sub(T, sv, w, lane);
   STAMP(5);
   // contact list in foot order (ftsolver contact columns)
   const uint32_t cmask = half_ballot(lane < nf && w.contact(0, lane));
@@ -2275,31 +2180,19 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   STAMP(6);
   // tier 2 (aug_solve) and the general path share the rollout's global workspace (SolveWS): the
   // general path runs only after tier 2 declined. may_general = false (the fixup's idle half) skips both
-#ifdef HS_EXP_NO_SOLVE  // timing experiment only: no contact solve (y = 0)
-  if (lane < k) sv.y[lane] = 0;
-  wave_sync();
-  if (true) {
-#else
-#ifndef HS_DEFER_AUG
-#define HS_DEFER_AUG 0
-#endif
-  if (a.solve_mode == HS_SOLVE_AUTO &&
-      fast_solve<!(DEFER && HS_DEFER_AUG)>(T, sv, fl, G->aug, w, nc, may_general, lane)) {
-#endif
+  bool fast_near = false;
+  if (a.solve_mode == HS_SOLVE_AUTO && fast_solve(T, sv, fl, G->aug, w, nc, may_general, lane, fast_near)) {
     if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
     if (nc == 1) flags |= HS_FLAG_FULL_RANK;
   } else {
-#ifdef HS_EXP_NO_GENERAL  // timing experiment only: no general path (its steps keep y unset)
-    flags = HS_FLAG_GENERAL;
-#else
     if constexpr (DEFER) {
       deferred = true;  // uniform over the half-wave: its outputs come from the fixup launch
       live = false;
     } else if (may_general) {
       flags = general_solve(T, sv, G->gen, w, k, lane) | HS_FLAG_GENERAL;
     }
-#endif
   }
+  if (fast_near) flags |= HS_FLAG_NEAR_RANK;  // the closed form's routing itself was a near decision
   STAMP(7);
 
   // S4: x = x_part + N y for the hinge torque rows, motor torques (periodic.cpp:328-343),
@@ -2418,7 +2311,8 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
 // u_hi = (jpos_h - pos_i) x jz_h on the subtree of hinge h -- C = [I; [fpos -
 // p_0]x] and jz_h . [(jpos_h - fpos)x] (the tree basis seen by those rows),
 // d = (torso part of x_part, z - jz . x_part). Rank-deficient normal matrix
-// (a straight leg): HS_FLAG_GENERAL, Tikhonov 1e-12 of its largest diagonal.
+// (a straight leg): HS_FLAG_GENERAL and the basic solution (the dependent
+// forces, in foot order, at 0: SparseQR's kind of answer, ftsolver.cpp:349-353).
 // ---------------------------------------------------------------------------
 
 __device__ inline void cross3(const real* a, const real* b, real* c) {
@@ -2437,8 +2331,8 @@ __device__ inline void cross3(const real* a, const real* b, real* c) {
 // kForcesBlockGuard of its diagonal), the Schur complement of diag(B_f) in the KKT system gives
 //   (S + sum_f C~_f B_f^-1 C~_f^T) lam = sum_f C~_f B_f^-1 r_f - d~,   y_f = B_f^-1 (r_f - C~_f^T lam),
 // a 6 x 6 system (>= I); otherwise (a straight leg: B_f singular) N is formed and factorized as a
-// dense 3 nf x 3 nf Cholesky, pivot guard kFastPivotGuard, HS_FLAG_GENERAL and the Tikhonov pass when
-// it trips. Lanes: one per limb for the limb's blocks (M_l = L D L^T: every product Y_a^T D^-1 Y_b,
+// dense 3 nf x 3 nf Cholesky, pivot guard kFastPivotGuard: a pivot under it drops its force component
+// (HS_FLAG_GENERAL, the basic solution; chol_packed). Lanes: one per limb for the limb's blocks (M_l = L D L^T: every product Y_a^T D^-1 Y_b,
 // Y = L^-1 [W_mt | C_m | d_m]), one per packed entry for the sums over limbs (in limb order).
 constexpr real kForcesBlockGuard = HS_REAL_IS_FLOAT ? real(1e-3) : real(1e-6);
 constexpr int FSUM = 27;  // packed 6 x 6 lower triangle (21) + a 6-vector
@@ -2661,34 +2555,29 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
       }
   }
   wave_sync();
-  real eps = 0;
-  for (int pass = 0; pass < 2; pass++) {
-    for (TriWalk<1> t(lane); t.r < nq; t.next()) {  // V^T D^-1 V and its rhs, entry by entry
-      const int p = t.r, q = (t.c == p + 1) ? nq : t.c;
-      real s = 0;
-      for (int k = 0; k < 6; k++) s += Vm[k * HS_KMAX + p] * rdS[k] * ((q < nq) ? Vm[k * HS_KMAX + q] : vv[k]);
-      if (q < nq) N[pk(p, q)] = s + ((p == q) ? eps : real(0));
-      else rr[p] = s;
-    }
-    wave_sync();
-    if (lane < nl) {  // + the feet's own blocks
-      const int q0 = 3 * f;
-      N[pk(q0, q0)] += Bd[0];
-      N[pk(q0 + 1, q0)] += Bd[1];
-      N[pk(q0 + 1, q0 + 1)] += Bd[2];
-      N[pk(q0 + 2, q0)] += Bd[3];
-      N[pk(q0 + 2, q0 + 1)] += Bd[4];
-      N[pk(q0 + 2, q0 + 2)] += Bd[5];
-      for (int k = 0; k < 3; k++) rr[q0 + k] += rb[k];
-    }
-    wave_sync();
-    if (pass == 0) {
-      for (int p = 0; p < nq; p++) eps = fmax(eps, N[pk(p, p)]);
-      eps *= real(1e-12);
-    }
-    if (chol_packed(N, nq, pass == 0 ? kFastPivotGuard : real(0), lane)) break;
-    flags = HS_FLAG_GENERAL;  // least squares not unique
+  for (TriWalk<1> t(lane); t.r < nq; t.next()) {  // V^T D^-1 V and its rhs, entry by entry
+    const int p = t.r, q = (t.c == p + 1) ? nq : t.c;
+    real s = 0;
+    for (int k = 0; k < 6; k++) s += Vm[k * HS_KMAX + p] * rdS[k] * ((q < nq) ? Vm[k * HS_KMAX + q] : vv[k]);
+    if (q < nq) N[pk(p, q)] = s;
+    else rr[p] = s;
   }
+  wave_sync();
+  if (lane < nl) {  // + the feet's own blocks
+    const int q0 = 3 * f;
+    N[pk(q0, q0)] += Bd[0];
+    N[pk(q0 + 1, q0)] += Bd[1];
+    N[pk(q0 + 1, q0 + 1)] += Bd[2];
+    N[pk(q0 + 2, q0)] += Bd[3];
+    N[pk(q0 + 2, q0 + 1)] += Bd[4];
+    N[pk(q0 + 2, q0 + 2)] += Bd[5];
+    for (int k = 0; k < 3; k++) rr[q0 + k] += rb[k];
+  }
+  wave_sync();
+  bool rank_near = false;  // a rank decision within kNearBand of the guard (HS_FLAG_NEAR_RANK)
+  const uint32_t dropped = chol_packed(N, nq, kFastPivotGuard, lane, rank_near);
+  if (dropped) flags = HS_FLAG_GENERAL;  // least squares not unique: its basic solution
+  if (rank_near) flags |= HS_FLAG_NEAR_RANK;
   STAMP(8);
   if (lane == 0) {  // the two triangular solves with y in registers (nq <= HS_KMAX)
     real yv[HS_KMAX];
@@ -2700,7 +2589,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
         real s = yv[i];
 #pragma unroll
         for (int k = 0; k < i; k++) s -= N[pk(i, k)] * yv[k];
-        yv[i] = s / N[pk(i, i)];
+        yv[i] = ((dropped >> i) & 1) ? real(0) : s / N[pk(i, i)];
       }
     }
 #pragma unroll
@@ -2710,7 +2599,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
 #pragma unroll
         for (int k = i + 1; k < HS_KMAX; k++)
           if (k < nq) s -= N[pk(k, i)] * yv[k];
-        yv[i] = s / N[pk(i, i)];
+        yv[i] = ((dropped >> i) & 1) ? real(0) : s / N[pk(i, i)];
       }
     }
 #pragma unroll
@@ -2758,9 +2647,6 @@ static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 // The fused path's setup pass (hs_run_calls: gait setup once per rollout, stored for every step):
 // the rollout kernel's prologue and setup store alone, as its own small kernel (2 x 320 B of LDS, few
 // registers) so the pass does not carry the step kernel's code, registers and LDS
-#ifndef HS_SETUP_WAVES
-#define HS_SETUP_WAVES 1  // wavefronts per workgroup of the setup pass
-#endif
 // One wavefront's gait setup (wavefront wid_raw of the batch; sst: two SetupL in LDS)
 __device__ __attribute__((always_inline)) inline void setup_wave(const hs_topo* __restrict__ T0, const hs_run_args& a,
                                                                  RolloutWS* __restrict__ rws, const hs::launch_map& mp,
@@ -2797,11 +2683,10 @@ __device__ __attribute__((always_inline)) inline void setup_wave(const hs_topo* 
   }
 }
 
-__global__ __launch_bounds__(WAVE * HS_SETUP_WAVES) void hs_setup_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
-                                                                        RolloutWS* __restrict__ rws, hs::launch_map mp) {
-  __shared__ SetupL sst_all[2 * HS_SETUP_WAVES];
-  setup_wave(T0, a, rws, mp, (int)blockIdx.x * HS_SETUP_WAVES + (int)(threadIdx.x / WAVE),
-             sst_all + 2 * (threadIdx.x / WAVE));
+__global__ __launch_bounds__(WAVE) void hs_setup_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
+                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
+  __shared__ SetupL sst[2];
+  setup_wave(T0, a, rws, mp, (int)blockIdx.x, sst);
 }
 
 // The IK table of a call (hs::ktab_range): one lane per (rollout slot, sample, limb), the
@@ -2841,15 +2726,7 @@ __device__ inline void ktab_item(const hs_topo* __restrict__ T0, const hs_run_ar
   straight_ik(T, g, a.params[b], ws.st, t, L, J, a.ignore_reach != 0, ja, bad);
   real* e = rws[b].ktab[s][L];
 #pragma unroll
-  for (int kk = 0; kk < 3; kk++) {
-    e[kk] = ja[kk];
-#if HS_KT_SINCOS
-    real sq, cq;
-    sincos(ja[kk], &sq, &cq);
-    e[3 + kk] = sq;
-    e[6 + kk] = cq;
-#endif
-  }
+  for (int kk = 0; kk < 3; kk++) e[kk] = ja[kk];
   e[KT_W - 1] = bad ? real(1) : real(0);
 }
 
@@ -2858,7 +2735,7 @@ __device__ inline void ktab_item(const hs_topo* __restrict__ T0, const hs_run_ar
 // when the batch's wavefront count is a multiple of 8), so block t = 8 q + x takes the items of
 // wavefront 8 (q / bpw) + x: its table rows are written on the XCD whose L2 the steps read them from
 __host__ __device__ inline int ktab_blocks_per_wave(int nt, int nli) { return (2 * nt * nli + WAVE - 1) / WAVE; }
-__global__ __launch_bounds__(WAVE, HS_KTAB_WAVES) void hs_ktab_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
+__global__ __launch_bounds__(WAVE) void hs_ktab_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
                                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
   const int nli = ktab_lanes(mp);
   const int bpw = ktab_blocks_per_wave(mp.ktab_n, nli);
@@ -2868,71 +2745,6 @@ __global__ __launch_bounds__(WAVE, HS_KTAB_WAVES) void hs_ktab_kernel(const hs_t
   int s, L;
   const int b = ktab_item_rollout(T0, a, mp, w, local, s, L);
   if (b >= 0) ktab_item(T0, a, rws, mp, w, b, s, L);
-}
-
-// The setup pass and the IK table in one launch (hs_run_calls): blocks take tickets in the order
-// they start (an atomic counter, as in a decoupled look-back); the first n_waves tickets run the gait
-// setup of a wavefront and then publish it (prep_ready[wid] = prep_epoch, a release at agent scope),
-// the rest run table items, each lane waiting (acquire) for its rollout's setup. A table block waits
-// only on setup blocks that already hold a ticket, hence run, so the wait ends; the table's work
-// overlaps the setup pass's latency instead of following it.
-#ifndef HS_PREP_WAVES
-#define HS_PREP_WAVES 1
-#endif
-#ifndef HS_PREP_SLEEP
-#define HS_PREP_SLEEP 16  // s_sleep units (64 clocks) between polls
-#endif
-#ifndef HS_PREP
-#define HS_PREP 0  // 1: the setup pass and the IK table in one launch; measured far slower (the table
-                   // blocks' polls: 206 us against 13 + 18 us for the two launches), so off
-#endif
-#ifndef HS_PREP_RMW
-#define HS_PREP_RMW 0  // poll with an atomic read-modify-write (performed at the memory side) instead of a load
-#endif
-__global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
-                                                                      RolloutWS* __restrict__ rws, hs::launch_map mp) {
-  __shared__ SetupL sst[2];
-  __shared__ uint32_t tk_s;
-  if (threadIdx.x == 0) {
-    const uint32_t tk = atomicAdd(mp.prep_ctr, 1u);
-    if (tk + 1 == gridDim.x) atomicExch(mp.prep_ctr, 0u);  // every block holds its ticket: zero for the next call
-    tk_s = tk;
-  }
-  __syncthreads();
-  const uint32_t tk = tk_s;
-  if (tk < (uint32_t)mp.n_waves) {
-    setup_wave(T0, a, rws, mp, (int)tk, sst);
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_store(mp.prep_ready + tk, mp.prep_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  const int64_t item = (int64_t)(tk - (uint32_t)mp.n_waves) * WAVE + threadIdx.x;
-  const int per_wave = 2 * mp.ktab_n * ktab_lanes(mp);
-  const int wid = (int)(item / per_wave);
-  int s, L;
-  const int b = ktab_item_rollout(T0, a, mp, wid, (int)(item % per_wave), s, L);
-  if (b < 0) return;
-  // bounded (~0.3 s): a setup that never published would leave NaN joint values, not a hung GPU
-  // (relaxed polls, then one acquire: an acquire per poll invalidates the caches the setup waves use)
-  auto poll = [&]() {
-#if HS_PREP_RMW
-    return __hip_atomic_fetch_or(mp.prep_ready + wid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    return __hip_atomic_load(mp.prep_ready + wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-  };
-  for (int spin = 0; poll() != mp.prep_epoch; spin++) {
-    if (spin >= (1 << 20)) {
-      real* e = rws[b].ktab[s][L];
-      for (int i = 0; i < KT_W; i++) e[i] = __builtin_nan("");
-      return;
-    }
-    __builtin_amdgcn_s_sleep(HS_PREP_SLEEP);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  ktab_item(T0, a, rws, mp, wid, b, s, L);
 }
 
 // One wavefront's step: fused step fstep (0 outside fused launches) of batch wavefront wid. only_sub
@@ -2976,20 +2788,9 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
     h_row = s;
   }
   const int nl = T->n_limbs;
-  // the gait setup of the rollout, stored by the call's setup pass (hs_setup_kernel / hs_prep_kernel;
+  // the gait setup of the rollout, stored by the call's setup pass (hs_setup_kernel;
   // the idle half reads its neighbour's): read from global memory where it is used
-#if HS_ST_LDS
-  {
-    constexpr int NW = sizeof(SetupL) / sizeof(real);
-    const real* cache = reinterpret_cast<const real*>(&rws[bb].st);
-    real* lds = reinterpret_cast<real*>(&smem[sub].st);
-    for (int e = lane; e < NW; e += HALF) lds[e] = cache[e];
-    wave_sync();
-  }
-  const SetupL& st = smem[sub].st;
-#else
   const SetupL& st = rws[bb].st;
-#endif
   const int i = k0 + 2;  // centre sample of this launch's step
   const int sl = lane / nl, L = lane % nl;
   const real* kt = mp.ktab_n > 0 ? &rws[bb].ktab[0][0][0] : nullptr;
@@ -3000,7 +2801,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   const GaitR g = load_gait(a.params[bb]);
   const bool ignore_reach = a.ignore_reach != 0;
   const bool straight = g.curvature == 0 && !g.rec_xf;
-#if HS_CURVED_LDS && !HS_ST_LDS
+#if HS_CURVED_LDS
   // a wave with a turning or transformed gait: the record in LDS for the turning path's many reads
   if (__ballot(!straight)) {
     constexpr int NW = sizeof(SetupL) / sizeof(real);
@@ -3057,12 +2858,6 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   if (mp.fused_w) {  // this step's joint sum of positive work, summed over the steps in order by the reduce
     if (lane == 0 && live)
       reinterpret_cast<real*>(mp.fused_work)[(size_t)(mp.fused_s0 + fstep) * a.n_rollouts + b] = work;
-#if HS_EXP_FENCE  // timing experiment: the agent-scope release and ticket a last-wave reduce would need
-    if (DEFER) {
-      __threadfence();
-      if (threadIdx.x == 0) atomicAdd(mp.fix_count, 0);
-    }
-#endif
     return;
   }
   if (lane == 0 && live) {
@@ -3247,14 +3042,7 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   hipStream_t st = (hipStream_t)a.stream;
   RolloutWS* ws = (RolloutWS*)workspace;
   if (mp.setup_only) {
-    if (HS_PREP && mp.ktab_n > 0 && mp.prep_ctr) {  // the setup pass and the IK table in one launch
-      const int64_t items = 2 * (int64_t)mp.n_waves * mp.ktab_n * (mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX);
-      hipLaunchKernelGGL(hs_prep_kernel, dim3((unsigned)(mp.n_waves + (items + WAVE - 1) / WAVE)), dim3(WAVE), 0, st,
-                         d_topo, a, ws, mp);
-      return (int)hipGetLastError();
-    }
-    hipLaunchKernelGGL(hs_setup_kernel, dim3((mp.n_waves + HS_SETUP_WAVES - 1) / HS_SETUP_WAVES),
-                       dim3(WAVE * HS_SETUP_WAVES), 0, st, d_topo, a, ws, mp);
+    hipLaunchKernelGGL(hs_setup_kernel, dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
     if (mp.ktab_n > 0) {  // the call's IK table, from the frames the setup pass stored
       const int64_t blocks =
           8 * (int64_t)ktab_blocks_per_wave(mp.ktab_n, mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX) * ((mp.n_waves + 7) / 8);

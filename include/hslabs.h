@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 12
+#define HSLABS_ABI_VERSION 13
 
 enum {
   HS_OK = 0,
@@ -41,6 +41,17 @@ enum {
 #define HS_FLAG_NO_CONTACT  32u  /* no foot in contact (k = 0) */
 #define HS_FLAG_GENERAL     64u  /* closed-form solve declined (conditioning guard): Eigen-style
                                     FullPivLU/ColPivQR path used (informational) */
+#define HS_FLAG_NEAR_RANK  256u  /* a rank or routing decision of the step lay within rounding of its
+                                    threshold, so another rounding (another basis, FMA contraction,
+                                    the other precision) may decide it the other way: a FullPivLU pivot
+                                    within 4x of the rank threshold in use (ftsolver.cpp:208-214), the
+                                    threshold doubled (:212-214), rel_error in [1e-7, 1e-5] against the
+                                    loop's 1e-6 (:228-232), a ColPivQR column norm within 4x of its
+                                    nonzero-pivot threshold, the closed form's collinearity guard or
+                                    pivot guards within 4x of theirs; solve_forces: a normal-matrix
+                                    pivot within 4x of its rank guard (ftsolver.cpp:349-353). The
+                                    step's outputs are the path's answer; equality with another
+                                    implementation is only expected where neither side sets this. */
 
 /* Gait setup of one rollout: the fields of pgsconfigparams (pergen.h:137-146),
  * same meaning and units as a pgs_config.txt line (player.cpp:170-208), plus
@@ -415,9 +426,11 @@ int hs_comm_reduce_best(hs_comm_t comm, uint64_t* key, void* stream);
  * must run on the comm's device only), all-reduced over the communicator, decoded on every rank.
  * The reduce runs in the comm's own 8-byte device buffer: the batch's per-device keys keep their
  * local values (a later hs_select_best still returns this process's minimum). Collective: every
- * rank must call it. A rank whose batch fails the checks (not run, another device, null outputs)
- * still takes part, contributing the largest key, and then returns the error, so its peers complete
- * (with the minimum over the other ranks); a null comm returns at once and leaves the peers waiting. */
+ * rank must call it. A rank whose batch fails the checks (not run, another device, null outputs) or
+ * whose local keys cannot be read back still takes part, contributing the largest key, and then
+ * returns the error, so its peers complete (with the minimum over the other ranks). Two failures
+ * return before the collective and leave the peers waiting: a null comm, and a HIP runtime error on
+ * the comm's own device while staging the key (the communicator is unusable then). */
 int hs_select_best_comm(hs_batch_t batch, hs_comm_t comm, float* cot, int64_t* rollout_id);
 
 /*

@@ -1036,6 +1036,41 @@ void upper_solve_inplace(const Mat& U, int n, double* x) {
   }
 }
 
+// Decisions taken within rounding of a threshold (hard part 2:
+// such samples are flagged, not silently compared). Each decision the solve takes against a
+// threshold reports its margin: |log(value / threshold)| / log(band), so a margin <= 1 means the
+// value lies within the decision's band of its threshold, where another rounding (another basis,
+// FMA contraction, single precision) may decide the other way:
+//   FullPivLU rank (ftsolver.cpp:208-214, Eigen's |u_ii| > maxpivot * thr): every pivot, band 4
+//   threshold doubled (ftsolver.cpp:212-214: setThreshold(2 thr) while rank > rank0): margin 0
+//   rel_error > 1e-6 (ftsolver.cpp:228-232): band 10, i.e. rel_error in [1e-7, 1e-5]
+//   ColPivHouseholderQR nonzero pivots (|col|^2 < threshold_helper (rows - k)): band 16 on the squares
+//   the closed form's routing: the collinearity guard (band 4) and its pivot guards (band 4)
+// The step then carries HSO_FLAG_NEAR_RANK (the kernel computes the same margins, HS_FLAG_NEAR_RANK).
+constexpr double kNearBand = 4.0, kNearBandRel = 10.0, kNearBandQR = 16.0;
+struct NearTrack {
+  double margin = INFINITY;
+  int cat = 0;  // the decision closest to its threshold: HSO_NEAR_*
+  double lu_kept = INFINITY, qr_kept = INFINITY;  // conditioning of the last pass: smallest kept pivot ratios
+#ifndef HSO_FLOPCOUNT
+  void note(double ratio, double band, int c) {
+    if (!(ratio > 0)) return;  // exact zeros are structural, not near anything
+    const double m = fabs(log(ratio)) / log(band);
+    if (m < margin) { margin = m; cat = c; }
+  }
+#endif
+  bool near() const { return margin <= 1.0; }
+};
+thread_local NearTrack tl_near;
+// diagnostics, not arithmetic of the path: the FLOP-counting build (hs_oracle_flops.cpp) leaves them out
+#ifdef HSO_FLOPCOUNT
+#define NEAR_NOTE(ratio, band, cat) ((void)0)
+#else
+#define NEAR_NOTE(ratio, band, cat) tl_near.note((ratio), (band), (cat))
+#endif
+enum { HSO_NEAR_LU = 1, HSO_NEAR_DOUBLED = 2, HSO_NEAR_REL = 3, HSO_NEAR_QR = 4, HSO_NEAR_COLLINEAR = 5,
+       HSO_NEAR_PIVOT = 6 };
+
 // Eigen FullPivLU (FullPivLU.h), restated.
 struct FPLU {
   int n = 0;
@@ -1176,6 +1211,7 @@ struct CPQR {
       for (int j = k + 1; j < cols; j++)
         if (nu[j] > bv) { bv = nu[j]; bi = j; }
       double bsq = bv * bv;
+      if (nonzero_pivots == size) NEAR_NOTE(bsq / (threshold_helper * (double)(rows - k)), kNearBandQR, HSO_NEAR_QR);
       if (nonzero_pivots == size && bsq < threshold_helper * (double)(rows - k)) nonzero_pivots = k;
       colsT[k] = bi;
       if (k != bi) {
@@ -1233,6 +1269,9 @@ struct FTOut {
   uint32_t flags = 0;
   int k = 0, rank0 = 0, iters = 0;
   double rel_error = 0;
+  double near_margin = INFINITY;  // the decision closest to its threshold (NearTrack)
+  int near_cat = 0;
+  double lu_kept = INFINITY, qr_kept = INFINITY;
 };
 
 // dynrecord::set_forcetorque_system (dynrec.cpp:227-297) as dense B0 (6n x 6n) and f
@@ -1393,7 +1432,19 @@ void solve_contact_forces(const hso_model* m, const std::vector<double>& jz, con
     iters++;
     FPLU lu;
     lu.compute(ntn0);
-    while (lu.rank() > rank0) lu.set_threshold(2 * lu.threshold());
+    while (lu.rank() > rank0) {
+      lu.set_threshold(2 * lu.threshold());
+      NEAR_NOTE(1.0, kNearBand, HSO_NEAR_DOUBLED);
+    }
+    for (int i = 0; i < lu.nonzero_pivots; i++)
+      NEAR_NOTE(fabs(lu.lu(i, i)) / (fabs(lu.maxpivot) * lu.threshold()), kNearBand, HSO_NEAR_LU);
+#ifndef HSO_FLOPCOUNT
+    tl_near.lu_kept = INFINITY;
+    for (int i = 0; i < lu.nonzero_pivots; i++) {
+      const double rr = fabs(lu.lu(i, i)) / fabs(lu.maxpivot);
+      if (rr > lu.threshold() && rr < tl_near.lu_kept) tl_near.lu_kept = rr;
+    }
+#endif
     std::vector<double> mntx0(k);
     for (int i = 0; i < k; i++) mntx0[i] = -ntx0[i];
     std::vector<double> y0 = lu.solve(mntx0);
@@ -1411,10 +1462,15 @@ void solve_contact_forces(const hso_model* m, const std::vector<double>& jz, con
     for (int j = 0; j < Bm.c; j++) for (int i = 0; i < k; i++) M(i, A.c + j) = Bm(i, j);
     CPQR qr;
     qr.compute(M);
+#ifndef HSO_FLOPCOUNT
+    tl_near.qr_kept = INFINITY;
+    for (int i = 0; i < qr.nonzero_pivots; i++) tl_near.qr_kept = std::min(tl_near.qr_kept, fabs(qr.qr(i, i)) / fabs(qr.qr(0, 0)));
+#endif
     std::vector<double> z = qr.solve(b);
     std::vector<double> mz = matvec(M, z);
     for (int i = 0; i < k; i++) mz[i] -= b[i];
     rel_error = vnorm(mz) / vnorm(b);
+    NEAR_NOTE(rel_error / 1e-6, kNearBandRel, HSO_NEAR_REL);
     rank0--;
     std::vector<double> zh(z.begin(), z.begin() + Ny.c);
     std::vector<double> nyz = matvec(Ny, zh);
@@ -1442,13 +1498,14 @@ void solve_contact_forces(const hso_model* m, const std::vector<double>& jz, con
 constexpr double kFastPivotGuard = 1e-10;
 
 // in-place Cholesky of an n x n SPD matrix (row-major a[i*n+j]); false if a pivot
-// falls below guard * max diagonal
+// falls below guard * max diagonal (a guarded pivot's distance to it goes to tl_near)
 bool chol(double* a, int n, double guard) {
   double mx = 0;
   for (int i = 0; i < n; i++) mx = std::max(mx, a[i * n + i]);
   for (int j = 0; j < n; j++) {
     double s = a[j * n + j];
     for (int k = 0; k < j; k++) s -= a[j * n + k] * a[j * n + k];
+    if (guard > 0) NEAR_NOTE(s / (guard * mx), kNearBand, HSO_NEAR_PIVOT);
     if (!(s > guard * mx)) return false;
     double l = sqrt(s), rl = 1.0 / l;  // one division per pivot, as the kernel
     a[j * n + j] = l;
@@ -1482,6 +1539,7 @@ bool ldl(double* a, int n, double guard) {
     for (int k = 0; k < j; k++) v[k] = a[j * n + k] * a[k * n + k];
     double dj = a[j * n + j];
     for (int k = 0; k < j; k++) dj -= a[j * n + k] * v[k];
+    if (guard > 0) NEAR_NOTE(dj / (guard * mx), kNearBand, HSO_NEAR_PIVOT);
     if (!(dj > guard * mx)) return false;
     const double r = 1.0 / dj;
     a[j * n + j] = dj;
@@ -1598,6 +1656,7 @@ bool zeroth_well_posed(const DynRec& d, const std::vector<int>& cf) {
   const double c2 = (c00 * c11 - c01 * c01) + (c00 * c22 - c02 * c02) + (c11 * c22 - c12 * c12);
   const double tq = q00 + q11 + q22;
   const double md = std::max(k, std::max(tq - q00, std::max(tq - q11, tq - q22)));
+  NEAR_NOTE(c2 / (kZerothGuard * k * (c00 + c11 + c22) * md), kNearBand, HSO_NEAR_COLLINEAR);
   return c2 >= kZerothGuard * k * (c00 + c11 + c22) * md;
 }
 
@@ -1740,11 +1799,14 @@ bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<d
 // (set_forcetorque_system_contacts with contact_feet_flag = false, dynrec.cpp:313-325)
 // realising the motor torques z, torso force/torque columns zeroed, least squares
 // over [B0 Bc_all; jz-rows] [x; y] = [f; z] (add_torque_constraints_to_B, 359-378).
-// SparseQR's basic solution leaves the zero torso columns at 0 and is the unique
-// LS solution of the remaining columns when they have full rank; here a dense
-// Householder QR of those columns. Rank deficiency (a straight leg's torques
-// cannot fix its foot force) returns false and the Tikhonov-regularized
-// (1e-12 * max diag) normal-equations solution.
+// SparseQR's basic solution leaves the zero torso columns at 0; the other columns are
+// factorized here by a column-by-column Householder QR in their natural order (the
+// joint wrenches, then the feet's force components). A force column whose pivot r_jj^2
+// falls to 1e-10 of the largest force column's squared norm after the wrenches' reflections
+// (the reduced normal matrix's largest diagonal; the kernel's chol_packed guard on the same
+// quantity) is dependent: it is dropped and its force component set to 0, the basic
+// solution of the rank-deficient least squares (a straight leg's torques cannot fix its
+// foot force along the leg). Returns false when a column was dropped.
 bool solve_forces(const hso_model* m, const DynRec& d, const double* z, std::vector<double>& y) {
   const int n = m->n, nf = m->nf, nmj = m->nmj;
   Mat B0;
@@ -1783,35 +1845,40 @@ bool solve_forces(const hso_model* m, const DynRec& d, const double* z, std::vec
     }
     b[6 * n + jj] = z[jj];
   }
-  HQR qr;
-  qr.compute(A);
-  double rmax = 0;
-  for (int i = 0; i < cols; i++) rmax = std::max(rmax, fabs(qr.qr(i, i)));
+  const double kRankGuard = 1e-10;  // the kernel's kFastPivotGuard on the reduced normal matrix
+  Mat R = A, bm(rows, 1);
+  for (int i = 0; i < rows; i++) bm(i, 0) = b[i];
+  std::vector<int> piv;  // kept columns in order (R's row t belongs to piv[t])
   bool full = true;
-  for (int i = 0; i < cols; i++) full = full && fabs(qr.qr(i, i)) > 1e-10 * rmax;
-  std::vector<double> u;
-  if (full) {
-    u = qr.solve(b);
-  } else {
-    Mat N(cols, cols);
-    std::vector<double> r(cols, 0.0);
-    double dmax = 0;
-    for (int i = 0; i < cols; i++) {
-      for (int j = 0; j < cols; j++) {
-        double s = 0;
-        for (int t = 0; t < rows; t++) s += A(t, i) * A(t, j);
-        N(i, j) = s;
+  double mxd = 0;
+  std::vector<double> ess;
+  for (int j = 0; j < cols; j++) {
+    const int k = (int)piv.size();
+    if (j == y0)  // the force columns' squared norms after the wrenches' reflections
+      for (int jj = y0; jj < cols; jj++) {
+        double s2 = 0;
+        for (int i = k; i < rows; i++) s2 += R(i, jj) * R(i, jj);
+        mxd = std::max(mxd, s2);
       }
-      for (int t = 0; t < rows; t++) r[i] += A(t, i) * b[t];
-      dmax = std::max(dmax, N(i, i));
+    if (j >= y0) {
+      double s2 = 0;  // r_jj^2 if kept: the column's squared norm on the rows not yet eliminated
+      for (int i = k; i < rows; i++) s2 += R(i, j) * R(i, j);
+      NEAR_NOTE(s2 / (kRankGuard * mxd), kNearBand, HSO_NEAR_PIVOT);
+      if (!(s2 > kRankGuard * mxd)) { full = false; continue; }
     }
-    for (int i = 0; i < cols; i++) N(i, i) += 1e-12 * dmax;
-    std::vector<double> nn(cols * cols);
-    for (int i = 0; i < cols; i++)
-      for (int j = 0; j < cols; j++) nn[i * cols + j] = N(i, j);
-    chol(nn.data(), cols, 0.0);
-    chol_solve(nn.data(), cols, r.data());
-    u = r;
+    double tau, beta;
+    make_householder(&R(k, j), rows - k, 1, tau, beta);
+    R(k, j) = beta;
+    ess.assign(&R(k, j) + 1, &R(k, j) + (rows - k));
+    apply_householder_left(R, k, ess.data(), tau, j + 1, cols);
+    apply_householder_left(bm, k, ess.data(), tau, 0, 1);
+    piv.push_back(j);
+  }
+  std::vector<double> u(cols, 0.0);  // dropped columns stay 0
+  for (int t = (int)piv.size() - 1; t >= 0; t--) {
+    double v = bm(t, 0);
+    for (int t2 = t + 1; t2 < (int)piv.size(); t2++) v -= R(t, piv[t2]) * u[piv[t2]];
+    u[piv[t]] = v / R(t, piv[t]);
   }
   y.assign(u.begin() + y0, u.begin() + y0 + 3 * nf);
   return full;
@@ -1820,6 +1887,7 @@ bool solve_forces(const hso_model* m, const DynRec& d, const double* z, std::vec
 // forcetorquesolver::solve_forcetorques, ftsolver.cpp:78-102
 void solve_forcetorques(const hso_model* m, const DynRec& d, int basis, FTOut& out) {
   int n = m->n;
+  tl_near = NearTrack();
   std::vector<double> jz(3 * n);
   for (int i = 0; i < n; i++) for (int j = 0; j < 3; j++) jz[3 * i + j] = d.jzaxis[i].v[j];
   Mat B0;
@@ -1876,6 +1944,11 @@ void solve_forcetorques(const hso_model* m, const DynRec& d, int basis, FTOut& o
     x[r] += s;
   }
   out.x = x;
+  out.near_margin = tl_near.margin;
+  out.near_cat = tl_near.cat;
+  out.lu_kept = tl_near.lu_kept;
+  out.qr_kept = tl_near.qr_kept;
+  if (tl_near.near()) out.flags |= HSO_FLAG_NEAR_RANK;
 }
 
 int load_model(const char* path, hso_model** out) {
@@ -1938,7 +2011,8 @@ int load_model(const char* path, hso_model** out) {
 
 // One rollout (periodic.cpp:77-96, 149-160, 192-202, 261-307, 328-343, 377-391)
 int run_rollout(const hso_model* m0, const hso_gait* g, int n_t, int k0, int H, int basis, int ignore_reach,
-                double* q, double* tau, double* cf, double* xo, uint32_t* flags, double* work_cot, double* diag) {
+                double* q, double* tau, double* cf, double* xo, uint32_t* flags, double* work_cot, double* diag,
+                double* nearv = nullptr) {
   hso_model mm = *m0;  // private model state (joint values live in the tree, model.h:38)
   hso_model* m = &mm;
   tl_ignore_reach = ignore_reach != 0;
@@ -1996,6 +2070,7 @@ int run_rollout(const hso_model* m0, const hso_gait* g, int n_t, int k0, int H, 
       diag[4 * h + 0] = ft.k; diag[4 * h + 1] = ft.rank0;
       diag[4 * h + 2] = ft.iters; diag[4 * h + 3] = ft.rel_error;
     }
+    if (nearv) { nearv[4 * h] = ft.near_margin; nearv[4 * h + 1] = ft.near_cat; nearv[4 * h + 2] = ft.lu_kept; nearv[4 * h + 3] = ft.qr_kept; }
     // compute_vel_traj (periodic.cpp:261-282) + work_over_period (285-307)
     double work_dt = 0;
     for (int jj = 0; jj < nmj; jj++) {
@@ -2056,7 +2131,9 @@ int run_forces(const hso_model* m0, const hso_gait* g, int n_t, int k0, int H, i
   for (int h = 0; h < H; h++) {
     int i = k0 + h + 2;
     std::vector<double> y;
+    tl_near = NearTrack();
     uint32_t fl = solve_forces(m, dr[i], tau_in + (size_t)h * nmj, y) ? 0u : HSO_FLAG_GENERAL;
+    if (tl_near.near()) fl |= HSO_FLAG_NEAR_RANK;
     if (unreach[i]) fl |= HSO_FLAG_UNREACH;
     for (double v : y) if (std::isnan(v)) fl |= HSO_FLAG_NAN;
     if (cf) std::copy(y.begin(), y.end(), cf + (size_t)h * 3 * nf);
@@ -2094,8 +2171,9 @@ int hso_forces(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, in
   return run_forces(m, g, n_t, k0, H, ignore_reach, tau_in, cf, flags);
 }
 
-int hso_batch(const hso_model* m, const hso_gait* params, int B, int n_t, int k0, int H, int basis,
-              int ignore_reach, int n_threads, double* tau, double* cf, double* work_cot, uint32_t* flags) {
+int hso_batch_near(const hso_model* m, const hso_gait* params, int B, int n_t, int k0, int H, int basis,
+                   int ignore_reach, int n_threads, double* tau, double* cf, double* work_cot, uint32_t* flags,
+                   double* nearv) {
   if (n_threads < 1) n_threads = 1;
   std::vector<int> rc(n_threads, 0);
   auto worker = [&](int tid) {
@@ -2104,7 +2182,8 @@ int hso_batch(const hso_model* m, const hso_gait* params, int B, int n_t, int k0
                           tau ? tau + (size_t)b * H * m->nmj : nullptr,
                           cf ? cf + (size_t)b * H * 3 * m->nf : nullptr, nullptr,
                           flags ? flags + (size_t)b * H : nullptr,
-                          work_cot ? work_cot + 2 * (size_t)b : nullptr, nullptr);
+                          work_cot ? work_cot + 2 * (size_t)b : nullptr, nullptr,
+                          nearv ? nearv + 4 * (size_t)b * H : nullptr);
       if (r) rc[tid] = r;
     }
   };
@@ -2114,6 +2193,31 @@ int hso_batch(const hso_model* m, const hso_gait* params, int B, int n_t, int k0
   for (auto& t : th) t.join();
   for (int r : rc) if (r) return r;
   return 0;
+}
+
+int hso_forces_batch(const hso_model* m, const hso_gait* params, int B, int n_t, int k0, int H, int ignore_reach,
+                     int n_threads, const double* tau_in, double* cf, uint32_t* flags) {
+  if (!m || !params || !tau_in || n_t <= 0 || k0 < 0 || H <= 0) return -1;
+  if (n_threads < 1) n_threads = 1;
+  std::vector<int> rc(n_threads, 0);
+  auto worker = [&](int tid) {
+    for (int b = tid; b < B; b += n_threads) {
+      int r = run_forces(m, &params[b], n_t, k0, H, ignore_reach, tau_in + (size_t)b * H * m->nmj,
+                         cf ? cf + (size_t)b * H * 3 * m->nf : nullptr, flags ? flags + (size_t)b * H : nullptr);
+      if (r) rc[tid] = r;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < n_threads; t++) th.emplace_back(worker, t);
+  worker(0);
+  for (auto& t : th) t.join();
+  for (int r : rc) if (r) return r;
+  return 0;
+}
+
+int hso_batch(const hso_model* m, const hso_gait* params, int B, int n_t, int k0, int H, int basis,
+              int ignore_reach, int n_threads, double* tau, double* cf, double* work_cot, uint32_t* flags) {
+  return hso_batch_near(m, params, B, n_t, k0, H, basis, ignore_reach, n_threads, tau, cf, work_cot, flags, nullptr);
 }
 
 double hso_lik_roundtrip(const hso_model* m, int n, uint64_t seed) {

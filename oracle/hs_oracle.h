@@ -50,6 +50,8 @@ enum { HSO_BASIS_ORTHO = 0, /* reference-faithful: orthonormal Q of QR(B^T) (fts
 #define HSO_FLAG_UNREACH     16u  /* an IK target was clamped (ignore_reach, lik.cpp:250-253) */
 #define HSO_FLAG_NO_CONTACT  32u  /* k == 0 */
 #define HSO_FLAG_GENERAL     64u  /* FAST mode: closed form declined, Eigen-style path used */
+#define HSO_FLAG_NEAR_RANK  256u  /* a rank / routing decision within rounding of its threshold (NearTrack):
+                                     another rounding may decide it the other way (HS_FLAG_NEAR_RANK) */
 
 typedef struct hso_model hso_model;
 
@@ -88,9 +90,17 @@ int hso_rollout(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, i
  * for ALL feet; flags HSO_FLAG_GENERAL when the least squares is rank deficient. */
 int hso_forces(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, int ignore_reach, const double* tau_in,
                double* cf, uint32_t* flags);
+/* hso_forces for B rollouts on n_threads threads: tau_in [B][H][nmj] -> cf [B][H][3 nf], flags [B][H] */
+int hso_forces_batch(const hso_model* m, const hso_gait* params, int B, int n_t, int k0, int H, int ignore_reach,
+                     int n_threads, const double* tau_in, double* cf, uint32_t* flags);
 int hso_batch(const hso_model* m, const hso_gait* params, int B, int n_t, int k0, int H,
               int basis, int ignore_reach, int n_threads, double* tau, double* cf,
               double* work_cot, uint32_t* flags);
+/* hso_batch plus, per step, the margin of the decision closest to its threshold and its kind
+ * (nearv [B][H][2]: margin, HSO_NEAR_* category; margin <= 1 sets HSO_FLAG_NEAR_RANK) */
+int hso_batch_near(const hso_model* m, const hso_gait* params, int B, int n_t, int k0, int H,
+                   int basis, int ignore_reach, int n_threads, double* tau, double* cf,
+                   double* work_cot, uint32_t* flags, double* nearv);
 
 /* Known-answer helpers (restated reference self-checks). */
 /* lik.cpp:371-404: bend_solver o limb_solver round trip; returns max error over n tries */

@@ -27,6 +27,9 @@ FLAG_NAN = 8
 FLAG_UNREACH = 16
 FLAG_NO_CONTACT = 32
 FLAG_GENERAL = 64
+FLAG_NEAR_RANK = 256  # a rank / routing decision within rounding of its threshold (hs_oracle.cpp NearTrack)
+NEAR_KINDS = {0: "none", 1: "LU pivot", 2: "threshold doubled", 3: "rel_error", 4: "QR pivot", 5: "collinear guard",
+              6: "pivot guard"}
 BASIS_FAST = 2
 
 
@@ -168,8 +171,13 @@ def _bind(path):
     L.hso_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, dp,
                             ctypes.POINTER(ctypes.c_uint32)]
+    L.hso_batch_near.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, dp,
+                                 ctypes.POINTER(ctypes.c_uint32), dp]
     L.hso_forces.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                              ctypes.c_int, dp, dp, ctypes.POINTER(ctypes.c_uint32)]
+    L.hso_forces_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, ctypes.POINTER(ctypes.c_uint32)]
     L.hso_lik_roundtrip.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]
     L.hso_lik_roundtrip.restype = ctypes.c_double
     L.hso_euler_roundtrip.argtypes = [dp, dp]
@@ -305,10 +313,27 @@ def forces(model: Model, gait: GaitParams, tau_in, n_t: int = 20, k0: int = 0, i
     return dict(cf=cf, flags=flags)
 
 
+def forces_batch(model: Model, gaits: list, tau_in, n_t: int = 20, k0: int = 0, ignore_reach: bool = True,
+                 n_threads: int = 1, L=None) -> dict:
+    """forces() for B rollouts on n_threads threads: tau_in [B][H][nmj] -> cf [B][H][3 nf], flags [B][H]."""
+    L = L or lib()
+    tau_in = np.ascontiguousarray(tau_in, dtype=np.float64)
+    B, H = tau_in.shape[:2]
+    arr = (Gait * B)(*[g.to_c() for g in gaits])
+    cf = np.zeros((B, H, 3 * model.nf))
+    flags = np.zeros((B, H), dtype=np.uint32)
+    rc = L.hso_forces_batch(model.handle, arr, B, n_t, k0, H, int(ignore_reach), n_threads, _ptr(tau_in), _ptr(cf),
+                            flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    if rc != 0:
+        raise RuntimeError(f"oracle forces_batch failed rc={rc}")
+    return dict(cf=cf, flags=flags)
+
+
 def batch(model: Model, gaits: list, n_t: int, k0: int, H: int, basis: int = BASIS_TREE,
           ignore_reach: bool = True, n_threads: int = 1, L=None) -> dict:
     """B rollouts on n_threads threads. L: another build of the same restatement (perf_lib) whose
-    hso_model the Model was loaded with (Model(path, L=...))."""
+    hso_model the Model was loaded with (Model(path, L=...)). near_margin / near_kind: per step, the
+    decision closest to its threshold (margin <= 1 sets FLAG_NEAR_RANK; NEAR_KINDS)."""
     L = L or lib()
     B = len(gaits)
     arr = (Gait * B)(*[g.to_c() for g in gaits])
@@ -316,11 +341,14 @@ def batch(model: Model, gaits: list, n_t: int, k0: int, H: int, basis: int = BAS
     cf = np.zeros((B, H, 3 * model.nf))
     wc = np.zeros((B, 2))
     flags = np.zeros((B, H), dtype=np.uint32)
-    rc = L.hso_batch(model.handle, arr, B, n_t, k0, H, basis, int(ignore_reach), n_threads,
-                         _ptr(tau), _ptr(cf), _ptr(wc), flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    near = np.zeros((B, H, 4))
+    rc = L.hso_batch_near(model.handle, arr, B, n_t, k0, H, basis, int(ignore_reach), n_threads,
+                          _ptr(tau), _ptr(cf), _ptr(wc), flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                          _ptr(near))
     if rc != 0:
         raise RuntimeError(f"oracle batch failed rc={rc}")
-    return dict(tau=tau, cf=cf, work=wc[:, 0], cot=wc[:, 1], flags=flags)
+    return dict(tau=tau, cf=cf, work=wc[:, 0], cot=wc[:, 1], flags=flags, near_margin=near[..., 0],
+                near_kind=near[..., 1].astype(np.int32), lu_kept=near[..., 2], qr_kept=near[..., 3])
 
 
 def lik_roundtrip(model: Model, n: int = 1000, seed: int = 1) -> float:

@@ -5,10 +5,17 @@ The oracle is the CPU restatement (oracle/, parity with the reference binary unp
 batches, full-rank steps included (measured on CPU: fast vs tree <= 3e-12, ortho vs tree <= 5e-13).
 
 Tolerances (written here, per the north_star): fp64 per-joint motor torque |GPU - oracle| <
-1e-6 N*m on EVERY step (the north_star bound) and < 1e-9 * max(1, |tau|) on every step (what the
-kernel achieves: ULPs of the device transcendentals amplified by the 1 / (4 dt^2) stencil); contact
-forces < 1e-8 * max(1, |f|); flags identical (HS_FLAG_GENERAL aside). fp32 (configs[2]): 1e-3 *
-max(1, |tau|) wherever the fp32 run chose the same contact set as the fp64 oracle.
+1e-6 N*m (the north_star bound) and < 1e-9 * max(1, |tau|) (what the kernel achieves: ULPs of the
+device transcendentals amplified by the 1 / (4 dt^2) stencil); contact forces < 1e-8 * max(1, |f|);
+flags identical (HS_FLAG_GENERAL and HS_FLAG_NEAR_RANK aside). fp32 (configs[2]): 1e-3 * max(1, |tau|)
+wherever the fp32 run chose the same contact set as the fp64 oracle.
+
+Every bound holds on EVERY step that neither side flags HS_FLAG_NEAR_RANK (include/hslabs.h; the
+oracle's HSO_FLAG_NEAR_RANK, hs_oracle.cpp NearTrack): a rank or routing decision within rounding of
+its threshold (FullPivLU pivots within 4x of the rank threshold, a doubled threshold, rel_error in
+[1e-7, 1e-5], ColPivQR pivots, the closed form's guards; ftsolver.cpp:205-232), where another rounding
+may take the decision the other way (hard part 2: flagged, not silently compared). The
+flagged steps are counted and printed; they must be finite.
 """
 import os
 
@@ -24,6 +31,24 @@ TAU_ABS = 1e-6  # north_star
 CF_REL = 1e-8
 FP32_TOL = 1e-3
 GEN = np.uint32(64)  # HS_FLAG_GENERAL: which solve path ran, not a property of the step
+NEAR = np.uint32(256)  # HS_FLAG_NEAR_RANK = HSO_FLAG_NEAR_RANK: a decision within rounding of its threshold
+IGN = GEN | NEAR  # flag bits that describe the arithmetic, not the step
+
+
+def near(*flags):
+    """steps that any of the given flag arrays marks HS_FLAG_NEAR_RANK"""
+    m = np.zeros(np.shape(flags[0]), dtype=bool)
+    for f in flags:
+        m |= (np.asarray(f).astype(np.uint32) & NEAR) != 0
+    return m
+
+
+def check_flags(g, r, what, skip=None):
+    """flags identical on the steps not skipped, HS_FLAG_GENERAL / HS_FLAG_NEAR_RANK aside"""
+    g, r = np.asarray(g).astype(np.uint32) & ~IGN, np.asarray(r).astype(np.uint32) & ~IGN
+    keep = np.ones(g.shape, bool) if skip is None else ~skip
+    bad = (g != r) & keep
+    assert not bad.any(), f"{what}: flags differ on {bad.sum()} unflagged steps"
 
 
 @pytest.fixture(scope="module")
@@ -48,7 +73,16 @@ def npy(t):
     return t.cpu().numpy()
 
 
-def check_tau(tau, ref, what):
+def check_tau(tau, ref, what, skip=None):
+    """both bounds on every step (rows [..., nmj]) outside `skip` (steps flagged near a decision on
+    either side); skipped steps must be finite, and are counted"""
+    if skip is not None:
+        assert np.isfinite(tau[skip]).all(), f"{what}: non-finite torques on flagged steps"
+        if skip.any():
+            print(f"{what}: {int(skip.sum())} of {skip.size} steps flagged HS_FLAG_NEAR_RANK, not compared")
+        tau, ref = tau[~skip], ref[~skip]
+    if tau.size == 0:
+        return
     scale = np.maximum(1, np.abs(ref).max(axis=-1, keepdims=True))
     err = np.abs(tau - ref)
     assert err.max() < TAU_ABS, f"{what}: max |dtau| {err.max():.3e} over the north_star bound"
@@ -56,7 +90,11 @@ def check_tau(tau, ref, what):
     assert (rel < TAU_REL).all(), f"{what}: {(rel >= TAU_REL).sum()} steps over {TAU_REL} (max {rel.max():.3e})"
 
 
-def check_cf(cf, ref, what):
+def check_cf(cf, ref, what, skip=None):
+    if skip is not None:
+        cf, ref = cf[~skip], ref[~skip]
+    if cf.size == 0:
+        return
     scale = np.maximum(1, np.abs(ref).max(axis=-1, keepdims=True))
     rel = (np.abs(cf - ref) / scale).max()
     assert rel < CF_REL, f"{what}: contact forces off by {rel:.3e}"
@@ -85,10 +123,13 @@ def test_configs1_full_size_matches_oracle_tree(gpu, hmodels, oracle_mod, omodel
     g = fused_cycle(gpu, hmodels["hexapod"], params)
     gaits = [record_to_oracle_gait(oracle_mod, r) for r in params]
     r = oracle_mod.batch(omodels["hexapod"], gaits, 20, 0, 20, basis=oracle_mod.BASIS_TREE, n_threads=threads())
-    check_tau(g["tau"], r["tau"], "configs[1] vs tree")
-    check_cf(g["cf"], r["cf"], "configs[1] vs tree")
-    assert np.array_equal(g["flags"].astype(np.uint32) & ~GEN, r["flags"])
-    np.testing.assert_allclose(g["work_cot"][:, 0], r["work"], rtol=1e-9, atol=1e-12)
+    skip = near(g["flags"], r["flags"])
+    assert not near(g["flags"]).any()  # the closed form's guards sit far from their thresholds on these gaits
+    check_tau(g["tau"], r["tau"], "configs[1] vs tree", skip)
+    check_cf(g["cf"], r["cf"], "configs[1] vs tree", skip)
+    check_flags(g["flags"], r["flags"], "configs[1] vs tree", skip)
+    whole = ~skip.any(axis=1)  # the work sums every step of the rollout
+    np.testing.assert_allclose(g["work_cot"][whole, 0], r["work"][whole], rtol=1e-9, atol=1e-12)
 
 
 def test_configs3_last_rank_shard_matches_oracle(gpu, hmodels, oracle_mod, omodels):
@@ -122,10 +163,12 @@ def test_configs3_last_rank_shard_matches_oracle(gpu, hmodels, oracle_mod, omode
     g = {k: npy(getattr(b, k)) for k in ("tau", "cf", "flags", "work_cot")}
     gaits = [record_to_oracle_gait(oracle_mod, r) for r in params]
     r = oracle_mod.batch(omodels["hexapod"], gaits, 20, 0, K, basis=oracle_mod.BASIS_TREE, n_threads=threads())
-    check_tau(g["tau"], r["tau"], "configs[3] last rank vs tree")
-    check_cf(g["cf"], r["cf"], "configs[3] last rank vs tree")
-    assert np.array_equal(g["flags"].astype(np.uint32) & ~GEN, r["flags"])
-    np.testing.assert_allclose(g["work_cot"][:, 0], r["work"], rtol=1e-9, atol=1e-12)
+    skip = near(g["flags"], r["flags"])
+    check_tau(g["tau"], r["tau"], "configs[3] last rank vs tree", skip)
+    check_cf(g["cf"], r["cf"], "configs[3] last rank vs tree", skip)
+    check_flags(g["flags"], r["flags"], "configs[3] last rank vs tree", skip)
+    whole = ~skip.any(axis=1)
+    np.testing.assert_allclose(g["work_cot"][whole, 0], r["work"][whole], rtol=1e-9, atol=1e-12)
     # the per-step launches accumulate the same work in the same order
     seq = gpu.DeviceBatch(model, params, n_t=20, k0=0, horizon=1, outputs=("work_cot",), rollout_id_base=id0)
     seq.work_cot.zero_()
@@ -150,9 +193,10 @@ def test_configs1_sample_matches_oracle_ortho(gpu, hmodels, oracle_mod, omodels)
     g = fused_cycle(gpu, hmodels["hexapod"], params)
     gaits = [record_to_oracle_gait(oracle_mod, r) for r in params]
     r = oracle_mod.batch(omodels["hexapod"], gaits, 20, 0, 20, basis=oracle_mod.BASIS_ORTHO, n_threads=threads())
-    check_tau(g["tau"], r["tau"], "configs[1] sample vs ortho")
-    check_cf(g["cf"], r["cf"], "configs[1] sample vs ortho")
-    assert np.array_equal(g["flags"].astype(np.uint32) & ~GEN, r["flags"])
+    skip = near(g["flags"], r["flags"])
+    check_tau(g["tau"], r["tau"], "configs[1] sample vs ortho", skip)
+    check_cf(g["cf"], r["cf"], "configs[1] sample vs ortho", skip)
+    check_flags(g["flags"], r["flags"], "configs[1] sample vs ortho", skip)
 
 
 @pytest.mark.parametrize("sid", PGS_IDS)
@@ -170,10 +214,12 @@ def test_reference_solve_mode_pgs_setups(gpu, hmodels, oracle_mod, omodels, sid)
     r = oracle_mod.rollout(omodels[name], to_oracle_gait(oracle_mod, p), 20, basis=oracle_mod.BASIS_TREE)
     flags = npy(b.flags)[0].astype(np.uint32)
     assert ((flags & GEN) != 0).all(), "every step must take the Eigen-style path"
-    assert np.array_equal(flags & ~GEN, r["flags"] & ~GEN)
-    check_tau(npy(b.tau)[0], r["tau"], f"pgs {sid} reference mode")
-    check_cf(npy(b.cf)[0], r["cf"], f"pgs {sid} reference mode")
-    assert float(npy(b.work_cot)[0, 1]) == pytest.approx(r["cot"], rel=1e-9, abs=1e-12)
+    skip = near(flags, r["flags"])
+    check_flags(flags, r["flags"], f"pgs {sid} reference mode", skip)
+    check_tau(npy(b.tau)[0], r["tau"], f"pgs {sid} reference mode", skip)
+    check_cf(npy(b.cf)[0], r["cf"], f"pgs {sid} reference mode", skip)
+    if not skip.any():
+        assert float(npy(b.work_cot)[0, 1]) == pytest.approx(r["cot"], rel=1e-9, abs=1e-12)
 
 
 @pytest.mark.parametrize("name,curved", [("hexapod", False), ("hexapod", True), ("spider", True), ("myant", False)])
@@ -191,9 +237,10 @@ def test_reference_solve_mode_synthetic(gpu, hmodels, oracle_mod, omodels, name,
     gaits = [record_to_oracle_gait(oracle_mod, r) for r in params]
     r = oracle_mod.batch(omodels[name], gaits, 20, 0, 20, basis=oracle_mod.BASIS_TREE, n_threads=threads())
     assert ((g["flags"] & GEN) != 0).all()
-    assert np.array_equal(g["flags"].astype(np.uint32) & ~GEN, r["flags"])
-    check_tau(g["tau"], r["tau"], f"{name} reference mode")
-    check_cf(g["cf"], r["cf"], f"{name} reference mode")
+    skip = near(g["flags"], r["flags"])
+    check_flags(g["flags"], r["flags"], f"{name} reference mode", skip)
+    check_tau(g["tau"], r["tau"], f"{name} reference mode", skip)
+    check_cf(g["cf"], r["cf"], f"{name} reference mode", skip)
     seq = gpu.DeviceBatch(hmodels[name], params, n_t=20, k0=0, horizon=20, outputs=("tau", "cf", "flags"))
     seq.solve_mode = 1
     seq.run(best=False)
@@ -217,10 +264,11 @@ def test_full_rank_steps_match_oracle(gpu, hmodels, oracle_mod, omodels):
     assert fr.sum() >= 100, "the batch must contain single-contact steps"
     for basis in (oracle_mod.BASIS_TREE, oracle_mod.BASIS_FAST):
         r = oracle_mod.batch(omodels["myant"], gaits, 20, 0, 20, basis=basis, n_threads=threads())
-        assert np.array_equal(fr, (r["flags"] & 2) != 0)
-        check_tau(g["tau"][fr], r["tau"][fr], "full-rank steps")
-        check_cf(g["cf"][fr], r["cf"][fr], "full-rank steps")
-        check_tau(g["tau"], r["tau"], "myant batch")
+        skip = near(g["flags"], r["flags"])
+        assert np.array_equal(fr[~skip], ((r["flags"] & 2) != 0)[~skip])
+        check_tau(g["tau"][fr], r["tau"][fr], "full-rank steps", skip[fr])
+        check_cf(g["cf"][fr], r["cf"][fr], "full-rank steps", skip[fr])
+        check_tau(g["tau"], r["tau"], "myant batch", skip)
 
 
 def test_fp32_configs2_matches_fp64_oracle(gpu, hmodels, oracle_mod, omodels):
@@ -243,7 +291,7 @@ def test_fp32_configs2_matches_fp64_oracle(gpu, hmodels, oracle_mod, omodels):
     r = oracle_mod.batch(omodels["spider"], gaits, 20, 0, H, basis=oracle_mod.BASIS_TREE, n_threads=threads())
     down32 = (np.abs(cf.reshape(B, H, -1, 3)).max(axis=3) > 0)
     down64 = (np.abs(r["cf"].reshape(B, H, -1, 3)).max(axis=3) > 0)
-    same = (down32 == down64).all(axis=2) & ((flags & ~GEN) == r["flags"])
+    same = (down32 == down64).all(axis=2) & ((flags & ~IGN) == (r["flags"] & ~IGN)) & ~near(flags, r["flags"])
     assert same.mean() > 0.995, f"contact sets differ on {(~same).sum()} of {same.size} steps"
     scale = np.maximum(1, np.abs(r["tau"]).max(axis=2))
     err = np.abs(tau - r["tau"]).max(axis=2) / scale
@@ -258,9 +306,10 @@ def test_fp32_reference_solve_mode_matches_fp64_oracle(gpu, hmodels, oracle_mod,
     The first stage's Gram is rank deficient by construction (>= 3 contacts), and in float its
     negligible pivots sit ~1e-6 relative to the largest, near FullPivLU's threshold (eps * k): a
     few steps in 10^3 resolve the rank differently from fp64 and land on another point of the
-    first stage's solution set. So the bound is statistical here: >= 99.5 % of those steps within
-    the fp32 bound (in the product the fp32 build takes the closed form, which has no rank
-    decisions, and falls back to this path only where the minimizer is not unique)."""
+    first stage's solution set. The fp32 kernel flags those decisions (HS_FLAG_NEAR_RANK, its own
+    pivots against its own threshold), so the bound holds on every unflagged step (in the product
+    the fp32 build takes the closed form, which has no rank decisions, and falls back to this path
+    only where the minimizer is not unique)."""
     import torch
 
     from hslabs_amd import synth
@@ -280,9 +329,14 @@ def test_fp32_reference_solve_mode_matches_fp64_oracle(gpu, hmodels, oracle_mod,
     down64 = (np.abs(r["cf"].reshape(B, H, -1, 3)).max(axis=3) > 0)
     same = (down32 == down64).all(axis=2)
     assert same.mean() > 0.99, f"contact sets differ on {(~same).sum()} of {same.size} steps"
+    assert np.isfinite(tau[same]).all()
+    skip = near(flags, r["flags"])
+    cmp = same & ~skip
+    print(f"{name} fp32 reference mode: {int((same & skip).sum())} of {int(same.sum())} same-contact steps "
+          f"flagged HS_FLAG_NEAR_RANK (fp32 {int(near(flags).sum())}, fp64 oracle {int(near(r['flags']).sum())})")
+    assert cmp.mean() > 0.8
     scale = np.maximum(1, np.abs(r["tau"]).max(axis=2))
     err = np.abs(tau - r["tau"]).max(axis=2) / scale
-    assert np.isfinite(tau[same]).all()
-    ok = err[same] < FP32_TOL
-    assert ok.mean() >= 0.995, f"fp32 reference mode vs fp64 oracle: {(~ok).sum()} of {ok.size} steps over the bound"
-    assert np.median(err[same]) < 1e-5
+    bad = err[cmp] >= FP32_TOL
+    assert not bad.any(), f"fp32 reference mode vs fp64 oracle: {bad.sum()} of {bad.size} unflagged steps over the bound"
+    assert np.median(err[cmp]) < 1e-5

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 from conftest import MODELS, PGS_CONFIG, PGS_IDS, record_to_oracle_gait, to_oracle_gait
-from test_gpu_parity import GEN, check_cf, check_tau, fused_cycle, npy, threads
+from test_gpu_parity import GEN, check_cf, check_flags, check_tau, fused_cycle, near, npy, threads
 
 pytestmark = pytest.mark.gpu
 
@@ -53,10 +53,12 @@ def test_pgs_setups(gpu, oracle_mod, sid, force, torque):
     r = oracle_mod.rollout(om, to_oracle_gait(oracle_mod, p), 20, basis=oracle_mod.BASIS_TREE)
     flags = npy(b.flags)[0].astype(np.uint32)
     assert ((flags & GEN) != 0).all(), "every step of a masked model takes the Eigen-style path"
-    assert np.array_equal(flags & ~GEN, r["flags"] & ~GEN)
-    check_tau(npy(b.tau)[0], r["tau"], f"pgs {sid} torso penalty ({force:d},{torque:d})")
-    check_cf(npy(b.cf)[0], r["cf"], f"pgs {sid} torso penalty ({force:d},{torque:d})")
-    assert float(npy(b.work_cot)[0, 1]) == pytest.approx(r["cot"], rel=1e-9, abs=1e-12)
+    skip = near(flags, r["flags"])
+    check_flags(flags, r["flags"], f"pgs {sid} torso penalty", skip)
+    check_tau(npy(b.tau)[0], r["tau"], f"pgs {sid} torso penalty ({force:d},{torque:d})", skip)
+    check_cf(npy(b.cf)[0], r["cf"], f"pgs {sid} torso penalty ({force:d},{torque:d})", skip)
+    if not skip.any():
+        assert float(npy(b.work_cot)[0, 1]) == pytest.approx(r["cot"], rel=1e-9, abs=1e-12)
 
 
 @pytest.mark.parametrize("force,torque", MASKS)
@@ -74,9 +76,10 @@ def test_synthetic(gpu, oracle_mod, name, curved, force, torque):
     gaits = [record_to_oracle_gait(oracle_mod, r) for r in params]
     r = oracle_mod.batch(om, gaits, 20, 0, 20, basis=oracle_mod.BASIS_TREE, n_threads=threads())
     assert ((g["flags"] & GEN) != 0).all()
-    assert np.array_equal(g["flags"].astype(np.uint32) & ~GEN, r["flags"])
-    check_tau(g["tau"], r["tau"], f"{name} torso penalty ({force:d},{torque:d})")
-    check_cf(g["cf"], r["cf"], f"{name} torso penalty ({force:d},{torque:d})")
+    skip = near(g["flags"], r["flags"])
+    check_flags(g["flags"], r["flags"], f"{name} torso penalty", skip)
+    check_tau(g["tau"], r["tau"], f"{name} torso penalty ({force:d},{torque:d})", skip)
+    check_cf(g["cf"], r["cf"], f"{name} torso penalty ({force:d},{torque:d})", skip)
     seq = gpu.DeviceBatch(hm, params, n_t=20, k0=0, horizon=20, outputs=("tau", "cf", "flags"))
     seq.run(best=False)
     torch.cuda.synchronize()

@@ -81,7 +81,7 @@ def test_basis_invariance(oracle_mod, omodels, sid):
     assert abs(ro["cot"] - rt["cot"]) <= 1e-9 * abs(ro["cot"])
     # the adaptive-rank loop converges first time on every shipped setup (ftsolver.cpp:228-232)
     assert (ro["diag"][:, 2] == 1).all() and (ro["diag"][:, 3] < 1e-6).all()
-    assert (ro["flags"] == 0).all()
+    assert ((ro["flags"] & ~np.uint32(oracle_mod.FLAG_NEAR_RANK)) == 0).all()  # rank decisions near a threshold aside
 
 
 # --- static stance (pgs ids 4, 5, 11): sum of contact forces = total weight (g = 1, m = 1) -------
@@ -457,7 +457,8 @@ def test_rec_transform_translation_keeps_the_dynamics(oracle_mod, omodels, sid):
         r = O.rollout(m, replace(g, rec_transform=(tr, (0.0, 0.0, 0.0))), 20, basis=O.BASIS_TREE)
         scale = max(1.0, np.abs(base["tau"]).max())
         assert np.abs(r["tau"] - base["tau"]).max() < 1e-9 * scale
-        assert np.array_equal(r["flags"], base["flags"])
+        nr = ~np.uint32(O.FLAG_NEAR_RANK)  # which decisions sit near a threshold moves with the rounding
+        assert np.array_equal(r["flags"] & nr, base["flags"] & nr)
         assert r["cot"] == pytest.approx(base["cot"], rel=1e-9)
         assert np.abs(r["cf"] - base["cf"]).max() < 1e-8 * max(1.0, np.abs(base["cf"]).max())
         assert np.abs(r["q"][:, :2] - base["q"][:, :2] - np.array(tr[:2])).max() < 1e-12
@@ -483,4 +484,88 @@ def test_zeroth_guard_routes_collinear_contacts(oracle_mod, omodels):
     assert ((rf["flags"][retry] & O.FLAG_GENERAL) != 0).all()
     scale = np.maximum(1, np.abs(rt["tau"]).max(axis=-1, keepdims=True))
     assert (np.abs(rf["tau"] - rt["tau"]) / scale).max() < 1e-9
-    assert np.array_equal(rf["flags"] & ~np.uint32(O.FLAG_GENERAL), rt["flags"])
+    nr = ~np.uint32(O.FLAG_GENERAL | O.FLAG_NEAR_RANK)  # which path ran, and its own near decisions
+    assert np.array_equal(rf["flags"] & nr, rt["flags"] & nr)
+    # every retry decided at a doubled threshold or a rel_error near the loop's 1e-6 is flagged
+    assert ((rt["flags"][retry] & O.FLAG_NEAR_RANK) != 0).mean() >= 0.5
+
+
+@pytest.mark.parametrize("name,curved", [("hexapod", False), ("hexapod", True), ("spider", True), ("myant", False)])
+def test_near_rank_flag_rare_on_plain_gaits(oracle_mod, omodels, name, curved):
+    """HSO_FLAG_NEAR_RANK (a rank or routing decision within rounding of its threshold, hs_oracle.cpp
+    NearTrack; the kernel's HS_FLAG_NEAR_RANK) is rare on the plain synthetic gaits the bench runs: the
+    closed form's guards sit far from their thresholds there (< 1 % of the steps in fast mode, the
+    kernel's path). The Eigen-style path on every step (tree mode) meets FullPivLU's threshold more
+    often: the zeroth-order Gram of >= 3 contacts has rank 6, and its rounding-level pivots sometimes
+    land within 4x of eps * k; those steps are the ones a parity comparison leaves out."""
+    from conftest import record_to_oracle_gait
+    from hslabs_amd import synth
+
+    O = oracle_mod
+    params = synth.gen_params(512, name, id0=31337, curved=curved)
+    gaits = [record_to_oracle_gait(O, r) for r in params]
+    rf = O.batch(omodels[name], gaits, 20, 0, 20, basis=O.BASIS_FAST, n_threads=8)
+    near = (rf["flags"] & O.FLAG_NEAR_RANK) != 0
+    kinds = {O.NEAR_KINDS[k]: int((rf["near_kind"][near] == k).sum()) for k in np.unique(rf["near_kind"][near])}
+    print(f"{name} curved={curved}: fast-mode near-rank steps {near.sum()} of {near.size} {kinds}")
+    assert near.mean() < 0.01
+    assert (rf["near_margin"][near] <= 1).all() and (rf["near_margin"][~near] > 1).all()
+    rt = O.batch(omodels[name], gaits, 20, 0, 20, basis=O.BASIS_TREE, n_threads=8)
+    print(f"  tree mode: {((rt['flags'] & O.FLAG_NEAR_RANK) != 0).mean():.2%} of the steps flagged")
+    assert ((rt["flags"] & O.FLAG_NEAR_RANK) != 0).mean() < 0.1
+
+
+def test_solve_forces_rank_deficient_basic_solution(oracle_mod, omodels):
+    """solve_forces where the least squares is (nearly) rank deficient (ftsolver.cpp:349-353: the
+    reference solves with SparseQR and returns its basic solution). With the torso lifted beyond
+    reach every leg is clamped straight down, and the feet's forces along the legs meet only the
+    torso's force / torque rows: the reduced normal matrix has a direction 1e-11 below its largest
+    eigenvalue. The oracle (and the kernel's chol_packed, on the same squared pivot) drop a force
+    column whose pivot falls to 1e-10 of the largest reduced diagonal, in the natural column order,
+    and return the basic solution, flagged HSO_FLAG_GENERAL. Checked against numpy: the dropped
+    components are exactly 0 and the answer is the least-squares solution over the kept columns
+    (residual orthogonal to them). Printed: how far it lies from the full least-squares solution
+    numpy's lstsq gives (the reference's SparseQR, whose threshold is ~20 (m + n) eps on |r_kk|,
+    keeps such a column and returns that ill-conditioned solution: parity there is not claimed)."""
+    O = oracle_mod
+    n_def = 0
+    cases = [(name, O.GaitParams(xml_file=f"{name}.xml", torso_pos=(0.0, 0.0, lift), step_duration=1.0, period=3.0,
+                                 step_length=0.2, step_height=0.05))
+             for name, lift in (("hexapod", 1.5), ("hexapod", 1.0), ("myant", 1.2))]
+    for name, g in cases:
+        m = omodels[name]
+        ro = O.rollout(m, g, 20, basis=O.BASIS_FAST)
+        z = ro["tau"] + 0.25 * np.cos(np.arange(20)[:, None] + np.arange(m.nmj)[None, :])
+        fo = O.forces(m, g, z, 20)
+        for step in np.nonzero((fo["flags"] & O.FLAG_GENERAL) != 0)[0]:
+            d = O.dynrec_dump(m, g, 20, int(step))
+            nf, n = len(d["footis"]), m.n
+            d2 = dict(d)
+            d2["contacts"] = np.ones(nf, np.int32)
+            B0, f, Bc = build_system(d2, n)
+            Tr = np.zeros((m.nmj, 6 * n))
+            for jj, h in enumerate(d["hinge_ids"]):
+                Tr[jj, 3 * n + 3 * h:3 * n + 3 * h + 3] = d["jz"][h]
+            A = np.block([[B0, Bc], [Tr, np.zeros((m.nmj, 3 * nf))]])
+            keep = [c for c in range(A.shape[1]) if not (c < 3 or 3 * n <= c < 3 * n + 3)]
+            A, b = A[:, keep], np.concatenate([f, z[step]])
+            assert np.isfinite(A).all() and np.isfinite(b).all(), f"{name} step {step}"
+            y = fo["cf"][step]
+            dropped = np.nonzero(y == 0)[0]
+            assert len(dropped) >= 1
+            kept = [c for c in range(A.shape[1]) if c - (A.shape[1] - 3 * nf) not in set(dropped)]
+            Ak = A[:, kept]
+            xk = np.linalg.lstsq(Ak, b, rcond=None)[0]  # the least squares over the kept columns
+            yk = np.zeros(3 * nf)
+            yk[[c - (A.shape[1] - 3 * nf) for c in kept if c >= A.shape[1] - 3 * nf]] = xk[-(3 * nf - len(dropped)):]
+            scale = max(1.0, np.abs(yk).max())
+            assert np.abs(y - yk).max() < 1e-7 * scale, f"{name} step {step}: {np.abs(y - yk).max():.3e}"
+            full = np.linalg.lstsq(A, b, rcond=None)[0][-3 * nf:]
+            res_b = np.linalg.norm(Ak @ xk - b)
+            res_f = np.linalg.norm(A @ np.linalg.lstsq(A, b, rcond=None)[0] - b)
+            n_def += 1
+            if n_def <= 4:
+                print(f"{name} step {step}: basic solution drops {len(dropped)} component(s); vs the full least squares "
+                      f"the forces differ by up to {np.abs(y - full).max():.3g} N (largest {np.abs(full).max():.3g} N), "
+                      f"residual {res_b:.6g} vs {res_f:.6g}")
+    assert n_def >= 5
