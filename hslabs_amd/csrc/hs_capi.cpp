@@ -140,14 +140,14 @@ int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::lau
   hipStream_t st = (hipStream_t)a.stream;
   // the best key covers the work of all n_calls calls: taken after the last one only
   if (c.key_steps == 0) c.key_steps = (int32_t)std::min<int64_t>((int64_t)n_calls * a.horizon, INT32_MAX);
-  // one gait setup per rollout per call: the setup pass of the fused path (hs_setup_kernel, with the
-  // straight gaits' IK table when it pays, hs_ktab_kernel) stores it and every launch loads it, so the
+  // one gait setup per rollout per call: the preparation pass of the fused path (hs_prep_kernel: the
+  // setup record, sample times and straight gaits' IK table) stores it and every launch loads it, so the
   // kinematics of these launches and of hs_run_calls' fused launches come from the same kernels
   hs::launch_map base = mp;
   base.setup_only = 1;
   base.setup_io = hs::SETUP_STORE;
   base.fix_n_counts = 0;
-  hs::ktab_range(a.k0, a.n_t, a.horizon, n_calls, &base.ktab_lo, &base.ktab_n);
+  hs::ktab_range(a.k0, a.n_t, a.horizon, n_calls, &base.ktab_lo, &base.ktab_n, &base.ttab_n);
   const int le0 = (a.precision == HS_PREC_F32) ? hs::launch_fused_f32(d, c, ws, base) : hs::launch_fused(d, c, ws, base);
   if (le0 != 0) return hip_fail((hipError_t)le0, "kernel launch (setup pass)");
   base.setup_only = 0;
@@ -252,7 +252,7 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   mp.setup_io = hs::SETUP_STORE;
   mp.fix_count = fix_counts;
   mp.fix_n_counts = n_chunks;
-  hs::ktab_range(a.k0, a.n_t, a.horizon, n_calls, &mp.ktab_lo, &mp.ktab_n);  // straight gaits' IK table (setup pass)
+  hs::ktab_range(a.k0, a.n_t, a.horizon, n_calls, &mp.ktab_lo, &mp.ktab_n, &mp.ttab_n);  // the preparation pass's rows
   int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   mp.setup_only = 0;
   mp.setup_io = hs::SETUP_LOAD;
@@ -529,7 +529,7 @@ int hs_run_forces_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls, con
   mp.fused_h = a->horizon;
   mp.setup_only = 1;
   mp.setup_io = hs::SETUP_STORE;
-  hs::ktab_range(a->k0, a->n_t, a->horizon, n_calls, &mp.ktab_lo, &mp.ktab_n);
+  hs::ktab_range(a->k0, a->n_t, a->horizon, n_calls, &mp.ktab_lo, &mp.ktab_n, &mp.ttab_n);
   int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   mp.setup_only = 0;
   mp.setup_io = hs::SETUP_LOAD;

@@ -65,10 +65,11 @@ struct launch_map {
   double red_total_mass;
   const double* red_rollout_mass;
   uint64_t* red_best_key;
-  // calls of straight gaits: > 0 = the setup pass also tabulates the limb IK of samples
-  // [ktab_lo, ktab_lo + ktab_n) per rollout (ktab_range), and the step launches read it instead of
-  // solving it; ktab_nl: limbs per sample the table kernel enumerates (the launch's largest model)
-  int32_t ktab_n, ktab_lo, ktab_nl;
+  // the call's preparation pass (hs_prep_kernel) stores the sample times of samples [ktab_lo,
+  // ktab_lo + ttab_n) and, for straight gaits when ktab_n > 0, the limb IK of samples [ktab_lo,
+  // ktab_lo + ktab_n) per rollout (ktab_range); the step launches read them. ktab_nl: limb lanes per
+  // rollout the pass enumerates (the launch's largest model)
+  int32_t ktab_n, ktab_lo, ktab_nl, ttab_n;
 };
 
 // Kernel launcher (hs_kernels.hip). `workspace` holds general_workspace_bytes()
@@ -77,10 +78,11 @@ struct launch_map {
 size_t general_workspace_bytes();
 // one fused step's general-path scratch per rollout (fused_gen holds [steps in a launch][B + 1] of them)
 size_t solve_workspace_bytes();
-// the samples an IK table for n_calls calls of `horizon` steps from k0 covers: [lo, lo + n), every
-// sample a step of those calls reads; n = 0 (no table) when that exceeds the table or the steps
-// would evaluate no more samples than the table does
-void ktab_range(int32_t k0, int32_t n_t, int32_t horizon, int64_t n_calls, int32_t* lo, int32_t* n);
+// the samples n_calls calls of `horizon` steps from k0 read: [lo, lo + n); the IK table holds all of
+// them (n_table = n) when they fit it, else none (n_table = 0); the sample-time table the first
+// n_ttab = min(n, its capacity)
+void ktab_range(int32_t k0, int32_t n_t, int32_t horizon, int64_t n_calls, int32_t* lo, int32_t* n_table,
+                int32_t* n_ttab);
 int launch_rollouts(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
 // single precision build of the same kernels (hs_kernels_f32.hip): outputs are float
 size_t general_workspace_bytes_f32();

@@ -341,62 +341,86 @@ __device__ inline void store34r(const A34& a, real* m) {
 // ---------------------------------------------------------------------------
 // S: gait setup, lanes L < n_limbs (pergen.cpp:453-507, 30-51, 143-153)
 // ---------------------------------------------------------------------------
-// kf (optional): also store the straight gait's frames (KinFrames: the torso frame, the chain's body
-// frames and the hip joint frames at the configured pose, products this setup forms anyway)
-__device__ __attribute__((always_inline)) inline void gait_setup(const hs_topo* T, const GaitR& g, int n_t, SetupL& st, int lane,
-                                                                 KinFrames* kf = nullptr) {
+// periodicgenerator::set_step_duration (pergen.cpp:30-51) for n limbs: the stepping fraction t_step and
+// pergen index j's lift-off time ts and shift xs (the loop's entry k = j = jj + i jmax)
+__device__ inline real step_fraction(const GaitR& g, int n) {
+  const real f = g.step_duration;
+  return f * (real(1) / 2 - real(1) / n) + real(1) / n;
+}
+__device__ inline void lift_off(int n, int j, real t_step, real& ts, real& xs) {
+  const int jmax = n / 2;
+  const int z = (jmax == 1) ? 1 : jmax - 1;
+  const int i = j / jmax, jj = j % jmax;
+  ts = jj * (real(1) / 2 - t_step) / z + real(i) / 2;
+  xs = ts + t_step / 2 - real(1) / 2;
+}
+
+// the torso frame at the configured pose (orient_torso); tsc: sincos3 of the configured angles
+__device__ inline A34 torso_frame(const hs_topo* T, const GaitR& g, const SC3& tsc) {
+  const real q6[6] = {g.torso_pos[0], g.torso_pos[1], g.torso_pos[2],
+                      g.torso_angles[0], g.torso_angles[1], g.torso_angles[2]};
+  return mul(mul(node_joint_parent(T, 0), free_joint_sc(q6, tsc)), node_pj(T, 0));
+}
+
+// Limb L's part of the gait setup from the torso frame A0: the hip joint frame J0 (poslimb,
+// lik.cpp:341-347) and the default foot position of its pergen index (get_limb_hip_pos, the foot
+// shift, set_limb_poss; pergen.cpp:453-507). kf (optional): store the chain body frames this limb owns
+// and its hip frame (KinFrames, the straight gaits' frames at tv = 0)
+__device__ __attribute__((always_inline)) inline void limb_setup(const hs_topo* T, const GaitR& g, const A34& A0, int L,
+                                                                 A34& J0, real* pos0, KinFrames* kf = nullptr) {
+  A34 A = A0;
+  for (int k = 1; k < T->limb_chain_len[L]; k++) {
+    const int v = T->limb_chain[L][k];
+    A = mul(A, node_pj(T, v));
+    if (kf && T->node[v].owner_limb == L) store34r(A, kf->Ab[v]);
+  }
+  const int c = T->limb_child[L];
+  J0 = mul(A, node_joint_parent(T, c));
+  if (kf) store34r(J0, kf->J0[L]);
+  const A34 Ac = mul(mul_hinge(J0, real(1), real(0)), node_pj(T, c));  // Rz(0): cos 0 = 1, sin 0 = 0
+  real pos[3] = {Ac(0, 3), Ac(1, 3), Ac(2, 3)};  // get_limb_hip_pos
+  if (g.foot_shift_type == 0) {                   // setup_foot_shift / shift_pos0
+    real sh[3] = {real(0), g.foot_shift, real(0)}, ls[3];
+    mulp(A0, sh, ls);
+    if (L % 2) for (int i = 0; i < 3; i++) ls[i] *= -1;
+    for (int i = 0; i < 3; i++) pos[i] += ls[i];
+  } else if (g.foot_shift_type == 1) {
+    real x = pos[0], y = pos[1];
+    real f = g.foot_shift / sqrt(x * x + y * y);
+    real d[3] = {x * f, y * f, real(0)};
+    for (int i = 0; i < 3; i++) pos[i] += d[i];
+  }
+  pos0[0] = pos[0];
+  pos0[1] = pos[1];
+  pos0[2] = (real)T->rcap;  // set_limb_poss
+}
+
+// compute_max_radius's distance of one default foot position from the turning centre (0, 1 / curvature)
+__device__ inline real turn_radius(const real* pos0, real curvature) {
+  const real cy = real(1) / curvature;
+  const real d0 = pos0[0] - real(0), d1 = pos0[1] - cy, d2 = pos0[2] - real(0);
+  real s = 0;
+  s += d0 * d0;
+  s += d1 * d1;
+  s += d2 * d2;
+  return sqrt(s);
+}
+
+// The whole setup on a half-wave (hs_pergen_rec_kernel), lanes L < n_limbs: SetupL in LDS
+__device__ __attribute__((always_inline)) inline void gait_setup(const hs_topo* T, const GaitR& g, int n_t, SetupL& st,
+                                                                 int lane) {
   const int nl = T->n_limbs;
+  const real t_step = step_fraction(g, nl);
   if (lane < nl) {
     const int L = lane;
-    real q6[6] = {g.torso_pos[0], g.torso_pos[1], g.torso_pos[2],
-                    g.torso_angles[0], g.torso_angles[1], g.torso_angles[2]};
-    const SC3 tsc = sincos3(q6[3], q6[4], q6[5]);
+    const SC3 tsc = sincos3(g.torso_angles[0], g.torso_angles[1], g.torso_angles[2]);
     if (L == 0) st.tsc = tsc;
-    A34 A0 = mul(mul(node_joint_parent(T, 0), free_joint_sc(q6, tsc)), node_pj(T, 0));  // orient_torso
-    A34 A = A0;
-    for (int k = 1; k < T->limb_chain_len[L]; k++) {
-      const int v = T->limb_chain[L][k];
-      A = mul(A, node_pj(T, v));
-      if (kf && T->node[v].owner_limb == L) store34r(A, kf->Ab[v]);
-    }
-    int c = T->limb_child[L];
-    const A34 J0 = mul(A, node_joint_parent(T, c));  // the hip joint frame (poslimb)
-    if (kf) {
-      store34r(J0, kf->J0[L]);
-      if (L == 0) store34r(A0, kf->A0);
-    }
-    A34 Ac = mul(mul_hinge(J0, real(1), real(0)), node_pj(T, c));  // Rz(0): cos 0 = 1, sin 0 = 0
-    real pos[3] = {Ac(0, 3), Ac(1, 3), Ac(2, 3)};  // get_limb_hip_pos
-    if (g.foot_shift_type == 0) {                   // setup_foot_shift / shift_pos0
-      real sh[3] = {real(0), g.foot_shift, real(0)}, ls[3];
-      mulp(A0, sh, ls);
-      if (L % 2) for (int i = 0; i < 3; i++) ls[i] *= -1;
-      for (int i = 0; i < 3; i++) pos[i] += ls[i];
-    } else if (g.foot_shift_type == 1) {
-      real x = pos[0], y = pos[1];
-      real f = g.foot_shift / sqrt(x * x + y * y);
-      real d[3] = {x * f, y * f, real(0)};
-      for (int i = 0; i < 3; i++) pos[i] += d[i];
-    }
-    int j = T->limb_pergen[L];
-    st.pos0[j][0] = pos[0];
-    st.pos0[j][1] = pos[1];
-    st.pos0[j][2] = (real)T->rcap;  // set_limb_poss
+    A34 J0;
+    const int j = T->limb_pergen[L];
+    limb_setup(T, g, torso_frame(T, g, tsc), L, J0, st.pos0[j]);
+    lift_off(nl, j, t_step, st.ts[j], st.xs[j]);
   }
-  if (lane == 0) {  // periodicgenerator::set_step_duration
-    real f = g.step_duration;
-    int n = nl;
-    real t_step = f * (real(1) / 2 - real(1) / n) + real(1) / n;
-    for (int i = 0; i < 2; i++) {
-      int jmax = n / 2;
-      int z = (jmax == 1) ? 1 : jmax - 1;
-      for (int jj = 0; jj < jmax; jj++) {
-        int k = jj + i * jmax;
-        real ts = jj * (real(1) / 2 - t_step) / z + real(i) / 2;
-        st.ts[k] = ts;
-        st.xs[k] = ts + t_step / 2 - real(1) / 2;
-      }
-    }
+  if (lane == 0) {
     st.t_step = t_step;
     st.v = g.step_length / g.period;  // pergensetup::set_TLh
     st.dt = g.period / n_t;           // record_trajectory
@@ -404,18 +428,11 @@ __device__ __attribute__((always_inline)) inline void gait_setup(const hs_topo* 
   wave_sync();
   if (lane == 0) {  // compute_max_radius
     real mr = 0;
-    if (g.curvature != 0) {
-      real cy = real(1) / g.curvature;
+    if (g.curvature != 0)
       for (int j = 0; j < nl; j++) {
-        real d0 = st.pos0[j][0] - real(0), d1 = st.pos0[j][1] - cy, d2 = st.pos0[j][2] - real(0);
-        real s = 0;
-        s += d0 * d0;
-        s += d1 * d1;
-        s += d2 * d2;
-        real rad = sqrt(s);
+        const real rad = turn_radius(st.pos0[j], g.curvature);
         if (rad > mr) mr = rad;
       }
-    }
     st.max_radius = mr;
   }
   wave_sync();
@@ -485,6 +502,22 @@ __device__ __attribute__((always_inline)) inline void node_features(const hs_top
   }
 }
 
+// periodicgenerator::limb_positions' step of one pergen index at time t (pergen.cpp:82-94): the
+// forward shift dx and lift dz of its foot, t_lift / xs its lift-off entries, t_step the stepping fraction
+__device__ inline void limb_step(const GaitR& g, real t, real t_lift, real xs, real t_step, real& dx, real& dz) {
+  const real tt = t / g.period;
+  const int t_int = int(tt);
+  const real t_frac = tt - t_int;
+  real stepf;
+  if (t_frac < t_lift) stepf = 0;
+  else if (t_frac < t_lift + t_step) stepf = (t_frac - t_lift) / t_step;
+  else stepf = 1;
+  real sx, sz;
+  step_profiles(stepf, sx, sz);
+  dx = (t_int + xs + sx) * g.step_length;
+  dz = sz * g.step_height;
+}
+
 // pergensetup::set_rec at time t for lik limb L (pergen.cpp:225-239): torso position o0 and Euler
 // angles o1 (turn_torso, pergen.cpp:386-397; `turned` when the torso frame was rotated), and the
 // limb's foot target (limb_positions of its pergen index, pergen.cpp:82-94, 160-183)
@@ -518,18 +551,9 @@ __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g
     euler_from(A1, o1);
   }
   // periodicgenerator::limb_positions for this limb's pergen index (pergen.cpp:82-94)
-  real tt = t / g.period;
-  int t_int = int(tt);
-  real t_frac = tt - t_int;
-  real t_lift = st.ts[j], stepf;
-  if (t_frac < t_lift) stepf = 0;
-  else if (t_frac < t_lift + st.t_step) stepf = (t_frac - t_lift) / st.t_step;
-  else stepf = 1;
-  real sx, sz;
-  step_profiles(stepf, sx, sz);
-  real dx = (t_int + st.xs[j] + sx) * g.step_length;
+  real dx, dz;
+  limb_step(g, t, st.ts[j], st.xs[j], st.t_step, dx, dz);
   real dy = 0;
-  real dz = sz * g.step_height;
   if (!STRAIGHT && g.curvature != 0) {  // turn_position (pergen.cpp:160-183)
     int s = (g.curvature > 0) ? 1 : -1;
     real x0 = st.pos0[j][0], y0 = st.pos0[j][1];
@@ -555,13 +579,17 @@ __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g
 }
 
 // sample times t_i = dt + dt + ... (i terms, periodic.cpp:171-181), stored once per rollout by the
-// gait-setup pass (the same additions in the same order) for i < HS_TTAB
-#define HS_TTAB 48
-__device__ inline real sample_time(const SetupL& st, const real* t_tab, int isample) {
-  if (t_tab && isample < HS_TTAB) return t_tab[isample];
+// call's preparation pass (the same additions in the same order) for the samples its steps read:
+// t_tab[r] = t_(lo + r), r < ttab_n
+__device__ inline real sample_time_sum(real dt, int isample) {
   real t = 0;
-  for (int i = 0; i < isample; i++) t += st.dt;
+  for (int i = 0; i < isample; i++) t += dt;
   return t;
+}
+__device__ inline real sample_time(const SetupL& st, const real* t_tab, int isample, int lo, int ttab_n) {
+  const int r = isample - lo;
+  if (t_tab && r >= 0 && r < ttab_n) return t_tab[r];
+  return sample_time_sum(st.dt, isample);
 }
 
 // limb FK with the new joint values (compute_dynrecs' recompute_modelnodes) from the hip joint frame
@@ -585,12 +613,13 @@ __device__ __attribute__((always_inline)) inline void limb_fk(const hs_topo* T, 
 template <bool STRAIGHT, class W>
 __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* T, const GaitR& g, const hs_gait_params& gp,
                                                                  const SetupL& st, int isample, int L, bool ignore_reach,
-                                                                 const W& w, int k, const real* t_tab) {
+                                                                 const W& w, int k, const real* t_tab, int tlo,
+                                                                 int ttab_n) {
   const int j = T->limb_pergen[L];
   const int ysign = T->limb_ysign[L];
   const int clen = T->limb_chain_len[L];
   const int lv[3] = {T->limb_node[L][0], T->limb_node[L][1], T->limb_node[L][2]};
-  const real t = sample_time(st, t_tab, isample);  // t accumulates dt (periodic.cpp:171-181)
+  const real t = sample_time(st, t_tab, isample, tlo, ttab_n);  // t accumulates dt (periodic.cpp:171-181)
   real o0[3], o1[3], target[3];
   bool turned;
   gait_record<STRAIGHT>(g, gp, st, t, j, o0, o1, turned, target);
@@ -631,13 +660,9 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
 
 // set_rec's foot target of limb L at time t and the limb IK from the hip frame J (kin_sample's
 // sequence from the gait record on); bad = unreachable (ignore_reach) or failed
-__device__ __attribute__((always_inline)) inline void straight_ik(const hs_topo* T, const GaitR& g,
-                                                                  const hs_gait_params& gp, const SetupL& st, real t,
-                                                                  int L, const A34& J, bool ignore_reach, real* ja,
-                                                                  bool& bad) {
-  real o0[3], o1[3], target[3];
-  bool turned;
-  gait_record<true>(g, gp, st, t, T->limb_pergen[L], o0, o1, turned, target);
+// the limb IK of limb L for a foot target, from its hip joint frame J (lik.cpp:341-347, 151-223)
+__device__ __attribute__((always_inline)) inline void hip_ik(const hs_topo* T, int L, const A34& J, const real* target,
+                                                             bool ignore_reach, real* ja, bool& bad) {
   const A34 Jinv = invert(J);
   real pl[3];
   mulp(Jinv, target, pl);
@@ -645,6 +670,16 @@ __device__ __attribute__((always_inline)) inline void straight_ik(const hs_topo*
   const real ls[3] = {(real)T->ls[0], (real)T->ls[1], (real)T->ls[2]};
   limb_ik(T->lik_kind, ls, T->limb_ysign[L], pl, ja, ignore_reach, unreach, fail);
   bad = unreach || fail;
+}
+
+__device__ __attribute__((always_inline)) inline void straight_ik(const hs_topo* T, const GaitR& g,
+                                                                  const hs_gait_params& gp, const SetupL& st, real t,
+                                                                  int L, const A34& J, bool ignore_reach, real* ja,
+                                                                  bool& bad) {
+  real o0[3], o1[3], target[3];
+  bool turned;
+  gait_record<true>(g, gp, st, t, T->limb_pergen[L], o0, o1, turned, target);
+  hip_ik(T, L, J, target, ignore_reach, ja, bad);
 }
 
 // What kin_sample_straight loads that no computed value feeds (the sample time, the torso speed, the
@@ -658,9 +693,9 @@ struct StraightPre {
 // (kt: the table, whose row r holds sample lo + r)
 __device__ __attribute__((always_inline)) inline StraightPre straight_preload(const SetupL& st, const real* t_tab,
                                                                              const KinFrames& kf, const real* kt,
-                                                                             int isample, int lo, int L) {
+                                                                             int isample, int lo, int ttab_n, int L) {
   StraightPre p;
-  p.t = sample_time(st, t_tab, isample);
+  p.t = sample_time(st, t_tab, isample, lo, ttab_n);
   p.v = st.v;
   p.J0 = load34r(kf.J0[L]);
   if (kt) {
@@ -2629,122 +2664,136 @@ __device__ __attribute__((always_inline)) inline void forces_step(const hs_topo*
   STAMP(11);
 }
 
-// Global per-rollout workspace: the general path's scratch and the gait-setup cache that
-// carries SetupL from the first launch of a call to the later ones (hs::SETUP_*).
+// Global per-rollout workspace: the general path's scratch, and the call's gait setup record, sample
+// times, straight-gait frames and IK table, stored by the call's preparation pass (hs_prep_kernel) for
+// every step launch of the call.
 #ifndef HS_KTAB
-#define HS_KTAB 64  // samples the IK table can hold: n_t + horizon + 3 of a fused call
+#define HS_KTAB 64  // table rows: the samples [ktab_lo, ktab_lo + n) a call's steps read (hs::ktab_range)
 #endif
 struct RolloutWS {
   SolveWS sol;
   SetupL st;
-  real t_tab[HS_TTAB];  // sample times (sample_time), with the setup cache
-  KinFrames kf;         // a straight gait's frames (with the setup cache)
-  real ktab[HS_KTAB][HS_LMAX][KT_W];  // fused calls of straight gaits: limb L at sample i (straight_ik,
-                                      // hs_ktab_kernel)
+  real t_tab[HS_KTAB];  // sample times of the call's rows (sample_time): t_tab[r] = t_(ktab_lo + r)
+  KinFrames kf;         // a straight gait's frames
+  real ktab[HS_KTAB][HS_LMAX][KT_W];  // straight gaits: limb L's joint values at sample ktab_lo + r
 };
 static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 
-// The fused path's setup pass (hs_run_calls: gait setup once per rollout, stored for every step):
-// the rollout kernel's prologue and setup store alone, as its own small kernel (2 x 320 B of LDS, few
-// registers) so the pass does not carry the step kernel's code, registers and LDS
-// One wavefront's gait setup (wavefront wid_raw of the batch; sst: two SetupL in LDS)
-__device__ __attribute__((always_inline)) inline void setup_wave(const hs_topo* __restrict__ T0, const hs_run_args& a,
-                                                                 RolloutWS* __restrict__ rws, const hs::launch_map& mp,
-                                                                 int wid_raw, SetupL* sst) {
-  const int sub = (threadIdx.x % WAVE) / HALF, lane = threadIdx.x % HALF;
-  // past the batch's last wavefront: recompute the last one's setup and store nothing (the
-  // workgroup's barriers need every wavefront)
-  const bool wave_live = wid_raw < mp.n_waves;
-  const int wid = wave_live ? wid_raw : mp.n_waves - 1;
-  if (wid_raw == 0)  // the call's fixup counters, before its step launches append to them
-    for (int i = threadIdx.x; i < mp.fix_n_counts; i += WAVE) mp.fix_count[i] = 0;
-  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[wid] : T0;
-  int b;
-  bool live;
-  if (mp.wave_rollouts) {
-    b = mp.wave_rollouts[2 * wid + sub];
-    live = b >= 0;
-    if (!live) b = mp.wave_rollouts[2 * wid];
-  } else {
-    b = wid * 2 + sub;
-    live = b < a.n_rollouts;
-    if (!live) b = a.n_rollouts - 1;
-  }
-  if (!wave_live) live = false;
-  const GaitR g = load_gait(a.params[b]);
-  // every lane of the wave takes part (wave_sync inside); the frames too
-  gait_setup(T, g, a.n_t, sst[sub], lane, live ? &rws[b].kf : nullptr);
-  if (live) {
-    constexpr int NW = sizeof(SetupL) / sizeof(real);
-    real* cache = reinterpret_cast<real*>(&rws[b].st);
-    const real* lds = reinterpret_cast<const real*>(&sst[sub]);
-    for (int e = lane; e < NW; e += HALF) cache[e] = lds[e];
-    for (int j = lane; j < HS_TTAB; j += HALF) rws[b].t_tab[j] = sample_time(sst[sub], nullptr, j);
-  }
-}
-
-__global__ __launch_bounds__(WAVE) void hs_setup_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
-                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
-  __shared__ SetupL sst[2];
-  setup_wave(T0, a, rws, mp, (int)blockIdx.x, sst);
-}
-
-// The IK table of a call (hs::ktab_range): one lane per (rollout slot, sample, limb), the
-// straight_ik of kin_sample_straight at sample s from the frames the setup pass stored. Item
-// ((2 wavefront + half) nt + sample) LMAX + limb; its wavefront, or -1 when it has nothing to do.
+// ---------------------------------------------------------------------------
+// The call's preparation pass (hs_prep_kernel): the gait setup of every rollout (pergensetup::
+// setup_pergen, pergen.cpp:453-507), its sample times (periodic.cpp:171-181) and, for straight
+// untransformed gaits, the IK table of the samples the call's steps read -- in one launch.
+//
+// Lane = (rollout, limb L, chunk of HS_PREP_ROWS table rows). Every lane runs its limb's setup (torso
+// frame, chain, hip frame J0, default foot position, lift-off entries) itself -- the lanes of one
+// wavefront do it in the same instructions, so the repetition costs one pass per wavefront -- and then
+// the rows of its chunk: the sample time, and for a straight gait J = J0 advanced by t v along the
+// torso's x and the limb IK at the foot target (straight_ik's operations). The chunk-0 lanes store the
+// setup record; max_radius (compute_max_radius, curved gaits) is the maximum over a rollout's limb
+// lanes, exchanged in LDS. A rollout's limb lanes form a group that never crosses a wavefront (groups of
+// nli lanes, floor(64 / nli) per wavefront). XCD-aware: block 8 jb + x runs groups of batch wavefronts
+// w = x (mod 8), whose step launches run on XCD x (blocks are dealt round-robin over the 8 XCDs,
+// MI355X_MICROARCH.md), so the record and rows are written into the L2 the steps read them from.
+// ---------------------------------------------------------------------------
+#ifndef HS_PREP_ROWS
+#define HS_PREP_ROWS 3  // table rows per lane
+#endif
+#ifndef HS_PREP_WAVES
+#define HS_PREP_WAVES 4  // waves per SIMD the register budget allows (<= 128 VGPRs)
+#endif
 __device__ inline int ktab_lanes(const hs::launch_map& mp) { return mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX; }
-// Item `local` of batch wavefront w (local < 2 nt nli: half, table row, limb; 32-bit arithmetic):
-// its rollout, or -1 when it has nothing to do (an idle half, a limb the model lacks, a curved gait)
-__device__ inline int ktab_item_rollout(const hs_topo* __restrict__ T0, const hs_run_args& a, const hs::launch_map& mp,
-                                       int w, int local, int& s, int& L) {
-  const int nli = ktab_lanes(mp);
-  L = local % nli;
-  const int r = local / nli;
-  s = r % mp.ktab_n;
-  const int sub = r / mp.ktab_n;
-  if (w >= mp.n_waves || sub > 1) return -1;
-  const int b = mp.wave_rollouts ? mp.wave_rollouts[2 * w + sub] : 2 * w + sub;
-  if (b < 0 || b >= a.n_rollouts) return -1;
-  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[w] : T0;
-  if (L >= T->n_limbs) return -1;
-  // kin_sample's turning / record-transform path (the step kernel's test, in the working precision)
-  if ((real)a.params[b].curvature != 0 || a.params[b].rec_transform_flag) return -1;
-  return b;
+__host__ __device__ inline int prep_chunks(int ttab_n) { return (ttab_n > 0 ? ttab_n + HS_PREP_ROWS - 1 : HS_PREP_ROWS) / HS_PREP_ROWS; }
+__host__ __device__ inline int64_t prep_blocks(int n_waves, int ttab_n, int nli) {
+  const int64_t groups_per_xcd = 2 * (int64_t)prep_chunks(ttab_n) * ((n_waves + 7) / 8);
+  const int gpw = WAVE / nli;
+  return 8 * ((groups_per_xcd + gpw - 1) / gpw);
 }
-__device__ inline void ktab_item(const hs_topo* __restrict__ T0, const hs_run_args& a, RolloutWS* __restrict__ rws,
-                                 const hs::launch_map& mp, int w, int b, int s, int L) {
-  const hs_topo* __restrict__ T = mp.wave_model ? T0 + mp.wave_model[w] : T0;
-  const GaitR g = load_gait(a.params[b]);
-  const RolloutWS& ws = rws[b];
-  const real t = sample_time(ws.st, ws.t_tab, mp.ktab_lo + s);  // table row s: sample ktab_lo + s
-  const real tv = t * ws.st.v;
+
+__global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
+                                                      RolloutWS* __restrict__ rws, hs::launch_map mp) {
+  __shared__ real rad[WAVE];
+  if (blockIdx.x == 0)  // the call's fixup counters, before its step launches append to them
+    for (int i = threadIdx.x; i < mp.fix_n_counts; i += WAVE) mp.fix_count[i] = 0;
+  const int nli = ktab_lanes(mp), gpw = WAVE / nli;
+  const int C = prep_chunks(mp.ttab_n);
+  const int gl = (int)threadIdx.x / nli, L = (int)threadIdx.x % nli;
+  const int gi = (int)(blockIdx.x / 8) * gpw + gl;  // group (q, sub, chunk) in XCD x's sequence
+  const int chunk = gi % C, sub = (gi / C) % 2, w = 8 * (gi / (2 * C)) + (int)(blockIdx.x % 8);
+  bool on = gl < gpw && w < mp.n_waves;
+  int b = 0;
+  const hs_topo* __restrict__ T = T0;
+  if (on) {
+    b = mp.wave_rollouts ? mp.wave_rollouts[2 * w + sub] : 2 * w + sub;
+    if (mp.wave_model) T = T0 + mp.wave_model[w];
+    on = b >= 0 && b < a.n_rollouts && L < T->n_limbs;
+  }
+  GaitR g;
+  A34 J0;
+  real pos0[3], ts = 0, xs = 0, t_step = 0, dt = 0, v = 0;
+  bool straight = false;
+  real my_rad = 0;
+  RolloutWS* __restrict__ ws = rws + b;
+  if (on) {
+    g = load_gait(a.params[b]);
+    straight = g.curvature == 0 && !g.rec_xf;  // kin_sample's turning / record-transform test
+    const int nl = T->n_limbs, j = T->limb_pergen[L];
+    const SC3 tsc = sincos3(g.torso_angles[0], g.torso_angles[1], g.torso_angles[2]);
+    const A34 A0 = torso_frame(T, g, tsc);
+    limb_setup(T, g, A0, L, J0, pos0, chunk == 0 ? &ws->kf : nullptr);
+    t_step = step_fraction(g, nl);
+    lift_off(nl, j, t_step, ts, xs);
+    v = g.step_length / g.period;  // pergensetup::set_TLh
+    dt = g.period / a.n_t;         // record_trajectory
+    if (chunk == 0) {
+      SetupL& st = ws->st;
+      for (int i = 0; i < 3; i++) st.pos0[j][i] = pos0[i];
+      st.ts[j] = ts;
+      st.xs[j] = xs;
+      if (L == 0) {
+        st.t_step = t_step;
+        st.v = v;
+        st.dt = dt;
+        st.tsc = tsc;
+        store34r(A0, ws->kf.A0);
+      }
+    }
+    if (g.curvature != 0) my_rad = turn_radius(pos0, g.curvature);
+  }
+  rad[threadIdx.x] = my_rad;
+  wave_sync();
+  if (on && chunk == 0 && L == 0) {  // compute_max_radius over the rollout's limbs
+    real mr = 0;
+    if (g.curvature != 0)
+      for (int l = 0; l < T->n_limbs; l++) {
+        const real r = rad[threadIdx.x + l];
+        if (r > mr) mr = r;
+      }
+    ws->st.max_radius = mr;
+  }
+  if (!on) return;
+  const int r0 = chunk * HS_PREP_ROWS, r1 = min(r0 + HS_PREP_ROWS, mp.ttab_n);
+  if (r0 >= r1) return;
+  const bool table = straight && mp.ktab_n > 0;
   const hs_aff34& Jp0 = T->node[0].J_A_parent;
   const real u[3] = {(real)Jp0.m[0], (real)Jp0.m[1], (real)Jp0.m[2]};
-  const A34 J = frame_at(load34r(ws.kf.J0[L]), u, tv);
-  real ja[3];
-  bool bad;
-  straight_ik(T, g, a.params[b], ws.st, t, L, J, a.ignore_reach != 0, ja, bad);
-  real* e = rws[b].ktab[s][L];
+  real t = sample_time_sum(dt, mp.ktab_lo + r0);
+#pragma unroll 1
+  for (int r = r0; r < r1; r++) {
+    if (r > r0) t += dt;  // the loop's next addition
+    if (L == 0) ws->t_tab[r] = t;
+    if (table) {  // straight_ik at sample ktab_lo + r
+      real dx, dz;
+      limb_step(g, t, ts, xs, t_step, dx, dz);
+      const real target[3] = {dx + pos0[0], real(0) + pos0[1], dz + pos0[2]};
+      real ja[3];
+      bool bad;
+      hip_ik(T, L, frame_at(J0, u, t * v), target, a.ignore_reach != 0, ja, bad);
+      real* e = ws->ktab[r][L];
 #pragma unroll
-  for (int kk = 0; kk < 3; kk++) e[kk] = ja[kk];
-  e[KT_W - 1] = bad ? real(1) : real(0);
-}
-
-// XCD-aware: blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), and
-// the setup pass and the step launches run batch wavefront wid on the XCD of block wid (fused steps:
-// when the batch's wavefront count is a multiple of 8), so block t = 8 q + x takes the items of
-// wavefront 8 (q / bpw) + x: its table rows are written on the XCD whose L2 the steps read them from
-__host__ __device__ inline int ktab_blocks_per_wave(int nt, int nli) { return (2 * nt * nli + WAVE - 1) / WAVE; }
-__global__ __launch_bounds__(WAVE) void hs_ktab_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
-                                                                      RolloutWS* __restrict__ rws, hs::launch_map mp) {
-  const int nli = ktab_lanes(mp);
-  const int bpw = ktab_blocks_per_wave(mp.ktab_n, nli);
-  const int x = (int)(blockIdx.x % 8), q = (int)(blockIdx.x / 8);
-  const int w = 8 * (q / bpw) + x;
-  const int local = (q % bpw) * WAVE + (int)threadIdx.x;
-  int s, L;
-  const int b = ktab_item_rollout(T0, a, mp, w, local, s, L);
-  if (b >= 0) ktab_item(T0, a, rws, mp, w, b, s, L);
+      for (int kk = 0; kk < 3; kk++) e[kk] = ja[kk];
+      e[KT_W - 1] = bad ? real(1) : real(0);
+    }
+  }
 }
 
 // One wavefront's step: fused step fstep (0 outside fused launches) of batch wavefront wid. only_sub
@@ -2788,7 +2837,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
     h_row = s;
   }
   const int nl = T->n_limbs;
-  // the gait setup of the rollout, stored by the call's setup pass (hs_setup_kernel;
+  // the gait setup of the rollout, stored by the call's preparation pass (hs_prep_kernel;
   // the idle half reads its neighbour's): read from global memory where it is used
   const SetupL& st = rws[bb].st;
   const int i = k0 + 2;  // centre sample of this launch's step
@@ -2796,7 +2845,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   const real* kt = mp.ktab_n > 0 ? &rws[bb].ktab[0][0][0] : nullptr;
 #if HS_PRELOAD
   const StraightPre pre = straight_preload(st, rws[bb].t_tab, rws[bb].kf, HS_KTE_PRELOAD ? kt : nullptr,
-                                           i - 2 + (sl < NS ? sl : 0), mp.ktab_lo, L);
+                                           i - 2 + (sl < NS ? sl : 0), mp.ktab_lo, mp.ttab_n, L);
 #endif
   const GaitR g = load_gait(a.params[bb]);
   const bool ignore_reach = a.ignore_reach != 0;
@@ -2827,13 +2876,13 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
       if (straight) {
 #if !HS_PRELOAD
         const StraightPre pre = straight_preload(st, t_tab, rws[bb].kf, HS_KTE_PRELOAD ? kt : nullptr, i - 2 + sl,
-                                                 mp.ktab_lo, L);
+                                                 mp.ktab_lo, mp.ttab_n, L);
 #endif
         kin_sample_straight(T, g, a.params[bb], st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
                             pre, rws[bb].kf, kt, mp.ktab_lo);
       } else {
         kin_sample<false>(T, g, a.params[bb], st_curved, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d},
-                          sl - 2, t_tab);
+                          sl - 2, t_tab, mp.ktab_lo, mp.ttab_n);
       }
     }
     wave_sync();
@@ -2965,7 +3014,8 @@ size_t general_workspace_bytes_f32() { return sizeof(RolloutWS); }
 size_t general_workspace_bytes() { return sizeof(RolloutWS); }
 size_t solve_workspace_bytes() { return sizeof(SolveWS); }  // >= the fp32 build's
 
-void ktab_range(int32_t k0, int32_t n_t, int32_t horizon, int64_t n_calls, int32_t* lo_out, int32_t* n_out) {
+void ktab_range(int32_t k0, int32_t n_t, int32_t horizon, int64_t n_calls, int32_t* lo_out, int32_t* n_out,
+                int32_t* ttab_out) {
   // call c starts at centre sample (k0 + c horizon) % n_t + 2 (the fused and the per-step paths
   // alike) and its steps read that first k0 + [0, horizon + NS - 1); the first k0s repeat with a
   // period dividing n_t
@@ -2976,10 +3026,10 @@ void ktab_range(int32_t k0, int32_t n_t, int32_t horizon, int64_t n_calls, int32
     lo = f < lo ? f : lo;
     hi = f + horizon + NS - 1 > hi ? f + horizon + NS - 1 : hi;
   }
-  const int64_t n = hi - lo;
-  const bool use = nc > 0 && n <= HS_KTAB && n_calls * horizon * NS > n;
-  *lo_out = use ? (int32_t)lo : 0;
-  *n_out = use ? (int32_t)n : 0;
+  const int64_t n = nc > 0 ? hi - lo : 0;
+  *lo_out = nc > 0 ? (int32_t)lo : 0;
+  *n_out = n <= HS_KTAB ? (int32_t)n : 0;                // the IK table: every sample, or none
+  *ttab_out = (int32_t)(n < HS_KTAB ? n : HS_KTAB);      // sample times: the first HS_KTAB samples
 }
 
 int launch_pergen_rec(const hs_topo* d_topo, const hs_gait_params* params, int32_t n_rollouts, const double* times,
@@ -3041,13 +3091,9 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   if (a.n_rollouts <= 0 || mp.n_waves <= 0) return 0;
   hipStream_t st = (hipStream_t)a.stream;
   RolloutWS* ws = (RolloutWS*)workspace;
-  if (mp.setup_only) {
-    hipLaunchKernelGGL(hs_setup_kernel, dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
-    if (mp.ktab_n > 0) {  // the call's IK table, from the frames the setup pass stored
-      const int64_t blocks =
-          8 * (int64_t)ktab_blocks_per_wave(mp.ktab_n, mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX) * ((mp.n_waves + 7) / 8);
-      hipLaunchKernelGGL(hs_ktab_kernel, dim3((unsigned)blocks), dim3(WAVE), 0, st, d_topo, a, ws, mp);
-    }
+  if (mp.setup_only) {  // the call's preparation pass: setup record, sample times, IK table
+    const int64_t blocks = prep_blocks(mp.n_waves, mp.ttab_n, mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX);
+    hipLaunchKernelGGL(hs_prep_kernel, dim3((unsigned)blocks), dim3(WAVE), 0, st, d_topo, a, ws, mp);
     return (int)hipGetLastError();
   }
   launch_map m = mp;

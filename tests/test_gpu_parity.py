@@ -291,12 +291,16 @@ def test_fp32_configs2_matches_fp64_oracle(gpu, hmodels, oracle_mod, omodels):
     r = oracle_mod.batch(omodels["spider"], gaits, 20, 0, H, basis=oracle_mod.BASIS_TREE, n_threads=threads())
     down32 = (np.abs(cf.reshape(B, H, -1, 3)).max(axis=3) > 0)
     down64 = (np.abs(r["cf"].reshape(B, H, -1, 3)).max(axis=3) > 0)
-    same = (down32 == down64).all(axis=2) & ((flags & ~IGN) == (r["flags"] & ~IGN)) & ~near(flags, r["flags"])
+    same = (down32 == down64).all(axis=2)
     assert same.mean() > 0.995, f"contact sets differ on {(~same).sum()} of {same.size} steps"
+    skip = near(flags, r["flags"])
+    cmp = same & ~skip
+    print(f"configs[2] fp32: {int((same & skip).sum())} of {int(same.sum())} same-contact steps flagged HS_FLAG_NEAR_RANK")
+    check_flags(flags, r["flags"], "configs[2] fp32 vs fp64 oracle", ~cmp)
     scale = np.maximum(1, np.abs(r["tau"]).max(axis=2))
     err = np.abs(tau - r["tau"]).max(axis=2) / scale
-    assert err[same].max() < FP32_TOL, f"fp32 vs fp64 oracle: {err[same].max():.3e}"
-    assert np.median(err[same]) < 1e-5
+    assert err[cmp].max() < FP32_TOL, f"fp32 vs fp64 oracle: {err[cmp].max():.3e}"
+    assert np.median(err[cmp]) < 1e-5
 
 
 @pytest.mark.parametrize("name", ["spider", "hexapod"])

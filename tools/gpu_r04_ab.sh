@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-4 call: GPU tests on the product library, then an interleaved A/B of tuning builds at the
+# driver command and at K = 200, then the driver job's kernel trace.   VARIANTS="base v1 ..."  TAG=...
+set -o pipefail
+R=$GRAFT_REPO_ROOT; TAG=${TAG:-r04_ab}; OUT=$R/gpurun_out/$TAG; mkdir -p $OUT; cd $R
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|assert" $OUT/tests.log | head -30; tail -30 $OUT/tests.log; exit 1; }
+  tail -1 $OUT/tests.log
+fi
+for args in "--steps 20 --warmup 5" "--steps 200 --warmup 20"; do
+  echo "== $args"
+  for i in 1 2; do
+  for v in ${VARIANTS:-base}; do
+    if [ $v = base ]; then unset HSLABS_VARIANT; else export HSLABS_VARIANT=$v; fi
+    timeout -k 10 120 python bench.py --no-cpu $args > $OUT/${v}.json 2>$OUT/${v}.err || { tail -5 $OUT/${v}.err; exit 1; }
+    python -c "import json;d=json.load(open('$OUT/${v}.json'));print('$v', round(d['value']/1e6,2), 'M steps/s; kernel us/step', round(d['roofline']['kernel_ms']*1e3,3))" | tee -a $OUT/ab.txt
+  done; done
+done
+unset HSLABS_VARIANT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu > $OUT/prof.log 2>&1 || { echo prof failed; tail -20 $OUT/prof.log; exit 1; }
+python3 $R/tools/trace_tail.py $OUT/prof/run_kernel_trace.csv 4 > $OUT/trace_tail.txt; cat $OUT/trace_tail.txt
+echo "call done"
