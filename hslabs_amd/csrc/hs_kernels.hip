@@ -222,6 +222,10 @@ constexpr real kRelTol = HS_REAL_IS_FLOAT ? real(1e-4) : real(1e-6);
 // within kNearBand of its threshold (rel_error: within 10x of kRelTol; ColPivQR's squared column norms:
 // within kNearBand^2) is flagged, since another rounding may take it the other way
 constexpr real kNearBand = real(4);
+// the Eigen-style path's conditioning test: the last pass's second-stage system with a kept ColPivQR pivot
+// under kCondQR of its first (condition above 1e7 in fp64, 1e4 in fp32): rounding-level changes of the
+// inputs move the answer by more than the parity bound there (oracle NearTrack::ill)
+constexpr real kCondQR = HS_REAL_IS_FLOAT ? real(1e-4) : real(1e-7);
 // v is within `band` of threshold t (both positive; a NaN is not)
 __device__ inline bool near_thr(real v, real t, real band) { return v >= t / band && v <= t * band; }
 
@@ -1387,6 +1391,7 @@ __device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
   int rank0 = k;
   int iters = 0;
   real rel_error = 0;
+  bool ill = false;  // the last pass's second stage ill-conditioned (kCondQR)
   do {
     iters++;
     real thr = kEps * (real)k;
@@ -1422,6 +1427,11 @@ __device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
     bool qr_near = false;
     int np = colpiv_qr(g, k, lane, qr_near);
     if (qr_near) flags |= HS_FLAG_NEAR_RANK;
+    {  // the smallest kept pivot of this pass (the last pass's decides)
+      real rmin = real(INFINITY);
+      for (int i = 0; i < np; i++) rmin = fmin(rmin, fabs(g.qr[i + i * LD]));
+      ill = np > 0 && rmin < kCondQR * fabs(g.qr[0]);
+    }
     STAMP(13);
     qr_solve(g, k, np, lane);
     STAMP(14);
@@ -1446,6 +1456,7 @@ __device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
     if (rel_error > kRelTol && rank0 <= 0) { flags |= HS_FLAG_LOOP_EXHAUST; break; }
   } while (rel_error > kRelTol && iters <= HS_KMAX + 1);
   if (iters > 1) flags |= HS_FLAG_RANK_RETRY;
+  if (ill) flags |= HS_FLAG_NEAR_RANK;
   return flags;
 }
 
@@ -2696,10 +2707,10 @@ static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 // MI355X_MICROARCH.md), so the record and rows are written into the L2 the steps read them from.
 // ---------------------------------------------------------------------------
 #ifndef HS_PREP_ROWS
-#define HS_PREP_ROWS 3  // table rows per lane
+#define HS_PREP_ROWS 6  // table rows per lane (measured: 2, 3, 6 rows at 2-4 waves/SIMD; 6 at 2 the fastest)
 #endif
 #ifndef HS_PREP_WAVES
-#define HS_PREP_WAVES 4  // waves per SIMD the register budget allows (<= 128 VGPRs)
+#define HS_PREP_WAVES 2  // waves per SIMD the register budget allows (196 VGPRs; 3 or 4 spill)
 #endif
 __device__ inline int ktab_lanes(const hs::launch_map& mp) { return mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX; }
 __host__ __device__ inline int prep_chunks(int ttab_n) { return (ttab_n > 0 ? ttab_n + HS_PREP_ROWS - 1 : HS_PREP_ROWS) / HS_PREP_ROWS; }

@@ -48,8 +48,11 @@ enum {
                                     threshold doubled (:212-214), rel_error in [1e-7, 1e-5] against the
                                     loop's 1e-6 (:228-232), a ColPivQR column norm within 4x of its
                                     nonzero-pivot threshold, the closed form's collinearity guard or
-                                    pivot guards within 4x of theirs; solve_forces: a normal-matrix
-                                    pivot within 4x of its rank guard (ftsolver.cpp:349-353). The
+                                    pivot guards within 4x of theirs; the Eigen-style path's second
+                                    stage ill-conditioned (a kept ColPivQR pivot under 1e-7 of the first,
+                                    1e-4 in fp32: rounding-level input changes move its answer beyond
+                                    the parity bound); solve_forces: a normal-matrix pivot within 4x of
+                                    its rank guard (ftsolver.cpp:349-353). The
                                     step's outputs are the path's answer; equality with another
                                     implementation is only expected where neither side sets this. */
 

@@ -1046,12 +1046,17 @@ void upper_solve_inplace(const Mat& U, int n, double* x) {
 //   rel_error > 1e-6 (ftsolver.cpp:228-232): band 10, i.e. rel_error in [1e-7, 1e-5]
 //   ColPivHouseholderQR nonzero pivots (|col|^2 < threshold_helper (rows - k)): band 16 on the squares
 //   the closed form's routing: the collinearity guard (band 4) and its pivot guards (band 4)
+// and one conditioning test: the second stage's system (the last pass's m, ftsolver.cpp:222-227) with a
+// kept ColPivQR pivot under kCondQR of its first (a condition number above 1e7: a rounding-level change
+// of the inputs -- another basis, FMA contraction -- moves the answer by more than the parity bound;
+// the reference's own SparseQR and tree bases disagree there, tests/test_oracle.py).
 // The step then carries HSO_FLAG_NEAR_RANK (the kernel computes the same margins, HS_FLAG_NEAR_RANK).
-constexpr double kNearBand = 4.0, kNearBandRel = 10.0, kNearBandQR = 16.0;
+constexpr double kNearBand = 4.0, kNearBandRel = 10.0, kNearBandQR = 16.0, kCondQR = 1e-7;
 struct NearTrack {
   double margin = INFINITY;
   int cat = 0;  // the decision closest to its threshold: HSO_NEAR_*
   double lu_kept = INFINITY, qr_kept = INFINITY;  // conditioning of the last pass: smallest kept pivot ratios
+  bool ill = false;                               // the last pass's qr_kept < kCondQR
 #ifndef HSO_FLOPCOUNT
   void note(double ratio, double band, int c) {
     if (!(ratio > 0)) return;  // exact zeros are structural, not near anything
@@ -1059,7 +1064,7 @@ struct NearTrack {
     if (m < margin) { margin = m; cat = c; }
   }
 #endif
-  bool near() const { return margin <= 1.0; }
+  bool near() const { return margin <= 1.0 || ill; }
 };
 thread_local NearTrack tl_near;
 // diagnostics, not arithmetic of the path: the FLOP-counting build (hs_oracle_flops.cpp) leaves them out
@@ -1069,7 +1074,7 @@ thread_local NearTrack tl_near;
 #define NEAR_NOTE(ratio, band, cat) tl_near.note((ratio), (band), (cat))
 #endif
 enum { HSO_NEAR_LU = 1, HSO_NEAR_DOUBLED = 2, HSO_NEAR_REL = 3, HSO_NEAR_QR = 4, HSO_NEAR_COLLINEAR = 5,
-       HSO_NEAR_PIVOT = 6 };
+       HSO_NEAR_PIVOT = 6, HSO_NEAR_COND = 7 };
 
 // Eigen FullPivLU (FullPivLU.h), restated.
 struct FPLU {
@@ -1465,6 +1470,7 @@ void solve_contact_forces(const hso_model* m, const std::vector<double>& jz, con
 #ifndef HSO_FLOPCOUNT
     tl_near.qr_kept = INFINITY;
     for (int i = 0; i < qr.nonzero_pivots; i++) tl_near.qr_kept = std::min(tl_near.qr_kept, fabs(qr.qr(i, i)) / fabs(qr.qr(0, 0)));
+    tl_near.ill = tl_near.qr_kept < kCondQR;
 #endif
     std::vector<double> z = qr.solve(b);
     std::vector<double> mz = matvec(M, z);
@@ -1945,7 +1951,7 @@ void solve_forcetorques(const hso_model* m, const DynRec& d, int basis, FTOut& o
   }
   out.x = x;
   out.near_margin = tl_near.margin;
-  out.near_cat = tl_near.cat;
+  out.near_cat = (tl_near.ill && !(tl_near.margin <= 1.0)) ? HSO_NEAR_COND : tl_near.cat;
   out.lu_kept = tl_near.lu_kept;
   out.qr_kept = tl_near.qr_kept;
   if (tl_near.near()) out.flags |= HSO_FLAG_NEAR_RANK;

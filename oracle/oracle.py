@@ -29,7 +29,7 @@ FLAG_NO_CONTACT = 32
 FLAG_GENERAL = 64
 FLAG_NEAR_RANK = 256  # a rank / routing decision within rounding of its threshold (hs_oracle.cpp NearTrack)
 NEAR_KINDS = {0: "none", 1: "LU pivot", 2: "threshold doubled", 3: "rel_error", 4: "QR pivot", 5: "collinear guard",
-              6: "pivot guard"}
+              6: "pivot guard", 7: "ill-conditioned second stage"}
 BASIS_FAST = 2
 
 
