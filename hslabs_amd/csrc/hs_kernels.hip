@@ -159,7 +159,6 @@ struct OneStore {
   union {
     StencilL<NM> sten;
     FastL fl;  // written only after D has consumed the stencil
-    WorkL wk;
     typename std::conditional<FORCES, ForceL, WorkL>::type fr;  // forces-given-torques mode
   };
   CentreL<NM> c;
@@ -184,7 +183,7 @@ constexpr int KT_W = 4;
 struct KinFrames {
   real A0[12];              // the torso (node 0)
   real J0[HS_LMAX][12];     // each limb's hip joint frame
-  real Ab[HS_NMAX][12];     // body nodes of the limb chains, by node id (written by the owner limb)
+  real Ao[HS_LMAX][HS_OWN_MAX][12];  // the chain bodies each limb computes (hs_topo::limb_own)
 };
 
 template <int NM>
@@ -373,10 +372,11 @@ __device__ inline A34 torso_frame(const hs_topo* T, const GaitR& g, const SC3& t
 __device__ __attribute__((always_inline)) inline void limb_setup(const hs_topo* T, const GaitR& g, const A34& A0, int L,
                                                                  A34& J0, real* pos0, KinFrames* kf = nullptr) {
   A34 A = A0;
+  int own = 0;
   for (int k = 1; k < T->limb_chain_len[L]; k++) {
     const int v = T->limb_chain[L][k];
     A = mul(A, node_pj(T, v));
-    if (kf && T->node[v].owner_limb == L) store34r(A, kf->Ab[v]);
+    if (kf && T->node[v].owner_limb == L) store34r(A, kf->Ao[L][own++]);
   }
   const int c = T->limb_child[L];
   J0 = mul(A, node_joint_parent(T, c));
@@ -596,21 +596,57 @@ __device__ inline real sample_time(const SetupL& st, const real* t_tab, int isam
   return sample_time_sum(st.dt, isample);
 }
 
-// limb FK with the new joint values (compute_dynrecs' recompute_modelnodes) from the hip joint frame
-// J; nk: the limb_child's node
+// limb FK with the new joint values (compute_dynrecs' recompute_modelnodes, model.cpp:183-201) from the
+// hip joint frame J, and the dynamic features of the links (dynrec.cpp:134-155), on the limb's
+// precombined plan (hs_topo::link): per link k the hinge frame H = J_k Rz(q_k) (mul_hinge), its body frame
+// A_k = H pj_k seen through the products the features need -- pos = H (pj_k com), the rotation skew of
+// A_k (ust) from H's and pj_k's rotations, the foot H (pj_2 cap) -- and the next joint frame J_(k+1) =
+// H (pj_k Jp_(k+1)): one 3 x 4 product per link where the node-by-node form takes two
 // (sq, cq: sin and cos of the joint values ja)
 template <class W>
-__device__ __attribute__((always_inline)) inline void limb_fk(const hs_topo* T, const int* lv, NodeK nk, const A34& J,
-                                                              const real* ja, const real* sq, const real* cq, bool wq,
-                                                              const W& w, int k) {
-  A34 A;
+__device__ __attribute__((always_inline)) inline void limb_fk(const hs_topo* T, int L, const A34& J, const real* ja,
+                                                              const real* sq, const real* cq, bool wq, const W& w,
+                                                              int k) {
+  const int lv[3] = {T->limb_node[L][0], T->limb_node[L][1], T->limb_node[L][2]};
+  A34 Jv = J, H;
 #pragma unroll
   for (int kk = 0; kk < 3; kk++) {  // limb_child, its first kid, that one's first kid
-    if (kk > 0) nk = load_nodek(T, lv[kk]);
-    A34 Jv = (kk == 0) ? J : mul(A, nk.Jp);
-    A = mul(mul_hinge(Jv, cq[kk], sq[kk]), nk.pj);
-    if (wq) w.q(k)[6 + nk.hinge] = ja[kk];
-    node_features(T, lv[kk], nk, A, &Jv, w, k);
+    const hs_link& lk = T->link[L][kk];
+    if (kk > 0) Jv = mul(H, load34(lk.P));
+    H = mul_hinge(Jv, cq[kk], sq[kk]);
+    if (wq) w.q(k)[6 + lk.hinge] = ja[kk];
+    const int v = lv[kk];
+    if (w.want_pos(k)) {
+      const real c[3] = {(real)lk.com[0], (real)lk.com[1], (real)lk.com[2]};
+      real p[3];
+      mulp(H, c, p);
+      real* P = w.pos(k, v);
+      for (int i = 0; i < 3; i++) P[i] = p[i];
+    }
+    if (w.want_ust(k)) {  // (A(2,1) - A(1,2)) / 2 etc. of A = H pj: (r, c) = sum_m H(r, m) pj(m, c)
+      real R[9];
+#pragma unroll
+      for (int i = 0; i < 9; i++) R[i] = (real)lk.Rpj[i];
+      auto a_rc = [&](int r, int c) { return H(r, 0) * R[c * 3 + 0] + H(r, 1) * R[c * 3 + 1] + H(r, 2) * R[c * 3 + 2]; };
+      real* U = w.ust(k, v);
+      U[0] = (a_rc(2, 1) - a_rc(1, 2)) / 2;
+      U[1] = (a_rc(0, 2) - a_rc(2, 0)) / 2;
+      U[2] = (a_rc(1, 0) - a_rc(0, 1)) / 2;
+    }
+    if (w.want_centre(k)) {
+      real* Jp = w.jpos(k, v);
+      real* Jz = w.jz(k, v);
+      for (int i = 0; i < 3; i++) Jp[i] = Jv(i, 3);
+      for (int i = 0; i < 3; i++) Jz[i] = Jv(i, 2);
+      if (lk.foot >= 0) {
+        const real c[3] = {(real)lk.cap[0], (real)lk.cap[1], (real)lk.cap[2]};
+        real fp[3];
+        mulp(H, c, fp);
+        real* F = w.fpos(k, lk.foot);
+        for (int i = 0; i < 3; i++) F[i] = fp[i];
+        w.contact(k, lk.foot) = fp[2] < (real)(T->rcap + 1e-4);
+      }
+    }
   }
 }
 
@@ -659,7 +695,7 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
   real sq[3], cq[3];
 #pragma unroll
   for (int kk = 0; kk < 3; kk++) sincos(ja[kk], &sq[kk], &cq[kk]);
-  limb_fk(T, lv, nk, J, ja, sq, cq, wq, w, k);
+  limb_fk(T, L, J, ja, sq, cq, wq, w, k);
 }
 
 // set_rec's foot target of limb L at time t and the limb IK from the hip frame J (kin_sample's
@@ -735,11 +771,28 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
   }
 #endif
   if (L == 0) A0 = load34r(kf.A0);
-  const int clen = T->limb_chain_len[L];
-  for (int kk = 1; kk < clen; kk++) {
-    const int v = T->limb_chain[L][kk];
-    const NodeK nc = load_nodek(T, v);
-    if (nc.owner == L) node_features(T, v, nc, frame_at(load34r(kf.Ab[v]), u, tv), nullptr, w, k);
+  for (int m = 0; m < T->limb_own_n[L]; m++) {  // the chain bodies this limb computes (never a foot)
+    const int v = T->limb_own[L][m];
+    const A34 A = frame_at(load34r(kf.Ao[L][m]), u, tv);
+    if (w.want_pos(k)) {
+      const real c[3] = {(real)T->limb_own_com[L][m][0], (real)T->limb_own_com[L][m][1], (real)T->limb_own_com[L][m][2]};
+      real p[3];
+      mulp(A, c, p);
+      real* P = w.pos(k, v);
+      for (int i = 0; i < 3; i++) P[i] = p[i];
+    }
+    if (w.want_ust(k)) {
+      real* U = w.ust(k, v);
+      U[0] = (A(2, 1) - A(1, 2)) / 2;
+      U[1] = (A(0, 2) - A(2, 0)) / 2;
+      U[2] = (A(1, 0) - A(0, 1)) / 2;
+    }
+    if (w.want_centre(k)) {  // a body without a joint: J = its frame, no axis (node_features with J = null)
+      real* Jp = w.jpos(k, v);
+      real* Jz = w.jz(k, v);
+      for (int i = 0; i < 3; i++) Jp[i] = A(i, 3);
+      for (int i = 0; i < 3; i++) Jz[i] = real(0);
+    }
   }
   if (L == 0) {
     if (wq) {
@@ -770,8 +823,7 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
   }
   if (w.want_centre(k)) w.unreach(k, L) = bad ? 1 : 0;
   STAMP(22);
-  NodeK nk = load_nodek(T, lv[0]);
-  limb_fk(T, lv, nk, J, ja, sq, cq, wq, w, k);
+  limb_fk(T, L, J, ja, sq, cq, wq, w, k);
 }
 
 // ---------------------------------------------------------------------------
@@ -1519,24 +1571,32 @@ __device__ inline float group8_sum(float v) {
   return v;
 }
 
+// a real moved across lanes by DPP control CTRL (a double as two 32-bit moves)
+template <int CTRL>
+__device__ inline real dpp_r(real x) {
+#if HS_REAL_IS_FLOAT
+  return dpp_f<CTRL>(x);
+#else
+  const long long u = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_mov_dpp((int)u, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+#endif
+}
 // sum over the 4-lane quad (DPP quad_perm xor 1, xor 2): every lane of the quad gets the same value
 // (each addition is commutative in its two operands)
 __device__ inline real quad_sum(real v) {
-#if HS_REAL_IS_FLOAT
-  v += dpp_f<0xB1>(v);
-  v += dpp_f<0x4E>(v);
+  v += dpp_r<0xB1>(v);
+  v += dpp_r<0x4E>(v);
   return v;
-#else
-  auto dpp_d = [](double x, auto ctrl) {
-    const long long u = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_mov_dpp((int)u, decltype(ctrl)::value, 0xF, 0xF, true);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), decltype(ctrl)::value, 0xF, 0xF, true);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-  };
-  v += dpp_d(v, std::integral_constant<int, 0xB1>{});
-  v += dpp_d(v, std::integral_constant<int, 0x4E>{});
-  return v;
-#endif
+}
+// sum over the 32 lanes of this rollout: the quad's, the 8-lane half-row's (row_half_mirror), the
+// row's (row_mirror), then the other row of the half-wave (one permute); every lane gets the same value
+__device__ inline real half_sum(real v) {
+  v = quad_sum(v);
+  v += dpp_r<0x141>(v);
+  v += dpp_r<0x140>(v);
+  return v + __shfl_xor(v, 16);
 }
 
 // bit 0: well posed (take the closed form); bit 1: the ratio lies within kNearBand of the guard
@@ -2205,10 +2265,11 @@ __device__ inline void reduce_rollouts(const hs_run_args& a, real total_mass, co
 // step's half-wave stores nothing and `deferred` is set), so this instantiation has no call to the
 // out-of-line general path: the call alone costs the whole kernel SGPRs (spills in the hot solve
 // region) and 2.4 % of the step time
+// hinge_id, hinge_foot: this lane's motor's part and foot (lanes < nmj), loaded at the wave's start
 template <bool DEFER, class W, class SV>
 __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st, SV& sv,
-                     FastL& fl, WorkL& wk, const W& w, SolveWS* G, int b, bool live, int h,
-                     real& work, bool& deferred, bool may_general, int lane) {
+                     FastL& fl, const W& w, SolveWS* G, int b, bool live, int h,
+                     real& work, bool& deferred, bool may_general, int lane, int hinge_id, int hinge_foot) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
   STAMP(3);
   // D writes, and S1's first stage reads, part i's rows on lane i only: no sync between them
@@ -2244,12 +2305,11 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   // S4: x = x_part + N y for the hinge torque rows, motor torques (periodic.cpp:328-343),
   // and the step's positive work (compute_vel_traj + work_over_period, periodic.cpp:261-307)
   const size_t row = (size_t)b * a.horizon + h;
-  real tq = real(0);
+  real tq = real(0), wdl = real(0);
   if (lane < nmj) {
-    int h_id = T->hinge_ids[lane];
-    int fi = T->hinge_foot[lane];
-    int cc = -1;
-    for (int c = 0; c < nc; c++) if (sv.cfoot[c] == fi) cc = c;
+    const int h_id = hinge_id, fi = hinge_foot;
+    // contact index of foot fi: its rank among the feet down (the contact list's order)
+    const int cc = (fi >= 0 && ((cmask >> fi) & 1)) ? __popc(cmask & ((1u << fi) - 1)) : -1;
     const real* Jp = w.jpos(0, h_id);
     const real* Jz = w.jz(0, h_id);
     real d[3];
@@ -2272,7 +2332,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
     else if (dd < -kPi) dd += 2 * kPi;
     real jvel = dd / (2 * st.dt);
     real dw = tq * jvel;
-    wk.wd[lane] = (dw > 0) ? dw : 0;
+    wdl = (dw > 0) ? dw : 0;
     if (mp.pd_tau && live) {  // linear_feedback_control (player.cpp:417-432), target = get_motor_adas
       const size_t o = row * mp.st_tau + lane;
       const real q0 = w.q(0)[6 + lane];
@@ -2293,9 +2353,9 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   if (half_ballot(lane < nl && w.unreach(0, lane))) flags |= HS_FLAG_UNREACH;
   // contact forces z = -N_cont y (ftsolver.cpp:91, 276-284)
   if (live && a.cf && lane < mp.st_cf) {
-    int fi = lane / 3, j = lane % 3;
+    const int fi = lane / 3, j = lane % 3;
     real zv = (lane < 3 * nf) ? -real(0) : real(0);
-    for (int c = 0; c < nc; c++) if (sv.cfoot[c] == fi) zv = -(real(0) + (real(-1)) * sv.y[3 * c + j]);
+    if (lane < 3 * nf && ((cmask >> fi) & 1)) zv = -(real(0) + (real(-1)) * sv.y[3 * __popc(cmask & ((1u << fi) - 1)) + j]);
     outp(a.cf)[row * mp.st_cf + lane] = zv;
   }
   if (live && a.x) {  // full joint force/torque vector x += N y
@@ -2333,9 +2393,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
     outp(a.dq)[row * mp.st_q + lane] = v;
   }
   if (live && a.flags && lane == 0) a.flags[row] = flags;
-  wave_sync();
-  real work_dt = 0;  // summed in joint order like work_over_period
-  for (int jj = 0; jj < nmj; jj++) work_dt += wk.wd[jj];
+  const real work_dt = half_sum(wdl);  // the joints' positive work (work_over_period's sum)
   // work_over_period: work += work_dt * dt, one rounding (explicit, so the fused path's in-order
   // sum performs the same operation); fused steps hand back the joint sum itself
   if (mp.fused_w) work = work_dt;
@@ -2848,6 +2906,8 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
     h_row = s;
   }
   const int nl = T->n_limbs;
+  const bool hl = !FORCES && lane < T->nmj;  // S4's motor lanes: their topology entries, fetched early
+  const int hinge_id = hl ? T->hinge_ids[lane] : 0, hinge_foot = hl ? T->hinge_foot[lane] : -1;
   // the gait setup of the rollout, stored by the call's preparation pass (hs_prep_kernel;
   // the idle half reads its neighbour's): read from global memory where it is used
   const SetupL& st = rws[bb].st;
@@ -2904,8 +2964,8 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
     return;
   } else {
     bool deferred = false;
-    step<DEFER>(T, a, mp, st, sm.sv, sm.d.fl, sm.d.wk, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
-                deferred, !fix_idle, lane);
+    step<DEFER>(T, a, mp, st, sm.sv, sm.d.fl, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
+                deferred, !fix_idle, lane, hinge_id, hinge_foot);
     if (DEFER && deferred) {  // the fixup launch solves this (step, rollout) with the general path
       if (lane == 0 && live) {
         const int it = atomicAdd(mp.fix_count, 1);

@@ -531,6 +531,49 @@ int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& 
     const int h = t->hinge_ids[j];
     t->hinge_range[j] = h | ((h + t->node[h].size) << 8);
   }
+  // the per-limb kinematics plan (hs_topo::limb_own*, link): the products in double, like every
+  // topology entry (3x4 products summed as the kernels' mul, translation last)
+  auto mul34 = [](const hs_aff34& A, const hs_aff34& B) {
+    hs_aff34 C;
+    for (int c = 0; c < 4; c++)
+      for (int r = 0; r < 3; r++) {
+        double s = 0;
+        for (int k = 0; k < 3; k++) s = s + A.m[k * 3 + r] * B.m[c * 3 + k];
+        if (c == 3) s = s + A.m[9 + r];
+        C.m[c * 3 + r] = s;
+      }
+    return C;
+  };
+  auto mulp3 = [](const hs_aff34& A, const double* v, double* u) {
+    for (int r = 0; r < 3; r++) {
+      double s = 0;
+      for (int k = 0; k < 3; k++) s = s + A.m[k * 3 + r] * v[k];
+      u[r] = s + A.m[9 + r];
+    }
+  };
+  for (int L = 0; L < nl; L++) {
+    int m = 0;
+    for (int k = 1; k < t->limb_chain_len[L]; k++) {
+      const int v = t->limb_chain[L][k];
+      if (t->node[v].owner_limb != L) continue;
+      if (m == HS_OWN_MAX) { err = "too many chain bodies on one limb"; return HS_E_TOPOLOGY; }
+      if (t->node[v].foot >= 0) { err = "foot on a limb chain"; return HS_E_TOPOLOGY; }
+      t->limb_own[L][m] = v;
+      for (int i = 0; i < 3; i++) t->limb_own_com[L][m][i] = t->node[v].com[i];
+      m++;
+    }
+    t->limb_own_n[L] = m;
+    for (int k = 0; k < 3; k++) {
+      const hs_node& nd = t->node[t->limb_node[L][k]];
+      hs_link& lk = t->link[L][k];
+      lk.P = k > 0 ? mul34(t->node[t->limb_node[L][k - 1]].A_pj_body, nd.J_A_parent) : hs_aff34{};
+      for (int i = 0; i < 9; i++) lk.Rpj[i] = nd.A_pj_body.m[i];
+      mulp3(nd.A_pj_body, nd.com, lk.com);
+      mulp3(nd.A_pj_body, nd.cap, lk.cap);
+      lk.foot = nd.foot;
+      lk.hinge = nd.hinge;
+    }
+  }
   // each hinge may carry at most one foot below it (keeps the 1st-order Gram block diagonal)
   for (int fi = 0; fi < nf; fi++)
     for (int a = t->footis[fi]; a >= 0; a = t->node[a].parent) {

@@ -37,6 +37,17 @@ struct hs_node {
   int32_t size;         // nodes in this node's subtree (preorder table: the subtree is [i, i + size))
 };
 
+#define HS_OWN_MAX 2  // chain bodies one limb lane computes
+
+// one limb link for the rollout kernels' limb FK (hs_topo::link)
+struct hs_link {
+  hs_aff34 P;      // A_pj_body of the previous link times this link's J_A_parent (unused for link 0)
+  double Rpj[9];   // rotation of this link's A_pj_body, column-major [c * 3 + r]
+  double com[3];   // A_pj_body * com
+  double cap[3];   // A_pj_body * cap (the foot link)
+  int32_t foot, hinge;  // node[] foot / hinge of the link
+};
+
 struct hs_topo {
   int32_t n, nf, nmj, cfg;
   int32_t n_limbs, lik_kind, max_depth;
@@ -63,4 +74,14 @@ struct hs_topo {
   // (after node[], so the fields above keep their offsets) motor j's subtree in the preorder
   // table: hinge_ids[j] | (hinge_ids[j] + its size) << 8, one load for solve_forces' subtree tests
   int32_t hinge_range[HS_NMAX];
+  // Per-limb kinematics plan: everything a limb lane of the rollout kernels reads, at addresses that
+  // depend on the limb alone (no node-id chase). Chain bodies the limb computes (owner_limb == L, the
+  // root aside; never a foot), in chain order:
+  int32_t limb_own_n[HS_LMAX];
+  int32_t limb_own[HS_LMAX][HS_OWN_MAX];
+  double limb_own_com[HS_LMAX][HS_OWN_MAX][3];
+  // its three links precombined (limb_fk): with H_k = J_k Rz(q_k) the link's hinge frame and pj_k its
+  // A_pj_body, the body frame is A_k = H_k pj_k and the next joint frame J_(k+1) = H_k (pj_k Jp_(k+1)),
+  // one product per link; the features come from H_k: pos = H_k (pj_k com_k), the foot H_2 (pj_2 cap)
+  struct hs_link link[HS_LMAX][3];
 };

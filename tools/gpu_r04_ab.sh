@@ -17,6 +17,10 @@ for args in "--steps 20 --warmup 5" "--steps 200 --warmup 20"; do
   done; done
 done
 unset HSLABS_VARIANT
+if [ -n "$STAMPS" ]; then
+  FUSED=1 timeout -k 10 120 python tools/stamps.py > $OUT/stamps_fused.txt 2>&1 || { echo stamps failed; tail -5 $OUT/stamps_fused.txt; exit 1; }
+  grep -vE "amdgpu.ids" $OUT/stamps_fused.txt
+fi
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu > $OUT/prof.log 2>&1 || { echo prof failed; tail -20 $OUT/prof.log; exit 1; }
 python3 $R/tools/trace_tail.py $OUT/prof/run_kernel_trace.csv 4 > $OUT/trace_tail.txt; cat $OUT/trace_tail.txt
