@@ -753,7 +753,6 @@ template <class W>
 __device__ __attribute__((always_inline)) inline void kin_sample_straight(
     const hs_topo* T, const GaitR& g, const hs_gait_params& gp, const SetupL& st, int isample, int L,
     bool ignore_reach, const W& w, int k, const StraightPre& pre, const KinFrames& kf, const real* kt, int ktab_lo) {
-  const int lv[3] = {T->limb_node[L][0], T->limb_node[L][1], T->limb_node[L][2]};
   const real t = pre.t;
   const real tv = t * pre.v;  // gait_record's torso advance
   const bool wq = w.want_q(k);
@@ -2906,8 +2905,6 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
     h_row = s;
   }
   const int nl = T->n_limbs;
-  const bool hl = !FORCES && lane < T->nmj;  // S4's motor lanes: their topology entries, fetched early
-  const int hinge_id = hl ? T->hinge_ids[lane] : 0, hinge_foot = hl ? T->hinge_foot[lane] : -1;
   // the gait setup of the rollout, stored by the call's preparation pass (hs_prep_kernel;
   // the idle half reads its neighbour's): read from global memory where it is used
   const SetupL& st = rws[bb].st;
@@ -2919,6 +2916,10 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
                                            i - 2 + (sl < NS ? sl : 0), mp.ktab_lo, mp.ttab_n, L);
 #endif
   const GaitR g = load_gait(a.params[bb]);
+  // S4's motor lanes: their topology entries, issued after the loads above (vmcnt counts in order, so a
+  // wait for a value loaded first does not wait for these)
+  const bool hl = !FORCES && lane < T->nmj;
+  const int hinge_id = hl ? T->hinge_ids[lane] : 0, hinge_foot = hl ? T->hinge_foot[lane] : -1;
   const bool ignore_reach = a.ignore_reach != 0;
   const bool straight = g.curvature == 0 && !g.rec_xf;
 #if HS_CURVED_LDS
