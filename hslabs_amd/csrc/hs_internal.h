@@ -66,8 +66,8 @@ struct launch_map {
   const double* red_rollout_mass;
   uint64_t* red_best_key;
   // the call's preparation pass (hs_prep_kernel) stores the sample times of samples [ktab_lo,
-  // ktab_lo + ttab_n) and, for straight gaits when ktab_n > 0, the limb IK of samples [ktab_lo,
-  // ktab_lo + ktab_n) per rollout (ktab_range); the step launches read them. ktab_nl: limb lanes per
+  // ktab_lo + ttab_n) and, when ktab_n > 0, the limb IK (and for turning or transformed gaits the torso
+  // record) of samples [ktab_lo, ktab_lo + ktab_n) per rollout (ktab_range); the step launches read them. ktab_nl: limb lanes per
   // rollout the pass enumerates (the launch's largest model)
   int32_t ktab_n, ktab_lo, ktab_nl, ttab_n;
 };

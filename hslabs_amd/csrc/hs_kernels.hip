@@ -180,6 +180,9 @@ struct SetupL {
 // IK table entry (RolloutWS::ktab): the joint values of a limb at a sample, their sines and cosines,
 // then 1 if unreachable or failed
 constexpr int KT_W = 4;
+// torso record row (RolloutWS::ktor), turning or transformed gaits: the torso's q6 (set_rec's position and
+// Euler angles) and its frame A0 = J_A_parent free_joint(q6) A_pj_body at a sample
+constexpr int KR_W = 18;
 struct KinFrames {
   real A0[12];              // the torso (node 0)
   real J0[HS_LMAX][12];     // each limb's hip joint frame
@@ -242,7 +245,7 @@ __device__ inline void gsync() {
 #ifdef HS_STAMPS
 // diagnostic build only: per-phase shader-clock stamps of the first 4096 rollouts
 // (slots 16, 17: the constant 100 MHz clock at wave entry and exit, comparable across CUs)
-__device__ unsigned long long g_stamps[4096][24];
+__device__ unsigned long long g_stamps[4096][32];  // slots 24..31: hs_prep_kernel's
 #define STAMP(slot)                                                                                    \
   do {                                                                                                 \
     if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][slot] = __builtin_amdgcn_s_memtime(); \
@@ -522,14 +525,33 @@ __device__ inline void limb_step(const GaitR& g, real t, real t_lift, real xs, r
   dz = sz * g.step_height;
 }
 
+// What gait_record reads of the gait setup for one pergen index j: the rollout's entries and j's
+// (from the setup record, limb_rec, or from the preparation pass's registers)
+struct LimbRec {
+  real v, t_step, max_radius, ts, xs, pos0[3];
+  SC3 tsc;
+};
+__device__ __attribute__((always_inline)) inline LimbRec limb_rec(const SetupL& st, int j) {
+  LimbRec r;
+  r.v = st.v;
+  r.t_step = st.t_step;
+  r.max_radius = st.max_radius;
+  r.ts = st.ts[j];
+  r.xs = st.xs[j];
+  for (int i = 0; i < 3; i++) r.pos0[i] = st.pos0[j][i];
+  r.tsc = st.tsc;
+  return r;
+}
+
 // pergensetup::set_rec at time t for lik limb L (pergen.cpp:225-239): torso position o0 and Euler
 // angles o1 (turn_torso, pergen.cpp:386-397; `turned` when the torso frame was rotated), and the
-// limb's foot target (limb_positions of its pergen index, pergen.cpp:82-94, 160-183)
+// limb's foot target (limb_positions of its pergen index, pergen.cpp:82-94, 160-183); st: that
+// index's LimbRec
 // STRAIGHT: the caller knows curvature == 0 (a wave of straight gaits), so the turning code is left
 // out and the record is one basic block the scheduler can interleave with the torso FK
 template <bool STRAIGHT = false>
 __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g, const hs_gait_params& gp,
-                                                                  const SetupL& st, real t, int j, real* o0, real* o1,
+                                                                  const LimbRec& st, real t, real* o0, real* o1,
                                                                   bool& turned, real* target) {
   o0[0] = g.torso_pos[0]; o0[1] = g.torso_pos[1]; o0[2] = g.torso_pos[2];
   o1[0] = g.torso_angles[0]; o1[1] = g.torso_angles[1]; o1[2] = g.torso_angles[2];
@@ -556,11 +578,11 @@ __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g
   }
   // periodicgenerator::limb_positions for this limb's pergen index (pergen.cpp:82-94)
   real dx, dz;
-  limb_step(g, t, st.ts[j], st.xs[j], st.t_step, dx, dz);
+  limb_step(g, t, st.ts, st.xs, st.t_step, dx, dz);
   real dy = 0;
   if (!STRAIGHT && g.curvature != 0) {  // turn_position (pergen.cpp:160-183)
     int s = (g.curvature > 0) ? 1 : -1;
-    real x0 = st.pos0[j][0], y0 = st.pos0[j][1];
+    real x0 = st.pos0[0], y0 = st.pos0[1];
     real rc = real(1) / g.curvature;
     real rx = x0, ry = y0 - rc;
     real r = sqrt(rx * rx + ry * ry);
@@ -573,9 +595,9 @@ __device__ __attribute__((always_inline)) inline void gait_record(const GaitR& g
     dx = r * sg * sb;
     dy += -r * cg * sb;
   }
-  target[0] = dx + st.pos0[j][0];
-  target[1] = dy + st.pos0[j][1];
-  target[2] = dz + st.pos0[j][2];
+  target[0] = dx + st.pos0[0];
+  target[1] = dy + st.pos0[1];
+  target[2] = dz + st.pos0[2];
   if (!STRAIGHT && g.rec_xf) {  // set_rec's last step (pergen.cpp:238)
     transform_rec(gp, o0, o1, target);
     turned = true;  // the torso angles are no longer the configured ones
@@ -662,7 +684,7 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
   const real t = sample_time(st, t_tab, isample, tlo, ttab_n);  // t accumulates dt (periodic.cpp:171-181)
   real o0[3], o1[3], target[3];
   bool turned;
-  gait_record<STRAIGHT>(g, gp, st, t, j, o0, o1, turned, target);
+  gait_record<STRAIGHT>(g, gp, limb_rec(st, j), t, o0, o1, turned, target);
   STAMP(20);
   // set_jvalues_with_lik: torso + body chain FK, then limb IK (model.cpp:354-359, lik.cpp:89-99)
   real q6[6] = {o0[0], o0[1], o0[2], o1[0], o1[1], o1[2]};
@@ -718,7 +740,7 @@ __device__ __attribute__((always_inline)) inline void straight_ik(const hs_topo*
                                                                   bool& bad) {
   real o0[3], o1[3], target[3];
   bool turned;
-  gait_record<true>(g, gp, st, t, T->limb_pergen[L], o0, o1, turned, target);
+  gait_record<true>(g, gp, limb_rec(st, T->limb_pergen[L]), t, o0, o1, turned, target);
   hip_ik(T, L, J, target, ignore_reach, ja, bad);
 }
 
@@ -821,6 +843,42 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
     for (int kk = 0; kk < 3; kk++) sincos(ja[kk], &sq[kk], &cq[kk]);
   }
   if (w.want_centre(k)) w.unreach(k, L) = bad ? 1 : 0;
+  STAMP(22);
+  limb_fk(T, L, J, ja, sq, cq, wq, w, k);
+}
+
+// kin_sample for a turning or transformed gait from the preparation pass's rows: the torso's q6 and frame
+// at the sample (tor, a RolloutWS::ktor row: the gait record and torso FK kin_sample forms) and the limb's
+// joint values (kte, its ktab entry); the chain bodies and the hip frame from the torso frame as in
+// kin_sample, then the limb FK
+template <class W>
+__device__ __attribute__((always_inline)) inline void kin_sample_tab(const hs_topo* T, int L, const W& w, int k,
+                                                                     const real* tor, const real* kte) {
+  const int clen = T->limb_chain_len[L];
+  const bool wq = w.want_q(k);
+  const NodeK n0 = load_nodek(T, 0);
+  const A34 A0 = load34r(tor + 6);
+  if (L == 0) {
+    if (wq) for (int i = 0; i < 6; i++) w.q(k)[i] = tor[i];
+    node_features(T, 0, n0, A0, &n0.Jp, w, k);  // torso joint frame J = I * J_A_parent
+  }
+  A34 A = A0;
+  for (int kk = 1; kk < clen; kk++) {
+    const int v = T->limb_chain[L][kk];
+    const NodeK nc = load_nodek(T, v);
+    A = mul(A, nc.pj);
+    if (nc.owner == L) node_features(T, v, nc, A, nullptr, w, k);
+  }
+  const A34 J = mul(A, node_joint_parent(T, T->limb_child[L]));  // poslimb (lik.cpp:341-347)
+  STAMP(20);
+  real ja[3], sq[3], cq[3];
+#pragma unroll
+  for (int kk = 0; kk < 3; kk++) {
+    ja[kk] = kte[kk];
+    sincos(ja[kk], &sq[kk], &cq[kk]);
+  }
+  if (w.want_centre(k)) w.unreach(k, L) = kte[KT_W - 1] != 0 ? 1 : 0;
+  STAMP(21);
   STAMP(22);
   limb_fk(T, L, J, ja, sq, cq, wq, w, k);
 }
@@ -2743,20 +2801,23 @@ struct RolloutWS {
   SetupL st;
   real t_tab[HS_KTAB];  // sample times of the call's rows (sample_time): t_tab[r] = t_(ktab_lo + r)
   KinFrames kf;         // a straight gait's frames
-  real ktab[HS_KTAB][HS_LMAX][KT_W];  // straight gaits: limb L's joint values at sample ktab_lo + r
+  real ktab[HS_KTAB][HS_LMAX][KT_W];  // limb L's joint values at sample ktab_lo + r
+  real ktor[HS_KTAB][KR_W];           // turning or transformed gaits: the torso at sample ktab_lo + r
 };
 static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 
 // ---------------------------------------------------------------------------
 // The call's preparation pass (hs_prep_kernel): the gait setup of every rollout (pergensetup::
-// setup_pergen, pergen.cpp:453-507), its sample times (periodic.cpp:171-181) and, for straight
-// untransformed gaits, the IK table of the samples the call's steps read -- in one launch.
+// setup_pergen, pergen.cpp:453-507), its sample times (periodic.cpp:171-181) and the IK table of the
+// samples the call's steps read (with, for turning or transformed gaits, the torso record) -- in one launch.
 //
 // Lane = (rollout, limb L, chunk of HS_PREP_ROWS table rows). Every lane runs its limb's setup (torso
 // frame, chain, hip frame J0, default foot position, lift-off entries) itself -- the lanes of one
 // wavefront do it in the same instructions, so the repetition costs one pass per wavefront -- and then
 // the rows of its chunk: the sample time, and for a straight gait J = J0 advanced by t v along the
-// torso's x and the limb IK at the foot target (straight_ik's operations). The chunk-0 lanes store the
+// torso's x and the limb IK at the foot target (straight_ik's operations); for a turning or transformed
+// gait kin_sample's record, torso FK, chain and limb IK, the torso's q6 and frame stored per row
+// (RolloutWS::ktor, lane L = 0). The chunk-0 lanes store the
 // setup record; max_radius (compute_max_radius, curved gaits) is the maximum over a rollout's limb
 // lanes, exchanged in LDS. A rollout's limb lanes form a group that never crosses a wavefront (groups of
 // nli lanes, floor(64 / nli) per wavefront). XCD-aware: block 8 jb + x runs groups of batch wavefronts
@@ -2780,6 +2841,10 @@ __host__ __device__ inline int64_t prep_blocks(int n_waves, int ttab_n, int nli)
 __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
   __shared__ real rad[WAVE];
+  __shared__ real q6s[HS_PREP_ROWS][6][WAVE / 4];  // turning gaits' rows: [row][q6 entry][group] (>= 4 limbs)
+  __shared__ real tgs[HS_PREP_ROWS][3][WAVE];      // [row][target entry][lane]
+  RSTAMP(29);
+  STAMP(24);
   if (blockIdx.x == 0)  // the call's fixup counters, before its step launches append to them
     for (int i = threadIdx.x; i < mp.fix_n_counts; i += WAVE) mp.fix_count[i] = 0;
   const int nli = ktab_lanes(mp), gpw = WAVE / nli;
@@ -2800,12 +2865,13 @@ __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_t
   real pos0[3], ts = 0, xs = 0, t_step = 0, dt = 0, v = 0;
   bool straight = false;
   real my_rad = 0;
+  SC3 tsc;
   RolloutWS* __restrict__ ws = rws + b;
   if (on) {
     g = load_gait(a.params[b]);
     straight = g.curvature == 0 && !g.rec_xf;  // kin_sample's turning / record-transform test
     const int nl = T->n_limbs, j = T->limb_pergen[L];
-    const SC3 tsc = sincos3(g.torso_angles[0], g.torso_angles[1], g.torso_angles[2]);
+    tsc = sincos3(g.torso_angles[0], g.torso_angles[1], g.torso_angles[2]);
     const A34 A0 = torso_frame(T, g, tsc);
     limb_setup(T, g, A0, L, J0, pos0, chunk == 0 ? &ws->kf : nullptr);
     t_step = step_fraction(g, nl);
@@ -2827,41 +2893,92 @@ __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_t
     }
     if (g.curvature != 0) my_rad = turn_radius(pos0, g.curvature);
   }
+  STAMP(25);
   rad[threadIdx.x] = my_rad;
   wave_sync();
-  if (on && chunk == 0 && L == 0) {  // compute_max_radius over the rollout's limbs
-    real mr = 0;
-    if (g.curvature != 0)
-      for (int l = 0; l < T->n_limbs; l++) {
-        const real r = rad[threadIdx.x + l];
-        if (r > mr) mr = r;
-      }
-    ws->st.max_radius = mr;
-  }
+  real mr = 0;  // compute_max_radius over the rollout's limbs (every lane: turning rows read it)
+  if (on && g.curvature != 0)
+    for (int l = 0; l < T->n_limbs; l++) {
+      const real r = rad[threadIdx.x - L + l];
+      if (r > mr) mr = r;
+    }
+  if (on && chunk == 0 && L == 0) ws->st.max_radius = mr;
+  STAMP(26);
   if (!on) return;
   const int r0 = chunk * HS_PREP_ROWS, r1 = min(r0 + HS_PREP_ROWS, mp.ttab_n);
   if (r0 >= r1) return;
-  const bool table = straight && mp.ktab_n > 0;
+  const bool table = mp.ktab_n > 0;
   const hs_aff34& Jp0 = T->node[0].J_A_parent;
   const real u[3] = {(real)Jp0.m[0], (real)Jp0.m[1], (real)Jp0.m[2]};
+  const bool ir = a.ignore_reach != 0;
+  auto store_row = [&](int r, const real* ja, bool bad) {
+    real* e = ws->ktab[r][L];
+#pragma unroll
+    for (int kk = 0; kk < 3; kk++) e[kk] = ja[kk];
+    e[KT_W - 1] = bad ? real(1) : real(0);
+  };
   real t = sample_time_sum(dt, mp.ktab_lo + r0);
+  // kin_sample's foot target, hip frame and limb IK at samples ktab_lo + r, one loop per kind of gait
+  // (a lane's kind is fixed: the other loop's values are not live in this one)
+  if (!table || straight) {
 #pragma unroll 1
-  for (int r = r0; r < r1; r++) {
-    if (r > r0) t += dt;  // the loop's next addition
-    if (L == 0) ws->t_tab[r] = t;
-    if (table) {  // straight_ik at sample ktab_lo + r
-      real dx, dz;
-      limb_step(g, t, ts, xs, t_step, dx, dz);
-      const real target[3] = {dx + pos0[0], real(0) + pos0[1], dz + pos0[2]};
+    for (int r = r0; r < r1; r++) {
+      if (r > r0) t += dt;  // the loop's next addition
+      if (L == 0) ws->t_tab[r] = t;
+      if (table) {  // straight_ik's: J = J0 advanced by t v
+        real dx, dz;
+        limb_step(g, t, ts, xs, t_step, dx, dz);
+        const real target[3] = {dx + pos0[0], real(0) + pos0[1], dz + pos0[2]};
+        real ja[3];
+        bool bad;
+        hip_ik(T, L, frame_at(J0, u, t * v), target, ir, ja, bad);
+        store_row(r, ja, bad);
+      }
+      if (r == r0) STAMP(27);
+    }
+  } else {
+    // turning or transformed gaits (kin_sample's sequence), in two passes over the rows so that the gait
+    // record's values and the FK + IK's are not live together: (1) the record: the torso's q6 (lane L = 0,
+    // per group) and the foot targets to LDS; (2) the torso FK (free_joint: sincos of the configured
+    // angles when not turned, as free_joint_sc with the setup's), the chain, the hip frame, the limb IK
+    const LimbRec rl{v, t_step, mr, ts, xs, {pos0[0], pos0[1], pos0[2]}, tsc};
+    const hs_gait_params& gp = a.params[b];
+#pragma unroll 1
+    for (int r = r0; r < r1; r++) {
+      if (r > r0) t += dt;
+      if (L == 0) ws->t_tab[r] = t;
+      real o0[3], o1[3], target[3];
+      bool turned;
+      gait_record<false>(g, gp, rl, t, o0, o1, turned, target);
+      if (L == 0) {
+        const real q6[6] = {o0[0], o0[1], o0[2], o1[0], o1[1], o1[2]};
+        for (int i = 0; i < 6; i++) q6s[r - r0][i][gl] = q6[i];
+      }
+      for (int i = 0; i < 3; i++) tgs[r - r0][i][threadIdx.x] = target[i];
+    }
+    wave_sync();
+#pragma unroll 1
+    for (int r = r0; r < r1; r++) {
+      real q6[6], target[3];
+      for (int i = 0; i < 6; i++) q6[i] = q6s[r - r0][i][gl];
+      for (int i = 0; i < 3; i++) target[i] = tgs[r - r0][i][threadIdx.x];
+      const A34 A0 = mul(mul(node_joint_parent(T, 0), free_joint(q6)), node_pj(T, 0));
+      if (L == 0) {  // the torso record the step launches read (kin_sample_tab)
+        real* tr = ws->ktor[r];
+        for (int i = 0; i < 6; i++) tr[i] = q6[i];
+        store34r(A0, tr + 6);
+      }
+      A34 A = A0;
+      for (int k = 1; k < T->limb_chain_len[L]; k++) A = mul(A, node_pj(T, T->limb_chain[L][k]));
       real ja[3];
       bool bad;
-      hip_ik(T, L, frame_at(J0, u, t * v), target, a.ignore_reach != 0, ja, bad);
-      real* e = ws->ktab[r][L];
-#pragma unroll
-      for (int kk = 0; kk < 3; kk++) e[kk] = ja[kk];
-      e[KT_W - 1] = bad ? real(1) : real(0);
+      hip_ik(T, L, mul(A, node_joint_parent(T, T->limb_child[L])), target, ir, ja, bad);
+      store_row(r, ja, bad);
+      if (r == r0) STAMP(27);
     }
   }
+  STAMP(28);
+  RSTAMP(30);
 }
 
 // One wavefront's step: fused step fstep (0 outside fused launches) of batch wavefront wid. only_sub
@@ -2924,7 +3041,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   const bool straight = g.curvature == 0 && !g.rec_xf;
 #if HS_CURVED_LDS
   // a wave with a turning or transformed gait: the record in LDS for the turning path's many reads
-  if (__ballot(!straight)) {
+  if (!kt && __ballot(!straight)) {
     constexpr int NW = sizeof(SetupL) / sizeof(real);
     const real* cache = reinterpret_cast<const real*>(&rws[bb].st);
     real* lds = reinterpret_cast<real*>(&smem[sub].st);
@@ -2952,6 +3069,14 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
 #endif
         kin_sample_straight(T, g, a.params[bb], st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
                             pre, rws[bb].kf, kt, mp.ktab_lo);
+      } else if (kt) {  // a turning or transformed gait with the call's tables
+        const int r = i - 2 + sl - mp.ktab_lo;
+#if HS_PRELOAD && HS_KTE_PRELOAD
+        const real* kte = pre.kte;
+#else
+        const real* kte = kt + ((size_t)r * HS_LMAX + L) * KT_W;
+#endif
+        kin_sample_tab(T, L, OneWin<NM, FORCES>{&sm.d}, sl - 2, rws[bb].ktor[r], kte);
       } else {
         kin_sample<false>(T, g, a.params[bb], st_curved, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d},
                           sl - 2, t_tab, mp.ktab_lo, mp.ttab_n);
@@ -3055,7 +3180,7 @@ __global__ __launch_bounds__(WAVE) void hs_pergen_rec_kernel(const hs_topo* __re
   if (live && lane < nl) {
     real o0[3], o1[3], target[3];
     bool turned;
-    gait_record<false>(g, params[b], st[sub], (real)times[ti], T->limb_pergen[lane], o0, o1, turned, target);
+    gait_record<false>(g, params[b], limb_rec(st[sub], T->limb_pergen[lane]), (real)times[ti], o0, o1, turned, target);
     double* r = rec + it * (6 + 3 * nl);
     if (lane == 0)
       for (int i = 0; i < 3; i++) { r[i] = o0[i]; r[3 + i] = o1[i]; }
@@ -3069,11 +3194,11 @@ __global__ __launch_bounds__(WAVE) void hs_pergen_rec_kernel(const hs_topo* __re
 #if defined(HS_STAMPS) && !HS_REAL_IS_FLOAT
 extern "C" int hs_debug_read_stamps(unsigned long long* out, int n_rows) {
   if (n_rows > 4096) n_rows = 4096;
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 24 * n_rows, 0,
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 32 * n_rows, 0,
                                   hipMemcpyDeviceToHost);
 }
 extern "C" int hs_debug_clear_stamps() {
-  static unsigned long long zero[4096][24];
+  static unsigned long long zero[4096][32];
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
 }
 #endif

@@ -295,10 +295,11 @@ def test_fused_reference_mode_fixups_over_two_launches(gpu, hmodels):
 
 @pytest.mark.parametrize("n_t,pattern", [(20, "alternate"), (20, "pairs"), (70, "alternate")])
 def test_fused_straight_and_curved_rollouts(gpu, hmodels, n_t, pattern):
-    """Straight gaits take the frame / IK-table kinematics (kin_sample_straight, the table built by
-    the fused call's setup pass when n_t + H + 3 <= HS_KTAB; n_t = 70 has none), curved ones the
-    turning path. Waves holding one of each ("alternate") run both; "pairs" keeps each wave uniform.
-    The fused call equals the launch-per-step horizon run (IK solved inline) bitwise."""
+    """Straight gaits take the frame / IK-table kinematics (kin_sample_straight), curved ones the torso
+    record and the same table (kin_sample_tab). Waves holding one of each ("alternate") run both;
+    "pairs" keeps each wave uniform. Both sides build the call's tables (24 rows, hs::ktab_range, for the
+    fused call and for the launch-per-step horizon run alike), so the fused call equals the horizon run
+    bitwise; the table against the inline record, FK and IK is test_table_rows_match_inline_kinematics."""
     import torch
     from hslabs_amd import synth
 
@@ -350,3 +351,52 @@ def test_ik_table_rows_match_single_steps(gpu, hmodels, name, k0, H, n_calls):
             ref_tau, ref_q = npy(one.tau)[:, 0], npy(one.q)[:, 0]
             assert np.allclose(q[:, row], ref_q, rtol=0, atol=1e-12), (c, h)
             assert np.allclose(tau[:, row], ref_tau, rtol=1e-9, atol=1e-9), (c, h)
+
+
+@pytest.mark.parametrize("name,k0,H,n_calls,kind", [("hexapod", 7, 5, 3, "curved"), ("spider", 18, 1, 6, "curved"),
+                                                    ("hexapod", 13, 2, 9, "transformed"),
+                                                    ("myant", 3, 4, 4, "mixed"), ("hexapod", 0, 20, 1, "mixed")])
+def test_table_rows_match_inline_kinematics(gpu, hmodels, name, k0, H, n_calls, kind):
+    """The preparation pass tabulates every gait: straight ones (joint values), turning and record-
+    transformed ones (joint values and the torso record, kin_sample_tab). Every step of the fused call
+    equals the same step of a horizon run whose window is too long for a table (64 steps: 68 samples
+    > HS_KTAB, hs::ktab_range), where the step kernel forms the gait record, torso FK, chain and limb
+    IK inline (kin_sample, kin_sample_straight's straight_ik). The pass performs the inline sequence's
+    operations in the same order, so the steps are bitwise equal (round 4: max |dtau| 0 on every case);
+    a table row off by one sample, or a torso record of the wrong rollout, would move the torques by
+    O(1). "mixed" waves hold straight, turning and transformed rollouts together."""
+    import torch
+    from conftest import transformed
+    from hslabs_amd import synth
+
+    m = hmodels[name]
+    B, n_t = 64, 20
+    rng = np.random.default_rng(41)
+    p = synth.gen_params(B, name, id0=777, curved=kind != "transformed")
+    if kind == "transformed":
+        p, _ = transformed(p, rng, frac=0.7)
+    elif kind == "mixed":
+        plain = synth.gen_params(B, name, id0=777)
+        sel = np.arange(B) % 3 == 0
+        p[sel] = plain[sel]
+        p, _ = transformed(p, rng, frac=0.3)
+    outs = ("tau", "cf", "q", "flags")
+    fz = gpu.DeviceBatch(m, p, n_t=n_t, k0=k0, horizon=n_calls * H, outputs=outs)
+    fz.run_calls(n_calls, call_horizon=H)
+    ref = gpu.DeviceBatch(m, p, n_t=n_t, k0=0, horizon=64, outputs=outs)
+    ref.run(best=False)
+    torch.cuda.synchronize()
+    tau, q, fl = npy(fz.tau), npy(fz.q), npy(fz.flags).astype(np.uint32)
+    rtau, rq, rfl = npy(ref.tau), npy(ref.q), npy(ref.flags).astype(np.uint32)
+    cf, rcf = npy(fz.cf), npy(ref.cf)
+    near = 0
+    for c in range(n_calls):
+        for h in range(H):
+            kk = (k0 + c * H) % n_t + h
+            row = c * H + h
+            assert np.array_equal(q[:, row], rq[:, kk]), (c, h)
+            assert np.array_equal(tau[:, row], rtau[:, kk], equal_nan=True), (c, h)
+            assert np.array_equal(cf[:, row], rcf[:, kk], equal_nan=True), (c, h)
+            assert np.array_equal(fl[:, row], rfl[:, kk]), (c, h)
+            near += int(((fl[:, row] & gpu.capi.HS_FLAG_NEAR_RANK) != 0).sum())
+    print(f"{name} {kind}: {n_calls * H * B} steps bitwise equal ({near} near-rank flagged)")

@@ -46,7 +46,7 @@ def main():
     n = int(os.environ.get("N", "4096"))
     model = os.environ.get("MODEL", "hexapod")
     m = H.KinematicModel(os.path.join(ROOT, "models", f"{model}.xml"))
-    params = synth.gen_params(n, model)
+    params = synth.gen_params(n, model, curved=bool(os.environ.get("CURVED")))
     k0 = int(os.environ.get("K0", "0"))
     # horizon 2 (default): the stamps kept are the second launch's, which loads the gait setup
     # stored by the first (the steady state of hs_run_steps); HZ=1 stamps a computing launch
@@ -64,9 +64,20 @@ def main():
         H.run_host(m, params, n_t=20, k0=k0, horizon=hz, want=("tau",))  # warm
         L.hs_debug_clear_stamps()
         H.run_host(m, params, n_t=20, k0=k0, horizon=hz, want=("tau",))
-    st = np.zeros((4096, 24), dtype=np.uint64)
+    st = np.zeros((4096, 32), dtype=np.uint64)
     L.hs_debug_read_stamps(st.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), 4096)
-    st = st[:min((n + 1) // 2, 4096)].astype(np.int64)  # one row per wavefront (two rollouts)
+    st = st.astype(np.int64)
+    pr = st[st[:, 28] != 0]  # hs_prep_kernel's waves (fused: the call's preparation pass), slots 24..30
+    if fused and len(pr):
+        for name, x, y in (("p:setup", 24, 25), ("p:max radius", 25, 26), ("p:first row", 26, 27),
+                           ("p:other rows", 27, 28), ("p:TOTAL", 24, 28)):
+            d = pr[:, y] - pr[:, x]
+            print(f"{name:22s} mean {d.mean():10.0f}  p50 {np.median(d):10.0f}  p90 {np.percentile(d, 90):10.0f}  max {d.max():10.0f}  (n={len(pr)})")
+        t0 = pr[:, 29].min()
+        for name, col in (("p:wave start (us)", 29), ("p:wave end (us)", 30)):
+            d = (pr[:, col] - t0) / 100.0
+            print(f"{name:22s} mean {d.mean():10.2f}  p50 {np.median(d):10.2f}  p90 {np.percentile(d, 90):10.2f}  max {d.max():10.2f}")
+    st = st[:min((n + 1) // 2, 4096)]  # one row per wavefront (two rollouts)
     if fused:
         st = st[64:]  # the fixup + reduce launch's 64 workgroups restamp rows 0..63's entry slots
     if os.environ.get("STAMPS_RAW"):
