@@ -177,9 +177,9 @@ struct SetupL {
 // and each limb's hip joint frame (poslimb, lik.cpp:341-347) are a constant rotation with a
 // translation affine in tv: A(t) = [R | c + tv u], u = column 0 of the torso's J_A_parent. The gait
 // setup keeps them at tv = 0 (the products kin_sample forms, once per rollout instead of per sample).
-// IK table entry (RolloutWS::ktab): the joint values of a limb at a sample, their sines and cosines,
-// then 1 if unreachable or failed
-constexpr int KT_W = 4;
+// IK table entry (RolloutWS::ktab): the joint values of a limb at a sample; its unreachable-or-failed
+// flag is a byte of RolloutWS::kbad (24 B entries in fp64: the table is written and read once per call)
+constexpr int KT_W = 3;
 // torso record row (RolloutWS::ktor), turning or transformed gaits: the torso's q6 (set_rec's position and
 // Euler angles) and its frame A0 = J_A_parent free_joint(q6) A_pj_body at a sample
 constexpr int KR_W = 18;
@@ -230,6 +230,19 @@ constexpr real kNearBand = real(4);
 constexpr real kCondQR = HS_REAL_IS_FLOAT ? real(1e-4) : real(1e-7);
 // v is within `band` of threshold t (both positive; a NaN is not)
 __device__ inline bool near_thr(real v, real t, real band) { return v >= t / band && v <= t * band; }
+
+#ifndef HS_NT_OUT
+#define HS_NT_OUT 0  // output rows stored with the nontemporal hint (streamed past L2's working set)
+#endif
+// an output store: written once, never read back by the kernel
+template <class V>
+__device__ inline void out_store(V* p, V v) {
+#if HS_NT_OUT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 
 // The ABI's arrays are double*; in the fp32 build they hold floats.
 __device__ inline real* outp(double* p) { return reinterpret_cast<real*>(p); }
@@ -751,11 +764,13 @@ struct StraightPre {
   real t, v;
   A34 J0;
   real kte[KT_W];
+  bool bad;
 };
 // (kt: the table, whose row r holds sample lo + r)
 __device__ __attribute__((always_inline)) inline StraightPre straight_preload(const SetupL& st, const real* t_tab,
                                                                              const KinFrames& kf, const real* kt,
-                                                                             int isample, int lo, int ttab_n, int L) {
+                                                                             const uint8_t* kb, int isample, int lo,
+                                                                             int ttab_n, int L) {
   StraightPre p;
   p.t = sample_time(st, t_tab, isample, lo, ttab_n);
   p.v = st.v;
@@ -764,6 +779,7 @@ __device__ __attribute__((always_inline)) inline StraightPre straight_preload(co
     const real* e = kt + ((size_t)(isample - lo) * HS_LMAX + L) * KT_W;
 #pragma unroll
     for (int i = 0; i < KT_W; i++) p.kte[i] = e[i];
+    p.bad = kb[(isample - lo) * HS_LMAX + L] != 0;
   }
   return p;
 }
@@ -774,7 +790,8 @@ __device__ __attribute__((always_inline)) inline StraightPre straight_preload(co
 template <class W>
 __device__ __attribute__((always_inline)) inline void kin_sample_straight(
     const hs_topo* T, const GaitR& g, const hs_gait_params& gp, const SetupL& st, int isample, int L,
-    bool ignore_reach, const W& w, int k, const StraightPre& pre, const KinFrames& kf, const real* kt, int ktab_lo) {
+    bool ignore_reach, const W& w, int k, const StraightPre& pre, const KinFrames& kf, const real* kt,
+    const uint8_t* kb, int ktab_lo) {
   const real t = pre.t;
   const real tv = t * pre.v;  // gait_record's torso advance
   const bool wq = w.want_q(k);
@@ -783,12 +800,15 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
   A34 A0, J = pre.J0;
 #if HS_KTE_PRELOAD
   const real* kte = pre.kte;
+  const bool kbad = pre.bad;
 #else
   real kte[KT_W];  // the table row, loaded once the gait is known to be straight
+  bool kbad = false;
   if (kt) {
     const real* e = kt + ((size_t)(isample - ktab_lo) * HS_LMAX + L) * KT_W;
 #pragma unroll
     for (int i = 0; i < KT_W; i++) kte[i] = e[i];
+    kbad = kb[(isample - ktab_lo) * HS_LMAX + L] != 0;
   }
 #endif
   if (L == 0) A0 = load34r(kf.A0);
@@ -835,7 +855,7 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
       ja[kk] = kte[kk];
       sincos(ja[kk], &sq[kk], &cq[kk]);
     }
-    bad = kte[KT_W - 1] != 0;
+    bad = kbad;
     STAMP(21);
   } else {
     straight_ik(T, g, gp, st, t, L, J, ignore_reach, ja, bad);
@@ -853,7 +873,7 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
 // kin_sample, then the limb FK
 template <class W>
 __device__ __attribute__((always_inline)) inline void kin_sample_tab(const hs_topo* T, int L, const W& w, int k,
-                                                                     const real* tor, const real* kte) {
+                                                                     const real* tor, const real* kte, bool bad) {
   const int clen = T->limb_chain_len[L];
   const bool wq = w.want_q(k);
   const NodeK n0 = load_nodek(T, 0);
@@ -877,7 +897,7 @@ __device__ __attribute__((always_inline)) inline void kin_sample_tab(const hs_to
     ja[kk] = kte[kk];
     sincos(ja[kk], &sq[kk], &cq[kk]);
   }
-  if (w.want_centre(k)) w.unreach(k, L) = kte[KT_W - 1] != 0 ? 1 : 0;
+  if (w.want_centre(k)) w.unreach(k, L) = bad ? 1 : 0;
   STAMP(21);
   STAMP(22);
   limb_fk(T, L, J, ja, sq, cq, wq, w, k);
@@ -2405,7 +2425,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
       if (mp.pd_dq0) outp(mp.pd_dq0)[o] = jvel;
     }
   }
-  if (live && a.tau && lane < mp.st_tau) outp(a.tau)[row * mp.st_tau + lane] = tq;  // 0 past nmj
+  if (live && a.tau && lane < mp.st_tau) out_store(&outp(a.tau)[row * mp.st_tau + lane], tq);  // 0 past nmj
   if (half_ballot(lane < nmj && tq != tq) || half_ballot(lane < k && sv.y[lane] != sv.y[lane])) flags |= HS_FLAG_NAN;
   if (half_ballot(lane < nl && w.unreach(0, lane))) flags |= HS_FLAG_UNREACH;
   // contact forces z = -N_cont y (ftsolver.cpp:91, 276-284)
@@ -2413,7 +2433,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
     const int fi = lane / 3, j = lane % 3;
     real zv = (lane < 3 * nf) ? -real(0) : real(0);
     if (lane < 3 * nf && ((cmask >> fi) & 1)) zv = -(real(0) + (real(-1)) * sv.y[3 * __popc(cmask & ((1u << fi) - 1)) + j]);
-    outp(a.cf)[row * mp.st_cf + lane] = zv;
+    out_store(&outp(a.cf)[row * mp.st_cf + lane], zv);
   }
   if (live && a.x) {  // full joint force/torque vector x += N y
     for (int rI = lane; rI < 6 * n; rI += HALF) {
@@ -2438,7 +2458,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
     }
     for (int rI = 6 * n + lane; rI < mp.st_x; rI += HALF) outp(a.x)[row * mp.st_x + rI] = real(0);
   }
-  if (live && a.q && lane < mp.st_q) outp(a.q)[row * mp.st_q + lane] = (lane < cfg) ? w.q(0)[lane] : real(0);
+  if (live && a.q && lane < mp.st_q) out_store(&outp(a.q)[row * mp.st_q + lane], (lane < cfg) ? w.q(0)[lane] : real(0));
   if (live && a.dq && lane < mp.st_q) {  // compute_vel_traj (periodic.cpp:261-282)
     real v = real(0);
     if (lane < cfg) {
@@ -2447,9 +2467,9 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
       else if (d < -kPi) d += 2 * kPi;
       v = d / (2 * st.dt);
     }
-    outp(a.dq)[row * mp.st_q + lane] = v;
+    out_store(&outp(a.dq)[row * mp.st_q + lane], v);
   }
-  if (live && a.flags && lane == 0) a.flags[row] = flags;
+  if (live && a.flags && lane == 0) out_store(&a.flags[row], flags);
   const real work_dt = half_sum(wdl);  // the joints' positive work (work_over_period's sum)
   // work_over_period: work += work_dt * dt, one rounding (explicit, so the fused path's in-order
   // sum performs the same operation); fused steps hand back the joint sum itself
@@ -2803,6 +2823,7 @@ struct RolloutWS {
   KinFrames kf;         // a straight gait's frames
   real ktab[HS_KTAB][HS_LMAX][KT_W];  // limb L's joint values at sample ktab_lo + r
   real ktor[HS_KTAB][KR_W];           // turning or transformed gaits: the torso at sample ktab_lo + r
+  uint8_t kbad[HS_KTAB][HS_LMAX];     // 1: ktab[r][L]'s limb IK unreachable or failed
 };
 static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 
@@ -2825,7 +2846,7 @@ static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 // MI355X_MICROARCH.md), so the record and rows are written into the L2 the steps read them from.
 // ---------------------------------------------------------------------------
 #ifndef HS_PREP_ROWS
-#define HS_PREP_ROWS 6  // table rows per lane (measured: 2, 3, 6 rows at 2-4 waves/SIMD; 6 at 2 the fastest)
+#define HS_PREP_ROWS 5  // table rows per lane (round 4, B = 4096, 24 rows: 3, 4, 5, 6, 8 rows give 24.1, 25.0, 23.4, 24.9, 29.7 us)
 #endif
 #ifndef HS_PREP_WAVES
 #define HS_PREP_WAVES 2  // waves per SIMD the register budget allows (196 VGPRs; 3 or 4 spill)
@@ -2915,7 +2936,7 @@ __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_t
     real* e = ws->ktab[r][L];
 #pragma unroll
     for (int kk = 0; kk < 3; kk++) e[kk] = ja[kk];
-    e[KT_W - 1] = bad ? real(1) : real(0);
+    ws->kbad[r][L] = bad ? 1 : 0;
   };
   real t = sample_time_sum(dt, mp.ktab_lo + r0);
   // kin_sample's foot target, hip frame and limb IK at samples ktab_lo + r, one loop per kind of gait
@@ -3028,8 +3049,9 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   const int i = k0 + 2;  // centre sample of this launch's step
   const int sl = lane / nl, L = lane % nl;
   const real* kt = mp.ktab_n > 0 ? &rws[bb].ktab[0][0][0] : nullptr;
+  const uint8_t* kb = &rws[bb].kbad[0][0];
 #if HS_PRELOAD
-  const StraightPre pre = straight_preload(st, rws[bb].t_tab, rws[bb].kf, HS_KTE_PRELOAD ? kt : nullptr,
+  const StraightPre pre = straight_preload(st, rws[bb].t_tab, rws[bb].kf, HS_KTE_PRELOAD ? kt : nullptr, kb,
                                            i - 2 + (sl < NS ? sl : 0), mp.ktab_lo, mp.ttab_n, L);
 #endif
   const GaitR g = load_gait(a.params[bb]);
@@ -3064,19 +3086,21 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
     if (sl < NS) {
       if (straight) {
 #if !HS_PRELOAD
-        const StraightPre pre = straight_preload(st, t_tab, rws[bb].kf, HS_KTE_PRELOAD ? kt : nullptr, i - 2 + sl,
-                                                 mp.ktab_lo, mp.ttab_n, L);
+        const StraightPre pre = straight_preload(st, t_tab, rws[bb].kf, HS_KTE_PRELOAD ? kt : nullptr, kb,
+                                                 i - 2 + sl, mp.ktab_lo, mp.ttab_n, L);
 #endif
         kin_sample_straight(T, g, a.params[bb], st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
-                            pre, rws[bb].kf, kt, mp.ktab_lo);
+                            pre, rws[bb].kf, kt, kb, mp.ktab_lo);
       } else if (kt) {  // a turning or transformed gait with the call's tables
         const int r = i - 2 + sl - mp.ktab_lo;
 #if HS_PRELOAD && HS_KTE_PRELOAD
         const real* kte = pre.kte;
+        const bool kbad = pre.bad;
 #else
         const real* kte = kt + ((size_t)r * HS_LMAX + L) * KT_W;
+        const bool kbad = kb[r * HS_LMAX + L] != 0;
 #endif
-        kin_sample_tab(T, L, OneWin<NM, FORCES>{&sm.d}, sl - 2, rws[bb].ktor[r], kte);
+        kin_sample_tab(T, L, OneWin<NM, FORCES>{&sm.d}, sl - 2, rws[bb].ktor[r], kte, kbad);
       } else {
         kin_sample<false>(T, g, a.params[bb], st_curved, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d},
                           sl - 2, t_tab, mp.ktab_lo, mp.ttab_n);
