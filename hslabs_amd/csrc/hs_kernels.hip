@@ -231,19 +231,6 @@ constexpr real kCondQR = HS_REAL_IS_FLOAT ? real(1e-4) : real(1e-7);
 // v is within `band` of threshold t (both positive; a NaN is not)
 __device__ inline bool near_thr(real v, real t, real band) { return v >= t / band && v <= t * band; }
 
-#ifndef HS_NT_OUT
-#define HS_NT_OUT 0  // output rows stored with the nontemporal hint (streamed past L2's working set)
-#endif
-// an output store: written once, never read back by the kernel
-template <class V>
-__device__ inline void out_store(V* p, V v) {
-#if HS_NT_OUT
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
-}
-
 // The ABI's arrays are double*; in the fp32 build they hold floats.
 __device__ inline real* outp(double* p) { return reinterpret_cast<real*>(p); }
 __device__ inline const real* inp(const double* p) { return reinterpret_cast<const real*>(p); }
@@ -385,20 +372,18 @@ __device__ inline A34 torso_frame(const hs_topo* T, const GaitR& g, const SC3& t
 // lik.cpp:341-347) and the default foot position of its pergen index (get_limb_hip_pos, the foot
 // shift, set_limb_poss; pergen.cpp:453-507). kf (optional): store the chain body frames this limb owns
 // and its hip frame (KinFrames, the straight gaits' frames at tv = 0)
+// The chain's products come precombined from the loader (hs_topo::limb_own_rel, limb_hip_rel): one product
+// per frame, every load indexed by the limb alone
 __device__ __attribute__((always_inline)) inline void limb_setup(const hs_topo* T, const GaitR& g, const A34& A0, int L,
                                                                  A34& J0, real* pos0, KinFrames* kf = nullptr) {
-  A34 A = A0;
-  int own = 0;
-  for (int k = 1; k < T->limb_chain_len[L]; k++) {
-    const int v = T->limb_chain[L][k];
-    A = mul(A, node_pj(T, v));
-    if (kf && T->node[v].owner_limb == L) store34r(A, kf->Ao[L][own++]);
-  }
-  const int c = T->limb_child[L];
-  J0 = mul(A, node_joint_parent(T, c));
+  if (kf)
+    for (int m = 0; m < T->limb_own_n[L]; m++) store34r(mul(A0, load34(T->limb_own_rel[L][m])), kf->Ao[L][m]);
+  J0 = mul(A0, load34(T->limb_hip_rel[L]));
   if (kf) store34r(J0, kf->J0[L]);
-  const A34 Ac = mul(mul_hinge(J0, real(1), real(0)), node_pj(T, c));  // Rz(0): cos 0 = 1, sin 0 = 0
-  real pos[3] = {Ac(0, 3), Ac(1, 3), Ac(2, 3)};  // get_limb_hip_pos
+  // get_limb_hip_pos: the child's frame J0 Rz(0) pj_child (Rz(0) = I) at its translation
+  const real ct[3] = {(real)T->limb_child_t[L][0], (real)T->limb_child_t[L][1], (real)T->limb_child_t[L][2]};
+  real pos[3];
+  mulp(J0, ct, pos);
   if (g.foot_shift_type == 0) {                   // setup_foot_shift / shift_pos0
     real sh[3] = {real(0), g.foot_shift, real(0)}, ls[3];
     mulp(A0, sh, ls);
@@ -2425,7 +2410,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
       if (mp.pd_dq0) outp(mp.pd_dq0)[o] = jvel;
     }
   }
-  if (live && a.tau && lane < mp.st_tau) out_store(&outp(a.tau)[row * mp.st_tau + lane], tq);  // 0 past nmj
+  if (live && a.tau && lane < mp.st_tau) outp(a.tau)[row * mp.st_tau + lane] = tq;  // 0 past nmj
   if (half_ballot(lane < nmj && tq != tq) || half_ballot(lane < k && sv.y[lane] != sv.y[lane])) flags |= HS_FLAG_NAN;
   if (half_ballot(lane < nl && w.unreach(0, lane))) flags |= HS_FLAG_UNREACH;
   // contact forces z = -N_cont y (ftsolver.cpp:91, 276-284)
@@ -2433,7 +2418,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
     const int fi = lane / 3, j = lane % 3;
     real zv = (lane < 3 * nf) ? -real(0) : real(0);
     if (lane < 3 * nf && ((cmask >> fi) & 1)) zv = -(real(0) + (real(-1)) * sv.y[3 * __popc(cmask & ((1u << fi) - 1)) + j]);
-    out_store(&outp(a.cf)[row * mp.st_cf + lane], zv);
+    outp(a.cf)[row * mp.st_cf + lane] = zv;
   }
   if (live && a.x) {  // full joint force/torque vector x += N y
     for (int rI = lane; rI < 6 * n; rI += HALF) {
@@ -2458,7 +2443,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
     }
     for (int rI = 6 * n + lane; rI < mp.st_x; rI += HALF) outp(a.x)[row * mp.st_x + rI] = real(0);
   }
-  if (live && a.q && lane < mp.st_q) out_store(&outp(a.q)[row * mp.st_q + lane], (lane < cfg) ? w.q(0)[lane] : real(0));
+  if (live && a.q && lane < mp.st_q) outp(a.q)[row * mp.st_q + lane] = (lane < cfg) ? w.q(0)[lane] : real(0);
   if (live && a.dq && lane < mp.st_q) {  // compute_vel_traj (periodic.cpp:261-282)
     real v = real(0);
     if (lane < cfg) {
@@ -2467,9 +2452,9 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
       else if (d < -kPi) d += 2 * kPi;
       v = d / (2 * st.dt);
     }
-    out_store(&outp(a.dq)[row * mp.st_q + lane], v);
+    outp(a.dq)[row * mp.st_q + lane] = v;
   }
-  if (live && a.flags && lane == 0) out_store(&a.flags[row], flags);
+  if (live && a.flags && lane == 0) a.flags[row] = flags;
   const real work_dt = half_sum(wdl);  // the joints' positive work (work_over_period's sum)
   // work_over_period: work += work_dt * dt, one rounding (explicit, so the fused path's in-order
   // sum performs the same operation); fused steps hand back the joint sum itself

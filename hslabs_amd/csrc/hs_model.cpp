@@ -553,16 +553,23 @@ int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& 
   };
   for (int L = 0; L < nl; L++) {
     int m = 0;
+    hs_aff34 Q;  // pj of the chain bodies below the torso, multiplied in chain order
+    for (int i = 0; i < 12; i++) Q.m[i] = (i % 4 == 0 && i < 9) ? 1.0 : 0.0;
     for (int k = 1; k < t->limb_chain_len[L]; k++) {
       const int v = t->limb_chain[L][k];
+      Q = k == 1 ? t->node[v].A_pj_body : mul34(Q, t->node[v].A_pj_body);
       if (t->node[v].owner_limb != L) continue;
       if (m == HS_OWN_MAX) { err = "too many chain bodies on one limb"; return HS_E_TOPOLOGY; }
       if (t->node[v].foot >= 0) { err = "foot on a limb chain"; return HS_E_TOPOLOGY; }
       t->limb_own[L][m] = v;
+      t->limb_own_rel[L][m] = Q;
       for (int i = 0; i < 3; i++) t->limb_own_com[L][m][i] = t->node[v].com[i];
       m++;
     }
     t->limb_own_n[L] = m;
+    const hs_node& child = t->node[t->limb_child[L]];
+    t->limb_hip_rel[L] = t->limb_chain_len[L] > 1 ? mul34(Q, child.J_A_parent) : child.J_A_parent;
+    for (int i = 0; i < 3; i++) t->limb_child_t[L][i] = child.A_pj_body.m[9 + i];
     for (int k = 0; k < 3; k++) {
       const hs_node& nd = t->node[t->limb_node[L][k]];
       hs_link& lk = t->link[L][k];

@@ -84,4 +84,10 @@ struct hs_topo {
   // A_pj_body, the body frame is A_k = H_k pj_k and the next joint frame J_(k+1) = H_k (pj_k Jp_(k+1)),
   // one product per link; the features come from H_k: pos = H_k (pj_k com_k), the foot H_2 (pj_2 cap)
   struct hs_link link[HS_LMAX][3];
+  // the gait setup's chain products from the torso's body frame A0 (limb_setup, one product per frame):
+  // its owned bodies' frames A0 own_rel[m], its hip joint frame J0 = A0 hip_rel (poslimb, lik.cpp:341-347),
+  // and the limb child's A_pj_body translation (get_limb_hip_pos: J0 Rz(0) pj_child's column 3)
+  hs_aff34 limb_own_rel[HS_LMAX][HS_OWN_MAX];
+  hs_aff34 limb_hip_rel[HS_LMAX];
+  double limb_child_t[HS_LMAX][3];
 };
