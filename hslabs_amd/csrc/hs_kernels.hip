@@ -176,18 +176,33 @@ struct SetupL {
 // the limbs is jointless (the loader's topology check), so the torso frame, the chain's body frames
 // and each limb's hip joint frame (poslimb, lik.cpp:341-347) are a constant rotation with a
 // translation affine in tv: A(t) = [R | c + tv u], u = column 0 of the torso's J_A_parent. The gait
-// setup keeps them at tv = 0 (the products kin_sample forms, once per rollout instead of per sample).
+// setup keeps them at tv = 0 (the products kin_sample forms, once per rollout instead of per sample):
+// the hip frames whole, and for the torso and the chain bodies the features themselves -- a body's
+// position A(t) com = (R com + c) + tv u, its rotation's skew part (constant) and its frame origin
+// c + tv u -- so a sample adds tv u to two points.
 // IK table entry (RolloutWS::ktab): the joint values of a limb at a sample; its unreachable-or-failed
 // flag is a byte of RolloutWS::kbad (24 B entries in fp64: the table is written and read once per call)
 constexpr int KT_W = 3;
 // torso record row (RolloutWS::ktor), turning or transformed gaits: the torso's q6 (set_rec's position and
 // Euler angles) and its frame A0 = J_A_parent free_joint(q6) A_pj_body at a sample
 constexpr int KR_W = 18;
+constexpr int BF_W = 9;  // a body's features at tv = 0: position R com + c, skew part of R (ust), origin c
 struct KinFrames {
-  real A0[12];              // the torso (node 0)
-  real J0[HS_LMAX][12];     // each limb's hip joint frame
-  real Ao[HS_LMAX][HS_OWN_MAX][12];  // the chain bodies each limb computes (hs_topo::limb_own)
+  real J0[HS_LMAX][12];                 // each limb's hip joint frame
+  real own[HS_LMAX][HS_OWN_MAX][BF_W];  // the chain bodies each limb computes (hs_topo::limb_own)
+  real torso[6];                        // the torso (node 0): position and ust (its joint frame is J_A_parent)
 };
+// the features of a body with frame A (node_features' pos and ust; the origin for a jointless body's jpos)
+__device__ inline void store_body(const A34& A, const real* com, real* bf, int n) {
+  real p[3];
+  mulp(A, com, p);
+  for (int i = 0; i < 3; i++) bf[i] = p[i];
+  bf[3] = (A(2, 1) - A(1, 2)) / 2;
+  bf[4] = (A(0, 2) - A(2, 0)) / 2;
+  bf[5] = (A(1, 0) - A(0, 1)) / 2;
+  if (n > 6)
+    for (int i = 0; i < 3; i++) bf[6 + i] = A(i, 3);
+}
 
 template <int NM>
 struct SolveL {
@@ -377,7 +392,10 @@ __device__ inline A34 torso_frame(const hs_topo* T, const GaitR& g, const SC3& t
 __device__ __attribute__((always_inline)) inline void limb_setup(const hs_topo* T, const GaitR& g, const A34& A0, int L,
                                                                  A34& J0, real* pos0, KinFrames* kf = nullptr) {
   if (kf)
-    for (int m = 0; m < T->limb_own_n[L]; m++) store34r(mul(A0, load34(T->limb_own_rel[L][m])), kf->Ao[L][m]);
+    for (int m = 0; m < T->limb_own_n[L]; m++) {
+      const real com[3] = {(real)T->limb_own_com[L][m][0], (real)T->limb_own_com[L][m][1], (real)T->limb_own_com[L][m][2]};
+      store_body(mul(A0, load34(T->limb_own_rel[L][m])), com, kf->own[L][m], BF_W);
+    }
   J0 = mul(A0, load34(T->limb_hip_rel[L]));
   if (kf) store34r(J0, kf->J0[L]);
   // get_limb_hip_pos: the child's frame J0 Rz(0) pj_child (Rz(0) = I) at its translation
@@ -750,6 +768,8 @@ struct StraightPre {
   A34 J0;
   real kte[KT_W];
   bool bad;
+  real own0[BF_W];  // the limb's first chain body (limb_own_n > 0), and the torso (lane L = 0)
+  real tor[6];
 };
 // (kt: the table, whose row r holds sample lo + r)
 __device__ __attribute__((always_inline)) inline StraightPre straight_preload(const SetupL& st, const real* t_tab,
@@ -760,6 +780,10 @@ __device__ __attribute__((always_inline)) inline StraightPre straight_preload(co
   p.t = sample_time(st, t_tab, isample, lo, ttab_n);
   p.v = st.v;
   p.J0 = load34r(kf.J0[L]);
+#pragma unroll
+  for (int i = 0; i < BF_W; i++) p.own0[i] = kf.own[L][0][i];
+#pragma unroll
+  for (int i = 0; i < 6; i++) p.tor[i] = kf.torso[i];
   if (kt) {
     const real* e = kt + ((size_t)(isample - lo) * HS_LMAX + L) * KT_W;
 #pragma unroll
@@ -782,7 +806,7 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
   const bool wq = w.want_q(k);
   const NodeK n0 = load_nodek(T, 0);
   const real u[3] = {n0.Jp(0, 0), n0.Jp(1, 0), n0.Jp(2, 0)};
-  A34 A0, J = pre.J0;
+  A34 J = pre.J0;
 #if HS_KTE_PRELOAD
   const real* kte = pre.kte;
   const bool kbad = pre.bad;
@@ -796,27 +820,23 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
     kbad = kb[(isample - ktab_lo) * HS_LMAX + L] != 0;
   }
 #endif
-  if (L == 0) A0 = load34r(kf.A0);
   for (int m = 0; m < T->limb_own_n[L]; m++) {  // the chain bodies this limb computes (never a foot)
     const int v = T->limb_own[L][m];
-    const A34 A = frame_at(load34r(kf.Ao[L][m]), u, tv);
+    real bf[BF_W];
+#pragma unroll
+    for (int i = 0; i < BF_W; i++) bf[i] = m == 0 ? pre.own0[i] : kf.own[L][m][i];
     if (w.want_pos(k)) {
-      const real c[3] = {(real)T->limb_own_com[L][m][0], (real)T->limb_own_com[L][m][1], (real)T->limb_own_com[L][m][2]};
-      real p[3];
-      mulp(A, c, p);
       real* P = w.pos(k, v);
-      for (int i = 0; i < 3; i++) P[i] = p[i];
+      for (int i = 0; i < 3; i++) P[i] = fma(tv, u[i], bf[i]);
     }
     if (w.want_ust(k)) {
       real* U = w.ust(k, v);
-      U[0] = (A(2, 1) - A(1, 2)) / 2;
-      U[1] = (A(0, 2) - A(2, 0)) / 2;
-      U[2] = (A(1, 0) - A(0, 1)) / 2;
+      for (int i = 0; i < 3; i++) U[i] = bf[3 + i];
     }
     if (w.want_centre(k)) {  // a body without a joint: J = its frame, no axis (node_features with J = null)
       real* Jp = w.jpos(k, v);
       real* Jz = w.jz(k, v);
-      for (int i = 0; i < 3; i++) Jp[i] = A(i, 3);
+      for (int i = 0; i < 3; i++) Jp[i] = fma(tv, u[i], bf[6 + i]);
       for (int i = 0; i < 3; i++) Jz[i] = real(0);
     }
   }
@@ -828,7 +848,21 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
       q[2] = g.torso_pos[2];
       for (int i = 0; i < 3; i++) q[3 + i] = g.torso_angles[i];
     }
-    node_features(T, 0, n0, frame_at(A0, u, tv), &n0.Jp, w, k);  // torso joint frame J = I * J_A_parent
+    // node_features of the torso: its joint frame J = I * J_A_parent, not a foot
+    if (w.want_pos(k)) {
+      real* P = w.pos(k, 0);
+      for (int i = 0; i < 3; i++) P[i] = fma(tv, u[i], pre.tor[i]);
+    }
+    if (w.want_ust(k)) {
+      real* U = w.ust(k, 0);
+      for (int i = 0; i < 3; i++) U[i] = pre.tor[3 + i];
+    }
+    if (w.want_centre(k)) {
+      real* Jp = w.jpos(k, 0);
+      real* Jz = w.jz(k, 0);
+      for (int i = 0; i < 3; i++) Jp[i] = n0.Jp(i, 3);
+      for (int i = 0; i < 3; i++) Jz[i] = n0.Jp(i, 2);
+    }
   }
   STAMP(20);
   J = frame_at(J, u, tv);
@@ -2894,7 +2928,8 @@ __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_t
         st.v = v;
         st.dt = dt;
         st.tsc = tsc;
-        store34r(A0, ws->kf.A0);
+        const real com0[3] = {(real)T->node[0].com[0], (real)T->node[0].com[1], (real)T->node[0].com[2]};
+        store_body(A0, com0, ws->kf.torso, 6);
       }
     }
     if (g.curvature != 0) my_rad = turn_radius(pos0, g.curvature);
