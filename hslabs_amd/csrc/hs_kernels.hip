@@ -927,11 +927,12 @@ __device__ __attribute__((always_inline)) inline void kin_sample_tab(const hs_to
 // ---------------------------------------------------------------------------
 // SYNC = false: the caller's next phase reads only this lane's rows (particular_sub's first stage)
 template <bool SYNC = true, class W, class SV>
-__device__ __attribute__((always_inline)) inline void dynamics(const hs_topo* T, const SetupL& st, SV& sv, const W& w, int lane) {
+// dt: the sample spacing (SetupL::dt, read once at the wave's start)
+__device__ __attribute__((always_inline)) inline void dynamics(const hs_topo* T, real dt, SV& sv, const W& w, int lane) {
   const int n = T->n;
   if (lane < n) {
     const int i = lane;
-    const real inv = real(1) / (2 * st.dt);
+    const real inv = real(1) / (2 * dt);
     const real m = (real)T->mass[i];
     const real *Pp = w.pos(2, i), *P0 = w.pos(0, i), *Pm = w.pos(-2, i);
     const real *Up = w.ust(2, i), *U0 = w.ust(0, i), *Um = w.ust(-2, i);
@@ -2361,15 +2362,17 @@ __device__ inline void reduce_rollouts(const hs_run_args& a, real total_mass, co
 // step's half-wave stores nothing and `deferred` is set), so this instantiation has no call to the
 // out-of-line general path: the call alone costs the whole kernel SGPRs (spills in the hot solve
 // region) and 2.4 % of the step time
-// hinge_id, hinge_foot: this lane's motor's part and foot (lanes < nmj), loaded at the wave's start
+// hinge_id, hinge_foot: this lane's motor's part and foot (lanes < nmj), and dt (SetupL::dt), loaded at the
+// wave's start (a value read from the setup record later would be read again after every output store,
+// which may alias it)
 template <bool DEFER, class W, class SV>
-__device__ __attribute__((always_inline)) inline void step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st, SV& sv,
+__device__ __attribute__((always_inline)) inline void step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, real dt, SV& sv,
                      FastL& fl, const W& w, SolveWS* G, int b, bool live, int h,
                      real& work, bool& deferred, bool may_general, int lane, int hinge_id, int hinge_foot) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
   STAMP(3);
   // D writes, and S1's first stage reads, part i's rows on lane i only: no sync between them
-  dynamics<false>(T, st, sv, w, lane);
+  dynamics<false>(T, dt, sv, w, lane);
   STAMP(4);
   particular_sub(T, sv, w, lane);
   STAMP(5);
@@ -2426,7 +2429,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
     real dd = w.q(1)[6 + lane] - w.q(-1)[6 + lane];
     if (dd > kPi) dd -= 2 * kPi;
     else if (dd < -kPi) dd += 2 * kPi;
-    real jvel = dd / (2 * st.dt);
+    real jvel = dd / (2 * dt);
     real dw = tq * jvel;
     wdl = (dw > 0) ? dw : 0;
     if (mp.pd_tau && live) {  // linear_feedback_control (player.cpp:417-432), target = get_motor_adas
@@ -2484,7 +2487,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
       real d = w.q(1)[lane] - w.q(-1)[lane];
       if (d > kPi) d -= 2 * kPi;
       else if (d < -kPi) d += 2 * kPi;
-      v = d / (2 * st.dt);
+      v = d / (2 * dt);
     }
     outp(a.dq)[row * mp.st_q + lane] = v;
   }
@@ -2493,7 +2496,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   // work_over_period: work += work_dt * dt, one rounding (explicit, so the fused path's in-order
   // sum performs the same operation); fused steps hand back the joint sum itself
   if (mp.fused_w) work = work_dt;
-  else work = fma(work_dt, st.dt, work);
+  else work = fma(work_dt, dt, work);
   STAMP(8);
   RSTAMP(17);
 }
@@ -2812,10 +2815,10 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
 }
 
 template <class W, class SV>
-__device__ __attribute__((always_inline)) inline void forces_step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, const SetupL& st,
+__device__ __attribute__((always_inline)) inline void forces_step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, real dt,
                             SV& sv, ForceL& fr, const W& w, int b, bool live, int h, int lane) {
   const int nf = T->nf, cfg = T->cfg, nl = T->n_limbs, nq = 3 * nf;
-  dynamics(T, st, sv, w, lane);
+  dynamics(T, dt, sv, w, lane);
   particular(T, sv, w, lane);
   STAMP(10);
   const size_t row = (size_t)b * a.horizon + h;
@@ -3074,6 +3077,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   const StraightPre pre = straight_preload(st, rws[bb].t_tab, rws[bb].kf, HS_KTE_PRELOAD ? kt : nullptr, kb,
                                            i - 2 + (sl < NS ? sl : 0), mp.ktab_lo, mp.ttab_n, L);
 #endif
+  const real dt = st.dt;
   const GaitR g = load_gait(a.params[bb]);
   // S4's motor lanes: their topology entries, issued after the loads above (vmcnt counts in order, so a
   // wait for a value loaded first does not wait for these)
@@ -3130,11 +3134,11 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   }
   STAMP(2);
   if constexpr (FORCES) {
-    forces_step(T, a, mp, st, sm.sv, sm.d.fr, OneWin<NM, FORCES>{&sm.d}, b, live, h_row, lane);
+    forces_step(T, a, mp, dt, sm.sv, sm.d.fr, OneWin<NM, FORCES>{&sm.d}, b, live, h_row, lane);
     return;
   } else {
     bool deferred = false;
-    step<DEFER>(T, a, mp, st, sm.sv, sm.d.fl, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
+    step<DEFER>(T, a, mp, dt, sm.sv, sm.d.fl, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
                 deferred, !fix_idle, lane, hinge_id, hinge_foot);
     if (DEFER && deferred) {  // the fixup launch solves this (step, rollout) with the general path
       if (lane == 0 && live) {
