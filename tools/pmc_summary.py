@@ -98,8 +98,8 @@ def main():
     if "FETCH_SIZE" in med and "WRITE_SIZE" in med:
         traffic = int(round((2 * med["FETCH_SIZE"] + med["WRITE_SIZE"]) * 1024))
         lines.append(f"HBM traffic per step of the batch, step launch (FETCH_SIZE x2 + WRITE_SIZE): {traffic} bytes "
-                     f"(FETCH_SIZE alone x1: {int(med['FETCH_SIZE'] * 1024)} B; the x2 is calibrated for 16-B/lane "
-                     f"streaming loads, these are narrower, so the figure is an upper bound)")
+                     f"(FETCH_SIZE alone x1: {int(med['FETCH_SIZE'] * 1024)} B; x2 as calibrated on known byte counts at "
+                     f"8 and 16 B per lane and 24-byte records, profiles/r04_fetch_calibration.txt)")
         if not a.forces:
             jk = collect_job_kernels(a.root)
             extra = 0.0
