@@ -212,6 +212,7 @@ struct SolveL {
   };
   real y[HS_KMAX];
   int cfoot[HS_LMAX];
+  uint32_t fch[HS_LMAX][2];  // hs_topo::foot_chain8, copied at the wave's start (the contact blocks' chains)
 };
 
 template <int NM, bool FORCES>
@@ -2086,9 +2087,10 @@ __device__ __attribute__((always_inline)) inline bool fast_solve_lanes(const hs_
       real d0[3];
       for (int r = 0; r < 3; r++) d0[r] = P0[r] - fp[r];
       real Dp[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};  // packed lower 00 10 11 20 21 22
-      const int nch = T->foot_chain_len[fi];
+      const uint8_t* fch = reinterpret_cast<const uint8_t*>(sv.fch[fi]);
+      const int nch = fch[0];
       for (int m = s4; m < nch; m += 4) {
-        const int p = T->foot_chain[fi][m];
+        const int p = fch[1 + m];
         const real* Jp = w.jpos(0, p);
         const real* Jz = w.jz(0, p);
         real da[3], va[3][3];
@@ -2411,18 +2413,23 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
     const int cc = (fi >= 0 && ((cmask >> fi) & 1)) ? __popc(cmask & ((1u << fi) - 1)) : -1;
     const real* Jp = w.jpos(0, h_id);
     const real* Jz = w.jz(0, h_id);
-    real d[3];
-    if (cc >= 0) {
-      const real* fp = w.fpos(0, fi);
-      for (int rr = 0; rr < 3; rr++) d[rr] = Jp[rr] - fp[rr];
+    // every operand read in one batch, without branches (a hinge with no foot in contact takes y = 0:
+    // its terms are exact zeros, s stays +0 as when they were skipped)
+    const real* fp = w.fpos(0, fi >= 0 ? fi : 0);
+    const int yb = cc >= 0 ? 3 * cc : 0;
+    real d[3], y3[3];
+#pragma unroll
+    for (int rr = 0; rr < 3; rr++) {
+      d[rr] = Jp[rr] - fp[rr];
+      const real yv = sv.y[yb + rr];
+      y3[rr] = cc >= 0 ? yv : real(0);
     }
 #pragma unroll
     for (int r = 0; r < 3; r++) {
       real s = real(0);
-      if (cc >= 0)
 #pragma unroll
-        for (int jj = 0; jj < 3; jj++)
-          if (jj != r) s = s + cross_e(d, jj, r) * sv.y[3 * cc + jj];  // (d x e_r)[r] = 0: skipped
+      for (int jj = 0; jj < 3; jj++)
+        if (jj != r) s = s + cross_e(d, jj, r) * y3[jj];  // (d x e_r)[r] = 0: skipped
       real xr = sv.x[3 * n + 3 * h_id + r] + s;
       tq = tq + Jz[r] * xr;
     }
@@ -3083,6 +3090,9 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   // wait for a value loaded first does not wait for these)
   const bool hl = !FORCES && lane < T->nmj;
   const int hinge_id = hl ? T->hinge_ids[lane] : 0, hinge_foot = hl ? T->hinge_foot[lane] : -1;
+  // the foot chains (hs_topo::foot_chain8), to LDS with the kinematics' stores: the contact blocks then
+  // read them there instead of through two dependent global loads
+  const uint32_t fch_w = (!FORCES && lane < 2 * HS_LMAX) ? (&T->foot_chain8[0][0])[lane] : 0u;
   const bool ignore_reach = a.ignore_reach != 0;
   const bool straight = g.curvature == 0 && !g.rec_xf;
 #if HS_CURVED_LDS
@@ -3130,6 +3140,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
                           sl - 2, t_tab, mp.ktab_lo, mp.ttab_n);
       }
     }
+    if (!FORCES && lane < 2 * HS_LMAX) (&sm.sv.fch[0][0])[lane] = fch_w;
     wave_sync();
   }
   STAMP(2);

@@ -600,6 +600,11 @@ int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& 
       t->foot_chain[fi][m++] = a;
     }
     t->foot_chain_len[fi] = m;
+    uint8_t b[8] = {(uint8_t)m, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < m; k++) b[1 + k] = (uint8_t)t->foot_chain[fi][k];
+    for (int w = 0; w < 2; w++)
+      t->foot_chain8[fi][w] = (uint32_t)b[4 * w] | (uint32_t)b[4 * w + 1] << 8 | (uint32_t)b[4 * w + 2] << 16 |
+                              (uint32_t)b[4 * w + 3] << 24;
   }
   for (int j = 0; j < nh; j++) t->hinge_foot[j] = t->node[t->hinge_ids[j]].limb_below;
   if (sim) {

@@ -90,4 +90,7 @@ struct hs_topo {
   hs_aff34 limb_own_rel[HS_LMAX][HS_OWN_MAX];
   hs_aff34 limb_hip_rel[HS_LMAX];
   double limb_child_t[HS_LMAX][3];
+  // foot_chain packed for the rollout kernels' LDS copy: foot fi's bytes [len, chain[0], ..., chain[len - 1]]
+  // (len <= HS_CHAIN_MAX < 8, node ids < 256) in two little-endian words
+  uint32_t foot_chain8[HS_LMAX][2];
 };

@@ -59,6 +59,8 @@ def main():
         torch.cuda.synchronize()
         L.hs_debug_clear_stamps()
         b.run_calls(20, best=True)
+        if os.environ.get("B2B"):  # a second call queued behind the first: its stamps overwrite the first's
+            b.run_calls(20, best=True)
         torch.cuda.synchronize()
     else:
         H.run_host(m, params, n_t=20, k0=k0, horizon=hz, want=("tau",))  # warm
