@@ -57,6 +57,9 @@ def main():
         b = H.DeviceBatch(m, params, n_t=20, k0=k0, horizon=20, outputs=("tau", "cf", "work_cot", "flags"))
         b.run_calls(20, best=True)
         torch.cuda.synchronize()
+        # STEP=s: the fused launch's step s (its wavefronts are blocks s * n_waves ...); the preparation
+        # pass's rows are then not recorded
+        L.hs_debug_set_stamp_base(ctypes.c_uint(int(os.environ.get("STEP", "0")) * ((n + 1) // 2)))
         L.hs_debug_clear_stamps()
         b.run_calls(20, best=True)
         if os.environ.get("B2B"):  # a second call queued behind the first: its stamps overwrite the first's
@@ -80,7 +83,7 @@ def main():
             d = (pr[:, col] - t0) / 100.0
             print(f"{name:22s} mean {d.mean():10.2f}  p50 {np.median(d):10.2f}  p90 {np.percentile(d, 90):10.2f}  max {d.max():10.2f}")
     st = st[:min((n + 1) // 2, 4096)]  # one row per wavefront (two rollouts)
-    if fused:
+    if fused and not int(os.environ.get("STEP", "0")):
         st = st[64:]  # the fixup + reduce launch's 64 workgroups restamp rows 0..63's entry slots
     if os.environ.get("STAMPS_RAW"):
         np.save(os.environ["STAMPS_RAW"], st)
