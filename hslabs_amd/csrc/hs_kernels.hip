@@ -262,13 +262,16 @@ __device__ inline void gsync() {
 // diagnostic build only: per-phase shader-clock stamps of the first 4096 rollouts
 // (slots 16, 17: the constant 100 MHz clock at wave entry and exit, comparable across CUs)
 __device__ unsigned long long g_stamps[4096][32];  // slots 24..31: hs_prep_kernel's
+__device__ unsigned int g_stamp_base;  // row r holds block g_stamp_base + r (hs_debug_set_stamp_base)
 #define STAMP(slot)                                                                                    \
   do {                                                                                                 \
-    if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][slot] = __builtin_amdgcn_s_memtime(); \
+    const unsigned r_ = blockIdx.x - g_stamp_base;                                                     \
+    if (threadIdx.x == 0 && r_ < 4096u) g_stamps[r_][slot] = __builtin_amdgcn_s_memtime();             \
   } while (0)
-#define RSTAMP(slot)                                                                                       \
-  do {                                                                                                     \
-    if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime(); \
+#define RSTAMP(slot)                                                                                   \
+  do {                                                                                                 \
+    const unsigned r_ = blockIdx.x - g_stamp_base;                                                     \
+    if (threadIdx.x == 0 && r_ < 4096u) g_stamps[r_][slot] = __builtin_amdgcn_s_memrealtime();         \
   } while (0)
 #else
 #define STAMP(slot) do {} while (0)
@@ -3255,6 +3258,9 @@ extern "C" int hs_debug_read_stamps(unsigned long long* out, int n_rows) {
   if (n_rows > 4096) n_rows = 4096;
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 32 * n_rows, 0,
                                   hipMemcpyDeviceToHost);
+}
+extern "C" int hs_debug_set_stamp_base(unsigned int base) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_base), &base, sizeof(base), 0, hipMemcpyHostToDevice);
 }
 extern "C" int hs_debug_clear_stamps() {
   static unsigned long long zero[4096][32];
