@@ -25,6 +25,7 @@ for w in "--model spider --rollouts 16384 --horizon 32 --fp32" "--model spider -
   tail -1 $OUT/other_workloads.jsonl | python -c "import json,sys;d=json.loads(sys.stdin.read());print('$w', round(d['value']/1e6,3), 'M', d['unit'])"
 done
 FUSED=1 timeout -k 10 120 python tools/stamps.py > $OUT/stamps_fused.txt 2>&1 || { echo stamps failed; tail -5 $OUT/stamps_fused.txt; exit 1; }
+STEP=10 FUSED=1 timeout -k 10 120 python tools/stamps.py > $OUT/stamps_step10.txt 2>&1 || { echo stamps failed; tail -5 $OUT/stamps_step10.txt; exit 1; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu > $OUT/prof.log 2>&1 || { echo prof failed; tail -20 $OUT/prof.log; exit 1; }
 python3 $R/tools/trace_tail.py $OUT/prof/run_kernel_trace.csv 5 > $OUT/trace_tail.txt; cat $OUT/trace_tail.txt
@@ -38,4 +39,5 @@ python3 $R/tools/pmc_calib.py $OUT/calib > $OUT/calib.txt; cat $OUT/calib.txt
 PMC_OUT=$TAG/pmc bash $R/tools/gpu_pmc.sh || exit 1
 PMC_SET=diag PMC_OUT=$TAG/pmc_diag bash $R/tools/gpu_pmc.sh || exit 1
 PMC_OUT=$TAG/pmc_forces BENCH_ARGS="--forces --steps 20 --warmup 5" bash $R/tools/gpu_pmc.sh || exit 1
+if [ -n "$SPREAD" ]; then N=$SPREAD TAG=$TAG/spread bash $R/tools/gpu_spread_probe.sh || exit 1; fi
 echo "evidence call done"
