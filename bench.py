@@ -710,7 +710,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_over_algorithmic": None if traffic is None else round(traffic / alg_bytes, 3),
                          "traffic_note": pmc_note,
-                         "kernel": "hs_rollout_kernel (+ setup pass, IK table pass and work reduce, one step of the batch)",
+                         "kernel": "hs_rollout_kernel (+ the preparation pass (setup and IK table) and the work reduce, one step of the batch)",
                          "kernel_ms": round(kern_ms, 5), "alg_bytes_per_launch": alg_bytes},
             # the bound that binds: FP64 VALU issue/latency
             "fp64_valu": fp64,

@@ -141,7 +141,7 @@ int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::lau
   // the best key covers the work of all n_calls calls: taken after the last one only
   if (c.key_steps == 0) c.key_steps = (int32_t)std::min<int64_t>((int64_t)n_calls * a.horizon, INT32_MAX);
   // one gait setup per rollout per call: the preparation pass of the fused path (hs_prep_kernel: the
-  // setup record, sample times and straight gaits' IK table) stores it and every launch loads it, so the
+  // setup record, sample times, IK table and torso record) stores it and every launch loads it, so the
   // kinematics of these launches and of hs_run_calls' fused launches come from the same kernels
   hs::launch_map base = mp;
   base.setup_only = 1;
