@@ -393,37 +393,19 @@ __device__ inline A34 torso_frame(const hs_topo* T, const GaitR& g, const SC3& t
 // and its hip frame (KinFrames, the straight gaits' frames at tv = 0)
 // The chain's products come precombined from the loader (hs_topo::limb_own_rel, limb_hip_rel): one product
 // per frame, every load indexed by the limb alone
-// A limb's setup constants (hs_topo::limb_*), loaded before the gait parameters they do not depend on
-struct LimbPlan {
-  A34 hip, own0;  // limb_hip_rel, limb_own_rel[0] (limb_own_n > 0)
-  real ct[3], com0[3];
-  int own_n;
-};
-__device__ __attribute__((always_inline)) inline LimbPlan load_plan(const hs_topo* T, int L) {
-  LimbPlan p;
-  p.own_n = T->limb_own_n[L];
-  p.hip = load34(T->limb_hip_rel[L]);
-  p.own0 = load34(T->limb_own_rel[L][0]);
-  for (int i = 0; i < 3; i++) {
-    p.ct[i] = (real)T->limb_child_t[L][i];
-    p.com0[i] = (real)T->limb_own_com[L][0][i];
-  }
-  return p;
-}
 __device__ __attribute__((always_inline)) inline void limb_setup(const hs_topo* T, const GaitR& g, const A34& A0, int L,
-                                                                 const LimbPlan& pl, A34& J0, real* pos0,
-                                                                 KinFrames* kf = nullptr) {
+                                                                 A34& J0, real* pos0, KinFrames* kf = nullptr) {
   if (kf)
-    for (int m = 0; m < pl.own_n; m++) {
-      real com[3];
-      for (int i = 0; i < 3; i++) com[i] = m == 0 ? pl.com0[i] : (real)T->limb_own_com[L][m][i];
-      store_body(mul(A0, m == 0 ? pl.own0 : load34(T->limb_own_rel[L][m])), com, kf->own[L][m], BF_W);
+    for (int m = 0; m < T->limb_own_n[L]; m++) {
+      const real com[3] = {(real)T->limb_own_com[L][m][0], (real)T->limb_own_com[L][m][1], (real)T->limb_own_com[L][m][2]};
+      store_body(mul(A0, load34(T->limb_own_rel[L][m])), com, kf->own[L][m], BF_W);
     }
-  J0 = mul(A0, pl.hip);
+  J0 = mul(A0, load34(T->limb_hip_rel[L]));
   if (kf) store34r(J0, kf->J0[L]);
   // get_limb_hip_pos: the child's frame J0 Rz(0) pj_child (Rz(0) = I) at its translation
+  const real ct[3] = {(real)T->limb_child_t[L][0], (real)T->limb_child_t[L][1], (real)T->limb_child_t[L][2]};
   real pos[3];
-  mulp(J0, pl.ct, pos);
+  mulp(J0, ct, pos);
   if (g.foot_shift_type == 0) {                   // setup_foot_shift / shift_pos0
     real sh[3] = {real(0), g.foot_shift, real(0)}, ls[3];
     mulp(A0, sh, ls);
@@ -462,7 +444,7 @@ __device__ __attribute__((always_inline)) inline void gait_setup(const hs_topo* 
     if (L == 0) st.tsc = tsc;
     A34 J0;
     const int j = T->limb_pergen[L];
-    limb_setup(T, g, torso_frame(T, g, tsc), L, load_plan(T, L), J0, st.pos0[j]);
+    limb_setup(T, g, torso_frame(T, g, tsc), L, J0, st.pos0[j]);
     lift_off(nl, j, t_step, st.ts[j], st.xs[j]);
   }
   if (lane == 0) {
@@ -2909,10 +2891,6 @@ __host__ __device__ inline int64_t prep_blocks(int n_waves, int ttab_n, int nli)
   return 8 * ((groups_per_xcd + gpw - 1) / gpw);
 }
 
-// MIXED: a mixed-topology launch (launch_map::wave_model), whose groups of one wavefront may hold
-// different models; otherwise the topology pointer is the kernel argument itself, wave-uniform, so its
-// rollout-independent entries come through the scalar cache
-template <bool MIXED>
 __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
   __shared__ real rad[WAVE];
@@ -2932,7 +2910,7 @@ __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_t
   const hs_topo* __restrict__ T = T0;
   if (on) {
     b = mp.wave_rollouts ? mp.wave_rollouts[2 * w + sub] : 2 * w + sub;
-    if (MIXED) T = T0 + mp.wave_model[w];
+    if (mp.wave_model) T = T0 + mp.wave_model[w];
     on = b >= 0 && b < a.n_rollouts && L < T->n_limbs;
   }
   GaitR g;
@@ -2942,15 +2920,13 @@ __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_t
   real my_rad = 0;
   SC3 tsc;
   RolloutWS* __restrict__ ws = rws + b;
-  LimbPlan plan;
   if (on) {
-    plan = load_plan(T, L);  // issued before the gait parameters: its waits do not queue behind them
     g = load_gait(a.params[b]);
     straight = g.curvature == 0 && !g.rec_xf;  // kin_sample's turning / record-transform test
     const int nl = T->n_limbs, j = T->limb_pergen[L];
     tsc = sincos3(g.torso_angles[0], g.torso_angles[1], g.torso_angles[2]);
     const A34 A0 = torso_frame(T, g, tsc);
-    limb_setup(T, g, A0, L, plan, J0, pos0, chunk == 0 ? &ws->kf : nullptr);
+    limb_setup(T, g, A0, L, J0, pos0, chunk == 0 ? &ws->kf : nullptr);
     t_step = step_fraction(g, nl);
     lift_off(nl, j, t_step, ts, xs);
     v = g.step_length / g.period;  // pergensetup::set_TLh
@@ -3379,10 +3355,7 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   RolloutWS* ws = (RolloutWS*)workspace;
   if (mp.setup_only) {  // the call's preparation pass: setup record, sample times, IK table
     const int64_t blocks = prep_blocks(mp.n_waves, mp.ttab_n, mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX);
-    if (mp.wave_model)
-      hipLaunchKernelGGL(hs_prep_kernel<true>, dim3((unsigned)blocks), dim3(WAVE), 0, st, d_topo, a, ws, mp);
-    else
-      hipLaunchKernelGGL(hs_prep_kernel<false>, dim3((unsigned)blocks), dim3(WAVE), 0, st, d_topo, a, ws, mp);
+    hipLaunchKernelGGL(hs_prep_kernel, dim3((unsigned)blocks), dim3(WAVE), 0, st, d_topo, a, ws, mp);
     return (int)hipGetLastError();
   }
   launch_map m = mp;
