@@ -35,7 +35,7 @@ VARIANT_DIR = os.path.join(OUT_DIR, "variants")
 HEADERS = ["hs_topo.h", "hs_simtopo.h", "hs_ode.h", "hs_math.h", "hs_internal.h", os.path.join("..", "..", "include", "hslabs.h")]
 ARCH = os.environ.get("HSLABS_ARCH", "gfx950")
 CONTRACT = {"hs_sim.hip": "off", "hs_config.hip": "off"}  # per-source FMA contraction (default: fast)
-# per-source scheduler choice, measured (tools/gpu_sweep_libs.sh): the fp32 rollout kernel
+# per-source scheduler choice, measured in round 1 (interleaved A/B): the fp32 rollout kernel
 # (4 waves/SIMD, 128 VGPRs) gains 1.4 % with the iterative ILP scheduler; the fp64 rollout
 # kernel and the simulation are fastest with the default one
 SRC_FLAGS = {"hs_kernels_f32.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}

@@ -12,7 +12,7 @@ import os
 
 from . import build as _build
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 HS_OK = 0
 HS_FLAG_RANK_RETRY = 1
@@ -23,6 +23,7 @@ HS_FLAG_UNREACH = 16
 HS_FLAG_NO_CONTACT = 32
 HS_FLAG_GENERAL = 64
 HS_FLAG_NEAR_RANK = 256  # a rank / routing decision within rounding of its threshold (include/hslabs.h)
+HS_FLAG_DEPENDENT = 512  # solve_forces: a dependent force component dropped, the basic solution (include/hslabs.h)
 HS_PREC_F64 = 0
 HS_PREC_F32 = 1
 HS_SOLVE_AUTO = 0

@@ -43,6 +43,13 @@ void free_on_device(int dev, void* p) {
 
 }  // namespace
 
+// one rollout's workspace slot: either precision's RolloutWS (the fp32 build's general path computes
+// in double, so its slot is not simply half the fp64 one)
+static size_t ws_slot_bytes() {
+  const size_t a = hs::general_workspace_bytes(), b = hs::general_workspace_bytes_f32();
+  return a > b ? a : b;
+}
+
 int ws_pool::get(void* stream, size_t n, void** out) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -51,7 +58,7 @@ int ws_pool::get(void* stream, size_t n, void** out) {
     if (s.dev != dev || s.stream != stream) continue;
     if (s.n < n) {
       void* w = nullptr;
-      e = hipMalloc(&w, n * hs::general_workspace_bytes());  // fp64 slot >= fp32 slot
+      e = hipMalloc(&w, n * ws_slot_bytes());
       if (e != hipSuccess) return (int)e;
       retired.emplace_back(dev, s.ptr);
       s.ptr = w;
@@ -61,7 +68,7 @@ int ws_pool::get(void* stream, size_t n, void** out) {
     return 0;
   }
   void* w = nullptr;
-  e = hipMalloc(&w, n * hs::general_workspace_bytes());
+  e = hipMalloc(&w, n * ws_slot_bytes());
   if (e != hipSuccess) return (int)e;
   live.push_back({dev, stream, w, n});
   *out = w;
@@ -215,7 +222,7 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   const int32_t B = a.n_rollouts;
   const int32_t CHUNK = std::max(1, std::min(HS_FUSED_MAX_STEPS, HS_FUSED_WAVES / std::max(1, mp.n_waves)));
   const int32_t n_chunks = (int32_t)((S + CHUNK - 1) / CHUNK);
-  const size_t gwb = hs::general_workspace_bytes();
+  const size_t gwb = ws_slot_bytes();
   // steps the closed form declines (every step in HS_SOLVE_REFERENCE) are deferred to a fixup launch
   // after each step launch, so the step kernel carries no call to the general path; one counter per
   // launch (zeroed by the setup pass), then the items

@@ -113,14 +113,29 @@ struct WorkL {  // per-joint positive work of the step (outputs phase; FastL is 
 
 // Workspace of the general path (k x k matrices, leading dimension LD >= k).
 // SHARED: in LDS; otherwise (GenWS, the only instance) one global-memory slot per rollout.
+// The path computes in double in both builds (greal): in single precision FullPivLU's rank test
+// (pivots against eps * k) and ColPivQR's nonzero-pivot rule would decide on float rounding of the
+// Grams -- a third of the fp32 hexapod steps sat within the HS_FLAG_NEAR_RANK band (round 4) --
+// while the Grams of float inputs formed in double keep the exact rank structure (A^T A of a 6 x k A
+// has rank <= 6 to double rounding), so the decisions are the fp64 path's. Only the inputs (positions,
+// axes, the particular solution) are float there, and the forces are rounded to float once.
+using greal = double;
+// Eigen's epsilon / min and ftsolver.cpp:228-232's loop tolerance
+constexpr greal gEps = DBL_EPSILON;
+constexpr greal gTiny = DBL_MIN;
+constexpr greal gRelTol = 1e-6;
+// the conditioning test: the last pass's second-stage system with a kept ColPivQR pivot under gCondQR of
+// its first (condition above 1e7): rounding-level changes of the inputs move the answer by more than the
+// parity bound there (oracle NearTrack::ill)
+constexpr greal gCondQR = 1e-7;
 template <int LD_, bool SHARED_>
 struct GenMats {
   static constexpr int LD = LD_;
   static constexpr bool SHARED = SHARED_;
-  real ntn0[LD * LD], lu[LD * LD], Ny[LD * LD], qr[LD * LD];
-  real n1[LD / 3][9];  // 3x3 diagonal blocks of the first-order Gram (column-major)
-  real ntx0[LD], ntx1[LD], y0[LD], b[LD], z[LD], c[LD], hc[LD], nu[LD], nd[LD];
-  real u1[3][LD];  // torso rows of N in the first-order stage (switch_torso_penalty other than (1,1))
+  greal ntn0[LD * LD], lu[LD * LD], Ny[LD * LD], qr[LD * LD];
+  greal n1[LD / 3][9];  // 3x3 diagonal blocks of the first-order Gram (column-major)
+  greal ntx0[LD], ntx1[LD], y0[LD], b[LD], z[LD], c[LD], hc[LD], nu[LD], nd[LD];
+  greal u1[3][LD];  // torso rows of N in the first-order stage (switch_torso_penalty other than (1,1))
   int coupled;     // u1 is set: the first-order Gram couples the contacts
   int8_t rowsT[LD], colsT[LD], q[LD], piv[LD], rycol[LD], cperm[LD];
 };
@@ -231,21 +246,13 @@ __device__ inline void wave_sync() {
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
-// Precision-dependent constants (Eigen's epsilon / min, ftsolver.cpp:228-232's 1e-6 loop
-// tolerance, relaxed to 1e-4 in single precision).
-constexpr real kEps = HS_REAL_IS_FLOAT ? FLT_EPSILON : DBL_EPSILON;
-constexpr real kTiny = HS_REAL_IS_FLOAT ? FLT_MIN : DBL_MIN;
-constexpr real kRelTol = HS_REAL_IS_FLOAT ? real(1e-4) : real(1e-6);
 // HS_FLAG_NEAR_RANK bands (include/hslabs.h; oracle/hs_oracle.cpp NearTrack): a decision whose value lies
-// within kNearBand of its threshold (rel_error: within 10x of kRelTol; ColPivQR's squared column norms:
+// within kNearBand of its threshold (rel_error: within 10x of gRelTol; ColPivQR's squared column norms:
 // within kNearBand^2) is flagged, since another rounding may take it the other way
 constexpr real kNearBand = real(4);
-// the Eigen-style path's conditioning test: the last pass's second-stage system with a kept ColPivQR pivot
-// under kCondQR of its first (condition above 1e7 in fp64, 1e4 in fp32): rounding-level changes of the
-// inputs move the answer by more than the parity bound there (oracle NearTrack::ill)
-constexpr real kCondQR = HS_REAL_IS_FLOAT ? real(1e-4) : real(1e-7);
 // v is within `band` of threshold t (both positive; a NaN is not)
-__device__ inline bool near_thr(real v, real t, real band) { return v >= t / band && v <= t * band; }
+template <class T>
+__device__ inline bool near_thr(T v, T t, T band) { return v >= t / band && v <= t * band; }
 
 // The ABI's arrays are double*; in the fp32 build they hold floats.
 __device__ inline real* outp(double* p) { return reinterpret_cast<real*>(p); }
@@ -1083,11 +1090,12 @@ __device__ __attribute__((always_inline)) inline void particular_sub(const hs_to
 }
 
 // Tree-basis null-space entry for a torque row: (arm x e_jj)[row], arm = ref - fpos
-__device__ inline real cross_e(const real* d, int jj, int row) {
+template <class T>
+__device__ inline T cross_e(const T* d, int jj, int row) {
   // d x e0 = (0, d2, -d1); d x e1 = (-d2, 0, d0); d x e2 = (d1, -d0, 0)
-  if (jj == 0) return row == 0 ? real(0) : (row == 1 ? d[2] : -d[1]);
-  if (jj == 1) return row == 0 ? -d[2] : (row == 1 ? real(0) : d[0]);
-  return row == 0 ? d[1] : (row == 1 ? -d[0] : real(0));
+  if (jj == 0) return row == 0 ? T(0) : (row == 1 ? d[2] : -d[1]);
+  if (jj == 1) return row == 0 ? -d[2] : (row == 1 ? T(0) : d[0]);
+  return row == 0 ? d[1] : (row == 1 ? -d[0] : T(0));
 }
 
 // ===========================================================================
@@ -1115,12 +1123,12 @@ __device__ void build_grams(const hs_topo* T, const SV& sv, G& g, const W& w, in
     const real* fa = w.fpos(0, sv.cfoot[ci / 3]);
     const real* fb = w.fpos(0, sv.cfoot[cj / 3]);
     int ja = ci % 3, jb = cj % 3;
-    real da[3], db[3];
+    greal da[3], db[3];
     for (int r = 0; r < 3; r++) { da[r] = P0[r] - fa[r]; db[r] = P0[r] - fb[r]; }
-    real s = real(0);
+    greal s = greal(0);
     if (t_force0)
       for (int r = 0; r < 3; r++) {
-        real na = (r == ja) ? real(-1) : real(0), nb = (r == jb) ? real(-1) : real(0);
+        greal na = (r == ja) ? greal(-1) : greal(0), nb = (r == jb) ? greal(-1) : greal(0);
         s = s + na * nb;
       }
     if (t_torque0)
@@ -1130,17 +1138,17 @@ __device__ void build_grams(const hs_topo* T, const SV& sv, G& g, const W& w, in
   if (lane < k) {
     int ci = lane, ja = ci % 3;
     const real* fa = w.fpos(0, sv.cfoot[ci / 3]);
-    real da[3];
+    greal da[3];
     for (int r = 0; r < 3; r++) da[r] = P0[r] - fa[r];
-    real s = real(0);
+    greal s = greal(0);
     if (t_force0)
-      for (int r = 0; r < 3; r++) s = s + ((r == ja) ? real(-1) : real(0)) * (real(1) * sv.x[r]);
+      for (int r = 0; r < 3; r++) s = s + ((r == ja) ? greal(-1) : greal(0)) * (greal(1) * sv.x[r]);
     if (t_torque0)
-      for (int r = 0; r < 3; r++) s = s + cross_e(da, ja, r) * (real(1) * sv.x[3 * n + r]);
+      for (int r = 0; r < 3; r++) s = s + cross_e(da, ja, r) * (greal(1) * sv.x[3 * n + r]);
     g.ntx0[ci] = s;
     // the first-order torso rows (one group at most: mask0 is never empty), for the coupling terms
     for (int r = 0; r < 3; r++)
-      g.u1[r][ci] = !t_force0 ? ((r == ja) ? real(-1) : real(0)) : (!t_torque0 ? cross_e(da, ja, r) : real(0));
+      g.u1[r][ci] = !t_force0 ? ((r == ja) ? greal(-1) : greal(0)) : (!t_torque0 ? cross_e(da, ja, r) : greal(0));
   }
   if (lane == 0) g.coupled = tm != 3;
   // first order: torque rows of the non-root ancestors of each contact foot,
@@ -1156,19 +1164,19 @@ __device__ void build_grams(const hs_topo* T, const SV& sv, G& g, const W& w, in
     // ancestors of foot below the root, in ascending part order (top of the chain first)
     int chain[HS_NMAX], len = 0;
     for (int a = foot; a >= 0 && T->node[a].parent >= 0; a = T->node[a].parent) chain[len++] = a;
-    real s = real(0);
+    greal s = greal(0);
     if (!t_force0)  // torso force rows 0..2: N = -I per contact, x1 = x
       for (int r = 0; r < 3; r++) {
-        real na = (r == a_col) ? real(-1) : real(0);
-        real nb = is_vec ? real(1) * sv.x[r] : ((r == b_col) ? real(-1) : real(0));
+        greal na = (r == a_col) ? greal(-1) : greal(0);
+        greal nb = is_vec ? greal(1) * sv.x[r] : ((r == b_col) ? greal(-1) : greal(0));
         s = s + na * nb;
       }
     if (!t_torque0) {  // torso torque rows 3n..3n+2: N = [pos_0 - fpos]x
-      real d0[3];
+      greal d0[3];
       for (int r = 0; r < 3; r++) d0[r] = P0[r] - fp[r];
       for (int r = 0; r < 3; r++) {
-        real na = cross_e(d0, a_col, r);
-        real nb = is_vec ? real(1) * sv.x[3 * n + r] : cross_e(d0, b_col, r);
+        greal na = cross_e(d0, a_col, r);
+        greal nb = is_vec ? greal(1) * sv.x[3 * n + r] : cross_e(d0, b_col, r);
         s = s + na * nb;
       }
     }
@@ -1176,12 +1184,12 @@ __device__ void build_grams(const hs_topo* T, const SV& sv, G& g, const W& w, in
       int a = chain[t];
       const real* Ja = w.jpos(0, a);
       const real* Za = w.jz(0, a);
-      real d[3];
+      greal d[3];
       for (int r = 0; r < 3; r++) d[r] = Ja[r] - fp[r];
       for (int r = 0; r < 3; r++) {
-        real wz = Za[r];
-        real na = wz * cross_e(d, a_col, r);
-        real nb = is_vec ? wz * sv.x[3 * n + 3 * a + r] : wz * cross_e(d, b_col, r);
+        greal wz = Za[r];
+        greal na = wz * cross_e(d, a_col, r);
+        greal nb = is_vec ? wz * sv.x[3 * n + 3 * a + r] : wz * cross_e(d, b_col, r);
         s = s + na * nb;
       }
     }
@@ -1193,23 +1201,23 @@ __device__ void build_grams(const hs_topo* T, const SV& sv, G& g, const W& w, in
 
 // first-order Gram entry (block diagonal)
 template <class G>
-__device__ inline real ntn1_at(const G& g, int i, int j) {
-  return (i / 3 == j / 3) ? g.n1[i / 3][(j % 3) * 3 + (i % 3)] : real(0);
+__device__ inline greal ntn1_at(const G& g, int i, int j) {
+  return (i / 3 == j / 3) ? g.n1[i / 3][(j % 3) * 3 + (i % 3)] : greal(0);
 }
 // with torso rows in the first order (g.coupled): the off-block entries are their products, summed
 // in row order (the blocks already start with them)
 template <class G>
-__device__ inline real ntn1_full(const G& g, int i, int j) {
+__device__ inline greal ntn1_full(const G& g, int i, int j) {
   if (i / 3 == j / 3) return g.n1[i / 3][(j % 3) * 3 + (i % 3)];
-  real s = real(0);
+  greal s = greal(0);
   for (int r = 0; r < 3; r++) s = s + g.u1[r][i] * g.u1[r][j];
   return s;
 }
 
 // half-wave argmax with first-index tie break
-__device__ inline void wave_argmax(real& v, int& idx) {
+__device__ inline void wave_argmax(greal& v, int& idx) {
   for (int off = HALF / 2; off >= 1; off >>= 1) {
-    real ov = __shfl_xor(v, off);
+    greal ov = __shfl_xor(v, off);
     int oi = __shfl_xor(idx, off);
     if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
   }
@@ -1217,7 +1225,7 @@ __device__ inline void wave_argmax(real& v, int& idx) {
 
 struct LUInfo {
   int nz;          // nonzero pivots
-  real maxpivot;
+  greal maxpivot;
 };
 
 // Eigen FullPivLU::computeInPlace of ntn0 into g.lu (k x k)
@@ -1229,13 +1237,13 @@ __device__ LUInfo fullpiv_lu(G& g, int k, int lane) {
     g.lu[i + j * LD] = g.ntn0[i + j * LD];
   }
   gsync<G>();
-  LUInfo info{k, real(0)};
+  LUInfo info{k, greal(0)};
   for (int p = 0; p < k; p++) {
     const int m = k - p;
-    real best = real(-1);
+    greal best = greal(-1);
     int bidx = 1 << 30;
     for (int e = lane; e < m * m; e += HALF) {
-      real a = fabs(g.lu[(p + e % m) + (p + e / m) * LD]);
+      greal a = fabs(g.lu[(p + e % m) + (p + e / m) * LD]);
       if (a > best || (a == best && e < bidx)) { best = a; bidx = e; }
     }
     wave_argmax(best, bidx);
@@ -1248,19 +1256,19 @@ __device__ LUInfo fullpiv_lu(G& g, int k, int lane) {
     const int bi = p + bidx % m, bj = p + bidx / m;
     if (lane == 0) { g.rowsT[p] = bi; g.colsT[p] = bj; }
     if (bi != p && lane < k) {
-      real t = g.lu[p + lane * LD];
+      greal t = g.lu[p + lane * LD];
       g.lu[p + lane * LD] = g.lu[bi + lane * LD];
       g.lu[bi + lane * LD] = t;
     }
     gsync<G>();
     if (bj != p && lane < k) {
-      real t = g.lu[lane + p * LD];
+      greal t = g.lu[lane + p * LD];
       g.lu[lane + p * LD] = g.lu[lane + bj * LD];
       g.lu[lane + bj * LD] = t;
     }
     gsync<G>();
     if (p < k - 1) {
-      real piv = g.lu[p + p * LD];
+      greal piv = g.lu[p + p * LD];
       if (lane > p && lane < k) g.lu[lane + p * LD] /= piv;
       gsync<G>();
       const int mm = k - p - 1;
@@ -1281,18 +1289,18 @@ __device__ LUInfo fullpiv_lu(G& g, int k, int lane) {
 
 // any nonzero pivot within kNearBand of the rank threshold maxpivot * thr (the decisions lu_rank takes)
 template <class G>
-__device__ inline bool lu_near(const G& g, const LUInfo& info, real thr) {
+__device__ inline bool lu_near(const G& g, const LUInfo& info, greal thr) {
   constexpr int LD = G::LD;
-  const real pt = fabs(info.maxpivot) * thr;
+  const greal pt = fabs(info.maxpivot) * thr;
   bool nr = false;
-  for (int i = 0; i < info.nz; i++) nr |= near_thr(fabs(g.lu[i + i * LD]), pt, kNearBand);
+  for (int i = 0; i < info.nz; i++) nr |= near_thr(fabs(g.lu[i + i * LD]), pt, greal(kNearBand));
   return nr;
 }
 
 template <class G>
-__device__ inline int lu_rank(const G& g, const LUInfo& info, real thr) {
+__device__ inline int lu_rank(const G& g, const LUInfo& info, greal thr) {
   constexpr int LD = G::LD;
-  real pt = fabs(info.maxpivot) * thr;
+  greal pt = fabs(info.maxpivot) * thr;
   int r = 0;
   for (int i = 0; i < info.nz; i++) r += fabs(g.lu[i + i * LD]) > pt;
   return r;
@@ -1300,12 +1308,12 @@ __device__ inline int lu_rank(const G& g, const LUInfo& info, real thr) {
 
 // column-oriented upper-triangular solve of vec[0..r) against U (ld LD), all lanes
 template <class G>
-__device__ void upper_solve_shared(const real* U, real* vec, int r, int lane) {
+__device__ void upper_solve_shared(const greal* U, greal* vec, int r, int lane) {
   constexpr int LD = G::LD;
   for (int i = r - 1; i >= 0; i--) {
-    real ci = vec[i];
+    greal ci = vec[i];
     if (ci != 0) {
-      real xi = ci / U[i + i * LD];
+      greal xi = ci / U[i + i * LD];
       if (lane < i) vec[lane] -= xi * U[lane + i * LD];
       if (lane == i) vec[i] = xi;
     }
@@ -1319,13 +1327,13 @@ __device__ void lu_solve(G& g, const LUInfo& info, int k, int r, int lane) {
   constexpr int LD = G::LD;
   if (lane == 0) {
     for (int i = 0; i < k; i++) g.c[i] = -g.ntx0[i];
-    for (int p = 0; p < k; p++) { real t = g.c[p]; g.c[p] = g.c[g.rowsT[p]]; g.c[g.rowsT[p]] = t; }
+    for (int p = 0; p < k; p++) { greal t = g.c[p]; g.c[p] = g.c[g.rowsT[p]]; g.c[g.rowsT[p]] = t; }
   }
-  if (lane < k) g.y0[lane] = real(0);
+  if (lane < k) g.y0[lane] = greal(0);
   gsync<G>();
   if (r == 0) return;
   for (int j = 0; j < k; j++) {  // unit lower
-    real cj = g.c[j];
+    greal cj = g.c[j];
     if (lane > j && lane < k) g.c[lane] -= cj * g.lu[lane + j * LD];
     gsync<G>();
   }
@@ -1336,10 +1344,10 @@ __device__ void lu_solve(G& g, const LUInfo& info, int k, int r, int lane) {
 
 // FullPivLU::kernel() -> g.Ny (k x dimker); uses g.qr as scratch; g.piv/rycol set
 template <class G>
-__device__ void lu_kernel_image(G& g, const LUInfo& info, int k, int r, real thr, int lane) {
+__device__ void lu_kernel_image(G& g, const LUInfo& info, int k, int r, greal thr, int lane) {
   constexpr int LD = G::LD;
   if (lane == 0) {
-    real pt = info.maxpivot * thr;
+    greal pt = info.maxpivot * thr;
     int p = 0;
     for (int i = 0; i < info.nz; i++)
       if (fabs(g.lu[i + i * LD]) > pt) g.piv[p++] = i;
@@ -1348,21 +1356,21 @@ __device__ void lu_kernel_image(G& g, const LUInfo& info, int k, int r, real thr
   gsync<G>();
   const int dimker = k - r;
   if (dimker == 0) return;
-  real* mm = g.qr;  // r x k trapezoid
+  greal* mm = g.qr;  // r x k trapezoid
   for (int e = lane; e < r * k; e += HALF) {
     int i = e % r, j = e / r;
-    mm[i + j * LD] = (j >= i) ? g.lu[g.piv[i] + j * LD] : real(0);
+    mm[i + j * LD] = (j >= i) ? g.lu[g.piv[i] + j * LD] : greal(0);
   }
   gsync<G>();
   if (lane < r) {  // bring non-negligible pivots to the front (rows own a column swap each)
     for (int i = 0; i < r; i++) {
       int pc = g.piv[i];
-      if (pc != i) { real t = mm[lane + i * LD]; mm[lane + i * LD] = mm[lane + pc * LD]; mm[lane + pc * LD] = t; }
+      if (pc != i) { greal t = mm[lane + i * LD]; mm[lane + i * LD] = mm[lane + pc * LD]; mm[lane + pc * LD] = t; }
     }
   }
   gsync<G>();
   if (lane < dimker) {  // solve U11 X = U12, one right-hand column per lane
-    real* col = &mm[(r + lane) * LD];
+    greal* col = &mm[(r + lane) * LD];
     for (int i = r - 1; i >= 0; i--) {
       if (col[i] != 0) {
         col[i] /= mm[i + i * LD];
@@ -1374,16 +1382,16 @@ __device__ void lu_kernel_image(G& g, const LUInfo& info, int k, int r, real thr
   if (lane < r) {
     for (int i = r - 1; i >= 0; i--) {
       int pc = g.piv[i];
-      if (pc != i) { real t = mm[lane + i * LD]; mm[lane + i * LD] = mm[lane + pc * LD]; mm[lane + pc * LD] = t; }
+      if (pc != i) { greal t = mm[lane + i * LD]; mm[lane + i * LD] = mm[lane + pc * LD]; mm[lane + pc * LD] = t; }
     }
   }
   gsync<G>();
   for (int e = lane; e < k * dimker; e += HALF) {
     int i = e % k, kk = e / k;
     int row = g.q[i];
-    real v;
+    greal v;
     if (i < r) v = -mm[i + (r + kk) * LD];
-    else v = (i == r + kk) ? real(1) : real(0);
+    else v = (i == r + kk) ? greal(1) : greal(0);
     g.Ny[row + kk * LD] = v;
   }
   gsync<G>();
@@ -1391,9 +1399,9 @@ __device__ void lu_kernel_image(G& g, const LUInfo& info, int k, int r, real thr
 
 // entry (i, j) of m = [ntn1 Ny, ntn0 Ry] (ftsolver.cpp:222-226), evaluated where needed
 template <class G>
-__device__ inline real m_at(const G& g, int k, int dimker, int i, int j) {
+__device__ inline greal m_at(const G& g, int k, int dimker, int i, int j) {
   constexpr int LD = G::LD;
-  real s = real(0);
+  greal s = greal(0);
   if (j < dimker) {
     if (g.coupled) {
       for (int kk = 0; kk < k; kk++) s = s + ntn1_full(g, i, kk) * g.Ny[kk + j * LD];
@@ -1414,53 +1422,53 @@ template <class G>
 __device__ int colpiv_qr(G& g, int k, int lane, bool& near) {
   constexpr int LD = G::LD;
   if (lane < k) {
-    real s = 0;
+    greal s = 0;
     for (int i = 0; i < k; i++) s += g.qr[i + lane * LD] * g.qr[i + lane * LD];
     g.nd[lane] = sqrt(s);
     g.nu[lane] = g.nd[lane];
   }
   gsync<G>();
-  real mx = 0;
+  greal mx = 0;
   for (int j = 0; j < k; j++) mx = fmax(mx, g.nu[j]);
-  const real th = mx * kEps;
-  const real threshold_helper = th * th / (real)k;
-  const real ndt = sqrt(kEps);
+  const greal th = mx * gEps;
+  const greal threshold_helper = th * th / (greal)k;
+  const greal ndt = sqrt(gEps);
   int np = k;
   for (int p = 0; p < k; p++) {
     int bi = p;
-    real bv = g.nu[p];
+    greal bv = g.nu[p];
     for (int j = p + 1; j < k; j++)
       if (g.nu[j] > bv) { bv = g.nu[j]; bi = j; }
-    if (np == k) near |= near_thr(bv * bv, threshold_helper * (real)(k - p), kNearBand * kNearBand);
-    if (np == k && bv * bv < threshold_helper * (real)(k - p)) np = p;
+    if (np == k) near |= near_thr(bv * bv, threshold_helper * (greal)(k - p), greal(kNearBand) * greal(kNearBand));
+    if (np == k && bv * bv < threshold_helper * (greal)(k - p)) np = p;
     gsync<G>();
     if (lane == 0) g.cperm[p] = bi;
     if (bi != p) {
       if (lane < k) {
-        real t = g.qr[lane + p * LD];
+        greal t = g.qr[lane + p * LD];
         g.qr[lane + p * LD] = g.qr[lane + bi * LD];
         g.qr[lane + bi * LD] = t;
       }
       if (lane == 0) {
-        real t = g.nu[p]; g.nu[p] = g.nu[bi]; g.nu[bi] = t;
+        greal t = g.nu[p]; g.nu[p] = g.nu[bi]; g.nu[bi] = t;
         t = g.nd[p]; g.nd[p] = g.nd[bi]; g.nd[bi] = t;
       }
     }
     gsync<G>();
     // makeHouseholderInPlace on column p, rows p..k-1
     const int len = k - p;
-    real c0 = g.qr[p + p * LD];
-    real tail = 0;
+    greal c0 = g.qr[p + p * LD];
+    greal tail = 0;
     for (int i = 1; i < len; i++) tail += g.qr[p + i + p * LD] * g.qr[p + i + p * LD];
-    real tau, beta;
-    if (len == 1 || tail <= kTiny) {
+    greal tau, beta;
+    if (len == 1 || tail <= gTiny) {
       tau = 0;
       beta = c0;
       if (lane >= 1 && lane < len) g.qr[p + lane + p * LD] = 0;
     } else {
       beta = sqrt(c0 * c0 + tail);
       if (c0 >= 0) beta = -beta;
-      real den = c0 - beta;
+      greal den = c0 - beta;
       if (lane >= 1 && lane < len) g.qr[p + lane + p * LD] /= den;
       tau = (beta - c0) / beta;
     }
@@ -1472,20 +1480,20 @@ __device__ int colpiv_qr(G& g, int k, int lane, bool& near) {
       if (len == 1) {
         g.qr[p + j * LD] *= (1 - tau);
       } else if (tau != 0) {
-        real tmp = 0;
+        greal tmp = 0;
         for (int i = 1; i < len; i++) tmp += g.qr[p + i + p * LD] * g.qr[p + i + j * LD];
         tmp += g.qr[p + j * LD];
         g.qr[p + j * LD] -= tau * tmp;
         for (int i = 1; i < len; i++) g.qr[p + i + j * LD] -= tau * g.qr[p + i + p * LD] * tmp;
       }
       if (g.nu[j] != 0) {
-        real temp = fabs(g.qr[p + j * LD]) / g.nu[j];
+        greal temp = fabs(g.qr[p + j * LD]) / g.nu[j];
         temp = (1 + temp) * (1 - temp);
         temp = temp < 0 ? 0 : temp;
-        real ratio = g.nu[j] / g.nd[j];
-        real temp2 = temp * (ratio * ratio);
+        greal ratio = g.nu[j] / g.nd[j];
+        greal temp2 = temp * (ratio * ratio);
         if (temp2 <= ndt) {
-          real s = 0;
+          greal s = 0;
           for (int i = p + 1; i < k; i++) s += g.qr[i + j * LD] * g.qr[i + j * LD];
           g.nd[j] = sqrt(s);
           g.nu[j] = g.nd[j];
@@ -1503,16 +1511,16 @@ __device__ int colpiv_qr(G& g, int k, int lane, bool& near) {
 template <class G>
 __device__ void qr_solve(G& g, int k, int np, int lane) {
   constexpr int LD = G::LD;
-  if (lane < k) { g.c[lane] = g.b[lane]; g.z[lane] = real(0); }
+  if (lane < k) { g.c[lane] = g.b[lane]; g.z[lane] = greal(0); }
   gsync<G>();
   if (np == 0) return;
   for (int p = 0; p < np; p++) {
     const int len = k - p;
-    const real tau = g.hc[p];
+    const greal tau = g.hc[p];
     if (len == 1) {
       if (lane == p) g.c[p] *= (1 - tau);
     } else if (tau != 0) {
-      real tmp = 0;
+      greal tmp = 0;
       for (int i = 1; i < len; i++) tmp += g.qr[p + i + p * LD] * g.c[p + i];
       tmp += g.c[p];
       gsync<G>();
@@ -1543,11 +1551,11 @@ __device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
   STAMP(10);
   int rank0 = k;
   int iters = 0;
-  real rel_error = 0;
-  bool ill = false;  // the last pass's second stage ill-conditioned (kCondQR)
+  greal rel_error = 0;
+  bool ill = false;  // the last pass's second stage ill-conditioned (gCondQR)
   do {
     iters++;
-    real thr = kEps * (real)k;
+    greal thr = gEps * (greal)k;
     int r = lu_rank(g, info, thr);
     for (int guard = 0; guard < 2100 && r > rank0; guard++) {  // setThreshold doubling
       thr = 2 * thr;
@@ -1564,7 +1572,7 @@ __device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
     // b = -(ntx1 + ntn1 y0)
     if (lane < k) {
       int i = lane, b0 = (i / 3) * 3;
-      real t = real(0);
+      greal t = greal(0);
       if (g.coupled)
         for (int kk = 0; kk < k; kk++) t = t + ntn1_full(g, i, kk) * g.y0[kk];
       else
@@ -1581,33 +1589,33 @@ __device__ uint32_t contact_solve(SV& sv, G& g, int k, int lane) {
     int np = colpiv_qr(g, k, lane, qr_near);
     if (qr_near) flags |= HS_FLAG_NEAR_RANK;
     {  // the smallest kept pivot of this pass (the last pass's decides)
-      real rmin = real(INFINITY);
+      greal rmin = greal(INFINITY);
       for (int i = 0; i < np; i++) rmin = fmin(rmin, fabs(g.qr[i + i * LD]));
-      ill = np > 0 && rmin < kCondQR * fabs(g.qr[0]);
+      ill = np > 0 && rmin < gCondQR * fabs(g.qr[0]);
     }
     STAMP(13);
     qr_solve(g, k, np, lane);
     STAMP(14);
     // rel_error = |m z - b| / |b|
     if (lane < k) {
-      real s = real(0);
+      greal s = greal(0);
       for (int j = 0; j < k; j++) s = s + m_at(g, k, dimker, lane, j) * g.z[j];
       g.c[lane] = s - g.b[lane];
     }
     gsync<G>();
-    real rn = 0, bn = 0;
+    greal rn = 0, bn = 0;
     for (int i = 0; i < k; i++) { rn += g.c[i] * g.c[i]; bn += g.b[i] * g.b[i]; }
     rel_error = sqrt(rn) / sqrt(bn);
-    if (near_thr(rel_error, kRelTol, real(10))) flags |= HS_FLAG_NEAR_RANK;
+    if (near_thr(rel_error, gRelTol, greal(10))) flags |= HS_FLAG_NEAR_RANK;
     rank0--;
     if (lane < k) {
-      real s = real(0);
+      greal s = greal(0);
       for (int j = 0; j < dimker; j++) s = s + g.Ny[lane + j * LD] * g.z[j];
       sv.y[lane] = g.y0[lane] + s;
     }
     gsync<G>();
-    if (rel_error > kRelTol && rank0 <= 0) { flags |= HS_FLAG_LOOP_EXHAUST; break; }
-  } while (rel_error > kRelTol && iters <= HS_KMAX + 1);
+    if (rel_error > gRelTol && rank0 <= 0) { flags |= HS_FLAG_LOOP_EXHAUST; break; }
+  } while (rel_error > gRelTol && iters <= HS_KMAX + 1);
   if (iters > 1) flags |= HS_FLAG_RANK_RETRY;
   if (ill) flags |= HS_FLAG_NEAR_RANK;
   return flags;
@@ -1690,14 +1698,6 @@ __device__ inline real quad_sum(real v) {
   v += dpp_r<0xB1>(v);
   v += dpp_r<0x4E>(v);
   return v;
-}
-// sum over the 32 lanes of this rollout: the quad's, the 8-lane half-row's (row_half_mirror), the
-// row's (row_mirror), then the other row of the half-wave (one permute); every lane gets the same value
-__device__ inline real half_sum(real v) {
-  v = quad_sum(v);
-  v += dpp_r<0x141>(v);
-  v += dpp_r<0x140>(v);
-  return v + __shfl_xor(v, 16);
 }
 
 // bit 0: well posed (take the closed form); bit 1: the ratio lies within kNearBand of the guard
@@ -2305,6 +2305,14 @@ __device__ __attribute__((always_inline)) inline bool fast_solve(const hs_topo* 
   return ok;
 }
 
+// work_over_period's accumulation (periodic.cpp:301-302): work_dt *= dt_traj; work_period += work_dt --
+// two roundings, as the reference's x86-64 build performs them (this file is otherwise contracted)
+__device__ inline real work_add(real work, real work_dt, real dt) {
+#pragma clang fp contract(off)
+  const real wdt = work_dt * dt;
+  return work + wdt;
+}
+
 // selection COT of the best-rollout key (hs_best_key_cot, include/hslabs.h): one cycle's work over
 // sum m * |L|; |L| under HS_KEY_MIN_STEP_LENGTH gives NaN (never selected)
 __device__ inline real key_cot(real work, real mass, real L, int n_t, int steps) {
@@ -2340,7 +2348,7 @@ __device__ inline void reduce_rollouts(const hs_run_args& a, real total_mass, co
     for (int j = 0; j < 32; j++) v[j] = s + j < n_steps ? ws[(size_t)(s + j) * a.n_rollouts + b] : real(0);
 #pragma unroll
     for (int j = 0; j < 32; j++)
-      if (s + j < n_steps) w = fma(v[j], dt, w);
+      if (s + j < n_steps) w = work_add(w, v[j], dt);
   }
   const real L = (real)a.params[b].step_length;
   const real cot = w / (total_mass * L);
@@ -2409,7 +2417,8 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   // S4: x = x_part + N y for the hinge torque rows, motor torques (periodic.cpp:328-343),
   // and the step's positive work (compute_vel_traj + work_over_period, periodic.cpp:261-307)
   const size_t row = (size_t)b * a.horizon + h;
-  real tq = real(0), wdl = real(0);
+  real tq = real(0);
+  real* const wd = reinterpret_cast<WorkL&>(fl).wd;  // FastL is dead once y is known
   if (lane < nmj) {
     const int h_id = hinge_id, fi = hinge_foot;
     // contact index of foot fi: its rank among the feet down (the contact list's order)
@@ -2441,7 +2450,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
     else if (dd < -kPi) dd += 2 * kPi;
     real jvel = dd / (2 * dt);
     real dw = tq * jvel;
-    wdl = (dw > 0) ? dw : 0;
+    wd[lane] = (dw > 0) ? dw : 0;
     if (mp.pd_tau && live) {  // linear_feedback_control (player.cpp:417-432), target = get_motor_adas
       const size_t o = row * mp.st_tau + lane;
       const real q0 = w.q(0)[6 + lane];
@@ -2502,11 +2511,15 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
     outp(a.dq)[row * mp.st_q + lane] = v;
   }
   if (live && a.flags && lane == 0) a.flags[row] = flags;
-  const real work_dt = half_sum(wdl);  // the joints' positive work (work_over_period's sum)
-  // work_over_period: work += work_dt * dt, one rounding (explicit, so the fused path's in-order
-  // sum performs the same operation); fused steps hand back the joint sum itself
+  // the joints' positive work summed in joint order, as work_over_period's loop does (periodic.cpp:
+  // 294-300; a DPP tree sum rounds differently, which can reorder near-tied rollouts' COTs)
+  wave_sync();
+  real work_dt = real(0);
+  for (int jj = 0; jj < nmj; jj++) work_dt += wd[jj];
+  // work_over_period: work_dt *= dt; work += work_dt (two roundings, periodic.cpp:301-302); fused steps
+  // hand back the joint sum itself and the reduce performs the same two operations in step order
   if (mp.fused_w) work = work_dt;
-  else work = fma(work_dt, dt, work);
+  else work = work_add(work, work_dt, dt);
   STAMP(8);
   RSTAMP(17);
 }
@@ -2789,7 +2802,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
   wave_sync();
   bool rank_near = false;  // a rank decision within kNearBand of the guard (HS_FLAG_NEAR_RANK)
   const uint32_t dropped = chol_packed(N, nq, kFastPivotGuard, lane, rank_near);
-  if (dropped) flags = HS_FLAG_GENERAL;  // least squares not unique: its basic solution
+  if (dropped) flags = HS_FLAG_GENERAL | HS_FLAG_DEPENDENT;  // least squares not unique: its basic solution
   if (rank_near) flags |= HS_FLAG_NEAR_RANK;
   STAMP(8);
   if (lane == 0) {  // the two triangular solves with y in registers (nq <= HS_KMAX)
@@ -3168,16 +3181,25 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
       reinterpret_cast<real*>(mp.fused_work)[(size_t)(mp.fused_s0 + fstep) * a.n_rollouts + b] = work;
     return;
   }
-  if (lane == 0 && live) {
+  const bool out = lane == 0 && live;
+  if (out && a.work_cot) {
     real cot = work / ((real)T->total_mass * g.step_length);
-    if (a.work_cot) {
-      outp(a.work_cot)[2 * (size_t)b] = work;
-      outp(a.work_cot)[2 * (size_t)b + 1] = cot;
+    outp(a.work_cot)[2 * (size_t)b] = work;
+    outp(a.work_cot)[2 * (size_t)b + 1] = cot;
+  }
+  if (a.best_key) {
+    unsigned long long key = ~0ull;
+    if (out) key = best_key(key_cot(work, (real)T->total_mass, g.step_length, a.n_t, a.key_steps), a.rollout_id_base + b);
+    if constexpr (!DEFER) {  // both rollouts of the wave are here: their minimum first
+      const unsigned long long o = __shfl_xor(key, HALF);
+      key = o < key ? o : key;
     }
-    if (a.best_key) {
-      const real kc = key_cot(work, (real)T->total_mass, g.step_length, a.n_t, a.key_steps);
-      atomicMin((unsigned long long*)a.best_key, (unsigned long long)best_key(kc, a.rollout_id_base + b));
-    }
+    // The key only decreases, so any value read from it bounds the final minimum from above: a key not
+    // below it cannot win, and skipping its atomic keeps the last launch from queueing one atomic per
+    // wave on a single address (~20 us per call at B = 4096)
+    if ((DEFER ? lane : (int)threadIdx.x) == 0 && key != ~0ull &&
+        key < __hip_atomic_load((unsigned long long*)a.best_key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMin((unsigned long long*)a.best_key, key);
   }
 }
 

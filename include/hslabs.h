@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 13
+#define HSLABS_ABI_VERSION 14
 
 enum {
   HS_OK = 0,
@@ -50,11 +50,20 @@ enum {
                                     nonzero-pivot threshold, the closed form's collinearity guard or
                                     pivot guards within 4x of theirs; the Eigen-style path's second
                                     stage ill-conditioned (a kept ColPivQR pivot under 1e-7 of the first,
-                                    1e-4 in fp32: rounding-level input changes move its answer beyond
                                     the parity bound); solve_forces: a normal-matrix pivot within 4x of
                                     its rank guard (ftsolver.cpp:349-353). The
                                     step's outputs are the path's answer; equality with another
-                                    implementation is only expected where neither side sets this. */
+                                    implementation is only expected where neither side sets this, or
+                                    where the answer does not depend on the decision. */
+#define HS_FLAG_DEPENDENT  512u  /* solve_forces only (hs_run_forces*), with HS_FLAG_GENERAL: the least
+                                    squares is numerically rank deficient under the kernel's guard (a
+                                    reduced normal-matrix pivot under 1e-10 of its largest diagonal) and
+                                    the dropped force components are 0 -- the basic solution, one point
+                                    of a non-unique solution set. The reference's SparseQR
+                                    (ftsolver.cpp:349-353) drops a column only under
+                                    20 (rows + cols) eps max |column| (~1e-12 relative, its COLAMD
+                                    order), so on such steps it may keep the column and return the
+                                    ill-conditioned full solution: parity is not claimed here. */
 
 /* Gait setup of one rollout: the fields of pgsconfigparams (pergen.h:137-146),
  * same meaning and units as a pgs_config.txt line (player.cpp:170-208), plus

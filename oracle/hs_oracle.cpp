@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <limits>
 #include <map>
 #include <sstream>
 #include <string>
@@ -1813,7 +1814,15 @@ bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<d
 // quantity) is dependent: it is dropped and its force component set to 0, the basic
 // solution of the rank-deficient least squares (a straight leg's torques cannot fix its
 // foot force along the leg). Returns false when a column was dropped.
-bool solve_forces(const hso_model* m, const DynRec& d, const double* z, std::vector<double>& y) {
+// rule HSO_FORCES_SPARSEQR instead restates SparseQR's own rank rule (Eigen 3.3 SparseQR::factorize,
+// the solver ftsolver.cpp:349-353 calls, default threshold): every column of the literal system, the
+// zeroed torso columns included, is kept iff its Householder |beta| (its norm on the rows not yet
+// eliminated) is at least 20 (rows + cols) eps max_j |A_j|; a dropped column's unknown is 0
+// (_solve_impl's basic solution). The column order stays natural: the COLAMD pre-ordering
+// (COLAMDOrdering<int>, ftsolver.h:17) is not restated, so which of several dependent columns
+// SparseQR drops is not pinned. On full-rank systems both rules give the least-squares solution.
+bool solve_forces(const hso_model* m, const DynRec& d, const double* z, std::vector<double>& y,
+                  int rule = HSO_FORCES_KERNEL) {
   const int n = m->n, nf = m->nf, nmj = m->nmj;
   Mat B0;
   std::vector<double> f;
@@ -1852,6 +1861,53 @@ bool solve_forces(const hso_model* m, const DynRec& d, const double* z, std::vec
     b[6 * n + jj] = z[jj];
   }
   const double kRankGuard = 1e-10;  // the kernel's kFastPivotGuard on the reduced normal matrix
+  if (rule == HSO_FORCES_SPARSEQR) {
+    // the literal matrix: the torso force / torque columns present and zero (ftsolver.cpp:349)
+    const int cf = 6 * n + 3 * nf;
+    Mat F(rows, cf);
+    for (int j = 0; j < (int)keep.size(); j++)
+      for (int i = 0; i < rows; i++) F(i, keep[j]) = A(i, j);
+    for (int j = y0; j < cols; j++)
+      for (int i = 0; i < rows; i++) F(i, 6 * n + (j - y0)) = A(i, j);
+    double mx = 0;
+    for (int j = 0; j < cf; j++) {
+      double s2 = 0;
+      for (int i = 0; i < rows; i++) s2 += F(i, j) * F(i, j);
+      mx = std::max(mx, std::sqrt(s2));
+    }
+    if (mx == 0) mx = 1;
+    const double thr = 20.0 * (rows + cf) * mx * std::numeric_limits<double>::epsilon();
+    Mat bq(rows, 1);
+    for (int i = 0; i < rows; i++) bq(i, 0) = b[i];
+    std::vector<int> kept;
+    bool fullq = true;
+    std::vector<double> essq;
+    for (int j = 0; j < cf; j++) {
+      const int k = (int)kept.size();
+      if (k >= std::min(rows, cf)) { fullq = false; continue; }
+      double s2 = 0;  // |beta|^2: the column's norm on rows k.. (c0^2 + sqrNorm)
+      for (int i = k; i < rows; i++) s2 += F(i, j) * F(i, j);
+      if (!(std::sqrt(s2) >= thr)) {  // SparseQR: a zero pivot, the column moved to the end
+        if (!(j < 3 || (j >= 3 * n && j < 3 * n + 3))) fullq = false;  // the zero torso columns always drop
+        continue;
+      }
+      double tau, beta;
+      make_householder(&F(k, j), rows - k, 1, tau, beta);
+      F(k, j) = beta;
+      essq.assign(&F(k, j) + 1, &F(k, j) + (rows - k));
+      apply_householder_left(F, k, essq.data(), tau, j + 1, cf);
+      apply_householder_left(bq, k, essq.data(), tau, 0, 1);
+      kept.push_back(j);
+    }
+    std::vector<double> uq(cf, 0.0);
+    for (int t = (int)kept.size() - 1; t >= 0; t--) {
+      double v = bq(t, 0);
+      for (int t2 = t + 1; t2 < (int)kept.size(); t2++) v -= F(t, kept[t2]) * uq[kept[t2]];
+      uq[kept[t]] = v / F(t, kept[t]);
+    }
+    y.assign(uq.begin() + 6 * n, uq.end());
+    return fullq;
+  }
   Mat R = A, bm(rows, 1);
   for (int i = 0; i < rows; i++) bm(i, 0) = b[i];
   std::vector<int> piv;  // kept columns in order (R's row t belongs to piv[t])
@@ -2103,7 +2159,7 @@ int run_rollout(const hso_model* m0, const hso_gait* g, int n_t, int k0, int H, 
 
 // periodic::solve_contforces_given_torques (periodic.cpp:368-374) over steps
 // k0 .. k0+H-1 of one rollout; tau_in [H][nmj] -> cf [H][3 nf]
-int run_forces(const hso_model* m0, const hso_gait* g, int n_t, int k0, int H, int ignore_reach,
+int run_forces(const hso_model* m0, const hso_gait* g, int n_t, int k0, int H, int ignore_reach, int rule,
                const double* tau_in, double* cf, uint32_t* flags) {
   hso_model mm = *m0;
   hso_model* m = &mm;
@@ -2138,7 +2194,7 @@ int run_forces(const hso_model* m0, const hso_gait* g, int n_t, int k0, int H, i
     int i = k0 + h + 2;
     std::vector<double> y;
     tl_near = NearTrack();
-    uint32_t fl = solve_forces(m, dr[i], tau_in + (size_t)h * nmj, y) ? 0u : HSO_FLAG_GENERAL;
+    uint32_t fl = solve_forces(m, dr[i], tau_in + (size_t)h * nmj, y, rule) ? 0u : (HSO_FLAG_GENERAL | HSO_FLAG_DEPENDENT);
     if (tl_near.near()) fl |= HSO_FLAG_NEAR_RANK;
     if (unreach[i]) fl |= HSO_FLAG_UNREACH;
     for (double v : y) if (std::isnan(v)) fl |= HSO_FLAG_NAN;
@@ -2174,7 +2230,14 @@ int hso_rollout(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, i
 int hso_forces(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, int ignore_reach, const double* tau_in,
                double* cf, uint32_t* flags) {
   if (!m || !g || !tau_in || n_t <= 0 || k0 < 0 || H <= 0) return -1;
-  return run_forces(m, g, n_t, k0, H, ignore_reach, tau_in, cf, flags);
+  return run_forces(m, g, n_t, k0, H, ignore_reach, HSO_FORCES_KERNEL, tau_in, cf, flags);
+}
+
+int hso_forces_rule(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, int ignore_reach, int rule,
+                    const double* tau_in, double* cf, uint32_t* flags) {
+  if (!m || !g || !tau_in || n_t <= 0 || k0 < 0 || H <= 0) return -1;
+  if (rule != HSO_FORCES_KERNEL && rule != HSO_FORCES_SPARSEQR) return -2;
+  return run_forces(m, g, n_t, k0, H, ignore_reach, rule, tau_in, cf, flags);
 }
 
 int hso_batch_near(const hso_model* m, const hso_gait* params, int B, int n_t, int k0, int H, int basis,
@@ -2208,7 +2271,7 @@ int hso_forces_batch(const hso_model* m, const hso_gait* params, int B, int n_t,
   std::vector<int> rc(n_threads, 0);
   auto worker = [&](int tid) {
     for (int b = tid; b < B; b += n_threads) {
-      int r = run_forces(m, &params[b], n_t, k0, H, ignore_reach, tau_in + (size_t)b * H * m->nmj,
+      int r = run_forces(m, &params[b], n_t, k0, H, ignore_reach, HSO_FORCES_KERNEL, tau_in + (size_t)b * H * m->nmj,
                          cf ? cf + (size_t)b * H * 3 * m->nf : nullptr, flags ? flags + (size_t)b * H : nullptr);
       if (r) rc[tid] = r;
     }

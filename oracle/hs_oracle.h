@@ -50,6 +50,8 @@ enum { HSO_BASIS_ORTHO = 0, /* reference-faithful: orthonormal Q of QR(B^T) (fts
 #define HSO_FLAG_UNREACH     16u  /* an IK target was clamped (ignore_reach, lik.cpp:250-253) */
 #define HSO_FLAG_NO_CONTACT  32u  /* k == 0 */
 #define HSO_FLAG_GENERAL     64u  /* FAST mode: closed form declined, Eigen-style path used */
+#define HSO_FLAG_DEPENDENT  512u  /* solve_forces: a column dropped as dependent, the basic solution returned
+                                     (with HSO_FLAG_GENERAL; one point of a non-unique solution set) */
 #define HSO_FLAG_NEAR_RANK  256u  /* a rank / routing decision within rounding of its threshold (NearTrack):
                                      another rounding may decide it the other way (HS_FLAG_NEAR_RANK) */
 
@@ -90,6 +92,15 @@ int hso_rollout(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, i
  * for ALL feet; flags HSO_FLAG_GENERAL when the least squares is rank deficient. */
 int hso_forces(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, int ignore_reach, const double* tau_in,
                double* cf, uint32_t* flags);
+/* hso_forces under a chosen rank rule for the (numerically) rank-deficient least squares:
+ * HSO_FORCES_KERNEL (hso_forces: the kernel's pivot guard, 1e-10 of the reduced normal matrix's largest
+ * diagonal, force columns in natural order) or HSO_FORCES_SPARSEQR (Eigen SparseQR's default threshold,
+ * 20 (rows + cols) eps max column norm on |r_kk|, every column in natural order; COLAMD not restated).
+ * A dropped column sets HSO_FLAG_GENERAL | HSO_FLAG_DEPENDENT. */
+#define HSO_FORCES_KERNEL 0
+#define HSO_FORCES_SPARSEQR 1
+int hso_forces_rule(const hso_model* m, const hso_gait* g, int n_t, int k0, int H, int ignore_reach, int rule,
+                    const double* tau_in, double* cf, uint32_t* flags);
 /* hso_forces for B rollouts on n_threads threads: tau_in [B][H][nmj] -> cf [B][H][3 nf], flags [B][H] */
 int hso_forces_batch(const hso_model* m, const hso_gait* params, int B, int n_t, int k0, int H, int ignore_reach,
                      int n_threads, const double* tau_in, double* cf, uint32_t* flags);

@@ -28,6 +28,9 @@ FLAG_UNREACH = 16
 FLAG_NO_CONTACT = 32
 FLAG_GENERAL = 64
 FLAG_NEAR_RANK = 256  # a rank / routing decision within rounding of its threshold (hs_oracle.cpp NearTrack)
+FLAG_DEPENDENT = 512  # solve_forces: a column dropped as dependent, the basic solution returned
+FORCES_KERNEL = 0     # solve_forces' rank rules (hso_forces_rule): the kernel's pivot guard
+FORCES_SPARSEQR = 1   # Eigen SparseQR's default threshold (COLAMD order not restated)
 NEAR_KINDS = {0: "none", 1: "LU pivot", 2: "threshold doubled", 3: "rel_error", 4: "QR pivot", 5: "collinear guard",
               6: "pivot guard", 7: "ill-conditioned second stage"}
 BASIS_FAST = 2
@@ -176,6 +179,8 @@ def _bind(path):
                                  ctypes.POINTER(ctypes.c_uint32), dp]
     L.hso_forces.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                              ctypes.c_int, dp, dp, ctypes.POINTER(ctypes.c_uint32)]
+    L.hso_forces_rule.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, dp, dp, ctypes.POINTER(ctypes.c_uint32)]
     L.hso_forces_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(Gait), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, ctypes.POINTER(ctypes.c_uint32)]
     L.hso_lik_roundtrip.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]
@@ -299,15 +304,17 @@ def pd_torques(model: Model, gait: GaitParams, tsi: int, q, dq, k: float = 100.0
     return tau_ff + a1, q0, dq0
 
 
-def forces(model: Model, gait: GaitParams, tau_in, n_t: int = 20, k0: int = 0, ignore_reach: bool = True) -> dict:
-    """Contact forces of all feet given motor torques tau_in [H][nmj] (ftsolver.cpp:331-378)."""
+def forces(model: Model, gait: GaitParams, tau_in, n_t: int = 20, k0: int = 0, ignore_reach: bool = True,
+           rule: int = FORCES_KERNEL) -> dict:
+    """Contact forces of all feet given motor torques tau_in [H][nmj] (ftsolver.cpp:331-378); rule: the
+    rank rule of a (numerically) rank-deficient least squares (FORCES_KERNEL or FORCES_SPARSEQR)."""
     tau_in = np.ascontiguousarray(tau_in, dtype=np.float64)
     H = tau_in.shape[0]
     cf = np.zeros((H, 3 * model.nf))
     flags = np.zeros(H, dtype=np.uint32)
     g = gait.to_c()
-    rc = lib().hso_forces(model.handle, ctypes.byref(g), n_t, k0, H, int(ignore_reach), _ptr(tau_in), _ptr(cf),
-                          flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    rc = lib().hso_forces_rule(model.handle, ctypes.byref(g), n_t, k0, H, int(ignore_reach), rule, _ptr(tau_in),
+                               _ptr(cf), flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
     if rc != 0:
         raise RuntimeError(f"oracle forces failed rc={rc}")
     return dict(cf=cf, flags=flags)

@@ -6,8 +6,9 @@ main.cpp:38: set_rec_rotation((0, 0, -1.571)) on pgs id 8.
 
 Tolerances as tests/test_gpu_parity.py: records 1e-12; per-joint torques < 1e-6 N*m (north_star) and
 < 1e-9 * max(1, |tau|); contact forces < 1e-8 * max(1, |f|); flags identical -- on every step that
-neither the kernel nor the oracle flags HS_FLAG_NEAR_RANK (a rank or routing decision within rounding
-of its threshold, ftsolver.cpp:205-232)."""
+is not excluded by test_gpu_parity.compare: a step flagged HS_FLAG_NEAR_RANK (a rank or routing
+decision within rounding of its threshold, ftsolver.cpp:205-232) is still compared wherever the oracle's
+tree and ortho answers agree."""
 import os
 from dataclasses import replace
 
@@ -15,7 +16,7 @@ import numpy as np
 import pytest
 
 from conftest import MODELS, PGS_CONFIG, record_to_oracle_gait, to_oracle_gait, transformed
-from test_gpu_parity import check_cf, check_flags, check_tau, fused_cycle, near, threads
+from test_gpu_parity import as_batch, compare, fused_cycle, near, threads
 
 pytestmark = pytest.mark.gpu
 
@@ -72,14 +73,10 @@ def test_rollout_main_cpp_rotation(gpu, hmodels, omodels, oracle_mod):
     p = gpu.read_pgs_config(PGS_CONFIG, 8)
     p.set_rec_rotation(MAIN_CPP_38)
     res = gpu.run_host(hmodels["hexapod"], [p], n_t=20, k0=0, horizon=20)
+    og = to_oracle_gait(O, p)
     for basis in (O.BASIS_ORTHO, O.BASIS_TREE):
-        r = O.rollout(omodels["hexapod"], to_oracle_gait(O, p), 20, basis=basis)
-        skip = near(res["flags"][0], r["flags"])
-        check_tau(res["tau"][0], r["tau"], "pgs 8 rotated", skip)
-        check_cf(res["cf"][0], r["cf"], "pgs 8 rotated", skip)
-        check_flags(res["flags"][0], r["flags"], "pgs 8 rotated", skip)
-        if not skip.any():
-            assert float(res["work_cot"][0, 1]) == pytest.approx(r["cot"], rel=1e-9)
+        r = as_batch(O.rollout(omodels["hexapod"], og, 20, basis=basis))
+        compare(f"pgs 8 rotated vs basis {basis}", res, r, O, omodels["hexapod"], [og], basis, min_work=1.0)
     from hslabs_amd.api import params_array
 
     g = fused_cycle(gpu, hmodels["hexapod"], params_array([p]))
@@ -97,8 +94,10 @@ def test_rollout_random_transforms(gpu, hmodels, omodels, oracle_mod, name, curv
     Tilted and lifted records also produce ill-posed steps (stretched legs: torques of 100+ N*m, three
     nearly collinear feet, a first-order problem whose rank decision in ftsolver.cpp:205-232 sits at
     the loop's 1e-6 tolerance). There the answer depends on the rounding, and the step is flagged
-    HS_FLAG_NEAR_RANK by the side that met the decision near its threshold. Every step that neither
-    side flags is checked with the full bounds; the flagged ones must be finite and are counted."""
+    HS_FLAG_NEAR_RANK by the side that met the decision near its threshold. Every step is checked with
+    the full bounds except the flagged ones whose tree and ortho answers disagree (<= 2 %: 0.1 % of the
+    straight hexapod's steps, 1.0 % of the curved one's, none on spider and myant, measured on the
+    oracle); those must be finite and are counted."""
     from hslabs_amd import synth
 
     O = oracle_mod
@@ -108,16 +107,10 @@ def test_rollout_random_transforms(gpu, hmodels, omodels, oracle_mod, name, curv
     g = fused_cycle(gpu, hmodels[name], params)
     gaits = [record_to_oracle_gait(O, r) for r in params]
     r = O.batch(omodels[name], gaits, 20, 0, 20, basis=O.BASIS_TREE, n_threads=threads())
-    skip = near(g["flags"], r["flags"])
     what = f"{name} transformed (tilt {tilt})"
     print(f"{what}: kernel flags {int(near(g['flags']).sum())}, oracle flags {int(near(r['flags']).sum())} "
-          f"of {skip.size} steps")
-    assert skip.mean() < 0.1
-    check_tau(g["tau"], r["tau"], what, skip)
-    check_cf(g["cf"], r["cf"], what, skip)
-    check_flags(g["flags"], r["flags"], what, skip)
-    whole = ~skip.any(axis=1)  # the work sums every step of the rollout
-    np.testing.assert_allclose(g["work_cot"][whole, 0], r["work"][whole], rtol=1e-9, atol=1e-12)
+          f"of {g['flags'].size} steps")
+    compare(what, g, r, O, omodels[name], gaits, O.BASIS_TREE, max_excluded=0.02, min_work=0.8)
     plain = fused_cycle(gpu, hmodels[name], base)
     scale = np.maximum(1, np.abs(plain["tau"][~on]))
     assert (np.abs(plain["tau"][~on] - g["tau"][~on]) / scale).max() < 1e-12

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 from conftest import MODELS, PGS_CONFIG, PGS_IDS, record_to_oracle_gait, to_oracle_gait
-from test_gpu_parity import GEN, check_cf, check_flags, check_tau, fused_cycle, near, npy, threads
+from test_gpu_parity import GEN, as_batch, compare, fused_cycle, npy, threads
 
 pytestmark = pytest.mark.gpu
 
@@ -50,15 +50,13 @@ def test_pgs_setups(gpu, oracle_mod, sid, force, torque):
     b = gpu.DeviceBatch(hm, [p], n_t=20, k0=0, horizon=20, outputs=("tau", "cf", "flags", "work_cot"))
     b.run(best=False)
     torch.cuda.synchronize()
-    r = oracle_mod.rollout(om, to_oracle_gait(oracle_mod, p), 20, basis=oracle_mod.BASIS_TREE)
-    flags = npy(b.flags)[0].astype(np.uint32)
-    assert ((flags & GEN) != 0).all(), "every step of a masked model takes the Eigen-style path"
-    skip = near(flags, r["flags"])
-    check_flags(flags, r["flags"], f"pgs {sid} torso penalty", skip)
-    check_tau(npy(b.tau)[0], r["tau"], f"pgs {sid} torso penalty ({force:d},{torque:d})", skip)
-    check_cf(npy(b.cf)[0], r["cf"], f"pgs {sid} torso penalty ({force:d},{torque:d})", skip)
-    if not skip.any():
-        assert float(npy(b.work_cot)[0, 1]) == pytest.approx(r["cot"], rel=1e-9, abs=1e-12)
+    og = to_oracle_gait(oracle_mod, p)
+    r = as_batch(oracle_mod.rollout(om, og, 20, basis=oracle_mod.BASIS_TREE))
+    g = {k: npy(getattr(b, k)) for k in ("tau", "cf", "flags", "work_cot")}
+    g["flags"] = g["flags"].astype(np.uint32)
+    assert ((g["flags"] & GEN) != 0).all(), "every step of a masked model takes the Eigen-style path"
+    compare(f"pgs {sid} torso penalty ({force:d},{torque:d})", g, r, oracle_mod, om, [og], oracle_mod.BASIS_TREE,
+            min_work=1.0)
 
 
 @pytest.mark.parametrize("force,torque", MASKS)
@@ -76,10 +74,8 @@ def test_synthetic(gpu, oracle_mod, name, curved, force, torque):
     gaits = [record_to_oracle_gait(oracle_mod, r) for r in params]
     r = oracle_mod.batch(om, gaits, 20, 0, 20, basis=oracle_mod.BASIS_TREE, n_threads=threads())
     assert ((g["flags"] & GEN) != 0).all()
-    skip = near(g["flags"], r["flags"])
-    check_flags(g["flags"], r["flags"], f"{name} torso penalty", skip)
-    check_tau(g["tau"], r["tau"], f"{name} torso penalty ({force:d},{torque:d})", skip)
-    check_cf(g["cf"], r["cf"], f"{name} torso penalty ({force:d},{torque:d})", skip)
+    compare(f"{name} torso penalty ({force:d},{torque:d})", g, r, oracle_mod, om, gaits, oracle_mod.BASIS_TREE,
+            min_work=0.95)
     seq = gpu.DeviceBatch(hm, params, n_t=20, k0=0, horizon=20, outputs=("tau", "cf", "flags"))
     seq.run(best=False)
     torch.cuda.synchronize()

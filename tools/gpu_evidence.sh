@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-4 evidence call (run under gpurun) on the product library: GPU tests, smoke, the driver's bench
+# The round's evidence call (run under gpurun) on the product library: GPU tests, smoke, the driver's bench
 # command (with the CPU baseline) and repeats, K = 200, solve_forces, a kernel trace with stats, the PMC
 # traffic passes and the fused-path phase stamps. Stops at the first failure.   TAG=<outputs dir>
 set -o pipefail
-R=$GRAFT_REPO_ROOT; TAG=${TAG:-r04_final}; OUT=$R/gpurun_out/$TAG; mkdir -p $OUT; cd $R
+R=$GRAFT_REPO_ROOT; TAG=${TAG:-evidence}; OUT=$R/gpurun_out/$TAG; mkdir -p $OUT; cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { echo "tests failed"; tail -40 $OUT/tests.log; exit 1; }
 tail -1 $OUT/tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; cat $OUT/smoke.log; exit 1; }
