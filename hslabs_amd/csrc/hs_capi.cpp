@@ -140,13 +140,20 @@ int sim_device_state(hs_model_t m, const hs_topo** topo, const hs_simtopo** sim,
   return HS_OK;
 }
 
-// n_calls launches, k0 marching through the cycle (hs_run_steps semantics)
+// n_calls launches, k0 marching through the cycle (hs_run_steps semantics). total_mass / rollout_mass:
+// the model's, or a mixed plan's per-rollout masses (the best key's selection COT)
 int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::launch_map& mp, int32_t n_calls,
-                 void* const* kernel_events) {
+                 void* const* kernel_events, double total_mass, const double* rollout_mass) {
   hs_run_args c = a;
   hipStream_t st = (hipStream_t)a.stream;
   // the best key covers the work of all n_calls calls: taken after the last one only
   if (c.key_steps == 0) c.key_steps = (int32_t)std::min<int64_t>((int64_t)n_calls * a.horizon, INT32_MAX);
+  // With the work in work_cot the key is taken by the work reduce kernel after the last launch (n_steps
+  // = 0: it re-reads the accumulated work, writes the same values back and min-reduces each workgroup's
+  // 64 keys before its one atomic): taken in the step launch, every wavefront's atomic on the one key
+  // address queued behind the others' and the call's last launch ran 26-39 us instead of 19.6 us
+  // (profiles/r05_t1_steps_trace_tail.txt)
+  const bool key_reduce = a.best_key && a.work_cot && !mp.tau_in;
   // one gait setup per rollout per call: the preparation pass of the fused path (hs_prep_kernel: the
   // setup record, sample times, IK table and torso record) stores it and every launch loads it, so the
   // kinematics of these launches and of hs_run_calls' fused launches come from the same kernels
@@ -160,7 +167,7 @@ int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::lau
   base.setup_only = 0;
   for (int32_t i = 0; i < n_calls; i++) {
     c.k0 = (int32_t)(((int64_t)a.k0 + (int64_t)i * a.horizon) % a.n_t);
-    c.best_key = (i + 1 == n_calls) ? a.best_key : nullptr;
+    c.best_key = (i + 1 == n_calls && !key_reduce) ? a.best_key : nullptr;
     hs::launch_map mi = base;
     mi.setup_io = hs::SETUP_LOAD;
     hipError_t e = hipSuccess;
@@ -170,6 +177,14 @@ int launch_steps(const hs_topo* d, const hs_run_args& a, void* ws, const hs::lau
     if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
     if (kernel_events) e = hipEventRecord((hipEvent_t)kernel_events[2 * i + 1], st);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+  }
+  if (key_reduce) {
+    hs_run_args r = c;
+    r.best_key = a.best_key;
+    r.accumulate = 1;  // the work the launches accumulated; no step terms added
+    const int le = (a.precision == HS_PREC_F32) ? hs::launch_fused_reduce_f32(r, total_mass, rollout_mass, nullptr, 0)
+                                                : hs::launch_fused_reduce(r, total_mass, rollout_mass, nullptr, 0);
+    if (le != 0) return hip_fail((hipError_t)le, "kernel launch (best key)");
   }
   return HS_OK;
 }
@@ -458,7 +473,7 @@ int hs_run_steps(hs_model_t m, const hs_run_args* a, int32_t n_calls, void* cons
   rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);  // + the idle half-wave of an odd batch
   if (rc != HS_OK) return rc;
   return launch_steps(d, routed(*a, m->host.torso_mask), ws, hs::single_model_map(m->host, a->n_rollouts), n_calls,
-                      kernel_events);
+                      kernel_events, m->host.total_mass, nullptr);
 }
 
 int hs_run_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls) {
@@ -494,7 +509,7 @@ int hs_run_pd(hs_model_t m, const hs_run_args* a, const hs_pd_args* pd) {
   mp.pd_tau = pd->tau_cmd;
   mp.pd_q0 = pd->q_target;
   mp.pd_dq0 = pd->dq_target;
-  return launch_steps(d, routed(*a, m->host.torso_mask), ws, mp, 1, nullptr);
+  return launch_steps(d, routed(*a, m->host.torso_mask), ws, mp, 1, nullptr, m->host.total_mass, nullptr);
 }
 
 int hs_run_forces(hs_model_t m, const hs_run_args* a, const double* tau_in) {
@@ -508,7 +523,7 @@ int hs_run_forces(hs_model_t m, const hs_run_args* a, const double* tau_in) {
   if (rc != HS_OK) return rc;
   hs::launch_map mp = hs::single_model_map(m->host, a->n_rollouts);
   mp.tau_in = tau_in;
-  return launch_steps(d, *a, ws, mp, 1, nullptr);
+  return launch_steps(d, *a, ws, mp, 1, nullptr, m->host.total_mass, nullptr);
 }
 
 int hs_run_forces_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls, const double* tau_in) {
@@ -662,7 +677,7 @@ int hs_run_mixed_steps(hs_mixed_t p, const hs_run_args* a, int32_t n_calls, void
     e = (hipError_t)p->ws.get(a->stream, (size_t)p->n_rollouts + 1, &ws);
   }
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
-  return launch_steps(p->d_topos, routed(*a, p->torso_mask), ws, mp, n_calls, kernel_events);
+  return launch_steps(p->d_topos, routed(*a, p->torso_mask), ws, mp, n_calls, kernel_events, 0.0, p->d_rollout_mass);
 }
 
 int hs_run_mixed_calls(hs_mixed_t p, const hs_run_args* a, int32_t n_calls) {

@@ -162,12 +162,14 @@ struct CentreL {  // fields read after D
   int unreach[HS_LMAX];
 };
 
-struct ForceL {  // solve_forces by limbs (forces_solve): per limb S_l and e_l (a), per foot K_f and q_f
-                 // (b); the dense fallback reuses the space from a[0][27] on (336 reals in all)
-  real a[HS_LMAX][27];
-  real b[HS_LMAX][27];
-  real spare[12];
+struct ForceL {  // solve_forces by limbs (forces_solve); the dense fallback reuses it from sum on (336 reals)
+  real sum[27];           // the sums over the limbs: S and d~, or K and its right-hand side
+  real op[HS_LMAX][24];   // a limb's product operands: the rows of L^-1 [W_mt | d_m] and 1 / D_M, then V and 1 / D_B
+  real pr[HS_LMAX][27];   // a limb's products: S_l and e_l, then K_f and q_f
+  real spare[3];
 };
+static_assert(sizeof(ForceL) >= 336 * sizeof(real), "forces_solve's dense route uses 336 reals from ForceL::sum");
+static_assert(sizeof(ForceL) <= sizeof(FastL), "ForceL must not grow the step's LDS union");
 
 template <int NM, bool FORCES>
 struct OneStore {
@@ -2658,13 +2660,16 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     auto prod = [&](int a, int b) {  // (L^-1 R)_a^T D^-1 (L^-1 R)_b
       return R[0][a] * rdM[0] * R[0][b] + R[1][a] * rdM[1] * R[1][b] + R[2][a] * rdM[2] * R[2][b];
     };
+    // S_l = W_tm M^-1 W_mt and e_l = W_tm M^-1 d_m (27 products) are formed by all 32 lanes (below):
+    // their operands, the W_mt and d_m columns of L^-1 R and 1 / D_M, go to LDS
+    real* const op = fr.op[L];
 #pragma unroll
-    for (int e = 0; e < 21; e++) {  // S_l = W_tm M^-1 W_mt (packed lower)
-      const TriWalk<> t(e);
-      fr.a[L][e] = prod(t.r, t.c);
+    for (int k = 0; k < 3; k++) {
+#pragma unroll
+      for (int c = 0; c < 6; c++) op[7 * k + c] = R[k][c];
+      op[7 * k + 6] = R[k][9];
+      op[21 + k] = rdM[k];
     }
-#pragma unroll
-    for (int r = 0; r < 6; r++) fr.a[L][21 + r] = prod(r, 9);  // e_l = W_tm M^-1 d_m
     real d[3];
     for (int t = 0; t < 3; t++) d[t] = fp[t] - P0[t];
 #pragma unroll
@@ -2679,40 +2684,61 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     for (int jj = 0; jj < 3; jj++) rb[jj] = prod(6 + jj, 9);
     Bl[0] = Bd[0]; Bl[3] = Bd[1]; Bl[4] = Bd[2]; Bl[6] = Bd[3]; Bl[7] = Bd[4]; Bl[8] = Bd[5];
     okB = ldl_n<3>(Bl, kForcesBlockGuard, rdB);
-    if (okB) {  // K_f = C~ B^-1 C~^T, q_f = C~ B^-1 r_f, through V = L_B^-1 [C~^T | r_f]
-      real V[3][7];
-      for (int c = 0; c < 6; c++)
-        for (int k = 0; k < 3; k++) V[k][c] = Ct[3 * c + k];
-      for (int k = 0; k < 3; k++) V[k][6] = rb[k];
-#pragma unroll
-      for (int c = 0; c < 7; c++) {
-        V[1][c] -= Bl[3] * V[0][c];
-        V[2][c] -= Bl[6] * V[0][c] + Bl[7] * V[1][c];
-      }
-      auto vp = [&](int a, int b) {
-        return V[0][a] * rdB[0] * V[0][b] + V[1][a] * rdB[1] * V[1][b] + V[2][a] * rdB[2] * V[2][b];
-      };
-#pragma unroll
-      for (int e = 0; e < 21; e++) {
-        const TriWalk<> t(e);
-        fr.b[L][e] = vp(t.r, t.c);
-      }
-#pragma unroll
-      for (int r = 0; r < 6; r++) fr.b[L][21 + r] = vp(r, 6);
-    }
   }
   const bool fast = !dense && half_ballot(lane < nl && !okB) == 0;
   wave_sync();
   STAMP(4);
-  if (lane < FSUM) {  // sums over the limbs, in limb order; W_tt and the torso part of d added
+  // a limb's 27 products from its operands o (rows of 7 at 0, 7, 14; 1 / D at 21): entry e < 21 is the
+  // packed lower (r, c) of the 6 x 6 block, e >= 21 the 6-vector (column 6)
+  auto limb_products = [&]() {
+    for (int p = lane; p < 27 * nl; p += HALF) {
+      const int L = p / 27, e = p - 27 * L;
+      int a = e - 21, b = 6;
+      if (e < 21) {
+        const TriWalk<> t(e);
+        a = t.r;
+        b = t.c;
+      }
+      const real* o = fr.op[L];
+      fr.pr[L][e] = o[a] * o[21] * o[b] + o[7 + a] * o[22] * o[7 + b] + o[14 + a] * o[23] * o[14 + b];
+    }
+  };
+  limb_products();  // S_l, e_l
+  wave_sync();
+  if (lane < FSUM) {  // their sums over the limbs, in limb order
     real s = 0;
-    for (int L = 0; L < nl; L++) s += fast ? ((lane < 21) ? fr.b[L][lane] - fr.a[L][lane] : fr.b[L][lane] + fr.a[L][lane])
-                                          : fr.a[L][lane];
+    for (int L = 0; L < nl; L++) s += fr.pr[L][lane];
+    fr.sum[lane] = s;
+  }
+  if (fast && lane < nl) {  // K_f = C~ B^-1 C~^T, q_f = C~ B^-1 r_f, through V = L_B^-1 [C~^T | r_f]: V, 1 / D_B
+    real* const op = fr.op[lane];
+#pragma unroll
+    for (int c = 0; c < 7; c++) {
+      const real v0 = c < 6 ? Ct[3 * c] : rb[0];
+      const real v1 = (c < 6 ? Ct[3 * c + 1] : rb[1]) - Bl[3] * v0;
+      const real v2 = (c < 6 ? Ct[3 * c + 2] : rb[2]) - (Bl[6] * v0 + Bl[7] * v1);
+      op[c] = v0;
+      op[7 + c] = v1;
+      op[14 + c] = v2;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) op[21 + k] = rdB[k];
+  }
+  wave_sync();
+  if (fast) {
+    limb_products();  // K_f, q_f
+    wave_sync();
+  }
+  if (lane < FSUM) {  // W_tt and the torso part of d added
+    const real sa = fr.sum[lane];
+    real sb = 0;
+    if (fast)
+      for (int L = 0; L < nl; L++) sb += fr.pr[L][lane];
     const real dt = (lane < 21) ? real(0) : (lane < 24 ? sv.x[lane - 21] : sv.x[3 * n + lane - 24]);
     // fast: K = W_tt - sum S_l + sum K_f, rhs = sum (q_f + e_l) - d_t; else S = W_tt - sum S_l, d~ = d_t - sum e_l
-    const real v = (lane < 21) ? (fast ? wtt_entry(lane, ts, n) + s : wtt_entry(lane, ts, n) - s)
-                               : (fast ? s - dt : dt - s);
-    fr.a[0][lane] = v;  // lane reads column `lane` only, so slot 0 takes the sums in place
+    const real v = (lane < 21) ? (fast ? wtt_entry(lane, ts, n) + (sb - sa) : wtt_entry(lane, ts, n) - sa)
+                               : (fast ? (sb + sa) - dt : dt - sa);
+    fr.sum[lane] = v;  // lane reads column `lane` only
   }
   wave_sync();
   STAMP(5);
@@ -2722,8 +2748,8 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
 #pragma unroll
     for (int r = 0; r < 6; r++) {
 #pragma unroll
-      for (int c = 0; c < 6; c++) K[6 * r + c] = (c <= r) ? fr.a[0][pk(r, c)] : real(0);
-      lam[r] = fr.a[0][21 + r];
+      for (int c = 0; c < 6; c++) K[6 * r + c] = (c <= r) ? fr.sum[pk(r, c)] : real(0);
+      lam[r] = fr.sum[21 + r];
     }
     ldl_n<6>(K, real(0), rd);  // >= I
     ldl_solve_n<6>(K, rd, lam);
@@ -2743,7 +2769,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
   }
   // dense normal equations over the feet (a B_f near singular): N = diag(B_f) + V^T D_S^-1 V with
   // S = L_S D_S L_S^T, V = L_S^-1 C~, r = r_b + V^T D_S^-1 L_S^-1 d~
-  real* const base = &fr.a[0][0];
+  real* const base = fr.sum;
   real* const Vm = base + FSUM;       // [6][HS_KMAX]
   real* const vv = Vm + 6 * HS_KMAX;  // 6
   real* const rdS = vv + 6;           // 6
@@ -2896,27 +2922,48 @@ static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 #ifndef HS_PREP_WAVES
 #define HS_PREP_WAVES 2  // waves per SIMD the register budget allows (196 VGPRs; 3 or 4 spill)
 #endif
+#ifndef HS_PREP_WPB
+#define HS_PREP_WPB 1  // wavefronts per workgroup (each a group of lanes of its own: only wave-local exchanges)
+#endif
+// an exchange through LDS among the lanes of one wavefront: LDS operations of a wavefront complete in
+// order, so only the compiler must not move the accesses across it (no s_barrier: with several
+// wavefronts per workgroup they take different paths)
+__device__ inline void wave_lds_sync() {
+#if HS_PREP_WPB == 1
+  wave_sync();
+#else
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#endif
+}
 __device__ inline int ktab_lanes(const hs::launch_map& mp) { return mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX; }
 __host__ __device__ inline int prep_chunks(int ttab_n) { return (ttab_n > 0 ? ttab_n + HS_PREP_ROWS - 1 : HS_PREP_ROWS) / HS_PREP_ROWS; }
 __host__ __device__ inline int64_t prep_blocks(int n_waves, int ttab_n, int nli) {
   const int64_t groups_per_xcd = 2 * (int64_t)prep_chunks(ttab_n) * ((n_waves + 7) / 8);
   const int gpw = WAVE / nli;
-  return 8 * ((groups_per_xcd + gpw - 1) / gpw);
+  const int64_t waves_per_xcd = (groups_per_xcd + gpw - 1) / gpw;
+  return 8 * ((waves_per_xcd + HS_PREP_WPB - 1) / HS_PREP_WPB);
 }
 
-__global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
-                                                      RolloutWS* __restrict__ rws, hs::launch_map mp) {
-  __shared__ real rad[WAVE];
-  __shared__ real q6s[HS_PREP_ROWS][6][WAVE / 4];  // turning gaits' rows: [row][q6 entry][group] (>= 4 limbs)
-  __shared__ real tgs[HS_PREP_ROWS][3][WAVE];      // [row][target entry][lane]
+__global__ __launch_bounds__(WAVE * HS_PREP_WPB, HS_PREP_WAVES) void hs_prep_kernel(const hs_topo* __restrict__ T0,
+                                                                   hs_run_args a, RolloutWS* __restrict__ rws,
+                                                                   hs::launch_map mp) {
+  __shared__ real rad_s[HS_PREP_WPB][WAVE];
+  __shared__ real q6s_s[HS_PREP_WPB][HS_PREP_ROWS][6][WAVE / 4];  // turning rows: [row][q6 entry][group] (>= 4 limbs)
+  __shared__ real tgs_s[HS_PREP_WPB][HS_PREP_ROWS][3][WAVE];      // [row][target entry][lane]
+  const int wv = (int)threadIdx.x / WAVE, tl = (int)threadIdx.x % WAVE;  // wavefront in the block, its lane
+  real(&rad)[WAVE] = rad_s[wv];
+  real(&q6s)[HS_PREP_ROWS][6][WAVE / 4] = q6s_s[wv];
+  real(&tgs)[HS_PREP_ROWS][3][WAVE] = tgs_s[wv];
   RSTAMP(29);
   STAMP(24);
   if (blockIdx.x == 0)  // the call's fixup counters, before its step launches append to them
-    for (int i = threadIdx.x; i < mp.fix_n_counts; i += WAVE) mp.fix_count[i] = 0;
+    for (int i = threadIdx.x; i < mp.fix_n_counts; i += blockDim.x) mp.fix_count[i] = 0;
   const int nli = ktab_lanes(mp), gpw = WAVE / nli;
   const int C = prep_chunks(mp.ttab_n);
-  const int gl = (int)threadIdx.x / nli, L = (int)threadIdx.x % nli;
-  const int gi = (int)(blockIdx.x / 8) * gpw + gl;  // group (q, sub, chunk) in XCD x's sequence
+  const int gl = tl / nli, L = tl % nli;
+  // group (q, sub, chunk) in XCD x's sequence (x = blockIdx.x % 8: the block's XCD)
+  const int gi = ((int)(blockIdx.x / 8) * HS_PREP_WPB + wv) * gpw + gl;
   const int chunk = gi % C, sub = (gi / C) % 2, w = 8 * (gi / (2 * C)) + (int)(blockIdx.x % 8);
   bool on = gl < gpw && w < mp.n_waves;
   int b = 0;
@@ -2961,12 +3008,12 @@ __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_t
     if (g.curvature != 0) my_rad = turn_radius(pos0, g.curvature);
   }
   STAMP(25);
-  rad[threadIdx.x] = my_rad;
-  wave_sync();
+  rad[tl] = my_rad;
+  wave_lds_sync();
   real mr = 0;  // compute_max_radius over the rollout's limbs (every lane: turning rows read it)
   if (on && g.curvature != 0)
     for (int l = 0; l < T->n_limbs; l++) {
-      const real r = rad[threadIdx.x - L + l];
+      const real r = rad[tl - L + l];
       if (r > mr) mr = r;
     }
   if (on && chunk == 0 && L == 0) ws->st.max_radius = mr;
@@ -3021,14 +3068,14 @@ __global__ __launch_bounds__(WAVE, HS_PREP_WAVES) void hs_prep_kernel(const hs_t
         const real q6[6] = {o0[0], o0[1], o0[2], o1[0], o1[1], o1[2]};
         for (int i = 0; i < 6; i++) q6s[r - r0][i][gl] = q6[i];
       }
-      for (int i = 0; i < 3; i++) tgs[r - r0][i][threadIdx.x] = target[i];
+      for (int i = 0; i < 3; i++) tgs[r - r0][i][tl] = target[i];
     }
-    wave_sync();
+    wave_lds_sync();
 #pragma unroll 1
     for (int r = r0; r < r1; r++) {
       real q6[6], target[3];
       for (int i = 0; i < 6; i++) q6[i] = q6s[r - r0][i][gl];
-      for (int i = 0; i < 3; i++) target[i] = tgs[r - r0][i][threadIdx.x];
+      for (int i = 0; i < 3; i++) target[i] = tgs[r - r0][i][tl];
       const A34 A0 = mul(mul(node_joint_parent(T, 0), free_joint(q6)), node_pj(T, 0));
       if (L == 0) {  // the torso record the step launches read (kin_sample_tab)
         real* tr = ws->ktor[r];
@@ -3377,7 +3424,7 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   RolloutWS* ws = (RolloutWS*)workspace;
   if (mp.setup_only) {  // the call's preparation pass: setup record, sample times, IK table
     const int64_t blocks = prep_blocks(mp.n_waves, mp.ttab_n, mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX);
-    hipLaunchKernelGGL(hs_prep_kernel, dim3((unsigned)blocks), dim3(WAVE), 0, st, d_topo, a, ws, mp);
+    hipLaunchKernelGGL(hs_prep_kernel, dim3((unsigned)blocks), dim3(WAVE * HS_PREP_WPB), 0, st, d_topo, a, ws, mp);
     return (int)hipGetLastError();
   }
   launch_map m = mp;
