@@ -68,7 +68,12 @@ constexpr int HALF = 32;     // lanes per rollout: two rollouts per wavefront
 constexpr int NS = 5;        // samples in the derivative stencil (periodic.cpp:192-202)
 static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a rollout's lane maps exceed 32");
 #ifndef HS_MIN_WAVES
-#define HS_MIN_WAVES 3  // fp64: 12 workgroups/CU at 13.0 KB LDS (hexapod), <= 168 VGPRs
+#define HS_MIN_WAVES 3  // fp64 launch-per-step and fixup instantiations (the general-path call): <= 168 VGPRs
+#endif
+#ifndef HS_MIN_WAVES_DEFER
+// the fused step launch (hs::FIX_DEFER): 16 workgroups/CU at 10.1 KB of LDS (hexapod, round 5's PostL layout),
+// <= 128 VGPRs (96 B of spills)
+#define HS_MIN_WAVES_DEFER 4
 #endif
 #ifndef HS_MIN_WAVES_FORCES
 #define HS_MIN_WAVES_FORCES 3  // solve_forces mode (hs_run_forces): the control step's LDS layout
@@ -87,9 +92,9 @@ static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a
 constexpr int SCH_H = 21, SCH_N = 27;
 __host__ __device__ constexpr int sch_lower(int r, int q) { return r * (r + 1) / 2 + q; }
 
-struct SchurL {  // per-contact Schur complement (all D_c invertible)
-  real Dinv[HS_LMAX][9], S[HS_LMAX][SCH_N];
-  real Ssum[SCH_N];  // sum over contacts of the packed [S_c | h_c] (lane per entry)
+struct SchurL {  // Schur complement of the contacts (all D_c invertible)
+  real Dinv[HS_LMAX][9];
+  real Ssum[SCH_N];  // sum over contacts of the packed [S_c | h_c] (summed across the contact lanes)
   real lam[6];
 };
 
@@ -169,14 +174,29 @@ struct ForceL {  // solve_forces by limbs (forces_solve); the dense fallback reu
   real spare[3];
 };
 static_assert(sizeof(ForceL) >= 336 * sizeof(real), "forces_solve's dense route uses 336 reals from ForceL::sum");
-static_assert(sizeof(ForceL) <= sizeof(FastL), "ForceL must not grow the step's LDS union");
+static_assert(sizeof(ForceL) <= sizeof(StencilL<22>) + 96, "ForceL must not grow the hexapod's LDS union much");
+
+// What the control step keeps once D has consumed the stencil, in the stencil's place: D writes each
+// part's f rows over that part's own stencil rows (every lane reads its rows before it writes, one
+// wavefront in program order), the particular solution x overwrites f in place, the closed form's
+// blocks and the forces y follow it (round 5: the layout that brought the step to 10 KB of LDS per
+// workgroup, 4 waves per SIMD)
+template <int NM>
+struct PostL {
+  union {
+    real f[6 * NM];
+    real x[6 * NM];
+  };
+  FastL fl;
+  real y[HS_KMAX];
+};
 
 template <int NM, bool FORCES>
 struct OneStore {
   union {
     StencilL<NM> sten;
-    FastL fl;  // written only after D has consumed the stencil
-    typename std::conditional<FORCES, ForceL, WorkL>::type fr;  // forces-given-torques mode
+    // forces-given-torques mode: its blocks (x and y stay in SolveL, which forces_solve reads with them)
+    typename std::conditional<FORCES, ForceL, PostL<NM>>::type post;
   };
   CentreL<NM> c;
 };
@@ -222,20 +242,33 @@ __device__ inline void store_body(const A34& A, const real* com, real* bf, int n
 }
 
 template <int NM>
-struct SolveL {
+struct SolveXY {
   union {  // particular() overwrites each part's f with its x in place
     real f[6 * NM];
     real x[6 * NM];
   };
   real y[HS_KMAX];
+};
+struct SolveNone {};
+template <int NM, bool FORCES>
+struct SolveL {
+  typename std::conditional<FORCES, SolveXY<NM>, SolveNone>::type xy;  // the control step keeps them in PostL
   int cfoot[HS_LMAX];
   uint32_t fch[HS_LMAX][2];  // hs_topo::foot_chain8, copied at the wave's start (the contact blocks' chains)
+};
+// The solve's LDS arrays as the phases see them (sv.f, sv.x, sv.y, sv.cfoot, sv.fch)
+struct SolveRef {
+  real* f;
+  real* x;
+  real* y;
+  int* cfoot;
+  uint32_t (*fch)[2];
 };
 
 template <int NM, bool FORCES>
 struct Smem {
   OneStore<NM, FORCES> d;
-  SolveL<NM> sv;
+  SolveL<NM, FORCES> sv;
 #if HS_CURVED_LDS
   SetupL st;  // the setup pass's record, copied per step in waves with a curved gait
 #endif
@@ -1060,6 +1093,9 @@ __device__ __attribute__((always_inline)) inline void particular_sub(const hs_to
   real F[3] = {0, 0, 0}, V[3] = {0, 0, 0};
   const bool leafward = on && parent >= 0;
   if (leafward) {  // the subtree's range, in preorder
+#ifdef HS_PART_UNROLL
+#pragma unroll HS_PART_UNROLL
+#endif
     for (int m = 0; m < sz; m++) {
       const int kx = lane + m;
       for (int j = 0; j < 3; j++) { F[j] += sv.x[3 * kx + j]; V[j] += sv.x[3 * (n + kx) + j]; }
@@ -2083,7 +2119,8 @@ __device__ __attribute__((always_inline)) inline bool fast_solve_lanes(const hs_
   // joints s, s + 4, the quad adds them (DPP), every lane of the quad factorizes D_c, and the Schur
   // block's rows are split {s, 5 - s} (seven packed entries and two of h per lane; lane 3 repeats
   // lane 2's rows and stores D_c, g_c, d0_c and D_c^-1 instead) -- one instruction stream, the lanes
-  // differing only in data
+  // differing only in data. The blocks are summed over the contacts across the lanes (sch below)
+  real sch[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // this lane's 7 packed entries and 2 of h; 0 past nc
   {
     const int c = lane >> 2, s4 = lane & 3;
     if (c < nc) {
@@ -2155,12 +2192,12 @@ __device__ __attribute__((always_inline)) inline bool fast_solve_lanes(const hs_
           }
 #pragma unroll
           for (int t = 0; t < 7; t++) {  // row r0's r0 + 1 entries, then row r1's
-            const bool first = t <= r0;
-            const int r = first ? r0 : r1, q = first ? t : t - r0 - 1;
+            const bool first = t <= r0;  // entry (r0, t) or (r1, t - r0 - 1)
+            const int q = first ? t : t - r0 - 1;
             real v = 0;
 #pragma unroll
             for (int j = 0; j < 3; j++) v += (first ? E0[j] : E1[j]) * a_entry(d0, q, j);
-            if (s4 < 3) fl.sc.S[c][sch_lower(r, q)] = v;
+            if (s4 < 3) sch[t] = v;
           }
           real h0 = 0, h1 = 0;
           for (int j = 0; j < 3; j++) {
@@ -2168,12 +2205,34 @@ __device__ __attribute__((always_inline)) inline bool fast_solve_lanes(const hs_
             h1 += E1[j] * g[j];
           }
           if (s4 < 3) {
-            fl.sc.S[c][SCH_H + r0] = h0;
-            fl.sc.S[c][SCH_H + r1] = h1;
+            sch[7] = h0;
+            sch[8] = h1;
           }
         }
       }
       if (s4 == 0) fl.ok[c] = ok | coll;
+    }
+  }
+  // sum over the contacts c = 0 .. 7 of lanes 4 c + s: within each 16-lane row by DPP (row_shr 4, then
+  // 8: lane 12 + s holds its row's four contacts), then the two rows (xor 16). Lanes 12 .. 14 store the
+  // packed [S | h] (a pairwise order, not the contacts' sequence: ULPs of the Schur complement)
+#pragma unroll
+  for (int e = 0; e < 9; e++) {
+    real v = sch[e];
+    v += dpp_r<0x114>(v);
+    v += dpp_r<0x118>(v);
+    sch[e] = v + __shfl_xor(v, 16);
+  }
+  {
+    const int s4 = lane & 3, r0 = s4, r1 = 5 - s4;
+    if ((lane & ~3) == 12 && s4 < 3) {
+#pragma unroll
+      for (int t = 0; t < 7; t++) {
+        const bool first = t <= r0;
+        fl.sc.Ssum[first ? sch_lower(r0, t) : sch_lower(r1, t - r0 - 1)] = sch[t];
+      }
+      fl.sc.Ssum[SCH_H + r0] = sch[7];
+      fl.sc.Ssum[SCH_H + r1] = sch[8];
     }
   }
   wave_sync();
@@ -2243,14 +2302,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve_lanes(const hs_
       }
       fl.ok[0] = ok;
     }
-  } else {  // Schur complement of the 6 zeroth-order constraints
-    // entry sums in contact order, one lane per packed entry: the lower triangle (21) and h (6)
-    if (lane < SCH_N) {
-      real s = 0;
-      for (int c = 0; c < nc; c++) s += fl.sc.S[c][lane];
-      fl.sc.Ssum[lane] = s;
-    }
-    wave_sync();
+  } else {  // Schur complement of the 6 zeroth-order constraints (its entries summed above)
     if (lane == 0) {
       real Sm[36], h[6];
 #pragma unroll
@@ -3128,6 +3180,18 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   SolveWS* G = mp.fused_gen ? &((SolveWS*)mp.fused_gen)[(size_t)fstep * (a.n_rollouts + 1) + (live ? b : a.n_rollouts)]
                             : &rws[live ? b : a.n_rollouts].sol;
   Smem<NM, FORCES>& sm = smem[sub];
+  SolveRef sv;
+  if constexpr (FORCES) {
+    sv.f = sm.sv.xy.f;
+    sv.x = sm.sv.xy.x;
+    sv.y = sm.sv.xy.y;
+  } else {
+    sv.f = sm.d.post.f;
+    sv.x = sm.d.post.x;
+    sv.y = sm.d.post.y;
+  }
+  sv.cfoot = sm.sv.cfoot;
+  sv.fch = sm.sv.fch;
   real work = (live && a.accumulate && a.work_cot && !mp.fused_w) ? outp(a.work_cot)[2 * (size_t)b] : real(0);
   int k0 = a.k0, h_row = mp.h_row;
   if (mp.fused_w) {
@@ -3203,16 +3267,16 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
                           sl - 2, t_tab, mp.ktab_lo, mp.ttab_n);
       }
     }
-    if (!FORCES && lane < 2 * HS_LMAX) (&sm.sv.fch[0][0])[lane] = fch_w;
+    if (!FORCES && lane < 2 * HS_LMAX) (&sv.fch[0][0])[lane] = fch_w;
     wave_sync();
   }
   STAMP(2);
   if constexpr (FORCES) {
-    forces_step(T, a, mp, dt, sm.sv, sm.d.fr, OneWin<NM, FORCES>{&sm.d}, b, live, h_row, lane);
+    forces_step(T, a, mp, dt, sv, sm.d.post, OneWin<NM, FORCES>{&sm.d}, b, live, h_row, lane);
     return;
   } else {
     bool deferred = false;
-    step<DEFER>(T, a, mp, dt, sm.sv, sm.d.fl, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
+    step<DEFER>(T, a, mp, dt, sv, sm.d.post.fl, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
                 deferred, !fix_idle, lane, hinge_id, hinge_foot);
     if (DEFER && deferred) {  // the fixup launch solves this (step, rollout) with the general path
       if (lane == 0 && live) {
@@ -3254,10 +3318,23 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
 // without it; SOLVE, the fixup launch over the deferred items (its own instantiation, so the loop
 // costs the other two nothing)
 template <int NM, bool FORCES, int MODE>
-__global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FLOAT ? HS_MIN_WAVES_F32 : HS_MIN_WAVES)) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
+#ifdef HS_ROLLOUT_VGPRS
+#define HS_ROLLOUT_ATTR __attribute__((amdgpu_waves_per_eu(HS_ROLLOUT_VGPRS, HS_ROLLOUT_VGPRS)))
+#else
+#define HS_ROLLOUT_ATTR
+#endif
+__global__ HS_ROLLOUT_ATTR __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES
+                                                     : (HS_REAL_IS_FLOAT ? HS_MIN_WAVES_F32
+                                                                         : (MODE == hs::FIX_DEFER ? HS_MIN_WAVES_DEFER
+                                                                                                  : HS_MIN_WAVES))) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
                                                                                  hs_run_args a, RolloutWS* __restrict__ rws,
                                                                                  hs::launch_map mp) {
+#ifdef HS_PROBE_DYN_LDS  // register-budget probe only (tools/isa_stats.py): LDS size hidden from the compiler
+  extern __shared__ char hs_dyn_lds[];
+  Smem<NM, FORCES>* smem = reinterpret_cast<Smem<NM, FORCES>*>(hs_dyn_lds);
+#else
   __shared__ Smem<NM, FORCES> smem[2];
+#endif
   RSTAMP(16);
   STAMP(15);
   if constexpr (MODE == hs::FIX_SOLVE) {  // the deferred (step, rollout) items

@@ -1750,7 +1750,9 @@ bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<d
   // nc >= 3: nearly collinear feet leave it to the Eigen-style path (the kernel's zeroth_well_posed)
   if (!zeroth_well_posed(d, cf)) return false;
   // Schur complement on the 6 zeroth-order constraints
-  double S[36] = {0}, h[6] = {0};
+  // per-contact blocks, summed over the contacts pairwise as the kernel's lanes do
+  // (((c3 + c2) + (c1 + c0)) + ((c7 + c6) + (c5 + c4)), absent contacts 0: hs_kernels.hip fast_solve_lanes)
+  double Sc[8][36] = {}, hc[8][6] = {};
   std::vector<double> Dinv(9 * nc);
   for (int c = 0; c < nc; c++) {
     double L[9];
@@ -1774,12 +1776,24 @@ bool fast_contact_solve(const hso_model* m, const DynRec& d, const std::vector<d
       for (int q = 0; q < 6; q++) {
         double s = 0;
         for (int j = 0; j < 3; j++) s += E[r * 3 + j] * Ac[q * 3 + j];
-        S[6 * r + q] += s;
+        Sc[c][6 * r + q] = s;
       }
       double s = 0;
       for (int j = 0; j < 3; j++) s += E[r * 3 + j] * g[3 * c + j];
-      h[r] += s;
+      hc[c][r] = s;
     }
+  }
+  auto pairwise = [](const double* v) { return ((v[3] + v[2]) + (v[1] + v[0])) + ((v[7] + v[6]) + (v[5] + v[4])); };
+  double S[36], h[6];
+  for (int e = 0; e < 36; e++) {
+    double v[8];
+    for (int c = 0; c < 8; c++) v[c] = Sc[c][e];
+    S[e] = pairwise(v);
+  }
+  for (int r = 0; r < 6; r++) {
+    double v[8];
+    for (int c = 0; c < 8; c++) v[c] = hc[c][r];
+    h[r] = pairwise(v);
   }
   double lam[6];
   for (int r = 0; r < 6; r++) lam[r] = a[r] - h[r];
