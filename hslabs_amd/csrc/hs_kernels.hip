@@ -71,9 +71,10 @@ static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a
 #define HS_MIN_WAVES 3  // fp64 launch-per-step and fixup instantiations (the general-path call): <= 168 VGPRs
 #endif
 #ifndef HS_MIN_WAVES_DEFER
-// the fused step launch (hs::FIX_DEFER): 16 workgroups/CU at 10.1 KB of LDS (hexapod, round 5's PostL layout),
-// <= 128 VGPRs (96 B of spills)
-#define HS_MIN_WAVES_DEFER 4
+// the fused step launch (hs::FIX_DEFER). Round 5's PostL layout fits 16 workgroups/CU (10.1 KB of LDS per
+// hexapod workgroup) and 4 waves/SIMD compile to 128 VGPRs with 96 B of spills, but measured no faster than 3
+// (277.9 vs 280-282 M steps/s at the driver command, same box: profiles/r05_ab_t2.txt)
+#define HS_MIN_WAVES_DEFER 3
 #endif
 #ifndef HS_MIN_WAVES_FORCES
 #define HS_MIN_WAVES_FORCES 3  // solve_forces mode (hs_run_forces): the control step's LDS layout
@@ -167,14 +168,12 @@ struct CentreL {  // fields read after D
   int unreach[HS_LMAX];
 };
 
-struct ForceL {  // solve_forces by limbs (forces_solve); the dense fallback reuses it from sum on (336 reals)
-  real sum[27];           // the sums over the limbs: S and d~, or K and its right-hand side
-  real op[HS_LMAX][24];   // a limb's product operands: the rows of L^-1 [W_mt | d_m] and 1 / D_M, then V and 1 / D_B
-  real pr[HS_LMAX][27];   // a limb's products: S_l and e_l, then K_f and q_f
-  real spare[3];
+struct ForceL {  // solve_forces by limbs (forces_solve): per limb S_l and e_l (a), per foot K_f and q_f
+                 // (b); the dense fallback reuses the space from a[0][27] on (336 reals in all)
+  real a[HS_LMAX][27];
+  real b[HS_LMAX][27];
+  real spare[12];
 };
-static_assert(sizeof(ForceL) >= 336 * sizeof(real), "forces_solve's dense route uses 336 reals from ForceL::sum");
-static_assert(sizeof(ForceL) <= sizeof(StencilL<22>) + 96, "ForceL must not grow the hexapod's LDS union much");
 
 // What the control step keeps once D has consumed the stencil, in the stencil's place: D writes each
 // part's f rows over that part's own stencil rows (every lane reads its rows before it writes, one
@@ -435,19 +434,37 @@ __device__ inline A34 torso_frame(const hs_topo* T, const GaitR& g, const SC3& t
 // and its hip frame (KinFrames, the straight gaits' frames at tv = 0)
 // The chain's products come precombined from the loader (hs_topo::limb_own_rel, limb_hip_rel): one product
 // per frame, every load indexed by the limb alone
+// A limb's setup constants (hs_topo::limb_*), loaded before the gait parameters they do not depend on
+struct LimbPlan {
+  A34 hip, own0;  // limb_hip_rel, limb_own_rel[0] (limb_own_n > 0)
+  real ct[3], com0[3];
+  int own_n;
+};
+__device__ __attribute__((always_inline)) inline LimbPlan load_plan(const hs_topo* T, int L) {
+  LimbPlan p;
+  p.own_n = T->limb_own_n[L];
+  p.hip = load34(T->limb_hip_rel[L]);
+  p.own0 = load34(T->limb_own_rel[L][0]);
+  for (int i = 0; i < 3; i++) {
+    p.ct[i] = (real)T->limb_child_t[L][i];
+    p.com0[i] = (real)T->limb_own_com[L][0][i];
+  }
+  return p;
+}
 __device__ __attribute__((always_inline)) inline void limb_setup(const hs_topo* T, const GaitR& g, const A34& A0, int L,
-                                                                 A34& J0, real* pos0, KinFrames* kf = nullptr) {
+                                                                 const LimbPlan& pl, A34& J0, real* pos0,
+                                                                 KinFrames* kf = nullptr) {
   if (kf)
-    for (int m = 0; m < T->limb_own_n[L]; m++) {
-      const real com[3] = {(real)T->limb_own_com[L][m][0], (real)T->limb_own_com[L][m][1], (real)T->limb_own_com[L][m][2]};
-      store_body(mul(A0, load34(T->limb_own_rel[L][m])), com, kf->own[L][m], BF_W);
+    for (int m = 0; m < pl.own_n; m++) {
+      real com[3];
+      for (int i = 0; i < 3; i++) com[i] = m == 0 ? pl.com0[i] : (real)T->limb_own_com[L][m][i];
+      store_body(mul(A0, m == 0 ? pl.own0 : load34(T->limb_own_rel[L][m])), com, kf->own[L][m], BF_W);
     }
-  J0 = mul(A0, load34(T->limb_hip_rel[L]));
+  J0 = mul(A0, pl.hip);
   if (kf) store34r(J0, kf->J0[L]);
   // get_limb_hip_pos: the child's frame J0 Rz(0) pj_child (Rz(0) = I) at its translation
-  const real ct[3] = {(real)T->limb_child_t[L][0], (real)T->limb_child_t[L][1], (real)T->limb_child_t[L][2]};
   real pos[3];
-  mulp(J0, ct, pos);
+  mulp(J0, pl.ct, pos);
   if (g.foot_shift_type == 0) {                   // setup_foot_shift / shift_pos0
     real sh[3] = {real(0), g.foot_shift, real(0)}, ls[3];
     mulp(A0, sh, ls);
@@ -486,7 +503,7 @@ __device__ __attribute__((always_inline)) inline void gait_setup(const hs_topo* 
     if (L == 0) st.tsc = tsc;
     A34 J0;
     const int j = T->limb_pergen[L];
-    limb_setup(T, g, torso_frame(T, g, tsc), L, J0, st.pos0[j]);
+    limb_setup(T, g, torso_frame(T, g, tsc), L, load_plan(T, L), J0, st.pos0[j]);
     lift_off(nl, j, t_step, st.ts[j], st.xs[j]);
   }
   if (lane == 0) {
@@ -2712,16 +2729,13 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     auto prod = [&](int a, int b) {  // (L^-1 R)_a^T D^-1 (L^-1 R)_b
       return R[0][a] * rdM[0] * R[0][b] + R[1][a] * rdM[1] * R[1][b] + R[2][a] * rdM[2] * R[2][b];
     };
-    // S_l = W_tm M^-1 W_mt and e_l = W_tm M^-1 d_m (27 products) are formed by all 32 lanes (below):
-    // their operands, the W_mt and d_m columns of L^-1 R and 1 / D_M, go to LDS
-    real* const op = fr.op[L];
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-#pragma unroll
-      for (int c = 0; c < 6; c++) op[7 * k + c] = R[k][c];
-      op[7 * k + 6] = R[k][9];
-      op[21 + k] = rdM[k];
+    for (int e = 0; e < 21; e++) {  // S_l = W_tm M^-1 W_mt (packed lower)
+      const TriWalk<> t(e);
+      fr.a[L][e] = prod(t.r, t.c);
     }
+#pragma unroll
+    for (int r = 0; r < 6; r++) fr.a[L][21 + r] = prod(r, 9);  // e_l = W_tm M^-1 d_m
     real d[3];
     for (int t = 0; t < 3; t++) d[t] = fp[t] - P0[t];
 #pragma unroll
@@ -2736,61 +2750,40 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     for (int jj = 0; jj < 3; jj++) rb[jj] = prod(6 + jj, 9);
     Bl[0] = Bd[0]; Bl[3] = Bd[1]; Bl[4] = Bd[2]; Bl[6] = Bd[3]; Bl[7] = Bd[4]; Bl[8] = Bd[5];
     okB = ldl_n<3>(Bl, kForcesBlockGuard, rdB);
+    if (okB) {  // K_f = C~ B^-1 C~^T, q_f = C~ B^-1 r_f, through V = L_B^-1 [C~^T | r_f]
+      real V[3][7];
+      for (int c = 0; c < 6; c++)
+        for (int k = 0; k < 3; k++) V[k][c] = Ct[3 * c + k];
+      for (int k = 0; k < 3; k++) V[k][6] = rb[k];
+#pragma unroll
+      for (int c = 0; c < 7; c++) {
+        V[1][c] -= Bl[3] * V[0][c];
+        V[2][c] -= Bl[6] * V[0][c] + Bl[7] * V[1][c];
+      }
+      auto vp = [&](int a, int b) {
+        return V[0][a] * rdB[0] * V[0][b] + V[1][a] * rdB[1] * V[1][b] + V[2][a] * rdB[2] * V[2][b];
+      };
+#pragma unroll
+      for (int e = 0; e < 21; e++) {
+        const TriWalk<> t(e);
+        fr.b[L][e] = vp(t.r, t.c);
+      }
+#pragma unroll
+      for (int r = 0; r < 6; r++) fr.b[L][21 + r] = vp(r, 6);
+    }
   }
   const bool fast = !dense && half_ballot(lane < nl && !okB) == 0;
   wave_sync();
   STAMP(4);
-  // a limb's 27 products from its operands o (rows of 7 at 0, 7, 14; 1 / D at 21): entry e < 21 is the
-  // packed lower (r, c) of the 6 x 6 block, e >= 21 the 6-vector (column 6)
-  auto limb_products = [&]() {
-    for (int p = lane; p < 27 * nl; p += HALF) {
-      const int L = p / 27, e = p - 27 * L;
-      int a = e - 21, b = 6;
-      if (e < 21) {
-        const TriWalk<> t(e);
-        a = t.r;
-        b = t.c;
-      }
-      const real* o = fr.op[L];
-      fr.pr[L][e] = o[a] * o[21] * o[b] + o[7 + a] * o[22] * o[7 + b] + o[14 + a] * o[23] * o[14 + b];
-    }
-  };
-  limb_products();  // S_l, e_l
-  wave_sync();
-  if (lane < FSUM) {  // their sums over the limbs, in limb order
+  if (lane < FSUM) {  // sums over the limbs, in limb order; W_tt and the torso part of d added
     real s = 0;
-    for (int L = 0; L < nl; L++) s += fr.pr[L][lane];
-    fr.sum[lane] = s;
-  }
-  if (fast && lane < nl) {  // K_f = C~ B^-1 C~^T, q_f = C~ B^-1 r_f, through V = L_B^-1 [C~^T | r_f]: V, 1 / D_B
-    real* const op = fr.op[lane];
-#pragma unroll
-    for (int c = 0; c < 7; c++) {
-      const real v0 = c < 6 ? Ct[3 * c] : rb[0];
-      const real v1 = (c < 6 ? Ct[3 * c + 1] : rb[1]) - Bl[3] * v0;
-      const real v2 = (c < 6 ? Ct[3 * c + 2] : rb[2]) - (Bl[6] * v0 + Bl[7] * v1);
-      op[c] = v0;
-      op[7 + c] = v1;
-      op[14 + c] = v2;
-    }
-#pragma unroll
-    for (int k = 0; k < 3; k++) op[21 + k] = rdB[k];
-  }
-  wave_sync();
-  if (fast) {
-    limb_products();  // K_f, q_f
-    wave_sync();
-  }
-  if (lane < FSUM) {  // W_tt and the torso part of d added
-    const real sa = fr.sum[lane];
-    real sb = 0;
-    if (fast)
-      for (int L = 0; L < nl; L++) sb += fr.pr[L][lane];
+    for (int L = 0; L < nl; L++) s += fast ? ((lane < 21) ? fr.b[L][lane] - fr.a[L][lane] : fr.b[L][lane] + fr.a[L][lane])
+                                          : fr.a[L][lane];
     const real dt = (lane < 21) ? real(0) : (lane < 24 ? sv.x[lane - 21] : sv.x[3 * n + lane - 24]);
     // fast: K = W_tt - sum S_l + sum K_f, rhs = sum (q_f + e_l) - d_t; else S = W_tt - sum S_l, d~ = d_t - sum e_l
-    const real v = (lane < 21) ? (fast ? wtt_entry(lane, ts, n) + (sb - sa) : wtt_entry(lane, ts, n) - sa)
-                               : (fast ? (sb + sa) - dt : dt - sa);
-    fr.sum[lane] = v;  // lane reads column `lane` only
+    const real v = (lane < 21) ? (fast ? wtt_entry(lane, ts, n) + s : wtt_entry(lane, ts, n) - s)
+                               : (fast ? s - dt : dt - s);
+    fr.a[0][lane] = v;  // lane reads column `lane` only, so slot 0 takes the sums in place
   }
   wave_sync();
   STAMP(5);
@@ -2800,8 +2793,8 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
 #pragma unroll
     for (int r = 0; r < 6; r++) {
 #pragma unroll
-      for (int c = 0; c < 6; c++) K[6 * r + c] = (c <= r) ? fr.sum[pk(r, c)] : real(0);
-      lam[r] = fr.sum[21 + r];
+      for (int c = 0; c < 6; c++) K[6 * r + c] = (c <= r) ? fr.a[0][pk(r, c)] : real(0);
+      lam[r] = fr.a[0][21 + r];
     }
     ldl_n<6>(K, real(0), rd);  // >= I
     ldl_solve_n<6>(K, rd, lam);
@@ -2821,7 +2814,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
   }
   // dense normal equations over the feet (a B_f near singular): N = diag(B_f) + V^T D_S^-1 V with
   // S = L_S D_S L_S^T, V = L_S^-1 C~, r = r_b + V^T D_S^-1 L_S^-1 d~
-  real* const base = fr.sum;
+  real* const base = &fr.a[0][0];
   real* const Vm = base + FSUM;       // [6][HS_KMAX]
   real* const vv = Vm + 6 * HS_KMAX;  // 6
   real* const rdS = vv + 6;           // 6
@@ -2972,10 +2965,11 @@ static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 #define HS_PREP_ROWS 5  // table rows per lane (round 4, B = 4096, 24 rows: 3, 4, 5, 6, 8 rows give 24.1, 25.0, 23.4, 24.9, 29.7 us)
 #endif
 #ifndef HS_PREP_WAVES
-#define HS_PREP_WAVES 2  // waves per SIMD the register budget allows (196 VGPRs; 3 or 4 spill)
+#define HS_PREP_WAVES 2  // waves per SIMD (253 VGPRs, no scratch; at 3 the turning rows spill 352 B: tools/isa_stats.py)
 #endif
 #ifndef HS_PREP_WPB
-#define HS_PREP_WPB 1  // wavefronts per workgroup (each a group of lanes of its own: only wave-local exchanges)
+#define HS_PREP_WPB 4  // wavefronts per workgroup (each a group of lanes of its own: only wave-local exchanges);
+                       // 4: the pass's wavefronts start sooner, 22.9 -> 20.5 us per driver job (r05_ab_t2.txt)
 #endif
 // an exchange through LDS among the lanes of one wavefront: LDS operations of a wavefront complete in
 // order, so only the compiler must not move the accesses across it (no s_barrier: with several
@@ -2997,6 +2991,10 @@ __host__ __device__ inline int64_t prep_blocks(int n_waves, int ttab_n, int nli)
   return 8 * ((waves_per_xcd + HS_PREP_WPB - 1) / HS_PREP_WPB);
 }
 
+// MIXED: a mixed-topology launch (launch_map::wave_model), whose lane groups of one wavefront may hold
+// different models; otherwise the topology pointer is the kernel argument itself, wave-uniform, so its
+// rollout-independent entries come through the scalar cache
+template <bool MIXED>
 __global__ __launch_bounds__(WAVE * HS_PREP_WPB, HS_PREP_WAVES) void hs_prep_kernel(const hs_topo* __restrict__ T0,
                                                                    hs_run_args a, RolloutWS* __restrict__ rws,
                                                                    hs::launch_map mp) {
@@ -3022,7 +3020,7 @@ __global__ __launch_bounds__(WAVE * HS_PREP_WPB, HS_PREP_WAVES) void hs_prep_ker
   const hs_topo* __restrict__ T = T0;
   if (on) {
     b = mp.wave_rollouts ? mp.wave_rollouts[2 * w + sub] : 2 * w + sub;
-    if (mp.wave_model) T = T0 + mp.wave_model[w];
+    if (MIXED) T = T0 + mp.wave_model[w];
     on = b >= 0 && b < a.n_rollouts && L < T->n_limbs;
   }
   GaitR g;
@@ -3032,13 +3030,15 @@ __global__ __launch_bounds__(WAVE * HS_PREP_WPB, HS_PREP_WAVES) void hs_prep_ker
   real my_rad = 0;
   SC3 tsc;
   RolloutWS* __restrict__ ws = rws + b;
+  LimbPlan plan;
   if (on) {
+    plan = load_plan(T, L);  // issued before the gait parameters: its waits do not queue behind them
     g = load_gait(a.params[b]);
     straight = g.curvature == 0 && !g.rec_xf;  // kin_sample's turning / record-transform test
     const int nl = T->n_limbs, j = T->limb_pergen[L];
     tsc = sincos3(g.torso_angles[0], g.torso_angles[1], g.torso_angles[2]);
     const A34 A0 = torso_frame(T, g, tsc);
-    limb_setup(T, g, A0, L, J0, pos0, chunk == 0 ? &ws->kf : nullptr);
+    limb_setup(T, g, A0, L, plan, J0, pos0, chunk == 0 ? &ws->kf : nullptr);
     t_step = step_fraction(g, nl);
     lift_off(nl, j, t_step, ts, xs);
     v = g.step_length / g.period;  // pergensetup::set_TLh
@@ -3501,7 +3501,10 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   RolloutWS* ws = (RolloutWS*)workspace;
   if (mp.setup_only) {  // the call's preparation pass: setup record, sample times, IK table
     const int64_t blocks = prep_blocks(mp.n_waves, mp.ttab_n, mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX);
-    hipLaunchKernelGGL(hs_prep_kernel, dim3((unsigned)blocks), dim3(WAVE * HS_PREP_WPB), 0, st, d_topo, a, ws, mp);
+    if (mp.wave_model)
+      hipLaunchKernelGGL(hs_prep_kernel<true>, dim3((unsigned)blocks), dim3(WAVE * HS_PREP_WPB), 0, st, d_topo, a, ws, mp);
+    else
+      hipLaunchKernelGGL(hs_prep_kernel<false>, dim3((unsigned)blocks), dim3(WAVE * HS_PREP_WPB), 0, st, d_topo, a, ws, mp);
     return (int)hipGetLastError();
   }
   launch_map m = mp;

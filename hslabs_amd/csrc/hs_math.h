@@ -199,38 +199,6 @@ __device__ inline real norm3(const real* v) {
 // (x - (-l0) = x + l0 and the angle offsets are exact). mod_twopi (visualization.cpp:73-79): atan2
 // is already in [-pi, pi], and theta in [0, 2 pi] (yxx) or [-pi/2, 3 pi/2] (zxx) needs at most one
 // subtraction of 2 pi.
-// acos for the limb IK (three per solve). fp64: asin(z) = z + z t P(t), t = z^2, |z| <= 1/2 (P: degree 11,
-// interpolating (asin(sqrt t) - sqrt t) / t^(3/2) at Chebyshev nodes of [0, 1/4] in 40-digit arithmetic,
-// tools/acos_fit.py); |x| <= 1/2: pi/2 - asin(x), else 2 asin(sqrt((1 - |x|) / 2)) for x > 0 and pi minus
-// that for x < 0. Within 1 ulp of glibc's acos (the reference's) on 10^5 points of [-1, 1] and at the
-// ends; ~35 VALU instructions, branch-free (the square root always taken), against ocml's ~93 -- the IK
-// table rows of the preparation pass were issue-bound on them. NaN outside [-1, 1] like acos.
-__device__ inline real hs_acos(real x) {
-#if HS_REAL_IS_FLOAT || defined(HS_OCML_ACOS)
-  return acos(x);
-#else
-  const double ax = fabs(x);
-  const bool mid = ax <= 0.5;
-  const double z = mid ? x : sqrt((1.0 - ax) * 0.5);
-  const double t = z * z;
-  double p = 0.028169218060881414;
-  p = p * t + -0.010749050339697808;
-  p = p * t + 0.01603551434914882;
-  p = p * t + 0.0078029494773533175;
-  p = p * t + 0.011875494382636922;
-  p = p * t + 0.013929652902326633;
-  p = p * t + 0.017355259955786323;
-  p = p * t + 0.02237204763174451;
-  p = p * t + 0.03038194736709848;
-  p = p * t + 0.044642857103423646;
-  p = p * t + 0.07500000000020764;
-  p = p * t + 0.1666666666666665;
-  const double as = z + z * t * p;  // asin(z)
-  const double r2 = 2 * as;
-  return mid ? 1.5707963267948966 - as : (x > 0 ? r2 : kPi - r2);
-#endif
-}
-
 __device__ inline void limb_ik(int kind, const real* ls, int ysign, const real* p, real* ja, bool ignore_reach,
                                bool& unreach, bool& fail) {
   const real l0 = ls[0], l1 = ls[1], l2 = ls[2];
@@ -249,13 +217,13 @@ __device__ inline void limb_ik(int kind, const real* ls, int ysign, const real* 
   const real phi = atan2(p[0], p[1]);
   const real c = (p[2] - z0) / l;
   const real toff = yxx ? (s0 > 0 ? real(0) : kPi) : (s0 > 0 ? -kPi / 2 : kPi / 2);
-  real theta = hs_acos(c) + toff;
+  real theta = acos(c) + toff;
   theta = (theta > kPi) ? theta - 2 * kPi : theta;
   const real ll = l * l;
   const real del = l2 * l2 - l1 * l1;
   const real sb = yxx ? real(s0) : real(1);  // s1 s0 (yxx) or s1 (zxx), s1 = 1 (bend)
-  const real beta = sb * hs_acos((ll - del) / (2 * l1 * l));
-  const real gamma = sb * hs_acos((ll + del) / (2 * l2 * l));
+  const real beta = sb * acos((ll - del) / (2 * l1 * l));
+  const real gamma = sb * acos((ll + del) / (2 * l2 * l));
   ja[0] = -phi;
   ja[1] = -theta + beta;
   ja[2] = -(beta + gamma);
