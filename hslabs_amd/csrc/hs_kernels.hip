@@ -3086,6 +3086,38 @@ __global__ __launch_bounds__(WAVE * HS_PREP_WPB, HS_PREP_WAVES) void hs_prep_ker
   real t = sample_time_sum(dt, mp.ktab_lo + r0);
   // kin_sample's foot target, hip frame and limb IK at samples ktab_lo + r, one loop per kind of gait
   // (a lane's kind is fixed: the other loop's values are not live in this one)
+#ifndef HS_PREP_ILP
+#define HS_PREP_ILP 1
+#endif
+#if HS_PREP_ILP > 1
+  if (table && straight) {
+    // the chunk's rows as HS_PREP_ILP independent chains at a time (the rows are latency-bound: one IK's
+    // dependent transcendental chain per lane at 2 waves/SIMD); rows past r1 are computed, not stored
+    for (int r = r0; r < r1; r += HS_PREP_ILP) {
+      real tr[HS_PREP_ILP], ja[HS_PREP_ILP][3];
+      bool bad[HS_PREP_ILP];
+#pragma unroll
+      for (int k = 0; k < HS_PREP_ILP; k++) {
+        if (k > 0 || r > r0) t += dt;  // the loop's additions, in order
+        tr[k] = t;
+      }
+#pragma unroll
+      for (int k = 0; k < HS_PREP_ILP; k++) {
+        real dx, dz;
+        limb_step(g, tr[k], ts, xs, t_step, dx, dz);
+        const real target[3] = {dx + pos0[0], real(0) + pos0[1], dz + pos0[2]};
+        hip_ik(T, L, frame_at(J0, u, tr[k] * v), target, ir, ja[k], bad[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < HS_PREP_ILP; k++)
+        if (r + k < r1) {
+          if (L == 0) ws->t_tab[r + k] = tr[k];
+          store_row(r + k, ja[k], bad[k]);
+        }
+    }
+    STAMP(27);
+  } else
+#endif
   if (!table || straight) {
 #pragma unroll 1
     for (int r = r0; r < r1; r++) {
