@@ -68,13 +68,10 @@ constexpr int HALF = 32;     // lanes per rollout: two rollouts per wavefront
 constexpr int NS = 5;        // samples in the derivative stencil (periodic.cpp:192-202)
 static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a rollout's lane maps exceed 32");
 #ifndef HS_MIN_WAVES
-#define HS_MIN_WAVES 3  // fp64 launch-per-step and fixup instantiations (the general-path call): <= 168 VGPRs
-#endif
-#ifndef HS_MIN_WAVES_DEFER
-// the fused step launch (hs::FIX_DEFER). Round 5's PostL layout fits 16 workgroups/CU (10.1 KB of LDS per
-// hexapod workgroup) and 4 waves/SIMD compile to 128 VGPRs with 96 B of spills, but measured no faster than 3
-// (277.9 vs 280-282 M steps/s at the driver command, same box: profiles/r05_ab_t2.txt)
-#define HS_MIN_WAVES_DEFER 3
+// fp64: <= 168 VGPRs. Round 5's PostL layout fits 16 workgroups/CU (10.1 KB of LDS per hexapod workgroup),
+// and the fused step launch compiles to 128 VGPRs with 96 B of spills at 4 waves/SIMD, but measured no
+// faster than at 3 (profiles/r05_ab_t2.txt, r05_ab_t3.txt)
+#define HS_MIN_WAVES 3
 #endif
 #ifndef HS_MIN_WAVES_FORCES
 #define HS_MIN_WAVES_FORCES 3  // solve_forces mode (hs_run_forces): the control step's LDS layout
@@ -438,11 +435,12 @@ __device__ inline A34 torso_frame(const hs_topo* T, const GaitR& g, const SC3& t
 struct LimbPlan {
   A34 hip, own0;  // limb_hip_rel, limb_own_rel[0] (limb_own_n > 0)
   real ct[3], com0[3];
-  int own_n;
+  int own_n, ysign;  // ysign: limb_ysign, read by the table rows' IK
 };
 __device__ __attribute__((always_inline)) inline LimbPlan load_plan(const hs_topo* T, int L) {
   LimbPlan p;
   p.own_n = T->limb_own_n[L];
+  p.ysign = T->limb_ysign[L];
   p.hip = load34(T->limb_hip_rel[L]);
   p.own0 = load34(T->limb_own_rel[L][0]);
   for (int i = 0; i < 3; i++) {
@@ -802,15 +800,21 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
 // set_rec's foot target of limb L at time t and the limb IK from the hip frame J (kin_sample's
 // sequence from the gait record on); bad = unreachable (ignore_reach) or failed
 // the limb IK of limb L for a foot target, from its hip joint frame J (lik.cpp:341-347, 151-223)
-__device__ __attribute__((always_inline)) inline void hip_ik(const hs_topo* T, int L, const A34& J, const real* target,
-                                                             bool ignore_reach, real* ja, bool& bad) {
+// (kind, ls, ysign: the model's IK variant, link lengths and the limb's side, read by the caller)
+__device__ __attribute__((always_inline)) inline void hip_ik_k(const A34& J, const real* target, int kind,
+                                                               const real* ls, int ysign, bool ignore_reach, real* ja,
+                                                               bool& bad) {
   const A34 Jinv = invert(J);
   real pl[3];
   mulp(Jinv, target, pl);
   bool unreach = false, fail = false;
-  const real ls[3] = {(real)T->ls[0], (real)T->ls[1], (real)T->ls[2]};
-  limb_ik(T->lik_kind, ls, T->limb_ysign[L], pl, ja, ignore_reach, unreach, fail);
+  limb_ik(kind, ls, ysign, pl, ja, ignore_reach, unreach, fail);
   bad = unreach || fail;
+}
+__device__ __attribute__((always_inline)) inline void hip_ik(const hs_topo* T, int L, const A34& J, const real* target,
+                                                             bool ignore_reach, real* ja, bool& bad) {
+  const real ls[3] = {(real)T->ls[0], (real)T->ls[1], (real)T->ls[2]};
+  hip_ik_k(J, target, T->lik_kind, ls, T->limb_ysign[L], ignore_reach, ja, bad);
 }
 
 __device__ __attribute__((always_inline)) inline void straight_ik(const hs_topo* T, const GaitR& g,
@@ -1110,9 +1114,6 @@ __device__ __attribute__((always_inline)) inline void particular_sub(const hs_to
   real F[3] = {0, 0, 0}, V[3] = {0, 0, 0};
   const bool leafward = on && parent >= 0;
   if (leafward) {  // the subtree's range, in preorder
-#ifdef HS_PART_UNROLL
-#pragma unroll HS_PART_UNROLL
-#endif
     for (int m = 0; m < sz; m++) {
       const int kx = lane + m;
       for (int j = 0; j < 3; j++) { F[j] += sv.x[3 * kx + j]; V[j] += sv.x[3 * (n + kx) + j]; }
@@ -3076,6 +3077,8 @@ __global__ __launch_bounds__(WAVE * HS_PREP_WPB, HS_PREP_WAVES) void hs_prep_ker
   const bool table = mp.ktab_n > 0;
   const hs_aff34& Jp0 = T->node[0].J_A_parent;
   const real u[3] = {(real)Jp0.m[0], (real)Jp0.m[1], (real)Jp0.m[2]};
+  const real ls[3] = {(real)T->ls[0], (real)T->ls[1], (real)T->ls[2]};
+  const int kind = T->lik_kind;
   const bool ir = a.ignore_reach != 0;
   auto store_row = [&](int r, const real* ja, bool bad) {
     real* e = ws->ktab[r][L];
@@ -3086,38 +3089,6 @@ __global__ __launch_bounds__(WAVE * HS_PREP_WPB, HS_PREP_WAVES) void hs_prep_ker
   real t = sample_time_sum(dt, mp.ktab_lo + r0);
   // kin_sample's foot target, hip frame and limb IK at samples ktab_lo + r, one loop per kind of gait
   // (a lane's kind is fixed: the other loop's values are not live in this one)
-#ifndef HS_PREP_ILP
-#define HS_PREP_ILP 1
-#endif
-#if HS_PREP_ILP > 1
-  if (table && straight) {
-    // the chunk's rows as HS_PREP_ILP independent chains at a time (the rows are latency-bound: one IK's
-    // dependent transcendental chain per lane at 2 waves/SIMD); rows past r1 are computed, not stored
-    for (int r = r0; r < r1; r += HS_PREP_ILP) {
-      real tr[HS_PREP_ILP], ja[HS_PREP_ILP][3];
-      bool bad[HS_PREP_ILP];
-#pragma unroll
-      for (int k = 0; k < HS_PREP_ILP; k++) {
-        if (k > 0 || r > r0) t += dt;  // the loop's additions, in order
-        tr[k] = t;
-      }
-#pragma unroll
-      for (int k = 0; k < HS_PREP_ILP; k++) {
-        real dx, dz;
-        limb_step(g, tr[k], ts, xs, t_step, dx, dz);
-        const real target[3] = {dx + pos0[0], real(0) + pos0[1], dz + pos0[2]};
-        hip_ik(T, L, frame_at(J0, u, tr[k] * v), target, ir, ja[k], bad[k]);
-      }
-#pragma unroll
-      for (int k = 0; k < HS_PREP_ILP; k++)
-        if (r + k < r1) {
-          if (L == 0) ws->t_tab[r + k] = tr[k];
-          store_row(r + k, ja[k], bad[k]);
-        }
-    }
-    STAMP(27);
-  } else
-#endif
   if (!table || straight) {
 #pragma unroll 1
     for (int r = r0; r < r1; r++) {
@@ -3129,7 +3100,7 @@ __global__ __launch_bounds__(WAVE * HS_PREP_WPB, HS_PREP_WAVES) void hs_prep_ker
         const real target[3] = {dx + pos0[0], real(0) + pos0[1], dz + pos0[2]};
         real ja[3];
         bool bad;
-        hip_ik(T, L, frame_at(J0, u, t * v), target, ir, ja, bad);
+        hip_ik_k(frame_at(J0, u, t * v), target, kind, ls, plan.ysign, ir, ja, bad);
         store_row(r, ja, bad);
       }
       if (r == r0) STAMP(27);
@@ -3350,23 +3321,10 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
 // without it; SOLVE, the fixup launch over the deferred items (its own instantiation, so the loop
 // costs the other two nothing)
 template <int NM, bool FORCES, int MODE>
-#ifdef HS_ROLLOUT_VGPRS
-#define HS_ROLLOUT_ATTR __attribute__((amdgpu_waves_per_eu(HS_ROLLOUT_VGPRS, HS_ROLLOUT_VGPRS)))
-#else
-#define HS_ROLLOUT_ATTR
-#endif
-__global__ HS_ROLLOUT_ATTR __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES
-                                                     : (HS_REAL_IS_FLOAT ? HS_MIN_WAVES_F32
-                                                                         : (MODE == hs::FIX_DEFER ? HS_MIN_WAVES_DEFER
-                                                                                                  : HS_MIN_WAVES))) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
+__global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FLOAT ? HS_MIN_WAVES_F32 : HS_MIN_WAVES)) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
                                                                                  hs_run_args a, RolloutWS* __restrict__ rws,
                                                                                  hs::launch_map mp) {
-#ifdef HS_PROBE_DYN_LDS  // register-budget probe only (tools/isa_stats.py): LDS size hidden from the compiler
-  extern __shared__ char hs_dyn_lds[];
-  Smem<NM, FORCES>* smem = reinterpret_cast<Smem<NM, FORCES>*>(hs_dyn_lds);
-#else
   __shared__ Smem<NM, FORCES> smem[2];
-#endif
   RSTAMP(16);
   STAMP(15);
   if constexpr (MODE == hs::FIX_SOLVE) {  // the deferred (step, rollout) items
