@@ -68,10 +68,16 @@ constexpr int HALF = 32;     // lanes per rollout: two rollouts per wavefront
 constexpr int NS = 5;        // samples in the derivative stencil (periodic.cpp:192-202)
 static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a rollout's lane maps exceed 32");
 #ifndef HS_MIN_WAVES
-// fp64: <= 168 VGPRs. Round 5's PostL layout fits 16 workgroups/CU (10.1 KB of LDS per hexapod workgroup),
-// and the fused step launch compiles to 128 VGPRs with 96 B of spills at 4 waves/SIMD, but measured no
-// faster than at 3 (profiles/r05_ab_t2.txt, r05_ab_t3.txt)
+// fp64: <= 168 VGPRs: the per-step launch (its general path called out of line, scratch frame) and the
+// fixup launch; 4 waves/SIMD measured 7-10 % slower for the per-step launch (profiles/r05_s4_ab.txt)
 #define HS_MIN_WAVES 3
+#endif
+#ifndef HS_MIN_WAVES_DEFER
+// the fused step launch (FIX_DEFER: no general-path call) at 4 waves/SIMD: 128 VGPRs, its spills (108 B)
+// in the per-wave entry and the paths the straight gaits with a table do not take (tools/spill_lines.py);
+// the PostL layout's 10.1 KB of LDS per hexapod workgroup fits 16 workgroups/CU. Same box, interleaved:
+// driver command 286.4 -> 296.2 M steps/s, K = 200 365.8 -> 381.9 M (profiles/r05_s4_ab.txt)
+#define HS_MIN_WAVES_DEFER 4
 #endif
 #ifndef HS_MIN_WAVES_FORCES
 #define HS_MIN_WAVES_FORCES 3  // solve_forces mode (hs_run_forces): the control step's LDS layout
@@ -793,7 +799,7 @@ __device__ __attribute__((always_inline)) inline void kin_sample(const hs_topo* 
   STAMP(22);
   real sq[3], cq[3];
 #pragma unroll
-  for (int kk = 0; kk < 3; kk++) sincos(ja[kk], &sq[kk], &cq[kk]);
+  for (int kk = 0; kk < 3; kk++) sincos_k(ja[kk], &sq[kk], &cq[kk]);
   limb_fk(T, L, J, ja, sq, cq, wq, w, k);
 }
 
@@ -939,14 +945,14 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
 #pragma unroll
     for (int kk = 0; kk < 3; kk++) {
       ja[kk] = kte[kk];
-      sincos(ja[kk], &sq[kk], &cq[kk]);
+      sincos_k(ja[kk], &sq[kk], &cq[kk]);
     }
     bad = kbad;
     STAMP(21);
   } else {
     straight_ik(T, g, gp, st, t, L, J, ignore_reach, ja, bad);
 #pragma unroll
-    for (int kk = 0; kk < 3; kk++) sincos(ja[kk], &sq[kk], &cq[kk]);
+    for (int kk = 0; kk < 3; kk++) sincos_k(ja[kk], &sq[kk], &cq[kk]);
   }
   if (w.want_centre(k)) w.unreach(k, L) = bad ? 1 : 0;
   STAMP(22);
@@ -981,7 +987,7 @@ __device__ __attribute__((always_inline)) inline void kin_sample_tab(const hs_to
 #pragma unroll
   for (int kk = 0; kk < 3; kk++) {
     ja[kk] = kte[kk];
-    sincos(ja[kk], &sq[kk], &cq[kk]);
+    sincos_k(ja[kk], &sq[kk], &cq[kk]);
   }
   if (w.want_centre(k)) w.unreach(k, L) = bad ? 1 : 0;
   STAMP(21);
@@ -3321,7 +3327,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
 // without it; SOLVE, the fixup launch over the deferred items (its own instantiation, so the loop
 // costs the other two nothing)
 template <int NM, bool FORCES, int MODE>
-__global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FLOAT ? HS_MIN_WAVES_F32 : HS_MIN_WAVES)) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
+__global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FLOAT ? HS_MIN_WAVES_F32 : (MODE == hs::FIX_DEFER ? HS_MIN_WAVES_DEFER : HS_MIN_WAVES))) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
                                                                                  hs_run_args a, RolloutWS* __restrict__ rws,
                                                                                  hs::launch_map mp) {
   __shared__ Smem<NM, FORCES> smem[2];

@@ -97,6 +97,41 @@ struct SC3 {
 
 #if HS_REAL_IS_FLOAT
 __device__ inline void sincos(float x, float* s, float* c) { sincosf(x, s, c); }
+__device__ inline void sincos_k(float x, float* s, float* c) { sincosf(x, s, c); }
+#else
+// sin and cos of an angle of moderate size (joint values, step phases: |x| < 2^20) for the rollout
+// kernels: n = rint(x 2/pi), r = x - n pi/2 in two FMAs (the first exact: r is a multiple of x's or
+// pi/2's ulp and |r| <= pi/4), then the fdlibm kernel polynomials on |r| <= pi/4 and the quadrant's
+// swap and signs -- about half the instructions of the library's sincos (whose reduction carries a
+// double-double tail and whose large-argument path shares the code), within ~1 ulp of it. Larger or
+// non-finite x: the library's sincos.
+__device__ inline void sincos_k(double x, double* s, double* c) {
+  if (!(fabs(x) < 0x1p20)) {
+    ::sincos(x, s, c);
+    return;
+  }
+  const double n = rint(x * 6.36619772367581382433e-01);  // 2/pi
+  const double r = fma(-n, 6.12323399573676603587e-17, fma(-n, 1.57079632679489655800e+00, x));
+  const double z = r * r;
+  // __kernel_sin (S1..S6) and __kernel_cos (C1..C6) of fdlibm, tail argument 0
+  const double ps = 8.33333333332248946124e-03 +
+                    z * (-1.98412698298579493134e-04 +
+                         z * (2.75573137070700676789e-06 + z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
+  const double sr = r + (z * r) * (-1.66666666666666324348e-01 + z * ps);
+  const double pc = z * (4.16666666666666019037e-02 +
+                         z * (-1.38888888888741095749e-03 +
+                              z * (2.48015872894767294178e-05 +
+                                   z * (-2.75573143513906633035e-07 +
+                                        z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+  const double hz = 0.5 * z, w = 1.0 - hz;
+  const double cr = w + (((1.0 - w) - hz) + z * pc);
+  const int q = (int)n;
+  double ss = (q & 1) ? cr : sr, cc = (q & 1) ? sr : cr;
+  if (q & 2) ss = -ss;
+  if ((q + 1) & 2) cc = -cc;
+  *s = ss;
+  *c = cc;
+}
 #endif
 
 __device__ inline SC3 sincos3(real phi, real theta, real psi) {
