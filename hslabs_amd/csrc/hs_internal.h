@@ -47,7 +47,8 @@ struct launch_map {
   double *pd_tau, *pd_q0, *pd_dq0;
   int32_t st_tau, st_cf, st_q, st_x;  // output row strides (mixed: maxima over the models)
   // fused steps (hs_run_calls): one launch runs fused_n steps x fused_w wavefronts, wavefront
-  // blockIdx = local step * fused_w + batch wavefront; global step s = fused_s0 + local step is
+  // blockIdx -> (local step, batch wavefront) by groups of batch wavefronts (fused_coords in
+  // hs_kernels.hip: a group's steps in order, its wavefronts fastest); global step s = fused_s0 + local step is
   // call s / fused_h, step s % fused_h of that call, output row s; the step's work goes to
   // fused_work[s][b] (summed in order afterwards), the general-path scratch to
   // fused_gen[local step][b]. setup_only: store the gait setup and return.

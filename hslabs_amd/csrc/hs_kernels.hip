@@ -3323,6 +3323,27 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   }
 }
 
+// A fused launch's block -> (local step, batch wavefront): groups of HS_FUSED_GROUP batch wavefronts
+// (a multiple of 8, so a wavefront's steps stay on its XCD, block % 8), each group's steps in order,
+// the group's wavefronts fastest. A rollout's steps then run close together in time, and its setup
+// record, frames and table rows, read by every step, are fetched into the XCD's L2 once per call
+// instead of once per sweep of the whole batch over a step (whose output stores evict them)
+#ifndef HS_FUSED_GROUP
+#define HS_FUSED_GROUP 256
+#endif
+__device__ inline void fused_coords(int blk, int W, int n, int& fstep, int& wid) {
+#if HS_FUSED_GROUP > 0
+  const int q = blk / (HS_FUSED_GROUP * n), g0 = q * HS_FUSED_GROUP;
+  const int gw = W - g0 < HS_FUSED_GROUP ? W - g0 : HS_FUSED_GROUP;  // the last group may be narrower
+  const int r = blk - g0 * n;
+  fstep = r / gw;
+  wid = g0 + r % gw;
+#else
+  fstep = blk / W;
+  wid = blk % W;
+#endif
+}
+
 // MODE (hs::FIX_*): NONE, the step with the general path out of line; DEFER, the fused step launch
 // without it; SOLVE, the fixup launch over the deferred items (its own instantiation, so the loop
 // costs the other two nothing)
@@ -3356,8 +3377,8 @@ __global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FL
     }
   } else {
     // fused steps: this wavefront's step and its wavefront within the batch
-    const int fstep = mp.fused_w ? (int)(blockIdx.x / mp.fused_w) : 0;
-    const int wid = mp.fused_w ? (int)(blockIdx.x % mp.fused_w) : (int)blockIdx.x;
+    int fstep = 0, wid = (int)blockIdx.x;
+    if (mp.fused_w) fused_coords((int)blockIdx.x, mp.fused_w, mp.fused_n, fstep, wid);
     rollout_wave<NM, FORCES, MODE == hs::FIX_DEFER>(T0, a, rws, mp, smem, fstep, wid, -1);
   }
 }
