@@ -871,7 +871,7 @@ __device__ __attribute__((always_inline)) inline StraightPre straight_preload(co
 // preloaded values (straight_preload)
 template <class W>
 __device__ __attribute__((always_inline)) inline void kin_sample_straight(
-    const hs_topo* T, const GaitR& g, const hs_gait_params& gp, const SetupL& st, int isample, int L,
+    const hs_topo* T, const hs_gait_params& gp, const SetupL& st, int isample, int L,
     bool ignore_reach, const W& w, int k, const StraightPre& pre, const KinFrames& kf, const real* kt,
     const uint8_t* kb, int ktab_lo) {
   const real t = pre.t;
@@ -916,10 +916,10 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
   if (L == 0) {
     if (wq) {
       real* q = w.q(k);
-      q[0] = g.torso_pos[0] + tv;
-      q[1] = g.torso_pos[1];
-      q[2] = g.torso_pos[2];
-      for (int i = 0; i < 3; i++) q[3 + i] = g.torso_angles[i];
+      q[0] = (real)gp.torso_pos[0] + tv;
+      q[1] = (real)gp.torso_pos[1];
+      q[2] = (real)gp.torso_pos[2];
+      for (int i = 0; i < 3; i++) q[3 + i] = (real)gp.torso_angles[i];
     }
     // node_features of the torso: its joint frame J = I * J_A_parent, not a foot
     if (w.want_pos(k)) {
@@ -950,7 +950,7 @@ __device__ __attribute__((always_inline)) inline void kin_sample_straight(
     bad = kbad;
     STAMP(21);
   } else {
-    straight_ik(T, g, gp, st, t, L, J, ignore_reach, ja, bad);
+    straight_ik(T, load_gait(gp), gp, st, t, L, J, ignore_reach, ja, bad);  // untabulated calls only
 #pragma unroll
     for (int kk = 0; kk < 3; kk++) sincos_k(ja[kk], &sq[kk], &cq[kk]);
   }
@@ -2453,13 +2453,12 @@ __device__ inline void reduce_rollouts(const hs_run_args& a, real total_mass, co
 // step's half-wave stores nothing and `deferred` is set), so this instantiation has no call to the
 // out-of-line general path: the call alone costs the whole kernel SGPRs (spills in the hot solve
 // region) and 2.4 % of the step time
-// hinge_id, hinge_foot: this lane's motor's part and foot (lanes < nmj), and dt (SetupL::dt), loaded at the
-// wave's start (a value read from the setup record later would be read again after every output store,
-// which may alias it)
+// dt (SetupL::dt) is loaded at the wave's start (a value read from the setup record later would be read
+// again after every output store, which may alias it)
 template <bool DEFER, class W, class SV>
 __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, const hs_run_args& a, const hs::launch_map& mp, real dt, SV& sv,
                      FastL& fl, const W& w, SolveWS* G, int b, bool live, int h,
-                     real& work, bool& deferred, bool may_general, int lane, int hinge_id, int hinge_foot) {
+                     real& work, bool& deferred, bool may_general, int lane) {
   const int n = T->n, nmj = T->nmj, nf = T->nf, cfg = T->cfg, nl = T->n_limbs;
   STAMP(3);
   // D writes, and S1's first stage reads, part i's rows on lane i only: no sync between them
@@ -2498,7 +2497,7 @@ __device__ __attribute__((always_inline)) inline void step(const hs_topo* T, con
   real tq = real(0);
   real* const wd = reinterpret_cast<WorkL&>(fl).wd;  // FastL is dead once y is known
   if (lane < nmj) {
-    const int h_id = hinge_id, fi = hinge_foot;
+    const int h_id = T->hinge_ids[lane], fi = T->hinge_foot[lane];  // this lane's motor's part and foot
     // contact index of foot fi: its rank among the feet down (the contact list's order)
     const int cc = (fi >= 0 && ((cmask >> fi) & 1)) ? __popc(cmask & ((1u << fi) - 1)) : -1;
     const real* Jp = w.jpos(0, h_id);
@@ -3221,16 +3220,11 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
                                            i - 2 + (sl < NS ? sl : 0), mp.ktab_lo, mp.ttab_n, L);
 #endif
   const real dt = st.dt;
-  const GaitR g = load_gait(a.params[bb]);
-  // S4's motor lanes: their topology entries, issued after the loads above (vmcnt counts in order, so a
-  // wait for a value loaded first does not wait for these)
-  const bool hl = !FORCES && lane < T->nmj;
-  const int hinge_id = hl ? T->hinge_ids[lane] : 0, hinge_foot = hl ? T->hinge_foot[lane] : -1;
-  // the foot chains (hs_topo::foot_chain8), to LDS with the kinematics' stores: the contact blocks then
-  // read them there instead of through two dependent global loads
-  const uint32_t fch_w = (!FORCES && lane < 2 * HS_LMAX) ? (&T->foot_chain8[0][0])[lane] : 0u;
+  // the gait's kind from two of its parameters; the whole record (GaitR) is loaded only on the paths that
+  // read it, so that it is not held in registers (at 4 waves/SIMD: spilled) across the step
+  const hs_gait_params& gp = a.params[bb];
   const bool ignore_reach = a.ignore_reach != 0;
-  const bool straight = g.curvature == 0 && !g.rec_xf;
+  const bool straight = (real)gp.curvature == 0 && !gp.rec_transform_flag;
 #if HS_CURVED_LDS
   // a wave with a turning or transformed gait: the record in LDS for the turning path's many reads
   if (!kt && __ballot(!straight)) {
@@ -3259,7 +3253,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
         const StraightPre pre = straight_preload(st, t_tab, rws[bb].kf, HS_KTE_PRELOAD ? kt : nullptr, kb,
                                                  i - 2 + sl, mp.ktab_lo, mp.ttab_n, L);
 #endif
-        kin_sample_straight(T, g, a.params[bb], st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
+        kin_sample_straight(T, gp, st, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d}, sl - 2,
                             pre, rws[bb].kf, kt, kb, mp.ktab_lo);
       } else if (kt) {  // a turning or transformed gait with the call's tables
         const int r = i - 2 + sl - mp.ktab_lo;
@@ -3272,11 +3266,13 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
 #endif
         kin_sample_tab(T, L, OneWin<NM, FORCES>{&sm.d}, sl - 2, rws[bb].ktor[r], kte, kbad);
       } else {
-        kin_sample<false>(T, g, a.params[bb], st_curved, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d},
+        kin_sample<false>(T, load_gait(gp), gp, st_curved, i - 2 + sl, L, ignore_reach, OneWin<NM, FORCES>{&sm.d},
                           sl - 2, t_tab, mp.ktab_lo, mp.ttab_n);
       }
     }
-    if (!FORCES && lane < 2 * HS_LMAX) (&sv.fch[0][0])[lane] = fch_w;
+    // the foot chains (hs_topo::foot_chain8), to LDS with the kinematics' stores: the contact blocks then
+    // read them there instead of through two dependent global loads
+    if (!FORCES && lane < 2 * HS_LMAX) (&sv.fch[0][0])[lane] = (&T->foot_chain8[0][0])[lane];
     wave_sync();
   }
   STAMP(2);
@@ -3286,7 +3282,7 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
   } else {
     bool deferred = false;
     step<DEFER>(T, a, mp, dt, sv, sm.d.post.fl, OneWin<NM, FORCES>{&sm.d}, G, b, live, h_row, work,
-                deferred, !fix_idle, lane, hinge_id, hinge_foot);
+                deferred, !fix_idle, lane);
     if (DEFER && deferred) {  // the fixup launch solves this (step, rollout) with the general path
       if (lane == 0 && live) {
         const int it = atomicAdd(mp.fix_count, 1);
@@ -3296,20 +3292,20 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
       return;
     }
   }
-  if (mp.fused_w) {  // this step's joint sum of positive work, summed over the steps in order by the reduce
+  if (DEFER || mp.fused_w) {  // this step's joint sum of positive work, summed over the steps in order by the reduce
     if (lane == 0 && live)
       reinterpret_cast<real*>(mp.fused_work)[(size_t)(mp.fused_s0 + fstep) * a.n_rollouts + b] = work;
     return;
   }
   const bool out = lane == 0 && live;
   if (out && a.work_cot) {
-    real cot = work / ((real)T->total_mass * g.step_length);
+    real cot = work / ((real)T->total_mass * (real)gp.step_length);
     outp(a.work_cot)[2 * (size_t)b] = work;
     outp(a.work_cot)[2 * (size_t)b + 1] = cot;
   }
   if (a.best_key) {
     unsigned long long key = ~0ull;
-    if (out) key = best_key(key_cot(work, (real)T->total_mass, g.step_length, a.n_t, a.key_steps), a.rollout_id_base + b);
+    if (out) key = best_key(key_cot(work, (real)T->total_mass, (real)gp.step_length, a.n_t, a.key_steps), a.rollout_id_base + b);
     if constexpr (!DEFER) {  // both rollouts of the wave are here: their minimum first
       const unsigned long long o = __shfl_xor(key, HALF);
       key = o < key ? o : key;
