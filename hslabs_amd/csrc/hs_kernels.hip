@@ -83,7 +83,14 @@ static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a
 #define HS_MIN_WAVES_FORCES 3  // solve_forces mode (hs_run_forces): the control step's LDS layout
 #endif
 #ifndef HS_MIN_WAVES_F32
-#define HS_MIN_WAVES_F32 4  // fp32: 9.9 KB LDS per hexapod workgroup; 128 VGPRs (216 B scratch)
+#define HS_MIN_WAVES_F32 4  // fp32: 5.5 KB LDS per hexapod workgroup; the per-step and fixup launches 128 VGPRs
+#endif
+#ifndef HS_MIN_WAVES_F32_DEFER
+// fp32's fused step launch at 5 waves/SIMD: 95 VGPRs, its 84 B of spills in the two-contact path only
+// (tools/spill_lines.py --file hs_kernels_f32.hip); same box against 4: configs[2] 551 -> 606 M steps/s,
+// hexapod fp32 K = 200 522 -> 570 M (profiles/r05_s11_ab.txt). At 6 (80 VGPRs) the entry and the outputs
+// spill and it is no faster
+#define HS_MIN_WAVES_F32_DEFER 5
 #endif
 
 // ---------------------------------------------------------------------------
@@ -3344,7 +3351,9 @@ __device__ inline void fused_coords(int blk, int W, int n, int& fstep, int& wid)
 // without it; SOLVE, the fixup launch over the deferred items (its own instantiation, so the loop
 // costs the other two nothing)
 template <int NM, bool FORCES, int MODE>
-__global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES : (HS_REAL_IS_FLOAT ? HS_MIN_WAVES_F32 : (MODE == hs::FIX_DEFER ? HS_MIN_WAVES_DEFER : HS_MIN_WAVES))) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
+__global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES
+                                                 : (HS_REAL_IS_FLOAT ? (MODE == hs::FIX_DEFER ? HS_MIN_WAVES_F32_DEFER : HS_MIN_WAVES_F32)
+                                                                     : (MODE == hs::FIX_DEFER ? HS_MIN_WAVES_DEFER : HS_MIN_WAVES))) void hs_rollout_kernel(const hs_topo* __restrict__ T0,
                                                                                  hs_run_args a, RolloutWS* __restrict__ rws,
                                                                                  hs::launch_map mp) {
   __shared__ Smem<NM, FORCES> smem[2];

@@ -20,13 +20,14 @@ def main():
     ap.add_argument("-D", action="append", default=[])
     ap.add_argument("--kernel", default="hs_rollout_kernelILi22ELb0ELi1E")
     ap.add_argument("--src", default=SRC, help="the csrc directory (e.g. an older commit's, tools/build_prev.py)")
+    ap.add_argument("--file", default="hs_kernels.hip", help="hs_kernels_f32.hip: the fp32 build")
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "k.s")
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast",
                         "--cuda-device-only", "-S", "-gline-tables-only", f"-I{args.src}",
                         f"-I{os.path.join(args.src, '..', '..', 'include')}", *[f"-D{d}" for d in args.D],
-                        os.path.join(args.src, "hs_kernels.hip"), "-o", out], check=True, capture_output=True)
+                        os.path.join(args.src, args.file), "-o", out], check=True, capture_output=True)
         s = open(out).read()
     files = {m.group(1): (m.group(3) or m.group(2)).split("/")[-1]
              for m in re.finditer(r'\.file\s+(\d+)\s+"([^"]*)"(?:\s+"([^"]*)")?', s)}
