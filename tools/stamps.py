@@ -57,7 +57,8 @@ def main():
         b = H.DeviceBatch(m, params, n_t=20, k0=k0, horizon=20, outputs=("tau", "cf", "work_cot", "flags"))
         b.run_calls(20, best=True)
         torch.cuda.synchronize()
-        # STEP=s: the fused launch's step s (its wavefronts are blocks s * n_waves ...); the preparation
+        # STEP=s: blocks s * n_waves ... of the fused launch (with the grouped block order, fused_coords,
+        # a window in the middle of the launch: group s * n_waves / (256 * 20)'s steps); the preparation
         # pass's rows are then not recorded
         L.hs_debug_set_stamp_base(ctypes.c_uint(int(os.environ.get("STEP", "0")) * ((n + 1) // 2)))
         L.hs_debug_clear_stamps()
