@@ -103,9 +103,10 @@ __device__ inline void sincos_k(float x, float* s, float* c) { sincosf(x, s, c);
 // kernels: n = rint(x 2/pi), r = x - n pi/2 in two FMAs (the first exact: r is a multiple of x's or
 // pi/2's ulp and |r| <= pi/4), then the fdlibm kernel polynomials on |r| <= pi/4 and the quadrant's
 // swap and signs -- about half the instructions of the library's sincos (whose reduction carries a
-// double-double tail and whose large-argument path shares the code), within ~1 ulp of it. Larger or
+// double-double tail and whose large-argument path shares the code), within 1 ulp (sin) / 2 ulp (cos) of
+// the C library's (tests/test_sincos_k.py runs it on the host); sin(-0) comes out +0. Larger or
 // non-finite x: the library's sincos.
-__device__ inline void sincos_k(double x, double* s, double* c) {
+__host__ __device__ inline void sincos_k(double x, double* s, double* c) {
   if (!(fabs(x) < 0x1p20)) {
     ::sincos(x, s, c);
     return;
