@@ -2978,7 +2978,7 @@ static_assert(sizeof(SetupL) % sizeof(real) == 0, "SetupL is copied as reals");
 #define HS_PREP_ROWS 5  // table rows per lane (round 4, B = 4096, 24 rows: 3, 4, 5, 6, 8 rows give 24.1, 25.0, 23.4, 24.9, 29.7 us)
 #endif
 #ifndef HS_PREP_WAVES
-#define HS_PREP_WAVES 2  // waves per SIMD (253 VGPRs, no scratch; at 3 the turning rows spill 352 B: tools/isa_stats.py)
+#define HS_PREP_WAVES 2  // waves per SIMD (251 VGPRs, 255 mixed, no scratch; at 3, 168 VGPRs and 336 B of spills: tools/isa_stats.py)
 #endif
 #ifndef HS_PREP_WPB
 #define HS_PREP_WPB 4  // wavefronts per workgroup (each a group of lanes of its own: only wave-local exchanges);
