@@ -1,6 +1,7 @@
 """Summarise tools/gpu_pmc.sh output (gpurun_out/<dir>/p*/run_counter_collection.csv) for
-hs_rollout_kernel's fused step launch: per-step medians of every counter over its dispatches (a
-dispatch's counts / the steps it ran = its wavefronts / the batch's wavefronts), per-wave figures, and the HBM traffic per step of the batch
+hs_rollout_kernel's fused step launch: per-step medians of every counter over the timed job's dispatches
+(a dispatch's counts / the steps it ran = its wavefronts / the batch's wavefronts; the warm-up job's
+shorter launches and its preparation pass are left out), per-wave figures, and the HBM traffic per step of the batch
 (MI355X_MICROARCH.md HBM/rocprofv3 section: FETCH_SIZE x2 on gfx950, sizes in KiB). The library
 hash the bench printed in the same passes goes into the JSON, and bench.py refuses the figures for
 any other library.
@@ -23,25 +24,28 @@ FORCES_LAUNCH = re.compile(r"hs_rollout_kernel<\d+, true, 0>")  # solve_forces' 
 
 
 def collect(root, n_waves, step_launch=STEP_LAUNCH):
+    """counter -> per-step values of the step launches of the timed job: in each pass, the dispatches with
+    the most steps (the bench's warm-up job runs fewer steps per launch and is left out)"""
     vals = defaultdict(dict)  # counter -> dispatch -> per-step value
     for path in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
         with open(path) as f:
-            for row in csv.DictReader(f):
-                if not step_launch.search(row["Kernel_Name"]):
-                    continue  # the setup pass and the fixup / reduce launch are separate kernels
-                grid = int(row.get("Grid_Size") or row.get("Grid_Size_X"))
-                steps = grid // 64 // n_waves
-                if steps < 1:
-                    continue
-                key = (path, row["Dispatch_Id"])
-                d = vals[row["Counter_Name"]]
-                d[key] = d.get(key, 0.0) + float(row["Counter_Value"]) / steps
+            rows = [r for r in csv.DictReader(f) if step_launch.search(r["Kernel_Name"])]
+        steps_of = {r["Dispatch_Id"]: int(r.get("Grid_Size") or r.get("Grid_Size_X")) // 64 // n_waves for r in rows}
+        most = max(steps_of.values(), default=0)
+        for row in rows:
+            steps = steps_of[row["Dispatch_Id"]]
+            if steps < 1 or steps != most:
+                continue
+            key = (path, row["Dispatch_Id"])
+            d = vals[row["Counter_Name"]]
+            d[key] = d.get(key, 0.0) + float(row["Counter_Value"]) / steps
     return {c: sorted(d.values()) for c, d in vals.items()}
 
 
 def collect_job_kernels(root):
     """The call's other kernels (setup pass, IK table pass, fixup + work reduce): counter -> kernel ->
-    per-dispatch values (one dispatch of each per job)."""
+    the timed job's value in each pass (its last dispatch of the kernel: the warm-up job's preparation
+    pass tabulates fewer rows)."""
     vals = defaultdict(lambda: defaultdict(list))
     for path in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
         per = defaultdict(float)
@@ -49,9 +53,12 @@ def collect_job_kernels(root):
             name = row["Kernel_Name"]
             for k in ("hs_setup_kernel", "hs_ktab_kernel", "hs_prep_kernel", "hs_rollout_kernel<22, false, 2>"):
                 if k in name:
-                    per[(row["Counter_Name"], k, row["Dispatch_Id"])] += float(row["Counter_Value"])
-        for (c, k, _), v in per.items():
-            vals[c][k].append(v)
+                    per[(row["Counter_Name"], k, int(row["Dispatch_Id"]))] += float(row["Counter_Value"])
+        last = {}
+        for (c, k, d) in per:
+            last[(c, k)] = max(last.get((c, k), d), d)
+        for (c, k), d in last.items():
+            vals[c][k].append(per[(c, k, d)])
     return vals
 
 
@@ -79,8 +86,8 @@ def main():
     med = {c: statistics.median(x) for c, x in v.items()}
     sha = lib_of(a.root)
     lines = [f"{KERNEL}, {a.workload} ({a.cmd}), rocprofv3 --pmc, one group per pass, library {sha}",
-             "per STEP of the batch (fused dispatch counts / its steps), median over the fused dispatches "
-             "(FETCH_SIZE/WRITE_SIZE in KiB)"]
+             "per STEP of the batch (fused dispatch counts / its steps), median over the timed job's fused "
+             "dispatches (FETCH_SIZE/WRITE_SIZE in KiB)"]
     for c in sorted(med, key=lambda c: (not c.endswith("_SIZE"), c)):
         lines.append(f"{c:28s} n={len(v[c]):3d} median={med[c]:.6g}")
     waves = med.get("SQ_WAVES")
