@@ -545,7 +545,7 @@ int hs_run_forces_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls, con
   c.tau = c.x = c.work_cot = nullptr;
   c.best_key = nullptr;
   // the run_fused scheme without the fixup and the work reduce: solve_forces has no declined steps
-  // to defer (its own solve covers every step) and no work. Its LDS layout runs 2 wavefronts / SIMD.
+  // to defer (its own solve covers every step) and no work. Its LDS layout runs 3 wavefronts / SIMD.
   const int32_t CHUNK = std::max(1, std::min(HS_FUSED_MAX_STEPS, HS_FUSED_WAVES / std::max(1, mp.n_waves)));
   const bool f32 = a->precision == HS_PREC_F32;
   mp.fused_h = a->horizon;
