@@ -282,14 +282,13 @@ def main_sim(args, torch, dist, world, rank, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    sb.step(args.steps, stream=stream, outputs=())  # one launch, K steps (state stays in LDS)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+
+    def timed():
+        ev0.record(stream)
+        sb.step(args.steps, stream=stream, outputs=())  # one launch, K steps (state stays in LDS)
+        ev1.record(stream)
+
+    elapsed = timed_window(timed, torch.cuda.synchronize)
     t = torch.tensor([elapsed, ev0.elapsed_time(ev1)], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -397,14 +396,13 @@ def main_forces(args, torch, dist, world, rank, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    job()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+
+    def timed():
+        ev0.record(stream)
+        job()
+        ev1.record(stream)
+
+    elapsed = timed_window(timed, torch.cuda.synchronize)
     kern_ms = ev0.elapsed_time(ev1) / K
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -483,6 +481,49 @@ def flops_for(workload_key):
 
 
 # ---------------------------------------------------------------------------------------------
+# the timed window (every mode)
+# ---------------------------------------------------------------------------------------------
+def timed_window(run, sync, clock=time.perf_counter):
+    """The timed region of every bench mode: a clock read, the job (its kernels and, with N > 1 ranks,
+    the one best-key all-reduce the control-loop job issues), the device synchronize, a clock read.
+    No other collective runs between the two reads: the ranks line up on a
+    barrier BEFORE the first read, and the slowest rank is taken AFTER the second by a MAX all-reduce
+    of the per-rank elapsed times."""
+    t0 = clock()
+    run()
+    sync()
+    return clock() - t0
+
+
+class CollectiveCounter:
+    """--stub-cpu instrumentation: counts the torch.distributed collectives issued and snapshots the
+    count at each clock read, so tests/test_bench_launcher.py can assert exactly one collective
+    inside the timed window."""
+    NAMES = ("barrier", "all_reduce", "broadcast", "all_gather", "all_gather_object", "broadcast_object_list",
+             "reduce", "reduce_scatter", "all_to_all", "gather", "scatter")
+
+    def __init__(self, dist):
+        self.n, self.reads = 0, []
+        for name in self.NAMES:
+            f = getattr(dist, name, None)
+            if f is not None:
+                setattr(dist, name, self._wrap(f))
+
+    def _wrap(self, f):
+        def g(*a, **k):
+            self.n += 1
+            return f(*a, **k)
+        return g
+
+    def clock(self):
+        self.reads.append(self.n)
+        return time.perf_counter()
+
+    def in_window(self):
+        return self.reads[1] - self.reads[0]
+
+
+# ---------------------------------------------------------------------------------------------
 # the control-loop bench
 # ---------------------------------------------------------------------------------------------
 def main_stub(args, world, rank):
@@ -497,15 +538,18 @@ def main_stub(args, world, rank):
 
     lay = job_layout(args, world, rank)
     params = synth.gen_params(lay["B"], args.model, id0=lay["id0"])
+    counter = CollectiveCounter(dist)
     if world > 1:
         dist.barrier()
-    t0 = time.perf_counter()
-    work = torch.from_numpy(params["period"] * params["step_height"] * (args.steps / args.n_t))
-    cot = hdist.select_cot(work, torch.from_numpy(params["step_length"]), 22.0, args.n_t, args.steps)
-    key = hdist.reduce_best(hdist.best_key(cot, lay["id0"]))
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    res = {}
+
+    def job():
+        work = torch.from_numpy(params["period"] * params["step_height"] * (args.steps / args.n_t))
+        cot = hdist.select_cot(work, torch.from_numpy(params["step_length"]), 22.0, args.n_t, args.steps)
+        res["key"] = hdist.reduce_best(hdist.best_key(cot, lay["id0"]))
+
+    elapsed = timed_window(job, lambda: None, counter.clock)
+    key = res["key"]
     t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -519,7 +563,8 @@ def main_stub(args, world, rank):
         print(json.dumps({"metric": METRIC, "value": lay["total"] * args.steps / float(t[0]), "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "scaling": lay["scaling"],
                           "config": {"workload": f"stub {lay['cfg']}", "total_rollouts": lay["total"]},
-                          "stub_shards": shards, "best_rollout": {"id": rid, "cot": c}}), flush=True)
+                          "stub_shards": shards, "best_rollout": {"id": rid, "cot": c},
+                          "collectives_in_timed_window": counter.in_window()}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -637,20 +682,19 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+
     # K steps, k0 = (s * H) mod n_t: fused (a setup pass, launches of up to 512k wavefronts, the in-order work
     # sum whose atomicMin leaves the shard's best key) or the native loop of K launches (key after the last).
     # Two HIP events on the launch stream bracket the kernels (per-launch events would drain the queue
     # between kernels): GPU time per step of the batch = GPU time / K.
-    ev0.record(stream)
-    job()
-    ev1.record(stream)
-    if comm is not None:
-        comm.reduce_best(batch.best_key, stream)  # the single collective: RCCL all-reduce(MIN) of 8 B
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    def timed():
+        ev0.record(stream)
+        job()
+        ev1.record(stream)
+        if comm is not None:
+            comm.reduce_best(batch.best_key, stream)  # the single collective: RCCL all-reduce(MIN) of 8 B
+
+    elapsed = timed_window(timed, torch.cuda.synchronize)
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:

@@ -1,15 +1,19 @@
 """Build the gfx950 shared library libhslabs.so in-tree (hslabs_amd/_build/).
 
 Only hipcc is needed (no cmake/ninja). Device code is compiled with
--ffp-contract=fast: a*b+c becomes one FMA (one rounding instead of the two of
+-ffp-contract=fast-honor-pragmas: a*b+c becomes one FMA (one rounding instead of the two of
 the reference's x86-64 ``g++ -O2`` build, which has no FMA). That is 12 % fewer
 cycles per step on gfx950 (the kernel is VALU-issue bound) and moves per-joint
 torques by <= 2.3e-12 against the unfused CPU restatement on every pgs setup
 (profiles/r01_parity_report.txt); host code (x86-64 baseline) is unaffected.
+"honor-pragmas" keeps the one place that must round twice, work_over_period's
+work_dt *= dt; work += work_dt (periodic.cpp:301-302, `work_add` under
+`#pragma clang fp contract(off)`): plain -ffp-contract=fast ignores that pragma
+and emitted one v_fmac_f64 there; tools/isa_check.py's
+`work_add_check` verifies the reduce kernel's ISA.
 The closed-loop simulation (hs_sim.hip) is the exception, built with
 -ffp-contract=off: its contact test (depth >= 0) is decided within rounding for
-stance feet, so it keeps the oracle's unfused rounding (clang ignores
-`#pragma clang fp contract` under -ffp-contract=fast, hence a per-file flag).
+stance feet, so it keeps the oracle's unfused rounding (a per-file flag).
 So is hs_config.hip (the per-configuration FK / IK of the model.h API), which is
 not on the hot path and keeps the reference's rounding.
 Sources compile to objects in parallel, then link.
@@ -34,7 +38,8 @@ LIBS = ["-L/opt/rocm/lib", "-lrccl"]
 VARIANT_DIR = os.path.join(OUT_DIR, "variants")
 HEADERS = ["hs_topo.h", "hs_simtopo.h", "hs_ode.h", "hs_math.h", "hs_internal.h", os.path.join("..", "..", "include", "hslabs.h")]
 ARCH = os.environ.get("HSLABS_ARCH", "gfx950")
-CONTRACT = {"hs_sim.hip": "off", "hs_config.hip": "off"}  # per-source FMA contraction (default: fast)
+# per-source FMA contraction (default: fast, except where a `#pragma clang fp contract(off)` says not)
+CONTRACT = {"hs_sim.hip": "off", "hs_config.hip": "off"}
 # per-source scheduler choice, measured in round 1 (interleaved A/B): the fp32 rollout kernel
 # (4 waves/SIMD, 128 VGPRs) gains 1.4 % with the iterative ILP scheduler; the fp64 rollout
 # kernel and the simulation are fastest with the default one
@@ -63,7 +68,7 @@ def _compile(out: str, defines=(), verbose: bool = False, flags=()) -> str:
     def obj(src):
         o = os.path.join(os.path.dirname(out), f"{tag}.{src}.o")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
-               f"-ffp-contract={CONTRACT.get(src, 'fast')}", "-Wall", "-Wno-unused-function",
+               f"-ffp-contract={CONTRACT.get(src, 'fast-honor-pragmas')}", "-Wall", "-Wno-unused-function",
                *SRC_FLAGS.get(src, []), *flags,
                *[f"-D{d}" for d in defines], os.path.join(SRC, src), "-o", o]
         if verbose:
@@ -101,6 +106,10 @@ def _isa_check(lib: str, fatal: bool) -> None:
         os.remove(lib)
         raise RuntimeError(f"{lib}: {bad} device function(s) with vector instructions at EXEC == 0 after a "
                            "divergent loop exit (tools/isa_check.py); the library was removed")
+    if not isa_check.work_add_check(lib, verbose=not fatal) and fatal:
+        os.remove(lib)
+        raise RuntimeError(f"{lib}: the fp64 work reduce contracts work_dt * dt + work into one FMA "
+                           "(tools/isa_check.py work_add_check); the library was removed")
 
 
 def build(force: bool = False, verbose: bool = False) -> str:

@@ -17,19 +17,23 @@
 //      (tree-built null basis, Gram matrices in a global-memory workspace),
 //   S4 motor torques, contact forces and positive work (periodic.cpp:261-343).
 //
-// LDS layout: a launch solves one step per rollout, so the five stencil
-// samples keep only what that step reads -- pos/ust at t-2dt, t, t+2dt, R at
-// t+-dt, q at t-dt..t+dt, joint/foot features at t -- and the stencil-only
-// block is reused by the fast solve once D has consumed it (9.5 KB per
-// hexapod rollout). A horizon H > 1 is H launches (hs_capi.cpp): the sampler
-// is latency-bound, so recomputing the window on 30 lanes costs about what a
-// sliding window's one new sample on 6 lanes would, at twice the occupancy.
+// LDS layout (PostL, round 5): a launch solves one step per rollout, so the
+// five stencil samples keep only what that step reads -- pos/ust at t-2dt, t,
+// t+2dt, q at t-dt..t+dt, joint/foot features at t -- and once D has consumed
+// the stencil, the particular solution x, the closed-form blocks and the forces
+// y live in its place: 5.1 KB per hexapod rollout, 10.1 KB per workgroup, 16
+// workgroups per CU = 4 waves/SIMD for the fused step launch. A horizon H > 1
+// is H steps (hs_capi.cpp), each recomputing its window on 30 lanes: the
+// sampler is latency-bound, and a ring of five full samples (26 KB per
+// rollout) measured half the throughput.
 //
 // The floating-point operation sequences follow oracle/hs_oracle.cpp's fast mode
 // (built with -ffp-contract=off like the reference's x86-64 g++ -O2), but this
-// file is compiled with -ffp-contract=fast (hslabs_amd/build.py): a*b+c is one
-// FMA, so results differ from the oracle by FMA roundings (<= 2.3e-12 on the
-// per-joint torques, profiles/r01_parity_report.txt) and by ULPs of the device
+// file is compiled with -ffp-contract=fast-honor-pragmas (hslabs_amd/build.py):
+// a*b+c is one FMA except where `#pragma clang fp contract(off)` says otherwise
+// (work_add: work_over_period's two roundings), so results differ from the
+// oracle by FMA roundings (<= 2.3e-12 on the per-joint torques,
+// profiles/r01_parity_report.txt) and by ULPs of the device
 // sin/cos/atan2/acos/asin.
 #include <hip/hip_runtime.h>
 
@@ -73,10 +77,11 @@ static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a
 #define HS_MIN_WAVES 3
 #endif
 #ifndef HS_MIN_WAVES_DEFER
-// the fused step launch (FIX_DEFER: no general-path call) at 4 waves/SIMD: 128 VGPRs, its spills (108 B)
-// in the per-wave entry and the paths the straight gaits with a table do not take (tools/spill_lines.py);
-// the PostL layout's 10.1 KB of LDS per hexapod workgroup fits 16 workgroups/CU. Same box, interleaved:
-// driver command 286.4 -> 296.2 M steps/s, K = 200 365.8 -> 381.9 M (profiles/r05_s4_ab.txt)
+// the fused step launch (FIX_DEFER: no general-path call) at 4 waves/SIMD: 128 VGPRs, its spills (52 B)
+// all in the two-contact 6 x 6 system (tools/spill_lines.py; the entry's 108 B of round 5's first 4-wave
+// build were removed, DESIGN.md section 4 Registers); the PostL layout's 10.1 KB of LDS per hexapod
+// workgroup fits 16 workgroups/CU. Same box, interleaved: driver command 286.4 -> 296.2 M steps/s,
+// K = 200 365.8 -> 381.9 M (profiles/r05_s4_ab.txt)
 #define HS_MIN_WAVES_DEFER 4
 #endif
 #ifndef HS_MIN_WAVES_FORCES
@@ -97,7 +102,7 @@ static_assert(NS * HS_LMAX <= HALF && 6 + HS_NMAX <= HALF && HS_KMAX <= HALF, "a
 // LDS layouts
 // ---------------------------------------------------------------------------
 // NM = part capacity of the LDS layouts (the host picks the smallest instantiation >= n,
-// so LDS per rollout follows the model: hexapod 9.5 KB).
+// so LDS per rollout follows the model: hexapod 5.1 KB in the PostL layout).
 
 // packed per-contact Schur entries: the lower triangle of S_c row by row (r (r + 1) / 2 + q), then h_c
 constexpr int SCH_H = 21, SCH_N = 27;
@@ -1010,13 +1015,14 @@ template <bool SYNC = true, class W, class SV>
 // dt: the sample spacing (SetupL::dt, read once at the wave's start)
 __device__ __attribute__((always_inline)) inline void dynamics(const hs_topo* T, real dt, SV& sv, const W& w, int lane) {
   const int n = T->n;
+  const int i = lane;
+  const real m = (real)T->mass[lane < n ? lane : 0];
+  real mr[3], amr[3];
   if (lane < n) {
-    const int i = lane;
     const real inv = real(1) / (2 * dt);
-    const real m = (real)T->mass[i];
     const real *Pp = w.pos(2, i), *P0 = w.pos(0, i), *Pm = w.pos(-2, i);
     const real *Up = w.ust(2, i), *U0 = w.ust(0, i), *Um = w.ust(-2, i);
-    real vp[3], vm[3], mr[3], wp[3], wm[3], amr[3];
+    real vp[3], vm[3], wp[3], wm[3];
     for (int j = 0; j < 3; j++) {
       vp[j] = Pp[j] - P0[j];
       vp[j] *= inv;
@@ -1039,6 +1045,14 @@ __device__ __attribute__((always_inline)) inline void dynamics(const hs_topo* T,
       amr[j] = wp[j] - wm[j];
       amr[j] *= inv;
     }
+  }
+  // PostL: f overlays the stencil, and lane i's f rows can land on another lane's stencil rows
+  // (pos[1][n + i - NM]). Every lane's reads above happen before any lane's writes below only because
+  // the wavefront executes them in program order: this wavefront-scope fence keeps the compiler from
+  // moving a write above another lane's read; it emits no instruction
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (lane < n) {
     for (int j = 0; j < 3; j++) {
       sv.f[3 * i + j] = mr[j];
       sv.f[3 * (n + i) + j] = amr[j];
@@ -3330,7 +3344,11 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
 // (a multiple of 8, so a wavefront's steps stay on its XCD, block % 8), each group's steps in order,
 // the group's wavefronts fastest. A rollout's steps then run close together in time, and its setup
 // record, frames and table rows, read by every step, are fetched into the XCD's L2 once per call
-// instead of once per sweep of the whole batch over a step (whose output stores evict them)
+// instead of once per sweep of the whole batch over a step (whose output stores evict them).
+// Exception: the last group, gw = W - g0 wavefronts, is narrower when W is not a multiple of
+// HS_FUSED_GROUP, and when gw is not a multiple of 8 either its wavefronts change XCD from step to step
+// (a locality loss only; every step is independent, outputs are unaffected). The BASELINE shapes have
+// none: W = 2048 (configs[1], [4]), 8192 (configs[2]), 16384 (configs[3]'s shard)
 #ifndef HS_FUSED_GROUP
 #define HS_FUSED_GROUP 256
 #endif

@@ -100,19 +100,23 @@ __device__ inline void sincos(float x, float* s, float* c) { sincosf(x, s, c); }
 __device__ inline void sincos_k(float x, float* s, float* c) { sincosf(x, s, c); }
 #else
 // sin and cos of an angle of moderate size (joint values, step phases: |x| < 2^20) for the rollout
-// kernels: n = rint(x 2/pi), r = x - n pi/2 in two FMAs (the first exact: r is a multiple of x's or
-// pi/2's ulp and |r| <= pi/4), then the fdlibm kernel polynomials on |r| <= pi/4 and the quadrant's
-// swap and signs -- about half the instructions of the library's sincos (whose reduction carries a
-// double-double tail and whose large-argument path shares the code), within 1 ulp (sin) / 2 ulp (cos) of
-// the C library's (tests/test_sincos_k.py runs it on the host); sin(-0) comes out +0. Larger or
-// non-finite x: the library's sincos.
+// kernels: n = rint(x 2/pi), r = x - n pi/2 in three FMAs against pi/2 = P1 + P2 + P3 (+ 5.6e-50): the
+// first is exact (r is a multiple of x's or P1's ulp and |r| <= pi/4 + 1), and the third term keeps r
+// accurate where x lies within rounding of a multiple of pi/2 (two terms left an absolute error of
+// n * 1.5e-33, thousands of ulps of r ~ 1e-16 at |x| ~ 2^19), then the fdlibm kernel
+// polynomials on |r| <= pi/4 and the quadrant's swap and signs -- about half the instructions of the
+// library's sincos (whose reduction carries a double-double tail and whose large-argument path shares
+// the code), within 1 ulp (sin) / 2 ulp (cos) of the C library's (tests/test_sincos_k.py runs it on the
+// host, near-multiples of pi/2 up to 2^20 included); sin(-0) comes out +0. Larger or non-finite x: the
+// library's sincos.
 __host__ __device__ inline void sincos_k(double x, double* s, double* c) {
   if (!(fabs(x) < 0x1p20)) {
     ::sincos(x, s, c);
     return;
   }
   const double n = rint(x * 6.36619772367581382433e-01);  // 2/pi
-  const double r = fma(-n, 6.12323399573676603587e-17, fma(-n, 1.57079632679489655800e+00, x));
+  const double r = fma(-n, -0x1.f1976b7ed8fbcp-110,
+                       fma(-n, 0x1.1a62633145c07p-54, fma(-n, 0x1.921fb54442d18p+0, x)));  // P3, P2, P1
   const double z = r * r;
   // __kernel_sin (S1..S6) and __kernel_cos (C1..C6) of fdlibm, tail argument 0
   const double ps = 8.33333333332248946124e-03 +

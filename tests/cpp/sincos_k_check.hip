@@ -1,7 +1,8 @@
 // Host-side check of hs_math.h's sincos_k (the rollout kernels' joint-value sines and cosines), compiled by
 // tests/test_sincos_k.py: the same function runs on the host here (__host__ __device__), against the C
 // library's sin and cos (the oracle's). Prints the largest ulp distance of each over seeded arguments in
-// |x| < 64 (2e6 of them, a third placed within 1e-9 of a multiple of pi/2), and the special cases.
+// |x| < 64 (2e6 of them, a third placed within 1e-9 of a multiple of pi/2), the doubles nearest to every
+// multiple of pi/2 below 2^20 and their neighbours, and the special cases.
 #include <cinttypes>
 #include <cmath>
 #include <cstdint>
@@ -36,6 +37,23 @@ int main() {
     if (us > ms) { ms = us; worst_s = x; }
     if (uc > mc) { mc = uc; worst_c = x; }
     max_abs = std::fmax(max_abs, std::fmax(std::fabs(s - S), std::fabs(c - C)));
+  }
+  // the hardest arguments of the range: the doubles nearest to n pi/2 (and their neighbours) for every
+  // n with |n pi/2| < 2^20, where r = x - n pi/2 is a few ulps of x and any reduction error shows
+  // (with a two-term pi/2 the error n * 1.5e-33 was thousands of ulps of r at |x| ~ 2^19)
+  const long double pio2 = 1.570796326794896619231321691639751442L;
+  for (int64_t n = 1; n * 1.5707963267948966 < 0x1p20; n++) {
+    const double x0 = (double)((long double)n * pio2);
+    for (int k = -1; k <= 1; k++) {
+      const double x = k < 0 ? std::nextafter(x0, 0.0) : k > 0 ? std::nextafter(x0, 1e300) : x0;
+      for (double xs : {x, -x}) {
+        double s, c;
+        hsd::sincos_k(xs, &s, &c);
+        const int64_t us = ulps(s, std::sin(xs)), uc = ulps(c, std::cos(xs));
+        if (us > ms) { ms = us; worst_s = xs; }
+        if (uc > mc) { mc = uc; worst_c = xs; }
+      }
+    }
   }
   std::printf("max_ulp_sin %" PRId64 " at %.17g\n", ms, worst_s);
   std::printf("max_ulp_cos %" PRId64 " at %.17g\n", mc, worst_c);

@@ -400,3 +400,84 @@ def test_table_rows_match_inline_kinematics(gpu, hmodels, name, k0, H, n_calls, 
             assert np.array_equal(fl[:, row], rfl[:, kk]), (c, h)
             near += int(((fl[:, row] & gpu.capi.HS_FLAG_NEAR_RANK) != 0).sum())
     print(f"{name} {kind}: {n_calls * H * B} steps bitwise equal ({near} near-rank flagged)")
+
+
+def _work_two_roundings(tau, dq, period, n_t, w0):
+    """work_over_period (periodic.cpp:285-307) restated from the step outputs: per step the motors'
+    positive work tau_j * jvel_j (jvel = the dq output of hinge j, compute_vel_traj's rate) summed in
+    joint order, then work_dt *= dt; work += work_dt with TWO roundings (numpy never contracts)"""
+    B, H, nmj = tau.shape
+    dt = period / float(n_t)
+    w = w0.copy()
+    for s in range(H):
+        dw = tau[:, s, :] * dq[:, s, 6:6 + nmj]
+        dw = np.where(dw > 0, dw, 0.0)
+        work_dt = np.zeros(B)
+        for j in range(nmj):
+            work_dt = work_dt + dw[:, j]
+        w = w + work_dt * dt
+    return w
+
+
+def _work_one_rounding(tau, dq, period, n_t, w0):
+    """the same with work + work_dt * dt as one correctly rounded FMA (exact rational arithmetic)"""
+    from fractions import Fraction
+
+    B, H, nmj = tau.shape
+    out = np.empty(B)
+    for b in range(B):
+        dt = period[b] / float(n_t)
+        w = float(w0[b])
+        for s in range(H):
+            dw = tau[b, s] * dq[b, s, 6:6 + nmj]
+            work_dt = 0.0
+            for v in np.where(dw > 0, dw, 0.0):
+                work_dt = work_dt + float(v)
+            w = float(Fraction(work_dt) * Fraction(dt) + Fraction(w))
+        out[b] = w
+    return out
+
+
+@pytest.mark.parametrize("path", ["fused", "fused_reference", "steps"])
+def test_work_rounds_twice_bitwise(gpu, hmodels, path):
+    """work_over_period's work_dt *= dt_traj; work_period += work_dt (periodic.cpp:
+    301-302) rounds twice in the reference's x86-64 build. The fused reduce (and the fixup + reduce
+    launch that ends an HS_SOLVE_AUTO call), the HS_SOLVE_REFERENCE fixups and the launch-per-step
+    path must give work_cot bitwise equal to that accumulation recomputed in numpy from the steps'
+    torques and joint rates, starting from a nonzero accumulated work; the one-FMA accumulation the
+    library shipped in round 5 differs on some rollouts (so the test can tell them apart).
+    tools/isa_check.py's work_add_check pins the same in the ISA."""
+    import torch
+    from hslabs_amd import synth
+
+    m = hmodels["hexapod"]
+    B, K = 4096 if path != "fused_reference" else 256, 20
+    p = synth.gen_params(B, "hexapod", id0=31337)
+    w0 = np.random.default_rng(5).uniform(0.0, 3.0, B)
+    b = gpu.DeviceBatch(m, p, n_t=20, k0=3, horizon=K if path != "steps" else 1,
+                        outputs=("tau", "dq", "flags", "work_cot"))
+    if path == "fused_reference":
+        b.solve_mode = gpu.capi.HS_SOLVE_REFERENCE
+    b.work_cot.zero_()
+    b.work_cot[:, 0] = torch.from_numpy(w0).to(b.work_cot.device)
+    if path == "steps":
+        tau, dq = [], []
+        for c in range(K):
+            b.k0 = (3 + c) % 20
+            b.run(best=False, accumulate=True)
+            tau.append(npy(b.tau))
+            dq.append(npy(b.dq))
+        tau, dq = np.concatenate(tau, axis=1), np.concatenate(dq, axis=1)
+    else:
+        b.run_calls(K, call_horizon=1, best=False, accumulate=True)
+        torch.cuda.synchronize()
+        tau, dq = npy(b.tau), npy(b.dq)
+    wc = npy(b.work_cot)
+    period = np.ascontiguousarray(p["period"], dtype=np.float64)
+    want = _work_two_roundings(tau, dq, period, 20, w0)
+    assert np.array_equal(wc[:, 0], want), f"{int((wc[:, 0] != want).sum())} of {B} rollouts' work differ"
+    cot = want / (m.total_mass * np.ascontiguousarray(p["step_length"], dtype=np.float64))
+    assert np.array_equal(wc[:, 1], cot)
+    if path == "fused":
+        fma = _work_one_rounding(tau[:512], dq[:512], period[:512], 20, w0[:512])
+        assert (fma != want[:512]).any(), "the one-rounding accumulation should differ somewhere"

@@ -46,6 +46,25 @@ v_writelane_b32 v167, s38, 42
 """
 
 
+# the fp64 work reduce's first steps (hs_fused_reduce_kernel, gfx950): built -ffp-contract=fast, the
+# `fp contract(off)` pragma in work_add was ignored and each step was one FMA; built
+# -ffp-contract=fast-honor-pragmas, a product rounded by v_mul_f64 and then summed
+FUSED_WORK = """\
+v_fma_f64 v[18:19], -v[18:19], v[24:25], v[22:23]
+v_fmac_f64_e32 v[2:3], v[16:17], v[18:19]
+v_fma_f64 v[18:19], v[16:17], v[22:23], v[2:3]
+v_fmac_f64_e32 v[18:19], v[16:17], v[20:21]
+"""
+TWO_ROUNDINGS = """\
+v_mul_f64 v[24:25], v[22:23], v[20:21]
+v_fma_f64 v[18:19], -v[18:19], v[24:25], v[22:23]
+v_mul_f64 v[20:21], v[16:17], v[20:21]
+v_add_f64 v[2:3], v[2:3], v[20:21]
+v_mul_f64 v[20:21], v[16:17], v[22:23]
+v_add_f64 v[20:21], v[2:3], v[20:21]
+"""
+
+
 def _isa():
     import sys
 
@@ -72,3 +91,17 @@ def test_product_library_is_clean(product):
     if not os.path.exists(os.path.join("/opt/rocm/lib/llvm/bin", "llvm-objdump")):
         pytest.skip("llvm-objdump not available")
     assert _isa().check(lib) == 0
+
+
+def test_work_add_pairs_count_two_roundings():
+    ic = _isa()
+    assert ic.mul_add_pairs(FUSED_WORK.splitlines()) == 0
+    # the first v_mul_f64 feeds an FMA (a division's Newton step), not an add: only two pairs
+    assert ic.mul_add_pairs(TWO_ROUNDINGS.splitlines()) == 2
+
+
+def test_product_work_reduce_rounds_twice(product):
+    """work_over_period's work_dt *= dt; work += work_dt (periodic.cpp:301-302) in the shipped binary"""
+    if not os.path.exists(os.path.join("/opt/rocm/lib/llvm/bin", "llvm-objdump")):
+        pytest.skip("llvm-objdump not available")
+    assert _isa().work_add_check(product.capi.lib_path())

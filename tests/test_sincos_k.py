@@ -2,7 +2,8 @@
 (a Cody-Waite reduction by pi/2 and fdlibm's kernel polynomials in place of the library sincos) -- run on
 the host (the function is __host__ __device__; tests/cpp/sincos_k_check.hip) against the C library's sin
 and cos, which the oracle uses: within 1 ulp (sin) and 2 ulp (cos) over 2e6 seeded arguments, a third of
-them within 1e-9 of a multiple of pi/2, the same signs at the special points except sin(-0) (+0 here: the
+them within 1e-9 of a multiple of pi/2, and over the doubles nearest to every multiple of pi/2 below 2^20
+(with their neighbours: the reduction's worst cases), the same signs at the special points except sin(-0) (+0 here: the
 reduction's x - 0 * pi/2 rounds to +0; the values compare equal), NaN for non-finite input."""
 import os
 import subprocess

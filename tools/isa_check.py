@@ -17,6 +17,12 @@ here. Every other vector ALU, memory or LDS instruction in such a block is repor
 
   python tools/isa_check.py [lib.so ...]   (default: the product library)
 Exit status 1 when any function shows the pattern. hslabs_amd/build.py runs it on every build.
+
+`work_add_check` is the second build-time check: work_over_period's accumulation `work_dt *= dt;
+work += work_dt` (periodic.cpp:301-302) rounds twice in the reference's x86-64 build, and the fp64
+work reduce (hs_fused_reduce_kernel, 32 steps unrolled) must issue it as a v_mul_f64 whose result a
+v_add_f64 consumes, not as one v_fma*_f64 (plain -ffp-contract=fast ignored the `fp contract(off)`
+pragma and fused all 32).
 """
 from __future__ import annotations
 
@@ -99,9 +105,48 @@ def check(lib: str, verbose: bool = True) -> int:
     return bad
 
 
+_MUL_F64 = re.compile(r"^v_mul_f64(?:_e(?:32|64))?\s+(v\[\d+:\d+\])")
+_ADD_F64 = re.compile(r"^v_add_f64(?:_e(?:32|64))?\s+v\[\d+:\d+\],\s*(\S+),\s*(\S+)")
+WORK_ADD_UNROLL = 32  # reduce_rollouts' unrolled step loop (hs_kernels.hip)
+
+
+def mul_add_pairs(instructions) -> int:
+    """v_add_f64 instructions that read the destination of the latest v_mul_f64 writing that register
+    pair: a product rounded before the sum (two roundings)"""
+    last_mul, pairs = {}, 0
+    for ins in instructions:
+        m = _MUL_F64.match(ins)
+        if m:
+            last_mul[m.group(1)] = True
+            continue
+        a = _ADD_F64.match(ins)
+        if a and any(last_mul.pop(r, False) for r in (a.group(1), a.group(2))):
+            pairs += 1
+    return pairs
+
+
+def work_add_check(lib: str, verbose: bool = True) -> bool:
+    """True when the fp64 work reduce of lib rounds work_dt * dt before the sum on all its unrolled
+    steps (at least WORK_ADD_UNROLL mul -> add pairs)"""
+    found = []
+    with tempfile.TemporaryDirectory() as td:
+        for co in code_objects(lib, td):
+            dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--mcpu=gfx950", co], check=True,
+                                 capture_output=True, text=True).stdout
+            for name, ins in _disasm_functions(dis).items():
+                if "hs_fused_reduce_kernel" in name and "hs_run_argsd" in name:  # the fp64 instantiation
+                    found.append(mul_add_pairs(ins))
+    ok = bool(found) and min(found) >= WORK_ADD_UNROLL
+    if verbose:
+        print(f"work_add_check: {os.path.basename(lib)}: fp64 reduce mul->add pairs {found} "
+              f"(need >= {WORK_ADD_UNROLL}): {'ok' if ok else 'FAIL'}", file=sys.stderr)
+    return ok
+
+
 if __name__ == "__main__":
     libs = sys.argv[1:] or [os.path.join(ROOT, "hslabs_amd", "_build", "libhslabs.so")]
-    total = sum(check(lib) for lib in libs)
+    bad_work = [lib for lib in libs if not work_add_check(lib)]
+    total = sum(check(lib) for lib in libs) + len(bad_work)
     print(f"isa_check: {total} function(s) with the EXEC == 0 spill pattern in {len(libs)} librar"
           f"{'y' if len(libs) == 1 else 'ies'}")
     sys.exit(1 if total else 0)
