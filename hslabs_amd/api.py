@@ -121,6 +121,9 @@ class KinematicModel:
         self.n_parts, self.nmj, self.nfeet = d.n_parts, d.nmj, d.nfeet
         self.config_dim, self.n_limbs, self.lik_kind = d.config_dim, d.n_limbs, d.lik_kind
         self.total_mass, self.rcap = d.total_mass, d.rcap
+        ok = ctypes.c_int32()
+        capi.check(L.hs_model_limb_lane(h, ctypes.byref(ok)), "hs_model_limb_lane")
+        self.limb_lane_ok = bool(ok.value)  # hs_run_calls' limb-lane kernel takes this model (ABI 15)
 
     def get_config_dim(self) -> int:
         return self.config_dim
@@ -197,6 +200,11 @@ class KinematicModel:
                 self.handle = None
         except Exception:
             pass
+
+
+def limb_launches() -> int:
+    """fused step launches this process made with the limb-lane kernel (hs_limb_launches)"""
+    return int(capi.load().hs_limb_launches())
 
 
 def params_array(params) -> np.ndarray:

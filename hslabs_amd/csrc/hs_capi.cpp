@@ -5,6 +5,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <mutex>
@@ -215,9 +216,23 @@ int check_args(const hs_model_s* m, const hs_run_args* a) {
 
 // hs_run_calls / hs_run_mixed_calls: a setup-only pass, launches of CHUNK steps over (step, wavefront),
 // the in-order work reduce. Each step in flight in a launch has its own general-path scratch.
+// The limb-lane kernel (hs_limb.h) takes the fused step launches of a call when the model is of its class
+// (hs_topo::limb_lane_ok), the call solves in HS_SOLVE_AUTO and asks for no x, q or dq rows (the kernel
+// writes tau, cf, flags and the work terms), and the preparation pass holds the IK table (the kernel reads
+// its rows); HS_LIMB=0 in the environment keeps hs_rollout_kernel's fused step launch (A/B, tests)
+std::atomic<int64_t> g_limb_launches{0};
+
+bool limb_kernel_wanted() {
+  const char* e = getenv("HS_LIMB");  // read per call: a test switches kernels within one process
+  return !(e && e[0] == '0');
+}
+bool limb_eligible(const hs_topo& host, const hs_run_args& a) {
+  return limb_kernel_wanted() && host.limb_lane_ok && a.solve_mode == HS_SOLVE_AUTO && !a.x && !a.q && !a.dq;
+}
+
 int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map mp, ws_pool& gen_pool,
               ws_pool& work_pool, ws_pool& fix_pool, std::mutex& mu, double total_mass, const double* rollout_mass,
-              int32_t n_calls) {
+              int32_t n_calls, bool limb = false) {
   const int64_t S = (int64_t)n_calls * a.horizon;  // steps, one output row each
   if (S > (1 << 24)) return fail(HS_E_ARG, "too many steps");
   // steps per launch: the launch refills the SIMDs from its queue of wavefronts (the batch's last
@@ -275,6 +290,8 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   mp.fix_count = fix_counts;
   mp.fix_n_counts = n_chunks;
   hs::ktab_range(a.k0, a.n_t, a.horizon, n_calls, &mp.ktab_lo, &mp.ktab_n, &mp.ttab_n);  // the preparation pass's rows
+  limb = limb && mp.ktab_n > 0 && !mp.wave_rollouts;
+  mp.prep_unit = limb ? 8 : 2;  // the rollouts' records written on the XCD whose step launches read them
   int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   mp.setup_only = 0;
   mp.setup_io = hs::SETUP_LOAD;
@@ -286,7 +303,11 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
     mp.fused_n = (int32_t)std::min<int64_t>(CHUNK, S - s0);
     mp.fix_mode = hs::FIX_DEFER;
     mp.fix_count = fix_counts + ci;
-    le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+    if (limb) {
+      le = f32 ? hs::launch_limb_f32(d, c, ws, mp) : hs::launch_limb(d, c, ws, mp);
+      g_limb_launches++;
+    }
+    else le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
     if (le != 0) break;
     // the same steps' declined (step, rollout) items, with the general path; after the last step
     // launch of an HS_SOLVE_AUTO call (few items, if any) together with the work reduce
@@ -346,6 +367,14 @@ struct hs_mixed_s {
 extern "C" {
 
 int hs_abi_version(void) { return HSLABS_ABI_VERSION; }
+
+int hs_model_limb_lane(hs_model_t m, int32_t* ok) {
+  if (!m || !ok) return fail(HS_E_ARG, "null argument");
+  *ok = m->host.limb_lane_ok;
+  return HS_OK;
+}
+
+int64_t hs_limb_launches(void) { return g_limb_launches.load(); }
 
 const char* hs_last_error(void) { return g_err.c_str(); }
 
@@ -485,9 +514,9 @@ int hs_run_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls) {
   void* ws = nullptr;
   rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);
   if (rc != HS_OK) return rc;
-  return run_fused(d, routed(*a, m->host.torso_mask), ws, hs::single_model_map(m->host, a->n_rollouts), m->fused_gen,
-                   m->fused_work,
-                   m->fused_fix, m->mu, m->host.total_mass, nullptr, n_calls);
+  const hs_run_args r = routed(*a, m->host.torso_mask);
+  return run_fused(d, r, ws, hs::single_model_map(m->host, a->n_rollouts), m->fused_gen, m->fused_work, m->fused_fix,
+                   m->mu, m->host.total_mass, nullptr, n_calls, limb_eligible(m->host, r));
 }
 
 int hs_run_pd(hs_model_t m, const hs_run_args* a, const hs_pd_args* pd) {

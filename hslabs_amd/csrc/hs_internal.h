@@ -71,6 +71,10 @@ struct launch_map {
   // record) of samples [ktab_lo, ktab_lo + ktab_n) per rollout (ktab_range); the step launches read them. ktab_nl: limb lanes per
   // rollout the pass enumerates (the launch's largest model)
   int32_t ktab_n, ktab_lo, ktab_nl, ttab_n;
+  // the preparation pass's XCD units: rollouts [u * prep_unit, (u + 1) * prep_unit) are written on XCD
+  // u % 8, where the step launches read them (0 or 2: hs_rollout_kernel's two rollouts per wavefront; 8:
+  // the limb-lane kernel's eight)
+  int32_t prep_unit;
 };
 
 // Kernel launcher (hs_kernels.hip). `workspace` holds general_workspace_bytes()
@@ -92,6 +96,10 @@ launch_map single_model_map(const hs_topo& t, int32_t n_rollouts);
 // one launch of mp.fused_n fused steps (or the setup-only pass when mp.setup_only)
 int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
 int launch_fused_f32(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
+// the same fused step launch by the limb-lane kernel (hs_limb.h): lane = (rollout, limb), 8 rollouts per
+// wavefront; the steps it does not take are deferred to the FIX_SOLVE launch like the fused launch's
+int launch_limb(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
+int launch_limb_f32(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp);
 // work_cot[b] = (w, w / (total_mass * step_length)) with w = (accumulate ? work_cot[b][0] : 0) + the steps'
 // work in step order, then the best key
 // (rollout_mass: per-rollout total mass of a mixed plan, else null and total_mass)

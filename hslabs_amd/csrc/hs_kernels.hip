@@ -3011,8 +3011,13 @@ __device__ inline void wave_lds_sync() {
 }
 __device__ inline int ktab_lanes(const hs::launch_map& mp) { return mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX; }
 __host__ __device__ inline int prep_chunks(int ttab_n) { return (ttab_n > 0 ? ttab_n + HS_PREP_ROWS - 1 : HS_PREP_ROWS) / HS_PREP_ROWS; }
-__host__ __device__ inline int64_t prep_blocks(int n_waves, int ttab_n, int nli) {
-  const int64_t groups_per_xcd = 2 * (int64_t)prep_chunks(ttab_n) * ((n_waves + 7) / 8);
+// XCD units of the pass: prep_unit rollouts each (2: hs_rollout_kernel's wavefronts, 8: the limb kernel's)
+__host__ __device__ inline int prep_units(const hs::launch_map& mp, int n_rollouts, int& R) {
+  R = mp.prep_unit > 2 && !mp.wave_rollouts ? mp.prep_unit : 2;
+  return R == 2 ? mp.n_waves : (n_rollouts + R - 1) / R;
+}
+__host__ __device__ inline int64_t prep_blocks(int n_units, int R, int ttab_n, int nli) {
+  const int64_t groups_per_xcd = R * (int64_t)prep_chunks(ttab_n) * ((n_units + 7) / 8);
   const int gpw = WAVE / nli;
   const int64_t waves_per_xcd = (groups_per_xcd + gpw - 1) / gpw;
   return 8 * ((waves_per_xcd + HS_PREP_WPB - 1) / HS_PREP_WPB);
@@ -3041,12 +3046,14 @@ __global__ __launch_bounds__(WAVE * HS_PREP_WPB, HS_PREP_WAVES) void hs_prep_ker
   const int gl = tl / nli, L = tl % nli;
   // group (q, sub, chunk) in XCD x's sequence (x = blockIdx.x % 8: the block's XCD)
   const int gi = ((int)(blockIdx.x / 8) * HS_PREP_WPB + wv) * gpw + gl;
-  const int chunk = gi % C, sub = (gi / C) % 2, w = 8 * (gi / (2 * C)) + (int)(blockIdx.x % 8);
-  bool on = gl < gpw && w < mp.n_waves;
+  int R;
+  const int n_units = prep_units(mp, a.n_rollouts, R);
+  const int chunk = gi % C, sub = (gi / C) % R, w = 8 * (gi / (R * C)) + (int)(blockIdx.x % 8);
+  bool on = gl < gpw && w < n_units;
   int b = 0;
   const hs_topo* __restrict__ T = T0;
   if (on) {
-    b = mp.wave_rollouts ? mp.wave_rollouts[2 * w + sub] : 2 * w + sub;
+    b = mp.wave_rollouts ? mp.wave_rollouts[2 * w + sub] : R * w + sub;
     if (MIXED) T = T0 + mp.wave_model[w];
     on = b >= 0 && b < a.n_rollouts && L < T->n_limbs;
   }
@@ -3406,6 +3413,8 @@ __global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES
   }
 }
 
+#include "hs_limb.h"
+
 #if !HS_REAL_IS_FLOAT
 // pergensetup::set_rec (pergen.cpp:225-239) after setup_pergen (pergen.cpp:453-507), for
 // n_rollouts x n_times (rollout, time) items, two per wavefront: the gait setup of the item's
@@ -3540,7 +3549,9 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   hipStream_t st = (hipStream_t)a.stream;
   RolloutWS* ws = (RolloutWS*)workspace;
   if (mp.setup_only) {  // the call's preparation pass: setup record, sample times, IK table
-    const int64_t blocks = prep_blocks(mp.n_waves, mp.ttab_n, mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX);
+    int R;
+    const int units = prep_units(mp, a.n_rollouts, R);
+    const int64_t blocks = prep_blocks(units, R, mp.ttab_n, mp.ktab_nl > 0 ? mp.ktab_nl : HS_LMAX);
     if (mp.wave_model)
       hipLaunchKernelGGL(hs_prep_kernel<true>, dim3((unsigned)blocks), dim3(WAVE * HS_PREP_WPB), 0, st, d_topo, a, ws, mp);
     else
@@ -3557,6 +3568,23 @@ int launch_fused(const hs_topo* d_topo, const hs_run_args& a, void* workspace, c
   if (mp.max_parts <= 18) launch_nm<18>(d_topo, a, ws, m, st);
   else if (mp.max_parts <= 22) launch_nm<22>(d_topo, a, ws, m, st);
   else launch_nm<HS_NMAX>(d_topo, a, ws, m, st);
+  return (int)hipGetLastError();
+}
+
+#if HS_REAL_IS_FLOAT
+int launch_limb_f32(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp) {
+#else
+int launch_limb(const hs_topo* d_topo, const hs_run_args& a, void* workspace, const launch_map& mp) {
+#endif
+  if (a.n_rollouts <= 0 || mp.fused_n <= 0) return 0;
+  hipStream_t st = (hipStream_t)a.stream;
+  RolloutWS* ws = (RolloutWS*)workspace;
+  launch_map m = mp;
+  m.fused_w = (a.n_rollouts + LGR - 1) / LGR;  // wavefronts per step: 8 rollouts each
+  const dim3 grid((unsigned)((int64_t)m.fused_w * mp.fused_n));
+  if (mp.max_parts <= 18) hipLaunchKernelGGL((hs_limb_kernel<18>), grid, dim3(WAVE), 0, st, d_topo, a, ws, m);
+  else if (mp.max_parts <= 22) hipLaunchKernelGGL((hs_limb_kernel<22>), grid, dim3(WAVE), 0, st, d_topo, a, ws, m);
+  else hipLaunchKernelGGL((hs_limb_kernel<HS_NMAX>), grid, dim3(WAVE), 0, st, d_topo, a, ws, m);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,636 @@
+// hs_limb.h -- the limb-lane step kernel (round 6), included by hs_kernels.hip inside its anonymous
+// namespace (both precisions).
+//
+// hs_rollout_kernel maps a rollout to 32 lanes and each phase to the lanes it can use: kinematics 30
+// (sample, limb) lanes, dynamics and the particular solution one lane per part, the contact blocks four
+// lanes per contact, the 6 x 6 Schur system one lane -- 16 % of the issued FP64 lane operations are
+// useful. This kernel maps a rollout to a group of 8 lanes, one per limb (the torso
+// on lane 7), and keeps a limb's whole step in its lane's registers: the limb FK at the stencil's three
+// pos / ust samples, the finite differences of its parts, its links' subtree sums, its contact's blocks
+// and its motors' torques -- the work of every phase is per limb, so 6 of 8 lanes are busy in every
+// phase, and 8 rollouts share a wavefront. Cross-limb exchanges: the chain bodies' subtree sums and the
+// root's through LDS, the contact blocks' Schur entries moved to lane = contact rank (ds_bpermute) and
+// summed by DPP in fast_solve_lanes' pairwise order, the motors' work summed in joint order from LDS.
+//
+// Every value is computed by the same operations in the same order as hs_rollout_kernel's fused step
+// (the same helpers, the same expressions), so the outputs are bitwise those of that kernel
+// (tests/test_gpu_limb.py). The kernel takes the common case: a call with the preparation pass's IK
+// table, a model of the limb-lane class (hs_topo::limb_lane_ok), HS_SOLVE_AUTO, no x / q / dq outputs,
+// a step with no contact or with >= 3 contacts that the closed form's tier 1 solves with no guard near
+// its threshold. Every other step is deferred to the fixup launch (hs_rollout_kernel FIX_SOLVE), which
+// computes it with hs_rollout_kernel's whole machinery (1 and 2 contacts, tier 2, the Eigen-style path,
+// HS_FLAG_NEAR_RANK): the same (step, rollout) items the fused step launch defers.
+
+#ifndef HS_LIMB_WAVES
+#define HS_LIMB_WAVES 2  // waves per SIMD the limb kernel is built for
+#endif
+
+constexpr int LG = 8;           // lanes per rollout group
+constexpr int LGR = WAVE / LG;  // rollouts per wavefront
+
+template <int NM>
+struct LimbLds {
+  real g[NM][6];     // per part g_i = (f_i, t_i + (P_i - p0) x f_i); a root kid's slot then its subtree sums
+  real a[6];         // the root's x (torso force, torque): the zeroth-order right-hand side
+  real wd[HS_NMAX];  // the motors' positive work of the step, in joint order
+};
+
+// a value of lane `src` of this lane's group (ds_bpermute)
+__device__ inline real grp_get(real v, int src) { return __shfl(v, src); }
+__device__ inline float grp_getf(float v, int src) { return __shfl(v, src); }
+// any lane of the 8-lane group
+__device__ inline bool grp_any(bool p, int gbase) { return ((__ballot(p) >> gbase) & 0xFFull) != 0; }
+__device__ inline uint32_t grp_or(uint32_t v) {
+  v |= (uint32_t)__shfl_xor((int)v, 1);
+  v |= (uint32_t)__shfl_xor((int)v, 2);
+  v |= (uint32_t)__shfl_xor((int)v, 4);
+  return v;
+}
+// sum over the group's lanes 0..7 holding per-contact values by rank (0 past nc): ((v3 + v2) + (v1 + v0)) +
+// ((v4 + v5) + (v6 + v7)) -- fast_solve_lanes' pairwise order over its contact lanes (row_shr 4, row_shr 8,
+// xor 16: (v3 + v2) + (v1 + v0) and (v7 + v6) + (v5 + v4), then their sum); every lane gets the total
+__device__ inline real rank8_sum(real v) {
+  v += dpp_r<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_r<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_r<0x141>(v);  // row_half_mirror: lane i <- 7 - i, the other quad's sum
+  return v;
+}
+
+// The same pointer, opaque to the optimizer: the three samples' FK read the same topology entries (a
+// limb's link products, rotations, COMs: 80 reals) and frames, and merged loads would keep them live
+// across all three -- 160 VGPRs on top of the samples' results. Loads through a fresh opaque pointer per
+// sample are issued again (L1 hits) where that sample uses them.
+__device__ inline const hs_topo* opaque_s(const hs_topo* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+// One link of limb_fk (its operations): the next joint frame Jv (from the previous link's hinge frame H),
+// the hinge frame H, the link's pos and ust, and at the centre sample its joint position and axis and
+// (the foot link) the foot
+template <bool CENTRE>
+__device__ __attribute__((always_inline)) inline void fk_link(const hs_topo* T, int L, int kk, A34& Jv, A34& H,
+                                                              real s, real c, real* P, real* U, real* Jp, real* Jz,
+                                                              real* fp, bool& contact) {
+  // (a scheduling barrier per link: the machine scheduler hoists the three links' constant loads, 80 reals,
+  // to the top of the sample's block for latency, and the register allocator then spills them)
+  __builtin_amdgcn_sched_barrier(0);
+  const hs_link& lk = opaque_s(T)->link[L][kk];
+  if (kk > 0) Jv = mul(H, load34(lk.P));
+  H = mul_hinge(Jv, c, s);
+  {
+    const real cm[3] = {(real)lk.com[0], (real)lk.com[1], (real)lk.com[2]};
+    mulp(H, cm, P);
+  }
+  {
+    real R[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) R[i] = (real)lk.Rpj[i];
+    auto a_rc = [&](int r, int c) { return H(r, 0) * R[c * 3 + 0] + H(r, 1) * R[c * 3 + 1] + H(r, 2) * R[c * 3 + 2]; };
+    U[0] = (a_rc(2, 1) - a_rc(1, 2)) / 2;
+    U[1] = (a_rc(0, 2) - a_rc(2, 0)) / 2;
+    U[2] = (a_rc(1, 0) - a_rc(0, 1)) / 2;
+  }
+  if (CENTRE) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) Jp[i] = Jv(i, 3);
+#pragma unroll
+    for (int i = 0; i < 3; i++) Jz[i] = Jv(i, 2);
+    if (kk == 2) {  // the foot link (hs_topo::limb_lane_ok)
+      const real cp[3] = {(real)lk.cap[0], (real)lk.cap[1], (real)lk.cap[2]};
+      mulp(H, cp, fp);
+      contact = fp[2] < (real)(T->rcap + 1e-4);
+    }
+  }
+}
+
+// dynamics()' finite differences of one part (dynrec.cpp:175-224) from its pos / ust at t - 2dt, t, t + 2dt
+__device__ inline void part_dyn(real m, real inv, const real* Pm, const real* P0, const real* Pp, const real* Um,
+                                const real* U0, const real* Up, real* f) {
+  real vp[3], vm[3], mr[3], wp[3], wm[3], amr[3];
+  for (int j = 0; j < 3; j++) {
+    vp[j] = Pp[j] - P0[j];
+    vp[j] *= inv;
+    vm[j] = P0[j] - Pm[j];
+    vm[j] *= inv;
+    real mp = vp[j] * m, mm = vm[j] * m;
+    mr[j] = mp - mm;
+    mr[j] *= inv;
+    wp[j] = Up[j] - U0[j];
+    wp[j] *= inv;
+    wm[j] = U0[j] - Um[j];
+    wm[j] *= inv;
+  }
+  for (int j = 0; j < 3; j++) {
+    amr[j] = wp[j] - wm[j];
+    amr[j] *= inv;
+  }
+  for (int j = 0; j < 3; j++) {
+    f[j] = mr[j];
+    f[3 + j] = amr[j];
+  }
+  f[2] += m * real(1);  // gravity, g = 1 (dynrec.cpp:291-295)
+}
+
+// particular_sub's first stage for one part: g = (f, t + (P - o) x f)
+__device__ inline void part_g(const real* P, const real* o, real* f) {
+  real d[3];
+  for (int j = 0; j < 3; j++) d[j] = P[j] - o[j];
+  f[3] += d[1] * f[2] - d[2] * f[1];
+  f[4] += d[2] * f[0] - d[0] * f[2];
+  f[5] += d[0] * f[1] - d[1] * f[0];
+}
+
+// pos and ust of a jointless chain body or of the torso at one sample: straight gaits from the setup's
+// features at tv = 0 (kin_sample_straight), turning ones from the body frame A (node_features)
+struct BodyS {
+  real P[3], U[3];
+};
+__device__ inline BodyS body_straight(const real* bf, const real* u, real tv) {
+  BodyS s;
+  for (int i = 0; i < 3; i++) s.P[i] = fma(tv, u[i], bf[i]);
+  for (int i = 0; i < 3; i++) s.U[i] = bf[3 + i];
+  return s;
+}
+__device__ inline BodyS body_frame(const A34& A, const real* com) {
+  BodyS s;
+  mulp(A, com, s.P);
+  s.U[0] = (A(2, 1) - A(1, 2)) / 2;
+  s.U[1] = (A(0, 2) - A(2, 0)) / 2;
+  s.U[2] = (A(1, 0) - A(0, 1)) / 2;
+  return s;
+}
+
+// Limb L's hip joint frame J at one sample and its chain body's pos / ust (limb_own_n <= 1, hs_topo::
+// limb_lane_ok): straight gaits from KinFrames at tv, turning ones from the torso record's frame and the
+// chain products (kin_sample_tab)
+__device__ __attribute__((always_inline)) inline A34 limb_frame(const hs_topo* T, int L, bool straight, const bool own,
+                                                                const RolloutWS& W, int row, const real* u, real tv,
+                                                                BodyS& ob) {
+#ifdef HS_LIMB_EXP_STRAIGHT
+  straight = true;
+#endif
+  if (straight) {
+    if (own) ob = body_straight(W.kf.own[L][0], u, tv);
+    return frame_at(load34r(W.kf.J0[L]), u, tv);
+  }
+  A34 A = load34r(W.ktor[row] + 6);
+  const int clen = T->limb_chain_len[L];
+  for (int kk = 1; kk < clen; kk++) {
+    const int v = T->limb_chain[L][kk];
+    A = mul(A, node_pj(T, v));
+    if (T->node[v].owner_limb == L) {
+      const real com[3] = {(real)T->node[v].com[0], (real)T->node[v].com[1], (real)T->node[v].com[2]};
+      ob = body_frame(A, com);
+    }
+  }
+  return mul(A, node_joint_parent(T, T->limb_child[L]));
+}
+
+// the links' pos and ust at an outer sample of the stencil (the limb FK without the centre's features)
+// (big: a joint value sincos_k_small does not take, |x| >= 2^20 or not finite: the step is deferred)
+__device__ inline bool sincos_big(real x) { return !(fabs(x) < (real)0x1p20); }
+__device__ __attribute__((always_inline)) inline void limb_outer(const hs_topo* T, int L, const A34& J, const real* ja,
+                                                                 real (&P)[3][3], real (&U)[3][3], bool& big) {
+  real sq[3], cq[3];
+#pragma unroll
+  for (int kk = 0; kk < 3; kk++) {
+    big |= sincos_big(ja[kk]);
+    sincos_k_small(ja[kk], &sq[kk], &cq[kk]);
+  }
+  A34 Jv = J, H;
+  real nul[3];
+  bool nc = false;
+#pragma unroll
+  for (int kk = 0; kk < 3; kk++) fk_link<false>(T, L, kk, Jv, H, sq[kk], cq[kk], P[kk], U[kk], nul, nul, nul, nc);
+}
+
+template <int NM>
+__global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_topo* __restrict__ T, hs_run_args a,
+                                                                      RolloutWS* __restrict__ rws, hs::launch_map mp) {
+  // the outer samples' pos / ust of every lane's links (kinematics), then the groups' exchange arrays:
+  // 18 KB per wavefront, 8 per CU at 2 waves / SIMD
+  __shared__ union {
+    real outer[36][WAVE];  // [Pm, Um, Pp, Up][link][component][lane]: one bank-conflict-free row per value
+    LimbLds<NM> g[LGR];
+  } sh;
+  LimbLds<NM>* lds = sh.g;
+  const int lane = (int)threadIdx.x, grp = lane >> 3, l = lane & 7, gbase = lane & ~7;
+  int fstep = 0, q = (int)blockIdx.x;
+  fused_coords((int)blockIdx.x, mp.fused_w, mp.fused_n, fstep, q);
+  const int b = q * LGR + grp;
+  const bool live = b < a.n_rollouts;
+  const int bb = live ? b : a.n_rollouts - 1;  // an idle group computes a copy and stores nothing
+  LimbLds<NM>& S = lds[grp];
+  const int s_glob = mp.fused_s0 + fstep, call = s_glob / mp.fused_h;
+  const int k0 = (int)(((int64_t)a.k0 + (int64_t)call * mp.fused_h) % a.n_t) + s_glob % mp.fused_h;
+  const int row0 = k0 - mp.ktab_lo;  // table row of sample i - 2 (centre i = k0 + 2)
+  const int nl = T->n_limbs, nmj = T->nmj;
+  const bool limb = l < nl, tlane = l == LG - 1;
+  const int L = limb ? l : 0;
+  const RolloutWS& W = rws[bb];
+  const hs_gait_params& gp = a.params[bb];
+  const bool straight = (real)gp.curvature == 0 && !gp.rec_transform_flag;
+  const real dt = W.st.dt;
+  const real v = W.st.v;
+  const NodeK n0 = load_nodek(T, 0);
+  const real u[3] = {n0.Jp(0, 0), n0.Jp(1, 0), n0.Jp(2, 0)};
+  real tv[5];
+#pragma unroll
+  for (int k = 0; k < 5; k += 2) tv[k] = W.t_tab[row0 + k] * v;  // gait_record's torso advance
+  // the torso COM at the centre sample (particular_sub's origin o = pos(0, 0)), on every lane
+  real o[3];
+  if (straight) {
+    for (int i = 0; i < 3; i++) o[i] = fma(tv[2], u[i], W.kf.torso[i]);
+  } else {
+    mulp(load34r(W.ktor[row0 + 2] + 6), n0.com, o);
+  }
+  const real inv = real(1) / (2 * dt);
+
+  // ---- K and D: the limb's links and its chain body (limb lanes), the torso (lane 7) ----
+  // Liveness drives the order (the step's peak registers are here): the outer samples' pos / ust first,
+  // then the centre link by link, each link's finite differences as soon as its centre values exist
+  real g3[3][6];  // the links' g (f, then f's torque part moved about o)
+  real Jp[3][3], Jz[3][3], fp[3];
+  bool contact = false;
+  bool own = false;  // this limb computes a chain body (limb_own_n = 1)
+  real gown[6];
+  real jvel[3];
+  bool bad = false, big = false;
+  const hs_topo* const T_ = T;
+  if (limb) {
+    const int row = row0;
+    own = T->limb_own_n[L] > 0;
+    // the outer samples (t - 2dt, t + 2dt): the links' pos / ust to LDS (36 reals; held in registers across
+    // the centre's FK they pushed the kernel past 256 VGPRs), the chain body's pos / ust kept
+    BodyS om, op, oc;
+    {
+      real P[3][3], U[3][3];
+      const hs_topo* Ts = opaque_s(T);
+      limb_outer(Ts, L, limb_frame(Ts, L, straight, own, W, row, u, tv[0], om), W.ktab[row][L], P, U, big);
+#pragma unroll
+      for (int kk = 0; kk < 3; kk++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          sh.outer[3 * kk + j][lane] = P[kk][j];
+          sh.outer[9 + 3 * kk + j][lane] = U[kk][j];
+        }
+    }
+    // (sched_barrier: the machine scheduler would interleave the independent samples for ILP, holding
+    // two samples' FK working sets at once)
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      real P[3][3], U[3][3];
+      const hs_topo* Ts = opaque_s(T);
+      limb_outer(Ts, L, limb_frame(Ts, L, straight, own, W, row + 4, u, tv[4], op), W.ktab[row + 4][L], P, U, big);
+#pragma unroll
+      for (int kk = 0; kk < 3; kk++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          sh.outer[18 + 3 * kk + j][lane] = P[kk][j];
+          sh.outer[27 + 3 * kk + j][lane] = U[kk][j];
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const hs_topo* T = opaque_s(T_);
+      const A34 J = limb_frame(T, L, straight, own, W, row + 2, u, tv[2], oc);
+      if (own) {  // the chain body's differences first: its three samples are dead before the links' FK
+        part_dyn((real)T->mass[T->limb_own[L][0]], inv, om.P, oc.P, op.P, om.U, oc.U, op.U, gown);
+        part_g(oc.P, o, gown);
+      }
+      const real* ja = W.ktab[row + 2][L];
+      real sq[3], cq[3];
+#pragma unroll
+      for (int kk = 0; kk < 3; kk++) {
+        big |= sincos_big(ja[kk]);
+        sincos_k_small(ja[kk], &sq[kk], &cq[kk]);
+      }
+      A34 Jv = J, H;
+#pragma unroll
+      for (int kk = 0; kk < 3; kk++) {
+        real P0[3], U0[3];
+        fk_link<true>(T, L, kk, Jv, H, sq[kk], cq[kk], P0, U0, Jp[kk], Jz[kk], fp, contact);
+        real Pm[3], Um[3], Pp[3], Up[3];
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          Pm[j] = sh.outer[3 * kk + j][lane];
+          Um[j] = sh.outer[9 + 3 * kk + j][lane];
+          Pp[j] = sh.outer[18 + 3 * kk + j][lane];
+          Up[j] = sh.outer[27 + 3 * kk + j][lane];
+        }
+        part_dyn((real)T->mass[T->limb_node[L][kk]], inv, Pm, P0, Pp, Um, U0, Up, g3[kk]);
+        part_g(P0, o, g3[kk]);
+      }
+    }
+    bad = W.kbad[row + 2][L] != 0;
+    // the motors' joint rates at the centre (compute_vel_traj's wrapped difference of q at t +- dt)
+#pragma unroll
+    for (int kk = 0; kk < 3; kk++) {
+      real dd = W.ktab[row + 3][L][kk] - W.ktab[row + 1][L][kk];
+      if (dd > kPi) dd -= 2 * kPi;
+      else if (dd < -kPi) dd += 2 * kPi;
+      jvel[kk] = dd / (2 * dt);
+    }
+  }
+  BodyS tb[3];
+  if (tlane) {  // the torso (node 0): its joint frame J = I * J_A_parent (node_features)
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (straight) tb[k] = body_straight(W.kf.torso, u, tv[2 * k]);
+      else tb[k] = body_frame(load34r(W.ktor[row0 + 2 * k] + 6), n0.com);
+    }
+  }
+  wave_sync();  // S.g overlays sh.outer: every lane's outer reads first
+  if (limb) {
+    // g to LDS (the chain bodies' and the root's subtree sums read them)
+#pragma unroll
+    for (int kk = 0; kk < 3; kk++)
+      for (int j = 0; j < 6; j++) S.g[T->limb_node[L][kk]][j] = g3[kk][j];
+    if (own)
+      for (int j = 0; j < 6; j++) S.g[T->limb_own[L][0]][j] = gown[j];
+  } else if (tlane) {
+    real g0[6];
+    part_dyn((real)T->mass[0], inv, tb[0].P, tb[1].P, tb[2].P, tb[0].U, tb[1].U, tb[2].U, g0);
+    part_g(tb[1].P, o, g0);
+    for (int j = 0; j < 6; j++) S.g[0][j] = g0[j];
+  }
+  wave_sync();
+
+  // ---- S1: subtree sums (particular_sub's stage 2) ----
+  // links: their own range (the limb's links are consecutive in preorder, sizes 3, 2, 1)
+  real xt[3][3];  // the links' x torque rows
+  real rawF[2][3], rawV[2][3];  // [0]: the chain body's subtree sums, [1]: the top link's
+  if (limb) {
+#pragma unroll
+    for (int kk = 0; kk < 3; kk++) {
+      real F[3] = {0, 0, 0}, V[3] = {0, 0, 0};
+#pragma unroll
+      for (int m = kk; m < 3; m++)
+        for (int j = 0; j < 3; j++) { F[j] += g3[m][j]; V[j] += g3[m][3 + j]; }
+      if (kk == 0) {  // the limb's top link: a root kid when its chain has no body (its sums for the root)
+        for (int j = 0; j < 3; j++) { rawF[1][j] = F[j]; rawV[1][j] = V[j]; }
+      }
+      real d[3];
+      for (int j = 0; j < 3; j++) d[j] = Jp[kk][j] - o[j];
+      V[0] -= d[1] * F[2] - d[2] * F[1];
+      V[1] -= d[2] * F[0] - d[0] * F[2];
+      V[2] -= d[0] * F[1] - d[1] * F[0];
+      for (int j = 0; j < 3; j++) xt[kk][j] = V[j];
+    }
+    // the chain body this limb owns: its preorder range, read from LDS
+    if (own) {
+      const int vv = T->limb_own[L][0], sz = T->node[vv].size;
+      real F[3] = {0, 0, 0}, V[3] = {0, 0, 0};
+      for (int r = 0; r < sz; r++)
+        for (int j = 0; j < 3; j++) { F[j] += S.g[vv + r][j]; V[j] += S.g[vv + r][3 + j]; }
+      for (int j = 0; j < 3; j++) { rawF[0][j] = F[j]; rawV[0][j] = V[j]; }
+    }
+  }
+  wave_sync();  // every range read above precedes the root kids' writes below
+  if (limb) {
+    if (own) {
+      const int vv = T->limb_own[L][0];
+      if (T->node[vv].parent == 0)
+        for (int j = 0; j < 3; j++) { S.g[vv][j] = rawF[0][j]; S.g[vv][3 + j] = rawV[0][j]; }
+    }
+    const int top = T->limb_node[L][0];
+    if (T->node[top].parent == 0)
+      for (int j = 0; j < 3; j++) { S.g[top][j] = rawF[1][j]; S.g[top][3 + j] = rawV[1][j]; }
+  }
+  wave_sync();
+  if (tlane) {  // the root: its own g plus its children's sums, in kids order; x_0 = (F, V - 0 x F)
+    real F[3], V[3];
+    for (int j = 0; j < 3; j++) { F[j] = S.g[0][j]; V[j] = S.g[0][3 + j]; }
+    const int nk = T->node[0].nkids;
+    for (int kk = 0; kk < HS_CMAX; kk++) {
+      if (kk >= nk) break;
+      const int c = T->node[0].kids[kk];
+      for (int j = 0; j < 3; j++) { F[j] += S.g[c][j]; V[j] += S.g[c][3 + j]; }
+    }
+    const real d[3] = {0, 0, 0};
+    V[0] -= d[1] * F[2] - d[2] * F[1];
+    V[1] -= d[2] * F[0] - d[0] * F[2];
+    V[2] -= d[0] * F[1] - d[1] * F[0];
+    for (int j = 0; j < 3; j++) { S.a[j] = F[j]; S.a[3 + j] = V[j]; }
+  }
+  wave_sync();  // S.a before the Schur system reads it
+
+  // ---- contact list in foot order (ftsolver's contact columns) ----
+  const int fiL = T->link[L][2].foot;
+  const uint32_t cm = grp_or((limb && contact) ? 1u << fiL : 0u);
+  const int nc = __popc(cm);
+  const bool mine = limb && contact;
+  // the limb lane holding contact rank l (lane l < nc of the group gathers that contact's values)
+  int src = 0;
+  for (int L2 = 0; L2 < nl; L2++) {
+    const int f2 = T->link[L2][2].foot;
+    if (((cm >> f2) & 1) && __popc(cm & ((1u << f2) - 1)) == l) src = L2;
+  }
+  src += gbase;
+  const bool slot = l < nc;
+  // the one- and two-contact closed forms and joint values outside sincos_k_small's range: the fixup's
+  bool defer = nc == 1 || nc == 2 || grp_any(big, gbase);
+  real y3[3] = {0, 0, 0};
+  real d0[3] = {0, 0, 0}, Dinv[9], gc[3];
+#ifdef HS_LIMB_EXP_NOSOLVE
+  defer |= nc >= 3;
+  if (false) {
+#else
+  if (nc >= 3) {
+#endif
+    // zeroth_well_posed: the feet's scatter, in single precision, the contacts' d0 on lanes 0 .. nc - 1
+    if (mine)
+      for (int r = 0; r < 3; r++) d0[r] = o[r] - fp[r];
+    float e0 = grp_getf(float(o[0] - fp[0]), src), e1 = grp_getf(float(o[1] - fp[1]), src),
+          e2 = grp_getf(float(o[2] - fp[2]), src);
+    if (!slot) e0 = e1 = e2 = 0.f;
+    {
+      const float s0 = group8_sum(e0), s1 = group8_sum(e1), s2 = group8_sum(e2);
+      const float q00 = group8_sum(e0 * e0), q11 = group8_sum(e1 * e1), q22 = group8_sum(e2 * e2);
+      const float q01 = group8_sum(e0 * e1), q02 = group8_sum(e0 * e2), q12 = group8_sum(e1 * e2);
+      const float k = float(nc);
+      const float c00 = k * q00 - s0 * s0, c11 = k * q11 - s1 * s1, c22 = k * q22 - s2 * s2;
+      const float c01 = k * q01 - s0 * s1, c02 = k * q02 - s0 * s2, c12 = k * q12 - s1 * s2;
+      const float c2 = (c00 * c11 - c01 * c01) + (c00 * c22 - c02 * c02) + (c11 * c22 - c12 * c12);
+      const float tq = q00 + q11 + q22;
+      const float md = fmaxf(k, fmaxf(tq - q00, fmaxf(tq - q11, tq - q22)));
+      const float t = kZerothGuard * k * (c00 + c11 + c22) * md;
+      const bool well = c2 >= t;
+      const bool nearz = c2 >= t / float(kNearBand) && c2 <= t * float(kNearBand);
+      defer |= !well || nearz;  // the same on every lane of the group (group8_sum)
+    }
+    // the contact's first-order block D_c, g_c (fast_solve_lanes: joint m of the foot's chain, foot link
+    // first, on lane m of a quad, summed ((m0 + m1) + (m2 + m3)); the chain's jointless bodies add zeros)
+    real sch[27];
+#pragma unroll
+    for (int e = 0; e < 27; e++) sch[e] = 0;
+    bool lnear = false, ok = true;
+    if (mine) {
+      real tD[3][6], tg[3][3];
+#pragma unroll
+      for (int m = 0; m < 3; m++) {
+        const int p = 2 - m;
+        real Dp[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+        real da[3], va[3][3];
+        for (int r = 0; r < 3; r++) da[r] = Jp[p][r] - fp[r];
+        cross_rows(da, va);
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+          const real w2 = Jz[p][r] * Jz[p][r];
+#pragma unroll
+          for (int i = 0; i < 3; i++) {
+            if (i == r) continue;
+#pragma unroll
+            for (int j = 0; j <= i; j++)
+              if (j != r) Dp[i * (i + 1) / 2 + j] += w2 * va[r][i] * va[r][j];
+            g[i] += w2 * va[r][i] * xt[p][r];
+          }
+        }
+        for (int e = 0; e < 6; e++) tD[m][e] = Dp[e];
+        for (int i = 0; i < 3; i++) tg[m][i] = g[i];
+      }
+      real Dp[6];
+#pragma unroll
+      for (int e = 0; e < 6; e++) Dp[e] = (tD[0][e] + tD[1][e]) + (tD[2][e] + real(0));
+#pragma unroll
+      for (int i = 0; i < 3; i++) gc[i] = (tg[0][i] + tg[1][i]) + (tg[2][i] + real(0));
+      const real D[9] = {Dp[0], Dp[1], Dp[3], Dp[1], Dp[2], Dp[4], Dp[3], Dp[4], Dp[5]};
+      real Lm[9];
+      for (int i = 0; i < 9; i++) Lm[i] = D[i];
+      real rl[3];
+      ok = ldl_n<3>(Lm, kFastPivotGuard, rl, lnear);
+      if (ok) {
+        for (int j = 0; j < 3; j++) {
+          real e[3] = {0, 0, 0};
+          e[j] = 1;
+          ldl_solve_n<3>(Lm, rl, e);
+          for (int i = 0; i < 3; i++) Dinv[3 * i + j] = e[i];
+        }
+        // the block's Schur entries: row r of E = A_c D_c^-1, then (E A_c^T)(r, q) for q <= r, and h_r
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+          real E[3];
+#pragma unroll
+          for (int j = 0; j < 3; j++) {
+            real acc = 0;
+#pragma unroll
+            for (int i = 0; i < 3; i++) acc += a_entry(d0, r, i) * Dinv[3 * i + j];
+            E[j] = acc;
+          }
+#pragma unroll
+          for (int qq = 0; qq <= r; qq++) {
+            real vv = 0;
+#pragma unroll
+            for (int j = 0; j < 3; j++) vv += E[j] * a_entry(d0, qq, j);
+            sch[sch_lower(r, qq)] = vv;
+          }
+          real hh = 0;
+          for (int j = 0; j < 3; j++) hh += E[j] * gc[j];
+          sch[SCH_H + r] = hh;
+        }
+      }
+    }
+    defer |= grp_any(mine && (!ok || lnear), gbase);
+    // the blocks summed over the contacts by rank
+    real Ssum[27];
+#pragma unroll
+    for (int e = 0; e < 27; e++) {
+      real vv = grp_get(sch[e], src);
+      Ssum[e] = rank8_sum(slot ? vv : real(0));
+    }
+    // the 6 x 6 Schur complement system (every lane of the group: the same values)
+    real lam[6];
+    {
+      real Sm[36], rl6[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j < 6; j++) Sm[6 * i + j] = (j <= i) ? Ssum[sch_lower(i, j)] : real(0);
+      for (int r = 0; r < 6; r++) lam[r] = S.a[r] - Ssum[SCH_H + r];
+      bool near6 = false;
+      const bool ok6 = ldl_n<6>(Sm, kFastPivotGuard, rl6, near6);
+      defer |= !ok6 || near6;
+      if (ok6) ldl_solve_n<6>(Sm, rl6, lam);
+    }
+    if (mine) {  // y_c = -D_c^-1 (g_c + A_c^T lam)
+      real t[3];
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        real s = gc[i];
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+          if (r < 3 && r != i) continue;
+          if (r >= 3 && r - 3 == i) continue;
+          s += a_entry(d0, r, i) * lam[r];
+        }
+        t[i] = s;
+      }
+      for (int i = 0; i < 3; i++) {
+        real s = 0;
+        for (int j = 0; j < 3; j++) s += Dinv[3 * i + j] * t[j];
+        y3[i] = -s;
+      }
+    }
+  }
+  if (defer) {  // the whole step to the fixup launch (hs_rollout_kernel FIX_SOLVE)
+    if (l == 0 && live) {
+      const int it = atomicAdd(mp.fix_count, 1);
+      mp.fix_items[2 * it] = fstep;
+      mp.fix_items[2 * it + 1] = b;  // 2 * wavefront + half of hs_rollout_kernel's layout
+    }
+    return;
+  }
+
+  // ---- S4: motor torques, contact forces, work (step()'s outputs) ----
+  const size_t orow = (size_t)b * a.horizon + s_glob;
+  bool nan = false;
+  if (limb) {
+#pragma unroll
+    for (int kk = 0; kk < 3; kk++) {
+      const int hh = T->link[L][kk].hinge;
+      real d[3], yy[3];
+#pragma unroll
+      for (int rr = 0; rr < 3; rr++) {
+        d[rr] = Jp[kk][rr] - fp[rr];
+        yy[rr] = mine ? y3[rr] : real(0);
+      }
+      real tq = real(0);
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        real s = real(0);
+#pragma unroll
+        for (int jj = 0; jj < 3; jj++)
+          if (jj != r) s = s + cross_e(d, jj, r) * yy[jj];
+        real xr = xt[kk][r] + s;
+        tq = tq + Jz[kk][r] * xr;
+      }
+      real dw = tq * jvel[kk];
+      S.wd[hh] = (dw > 0) ? dw : 0;
+      nan |= tq != tq;
+      if (live && a.tau) outp(a.tau)[orow * mp.st_tau + hh] = tq;
+    }
+    if (mine)
+      for (int j = 0; j < 3; j++) nan |= y3[j] != y3[j];
+    if (live && a.cf)
+      for (int j = 0; j < 3; j++) {
+        real zv = -real(0);
+        if (mine) zv = -(real(0) + (real(-1)) * y3[j]);
+        outp(a.cf)[orow * mp.st_cf + 3 * fiL + j] = zv;
+      }
+  }
+  const bool any_nan = grp_any(nan, gbase), any_bad = grp_any(limb && bad, gbase);
+  wave_sync();
+  if (l == 0 && live) {
+    uint32_t flags = 0;
+    if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
+    if (any_nan) flags |= HS_FLAG_NAN;
+    if (any_bad) flags |= HS_FLAG_UNREACH;
+    if (a.flags) a.flags[orow] = flags;
+    // the joints' positive work in joint order (work_over_period's loop, periodic.cpp:294-300), summed over
+    // the steps in order by the reduce
+    real work_dt = real(0);
+    for (int jj = 0; jj < nmj; jj++) work_dt += S.wd[jj];
+    reinterpret_cast<real*>(mp.fused_work)[(size_t)s_glob * a.n_rollouts + b] = work_dt;
+  }
+}

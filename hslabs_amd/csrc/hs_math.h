@@ -98,6 +98,7 @@ struct SC3 {
 #if HS_REAL_IS_FLOAT
 __device__ inline void sincos(float x, float* s, float* c) { sincosf(x, s, c); }
 __device__ inline void sincos_k(float x, float* s, float* c) { sincosf(x, s, c); }
+__device__ inline void sincos_k_small(float x, float* s, float* c) { sincosf(x, s, c); }
 #else
 // sin and cos of an angle of moderate size (joint values, step phases: |x| < 2^20) for the rollout
 // kernels: n = rint(x 2/pi), r = x - n pi/2 in three FMAs against pi/2 = P1 + P2 + P3 (+ 5.6e-50): the
@@ -109,11 +110,18 @@ __device__ inline void sincos_k(float x, float* s, float* c) { sincosf(x, s, c);
 // the code), within 1 ulp (sin) / 2 ulp (cos) of the C library's (tests/test_sincos_k.py runs it on the
 // host, near-multiples of pi/2 up to 2^20 included); sin(-0) comes out +0. Larger or non-finite x: the
 // library's sincos.
+// sincos_k's fast path alone (|x| < 2^20; larger or non-finite x give garbage): for callers that route
+// such arguments elsewhere (the limb-lane kernel defers those steps), without the library's Payne-Hanek
+// reduction inlined at every call site
+__host__ __device__ inline void sincos_k_small(double x, double* s, double* c);
 __host__ __device__ inline void sincos_k(double x, double* s, double* c) {
   if (!(fabs(x) < 0x1p20)) {
     ::sincos(x, s, c);
     return;
   }
+  sincos_k_small(x, s, c);
+}
+__host__ __device__ inline void sincos_k_small(double x, double* s, double* c) {
   const double n = rint(x * 6.36619772367581382433e-01);  // 2/pi
   const double r = fma(-n, -0x1.f1976b7ed8fbcp-110,
                        fma(-n, 0x1.1a62633145c07p-54, fma(-n, 0x1.921fb54442d18p+0, x)));  // P3, P2, P1

@@ -607,6 +607,21 @@ int load_model_file(const char* path, int lik_variant, hs_topo* t, std::string& 
                               (uint32_t)b[4 * w + 3] << 24;
   }
   for (int j = 0; j < nh; j++) t->hinge_foot[j] = t->node[t->hinge_ids[j]].limb_below;
+  {  // hs_topo::limb_lane_ok
+    bool ok = nl >= 1 && nl <= 7 && nf == nl && t->nmj == 3 * nl;
+    uint32_t feet = 0;
+    for (int L = 0; ok && L < nl; L++) {
+      const int v0 = t->limb_node[L][0], f = t->node[t->limb_node[L][2]].foot;
+      for (int k = 0; k < 3; k++) {
+        const hs_node& nd = t->node[t->limb_node[L][k]];
+        ok = ok && t->limb_node[L][k] == v0 + k && nd.size == 3 - k && nd.hinge >= 0 && nd.limb_below == f;
+        ok = ok && ((k == 2) ? nd.foot >= 0 : nd.foot < 0);
+      }
+      ok = ok && f >= 0 && f < 32 && !((feet >> f) & 1) && t->limb_own_n[L] <= 1;
+      if (ok) feet |= 1u << f;
+    }
+    t->limb_lane_ok = ok ? 1 : 0;
+  }
   if (sim) {
     for (int i = 0; i < n; i++) {
       int nt = 0;

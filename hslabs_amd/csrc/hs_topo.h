@@ -93,4 +93,9 @@ struct hs_topo {
   // foot_chain packed for the rollout kernels' LDS copy: foot fi's bytes [len, chain[0], ..., chain[len - 1]]
   // (len <= HS_CHAIN_MAX < 8, node ids < 256) in two little-endian words
   uint32_t foot_chain8[HS_LMAX][2];
+  // the limb-lane step kernel's topology class (hs_limb.h; set by the loader): every limb's three links
+  // consecutive in preorder with subtree sizes 3, 2, 1, its foot on the third link only, one limb per
+  // foot, every motor a limb link, at most one chain body per limb (limb_own_n <= 1), at most 7 limbs
+  // (lane 7 of a rollout's group is the torso's)
+  int32_t limb_lane_ok;
 };

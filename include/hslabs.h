@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define HSLABS_ABI_VERSION 14
+#define HSLABS_ABI_VERSION 15
 
 enum {
   HS_OK = 0,
@@ -537,6 +537,14 @@ int hs_sim_advance(hs_sim_t sim, int32_t n_steps, double* tau_cmd, double* q_mea
 /* HOST copies of the state: body [B][n_parts][HS_SIM_BODY_STRIDE], tsi [B] (either may be NULL). */
 int hs_sim_get_state(hs_sim_t sim, double* body, int32_t* tsi);
 void hs_sim_free(hs_sim_t sim);
+
+/* The fused step launches' kernel (ABI 15). hs_run_calls takes the limb-lane kernel (lane = (rollout,
+ * limb), eight rollouts per wavefront) for a model of its class (*ok = 1: every shipped
+ * model), HS_SOLVE_AUTO, no x / q / dq rows, and calls whose samples fit the IK table; its outputs are
+ * bitwise hs_rollout_kernel's (the steps it does not take go to the same fixup launch). HS_LIMB=0 in the
+ * environment keeps hs_rollout_kernel. hs_limb_launches: the limb-lane launches this process has made. */
+int hs_model_limb_lane(hs_model_t model, int32_t* ok);
+int64_t hs_limb_launches(void);
 
 const char* hs_last_error(void);
 int hs_abi_version(void);

@@ -1,0 +1,127 @@
+"""The limb-lane step kernel (hslabs_amd/csrc/hs_limb.h, round 6) against hs_rollout_kernel's fused step.
+
+hs_run_calls takes the limb-lane kernel for its fused step launches when the model is of its class
+(hs_topo::limb_lane_ok: hexapod, spider, myant), the call solves in HS_SOLVE_AUTO with the IK table and
+asks for no x / q / dq rows; HS_LIMB=0 in the environment keeps hs_rollout_kernel. The limb-lane kernel
+computes every value with the same operations in the same order, and defers to the fixup launch (the
+old kernel's general machinery) every step it does not take -- one or two contacts, tier 2, the
+Eigen-style path, a guard near its threshold -- so the two kernels' outputs are BITWISE equal: torques,
+contact forces, flags, the accumulated work and COT, and the best key. Parity with the oracle then
+follows from tests/test_gpu_parity.py, which runs the default (limb-lane) path.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import MODELS, transformed
+
+pytestmark = pytest.mark.gpu
+
+OUTS = ("tau", "cf", "flags", "work_cot")
+
+
+@pytest.fixture(scope="module")
+def gpu(product):
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return product
+
+
+@pytest.fixture(scope="module")
+def hmodels(gpu):
+    return {n: gpu.KinematicModel(os.path.join(MODELS, f"{n}.xml")) for n in ("hexapod", "spider", "myant")}
+
+
+def run(gpu, model, params, limb, K=20, Hc=1, k0=0, best=True, dtype=None, rollout_id_base=0):
+    import torch
+
+    old = os.environ.get("HS_LIMB")
+    os.environ["HS_LIMB"] = "1" if limb else "0"
+    try:
+        b = gpu.DeviceBatch(model, params, n_t=20, k0=k0, horizon=K * Hc, outputs=OUTS, dtype=dtype,
+                            rollout_id_base=rollout_id_base)
+        b.key_steps = K * Hc
+        b.work_cot.zero_()
+        b.reset_best()
+        b.run_calls(K, call_horizon=Hc, best=best, accumulate=True)
+        torch.cuda.synchronize()
+        out = {k: getattr(b, k).cpu().numpy() for k in OUTS}
+        out["best_key"] = int(b.best_key.item())
+        return out
+    finally:
+        if old is None:
+            os.environ.pop("HS_LIMB")
+        else:
+            os.environ["HS_LIMB"] = old
+
+
+def same(a, b, what):
+    for k in ("tau", "cf", "flags", "work_cot"):
+        assert np.array_equal(a[k], b[k], equal_nan=True), \
+            f"{what}: {k} differs on {int((a[k] != b[k]).sum())} entries (max {np.nanmax(np.abs(a[k].astype(float) - b[k].astype(float))):.3e})"
+    assert a["best_key"] == b["best_key"], what
+
+
+def test_models_are_of_the_limb_lane_class(gpu, hmodels):
+    for n, m in hmodels.items():
+        assert m.limb_lane_ok, n
+
+
+@pytest.mark.parametrize("name,curved,B", [("hexapod", False, 4096), ("hexapod", True, 1003), ("spider", True, 2048),
+                                            ("myant", False, 1024), ("spider", False, 517)])
+def test_limb_kernel_bitwise_equals_rollout_kernel(gpu, hmodels, name, curved, B):
+    """configs[1]'s shape (K = 20 calls of H = 1) and odd batches (idle lanes in the last wavefront):
+    straight and turning gaits (the torso record's frames), myant's one- and two-contact steps (deferred to
+    the fixup launch)"""
+    from hslabs_amd import synth
+
+    p = synth.gen_params(B, name, id0=4321, curved=curved)
+    n0 = gpu.api.limb_launches()
+    a = run(gpu, hmodels[name], p, True)
+    n1 = gpu.api.limb_launches()
+    b = run(gpu, hmodels[name], p, False)
+    assert n1 > n0 and gpu.api.limb_launches() == n1  # the limb-lane kernel ran in the first run only
+    same(a, b, f"{name} curved={curved} B={B}")
+    assert np.isfinite(a["tau"]).all()
+
+
+def test_limb_kernel_transformed_records(gpu, hmodels):
+    """record transforms (tilted, lifted: ill-posed steps the closed form declines, deferred) mixed with
+    plain gaits in one wavefront"""
+    from hslabs_amd import synth
+
+    rng = np.random.default_rng(17)
+    p, _ = transformed(synth.gen_params(512, "hexapod", id0=900, curved=True), rng, tilt=0.05)
+    same(run(gpu, hmodels["hexapod"], p, True), run(gpu, hmodels["hexapod"], p, False), "transformed hexapod")
+
+
+@pytest.mark.parametrize("K,Hc,k0", [(7, 3, 5), (45, 1, 13), (300, 1, 0)])
+def test_limb_kernel_call_shapes(gpu, hmodels, K, Hc, k0):
+    """calls of H > 1, k0 wrapping mod n_t, and more steps than one launch (256 per launch: two launches
+    and their fixups)"""
+    from hslabs_amd import synth
+
+    p = synth.gen_params(640, "hexapod", id0=77)
+    same(run(gpu, hmodels["hexapod"], p, True, K=K, Hc=Hc, k0=k0),
+         run(gpu, hmodels["hexapod"], p, False, K=K, Hc=Hc, k0=k0), f"K={K} H={Hc} k0={k0}")
+
+
+def test_limb_kernel_configs3_shard(gpu, hmodels):
+    """configs[3]'s per-rank shard (32,768 rollouts from id 229,376) with the best key"""
+    from hslabs_amd import synth
+
+    p = synth.gen_params(32768, "hexapod", id0=229376)
+    same(run(gpu, hmodels["hexapod"], p, True, rollout_id_base=229376),
+         run(gpu, hmodels["hexapod"], p, False, rollout_id_base=229376), "configs[3] shard")
+
+
+def test_limb_kernel_fp32(gpu, hmodels):
+    """the single-precision build (configs[2]'s spider, H = 32 rows per call)"""
+    import torch
+    from hslabs_amd import synth
+
+    p = synth.gen_params(2048, "spider", id0=5)
+    same(run(gpu, hmodels["spider"], p, True, K=2, Hc=32, dtype=torch.float32),
+         run(gpu, hmodels["spider"], p, False, K=2, Hc=32, dtype=torch.float32), "fp32 spider")

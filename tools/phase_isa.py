@@ -46,7 +46,7 @@ def main():
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "k.s")
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast",
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast-honor-pragmas",
                         "-DHS_STAMPS", f"-I{SRC}", f"-I{os.path.join(ROOT, 'include')}", *[f"-D{d}" for d in a.D],
                         "--cuda-device-only", "-S", os.path.join(SRC, "hs_kernels.hip"), "-o", out],
                        check=True, stderr=subprocess.DEVNULL)

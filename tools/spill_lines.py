@@ -24,7 +24,7 @@ def main():
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "k.s")
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast",
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast-honor-pragmas",
                         "--cuda-device-only", "-S", "-gline-tables-only", f"-I{args.src}",
                         f"-I{os.path.join(args.src, '..', '..', 'include')}", *[f"-D{d}" for d in args.D],
                         os.path.join(args.src, args.file), "-o", out], check=True, capture_output=True)
