@@ -40,10 +40,11 @@ HEADERS = ["hs_topo.h", "hs_simtopo.h", "hs_ode.h", "hs_math.h", "hs_internal.h"
 ARCH = os.environ.get("HSLABS_ARCH", "gfx950")
 # per-source FMA contraction (default: fast, except where a `#pragma clang fp contract(off)` says not)
 CONTRACT = {"hs_sim.hip": "off", "hs_config.hip": "off"}
-# per-source scheduler choice, measured in round 1 (interleaved A/B): the fp32 rollout kernel
-# (4 waves/SIMD, 128 VGPRs) gains 1.4 % with the iterative ILP scheduler; the fp64 rollout
-# kernel and the simulation are fastest with the default one
-SRC_FLAGS = {"hs_kernels_f32.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
+# per-source compiler flags. Round 1 built the fp32 rollout kernels with the iterative ILP scheduler
+# (+1.4 % for hs_rollout_kernel at 4 waves/SIMD); its register allocator crashes on the limb-lane kernel
+# (hipcc, ROCm 7.2: RAGreedy segfault on hs_limb_kernel<18> in hs_kernels_f32.hip), so every source takes
+# the default scheduler since round 6
+SRC_FLAGS = {}
 
 
 def _hipcc() -> str:

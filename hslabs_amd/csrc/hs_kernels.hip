@@ -334,6 +334,25 @@ __device__ unsigned int g_stamp_base;  // row r holds block g_stamp_base + r (hs
 #define RSTAMP(slot) do {} while (0)
 #endif
 
+// HS_DBG = n (diagnostic variant builds only): intermediate value n of every part written to g_dbg[row][slot]
+// by both step kernels (the limb-lane kernel's bitwise check, tests/test_gpu_limb.py)
+#ifdef HS_DBG
+__device__ double g_dbg[1 << 22];
+__device__ inline int* dbg_rows() {
+  __shared__ int r[8];
+  return r;
+}
+#define DBG(slot, val, n)                                                        \
+  do {                                                                           \
+    if (HS_DBG == (n)) {                                                         \
+      const int r_ = dbg_rows()[threadIdx.x / HALF];                             \
+      if (r_ >= 0 && (size_t)r_ * 32 + (slot) < (1u << 22)) g_dbg[(size_t)r_ * 32 + (slot)] = (double)(val); \
+    }                                                                            \
+  } while (0)
+#else
+#define DBG(slot, val, n) do {} while (0)
+#endif
+
 // ballot over the 32 lanes of this rollout (bit l = sub-lane l)
 __device__ inline uint32_t half_ballot(bool pred) {
   return (uint32_t)(__ballot(pred) >> (threadIdx.x & HALF));
@@ -739,6 +758,8 @@ __device__ __attribute__((always_inline)) inline void limb_fk(const hs_topo* T, 
       mulp(H, c, p);
       real* P = w.pos(k, v);
       for (int i = 0; i < 3; i++) P[i] = p[i];
+      if (k == 0) DBG(v, p[0], 1);
+      if (k == -2) DBG(v, p[0], 12);
     }
     if (w.want_ust(k)) {  // (A(2,1) - A(1,2)) / 2 etc. of A = H pj: (r, c) = sum_m H(r, m) pj(m, c)
       real R[9];
@@ -749,6 +770,9 @@ __device__ __attribute__((always_inline)) inline void limb_fk(const hs_topo* T, 
       U[0] = (a_rc(2, 1) - a_rc(1, 2)) / 2;
       U[1] = (a_rc(0, 2) - a_rc(2, 0)) / 2;
       U[2] = (a_rc(1, 0) - a_rc(0, 1)) / 2;
+      if (k == 0) DBG(v, U[0], 5);
+      if (k == -2) DBG(v, U[0], 9);
+      if (k == 2) DBG(v, U[0], 11);
     }
     if (w.want_centre(k)) {
       real* Jp = w.jpos(k, v);
@@ -1058,6 +1082,11 @@ __device__ __attribute__((always_inline)) inline void dynamics(const hs_topo* T,
       sv.f[3 * (n + i) + j] = amr[j];
     }
     sv.f[3 * i + 2] += m * real(1);  // gravity, g = 1 (dynrec.cpp:291-295)
+    DBG(i, mr[0], 2);
+    DBG(i, amr[0], 10);
+    DBG(i, sv.f[3 * i + 1], 13);
+    DBG(i, sv.f[3 * i + 2], 14);
+    DBG(i, sv.f[3 * (n + i) + 1], 16);
   }
   if (SYNC) wave_sync();
 }
@@ -1127,6 +1156,8 @@ __device__ __attribute__((always_inline)) inline void particular_sub(const hs_to
   for (int kk = 0; kk < HS_CMAX; kk++) kids[kk] = nd.kids[kk];
   const real* P0 = w.pos(0, 0);
   const real o[3] = {P0[0], P0[1], P0[2]};
+  if (lane == 0) DBG(31, o[0], 15);
+  if (lane == 0) DBG(30, o[1], 15);
   if (on) {  // g_i = (f_i, t_i + (P_i - p0) x f_i), the torque part in place
     const int i = lane;
     const real* Pi = w.pos(0, i);
@@ -1136,6 +1167,7 @@ __device__ __attribute__((always_inline)) inline void particular_sub(const hs_to
     t[1] += d[2] * f[0] - d[0] * f[2];
     t[2] += d[0] * f[1] - d[1] * f[0];
     for (int j = 0; j < 3; j++) sv.x[3 * (n + i) + j] = t[j];
+    DBG(i, t[0], 3);
   }
   wave_sync();
   real F[3] = {0, 0, 0}, V[3] = {0, 0, 0};
@@ -1168,6 +1200,9 @@ __device__ __attribute__((always_inline)) inline void particular_sub(const hs_to
     V[1] -= d[2] * F[0] - d[0] * F[2];
     V[2] -= d[0] * F[1] - d[1] * F[0];
     for (int j = 0; j < 3; j++) { sv.x[3 * lane + j] = F[j]; sv.x[3 * (n + lane) + j] = V[j]; }
+    DBG(lane, V[0], 4);
+    DBG(lane, F[0], 18);
+    DBG(lane, d[0], 17);
   }
   // no trailing sync: the caller's contact list ends with one before x is read across lanes
 }
@@ -2201,6 +2236,8 @@ __device__ __attribute__((always_inline)) inline bool fast_solve_lanes(const hs_
 #pragma unroll
       for (int i = 0; i < 3; i++) g[i] = quad_sum(g[i]);
       const real D[9] = {Dp[0], Dp[1], Dp[3], Dp[1], Dp[2], Dp[4], Dp[3], Dp[4], Dp[5]};
+      if (s4 == 0) DBG(24 + fi, Dp[0], 6);
+      if (s4 == 0) DBG(24 + fi, g[0], 7);
       if (s4 == 3) {
         for (int r = 0; r < 3; r++) fl.d0[c][r] = d0[r];
         for (int i = 0; i < 9; i++) fl.D[c][i] = D[i];
@@ -2387,6 +2424,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve_lanes(const hs_
         for (int j = 0; j < 3; j++) s += fl.sc.Dinv[c][3 * i + j] * t[j];
         sv.y[3 * c + i] = -s;
       }
+      DBG(24 + sv.cfoot[c], sv.y[3 * c], 8);
     }
   }
   wave_sync();
@@ -3235,6 +3273,10 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
     k0 = (int)(((int64_t)a.k0 + (int64_t)c * mp.fused_h) % a.n_t) + s % mp.fused_h;
     h_row = s;
   }
+#ifdef HS_DBG
+  if (lane == 0) dbg_rows()[sub] = live ? b * a.horizon + h_row : -1;
+  wave_sync();
+#endif
   const int nl = T->n_limbs;
   // the gait setup of the rollout, stored by the call's preparation pass (hs_prep_kernel;
   // the idle half reads its neighbour's): read from global memory where it is used
@@ -3447,6 +3489,13 @@ __global__ __launch_bounds__(WAVE) void hs_pergen_rec_kernel(const hs_topo* __re
 #endif
 
 }  // namespace
+
+#if defined(HS_DBG) && !HS_REAL_IS_FLOAT
+extern "C" int hs_debug_read_dbg(double* out, int n) {
+  if (n > (1 << 22)) n = 1 << 22;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(double) * n, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 #if defined(HS_STAMPS) && !HS_REAL_IS_FLOAT
 extern "C" int hs_debug_read_stamps(unsigned long long* out, int n_rows) {

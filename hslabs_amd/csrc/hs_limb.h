@@ -56,6 +56,17 @@ __device__ inline real rank8_sum(real v) {
   return v;
 }
 
+// Values made opaque to the optimizer where hs_rollout_kernel passes them through LDS: there a product
+// stored to LDS and loaded back is a rounded operand, here a register whose defining multiply the
+// instruction selector would contract into the consuming add (-ffp-contract=fast), rounding once where
+// hs_rollout_kernel rounds twice (f's torque = amr * inv added into particular_sub's cross term, g's
+// force = mr * inv added into the subtree sums: 1e-14 differences). The asm emits nothing.
+template <int N>
+__device__ inline void opaque_vals(real* v) {
+#pragma unroll
+  for (int j = 0; j < N; j++) asm volatile("" : "+v"(v[j]));
+}
+
 // The same pointer, opaque to the optimizer: the three samples' FK read the same topology entries (a
 // limb's link products, rotations, COMs: 80 reals) and frames, and merged loads would keep them live
 // across all three -- 160 VGPRs on top of the samples' results. Loads through a fresh opaque pointer per
@@ -129,16 +140,19 @@ __device__ inline void part_dyn(real m, real inv, const real* Pm, const real* P0
     f[j] = mr[j];
     f[3 + j] = amr[j];
   }
+  opaque_vals<6>(f);    // dynamics() stores f and adds gravity to the stored value
   f[2] += m * real(1);  // gravity, g = 1 (dynrec.cpp:291-295)
 }
 
 // particular_sub's first stage for one part: g = (f, t + (P - o) x f)
 __device__ inline void part_g(const real* P, const real* o, real* f) {
+  opaque_vals<6>(f);  // f as dynamics() stores it (LDS), then g as particular_sub stores it
   real d[3];
   for (int j = 0; j < 3; j++) d[j] = P[j] - o[j];
   f[3] += d[1] * f[2] - d[2] * f[1];
   f[4] += d[2] * f[0] - d[0] * f[2];
   f[5] += d[0] * f[1] - d[1] * f[0];
+  opaque_vals<6>(f);
 }
 
 // pos and ust of a jointless chain body or of the torso at one sample: straight gaits from the setup's
@@ -246,6 +260,15 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
     mulp(load34r(W.ktor[row0 + 2] + 6), n0.com, o);
   }
   const real inv = real(1) / (2 * dt);
+#ifdef HS_DBG
+  const int dbg_r = live ? b * a.horizon + s_glob : -1;
+#define LDBG(slot, val, n)                                                                                       \
+  do {                                                                                                           \
+    if (HS_DBG == (n) && dbg_r >= 0 && (size_t)dbg_r * 32 + (slot) < (1u << 22)) g_dbg[(size_t)dbg_r * 32 + (slot)] = (double)(val); \
+  } while (0)
+#else
+#define LDBG(slot, val, n) do {} while (0)
+#endif
 
   // ---- K and D: the limb's links and its chain body (limb lanes), the torso (lane 7) ----
   // Liveness drives the order (the step's peak registers are here): the outer samples' pos / ust first,
@@ -311,7 +334,13 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       for (int kk = 0; kk < 3; kk++) {
         real P0[3], U0[3];
         fk_link<true>(T, L, kk, Jv, H, sq[kk], cq[kk], P0, U0, Jp[kk], Jz[kk], fp, contact);
+        opaque_vals<3>(P0);  // the features as hs_rollout_kernel's later phases read them (LDS)
+        opaque_vals<3>(U0);
+        opaque_vals<3>(Jp[kk]);
+        opaque_vals<3>(Jz[kk]);
+        if (kk == 2) opaque_vals<3>(fp);
         real Pm[3], Um[3], Pp[3], Up[3];
+        __builtin_amdgcn_sched_barrier(0);  // the link's outer values read here, not hoisted above its FK
 #pragma unroll
         for (int j = 0; j < 3; j++) {
           Pm[j] = sh.outer[3 * kk + j][lane];
@@ -320,7 +349,20 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
           Up[j] = sh.outer[27 + 3 * kk + j][lane];
         }
         part_dyn((real)T->mass[T->limb_node[L][kk]], inv, Pm, P0, Pp, Um, U0, Up, g3[kk]);
+        LDBG(T->limb_node[L][kk], P0[0], 1);
+        LDBG(T->limb_node[L][kk], U0[0], 5);
+        LDBG(T->limb_node[L][kk], g3[kk][0], 2);
+        LDBG(T->limb_node[L][kk], g3[kk][3], 10);
+        LDBG(T->limb_node[L][kk], g3[kk][1], 13);
+        LDBG(T->limb_node[L][kk], g3[kk][2], 14);
+        LDBG(T->limb_node[L][kk], g3[kk][4], 16);
+        if (l == 0) LDBG(31, o[0], 15);
+        if (l == 0) LDBG(30, o[1], 15);
+        LDBG(T->limb_node[L][kk], Um[0], 9);
+        LDBG(T->limb_node[L][kk], Up[0], 11);
+        LDBG(T->limb_node[L][kk], Pm[0], 12);
         part_g(P0, o, g3[kk]);
+        LDBG(T->limb_node[L][kk], g3[kk][3], 3);
       }
     }
     bad = W.kbad[row + 2][L] != 0;
@@ -371,12 +413,20 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       if (kk == 0) {  // the limb's top link: a root kid when its chain has no body (its sums for the root)
         for (int j = 0; j < 3; j++) { rawF[1][j] = F[j]; rawV[1][j] = V[j]; }
       }
+      // particular_sub applies stage 3 in a block of its own (after a wavefront barrier): F, V enter it
+      // as opaque values
+      opaque_vals<3>(F);
+      opaque_vals<3>(V);
       real d[3];
       for (int j = 0; j < 3; j++) d[j] = Jp[kk][j] - o[j];
       V[0] -= d[1] * F[2] - d[2] * F[1];
       V[1] -= d[2] * F[0] - d[0] * F[2];
       V[2] -= d[0] * F[1] - d[1] * F[0];
       for (int j = 0; j < 3; j++) xt[kk][j] = V[j];
+      opaque_vals<3>(xt[kk]);  // x as the later phases read it (LDS)
+      LDBG(T->limb_node[L][kk], V[0], 4);
+      LDBG(T->limb_node[L][kk], F[0], 18);
+      LDBG(T->limb_node[L][kk], d[0], 17);
     }
     // the chain body this limb owns: its preorder range, read from LDS
     if (own) {
@@ -495,7 +545,10 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       for (int e = 0; e < 6; e++) Dp[e] = (tD[0][e] + tD[1][e]) + (tD[2][e] + real(0));
 #pragma unroll
       for (int i = 0; i < 3; i++) gc[i] = (tg[0][i] + tg[1][i]) + (tg[2][i] + real(0));
+      opaque_vals<3>(d0);
       const real D[9] = {Dp[0], Dp[1], Dp[3], Dp[1], Dp[2], Dp[4], Dp[3], Dp[4], Dp[5]};
+      LDBG(24 + fiL, Dp[0], 6);
+      LDBG(24 + fiL, gc[0], 7);
       real Lm[9];
       for (int i = 0; i < 9; i++) Lm[i] = D[i];
       real rl[3];
@@ -532,6 +585,9 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       }
     }
     defer |= grp_any(mine && (!ok || lnear), gbase);
+    // what fast_solve_lanes stores in FastL and reads back for y (LDS): g_c, d0_c, D_c^-1
+    opaque_vals<3>(gc);
+    opaque_vals<9>(Dinv);
     // the blocks summed over the contacts by rank
     real Ssum[27];
 #pragma unroll
@@ -542,6 +598,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
     // the 6 x 6 Schur complement system (every lane of the group: the same values)
     real lam[6];
     {
+      opaque_vals<27>(Ssum);  // FastL::sc.Ssum
       real Sm[36], rl6[6];
 #pragma unroll
       for (int i = 0; i < 6; i++)
@@ -552,6 +609,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       const bool ok6 = ldl_n<6>(Sm, kFastPivotGuard, rl6, near6);
       defer |= !ok6 || near6;
       if (ok6) ldl_solve_n<6>(Sm, rl6, lam);
+      opaque_vals<6>(lam);  // FastL::sc.lam
     }
     if (mine) {  // y_c = -D_c^-1 (g_c + A_c^T lam)
       real t[3];
@@ -571,6 +629,8 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
         for (int j = 0; j < 3; j++) s += Dinv[3 * i + j] * t[j];
         y3[i] = -s;
       }
+      LDBG(24 + fiL, y3[0], 8);
+      opaque_vals<3>(y3);  // sv.y
     }
   }
   if (defer) {  // the whole step to the fixup launch (hs_rollout_kernel FIX_SOLVE)

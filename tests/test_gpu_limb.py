@@ -117,11 +117,13 @@ def test_limb_kernel_configs3_shard(gpu, hmodels):
          run(gpu, hmodels["hexapod"], p, False, rollout_id_base=229376), "configs[3] shard")
 
 
-def test_limb_kernel_fp32(gpu, hmodels):
-    """the single-precision build (configs[2]'s spider, H = 32 rows per call)"""
+def test_limb_kernel_not_taken_in_fp32(gpu, hmodels):
+    """the single-precision build keeps hs_rollout_kernel (the limb-lane kernel's float build is not bitwise
+    its equal yet)"""
     import torch
     from hslabs_amd import synth
 
     p = synth.gen_params(2048, "spider", id0=5)
-    same(run(gpu, hmodels["spider"], p, True, K=2, Hc=32, dtype=torch.float32),
-         run(gpu, hmodels["spider"], p, False, K=2, Hc=32, dtype=torch.float32), "fp32 spider")
+    n0 = gpu.api.limb_launches()
+    run(gpu, hmodels["spider"], p, True, K=2, Hc=32, dtype=torch.float32)
+    assert gpu.api.limb_launches() == n0
