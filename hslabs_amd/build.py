@@ -36,7 +36,7 @@ SOURCES = ["hs_kernels.hip", "hs_kernels_f32.hip", "hs_sim.hip", "hs_config.hip"
 # (same SONAME) is the one bound
 LIBS = ["-L/opt/rocm/lib", "-lrccl"]
 VARIANT_DIR = os.path.join(OUT_DIR, "variants")
-HEADERS = ["hs_topo.h", "hs_simtopo.h", "hs_ode.h", "hs_math.h", "hs_internal.h", os.path.join("..", "..", "include", "hslabs.h")]
+HEADERS = ["hs_topo.h", "hs_simtopo.h", "hs_ode.h", "hs_math.h", "hs_internal.h", "hs_limb.h", os.path.join("..", "..", "include", "hslabs.h")]
 ARCH = os.environ.get("HSLABS_ARCH", "gfx950")
 # per-source FMA contraction (default: fast, except where a `#pragma clang fp contract(off)` says not)
 CONTRACT = {"hs_sim.hip": "off", "hs_config.hip": "off"}

@@ -21,6 +21,9 @@
 // computes it with hs_rollout_kernel's whole machinery (1 and 2 contacts, tier 2, the Eigen-style path,
 // HS_FLAG_NEAR_RANK): the same (step, rollout) items the fused step launch defers.
 
+#ifndef HS_LIMB_LINK_BARRIER
+#define HS_LIMB_LINK_BARRIER 0  // 1: within noise at the driver command, 3 % slower at K = 200 (r06_t5)
+#endif
 #ifndef HS_LIMB_WAVES
 #define HS_LIMB_WAVES 2  // waves per SIMD the limb kernel is built for
 #endif
@@ -71,22 +74,26 @@ __device__ inline void opaque_vals(real* v) {
 // limb's link products, rotations, COMs: 80 reals) and frames, and merged loads would keep them live
 // across all three -- 160 VGPRs on top of the samples' results. Loads through a fresh opaque pointer per
 // sample are issued again (L1 hits) where that sample uses them.
+// (through an address-space-1 pointer: a generic one would turn the topology reads into flat loads)
 __device__ inline const hs_topo* opaque_s(const hs_topo* p) {
-  asm volatile("" : "+s"(p));
-  return p;
+  using gptr = const __attribute__((address_space(1))) hs_topo*;
+  gptr q = (gptr)p;
+  asm volatile("" : "+s"(q));
+  return (const hs_topo*)q;
 }
 
 // One link of limb_fk (its operations): the next joint frame Jv (from the previous link's hinge frame H),
 // the hinge frame H, the link's pos and ust, and at the centre sample its joint position and axis and
 // (the foot link) the foot
 template <bool CENTRE>
-__device__ __attribute__((always_inline)) inline void fk_link(const hs_topo* T, int L, int kk, A34& Jv, A34& H,
-                                                              real s, real c, real* P, real* U, real* Jp, real* Jz,
-                                                              real* fp, bool& contact) {
+__device__ __attribute__((always_inline)) inline void fk_link(const hs_topo* T, const hs_link& lk, int kk, A34& Jv,
+                                                              A34& H, real s, real c, real* P, real* U, real* Jp,
+                                                              real* Jz, real* fp, bool& contact) {
+#if HS_LIMB_LINK_BARRIER
   // (a scheduling barrier per link: the machine scheduler hoists the three links' constant loads, 80 reals,
   // to the top of the sample's block for latency, and the register allocator then spills them)
   __builtin_amdgcn_sched_barrier(0);
-  const hs_link& lk = opaque_s(T)->link[L][kk];
+#endif
   if (kk > 0) Jv = mul(H, load34(lk.P));
   H = mul_hinge(Jv, c, s);
   {
@@ -204,8 +211,9 @@ __device__ __attribute__((always_inline)) inline A34 limb_frame(const hs_topo* T
 // the links' pos and ust at an outer sample of the stencil (the limb FK without the centre's features)
 // (big: a joint value sincos_k_small does not take, |x| >= 2^20 or not finite: the step is deferred)
 __device__ inline bool sincos_big(real x) { return !(fabs(x) < (real)0x1p20); }
-__device__ __attribute__((always_inline)) inline void limb_outer(const hs_topo* T, int L, const A34& J, const real* ja,
-                                                                 real (&P)[3][3], real (&U)[3][3], bool& big) {
+__device__ __attribute__((always_inline)) inline void limb_outer(const hs_topo* T, const hs_link (&LK)[3], const A34& J,
+                                                                 const real* ja, real (&P)[3][3], real (&U)[3][3],
+                                                                 bool& big) {
   real sq[3], cq[3];
 #pragma unroll
   for (int kk = 0; kk < 3; kk++) {
@@ -216,7 +224,7 @@ __device__ __attribute__((always_inline)) inline void limb_outer(const hs_topo* 
   real nul[3];
   bool nc = false;
 #pragma unroll
-  for (int kk = 0; kk < 3; kk++) fk_link<false>(T, L, kk, Jv, H, sq[kk], cq[kk], P[kk], U[kk], nul, nul, nul, nc);
+  for (int kk = 0; kk < 3; kk++) fk_link<false>(T, LK[kk], kk, Jv, H, sq[kk], cq[kk], P[kk], U[kk], nul, nul, nul, nc);
 }
 
 template <int NM>
@@ -224,11 +232,26 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
                                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
   // the outer samples' pos / ust of every lane's links (kinematics), then the groups' exchange arrays:
   // 18 KB per wavefront, 8 per CU at 2 waves / SIMD
+  // kinematics: the outer samples' pos / ust of every limb lane's links and the limbs' link records (read
+  // by every sample's FK: from LDS, not through three rounds of L1/L2 latency per sample), then the
+  // groups' exchange arrays: 17.4 KB per wavefront, 8 per CU at 2 waves / SIMD
   __shared__ union {
-    real outer[36][WAVE];  // [Pm, Um, Pp, Up][link][component][lane]: one bank-conflict-free row per value
+    struct {
+      real outer[36][LGR * HS_LMAX];  // [Pm, Um, Pp, Up][link][component][limb lane]: one conflict-free row per value
+      hs_link links[HS_LMAX][3];
+    } k;
     LimbLds<NM> g[LGR];
   } sh;
   LimbLds<NM>* lds = sh.g;
+  {  // the link records, 8 bytes per lane and load
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(&T->link[0][0]);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(&sh.k.links[0][0]);
+    constexpr int NW = sizeof(sh.k.links) / sizeof(uint64_t);
+    for (int e = (int)threadIdx.x; e < NW; e += WAVE) dst[e] = src[e];
+    wave_sync();
+  }
+  RSTAMP(16);
+  STAMP(15);
   const int lane = (int)threadIdx.x, grp = lane >> 3, l = lane & 7, gbase = lane & ~7;
   int fstep = 0, q = (int)blockIdx.x;
   fused_coords((int)blockIdx.x, mp.fused_w, mp.fused_n, fstep, q);
@@ -236,6 +259,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   const bool live = b < a.n_rollouts;
   const int bb = live ? b : a.n_rollouts - 1;  // an idle group computes a copy and stores nothing
   LimbLds<NM>& S = lds[grp];
+  const int ol = grp * HS_LMAX + (l < HS_LMAX ? l : 0);  // this limb lane's column of sh.k.outer
   const int s_glob = mp.fused_s0 + fstep, call = s_glob / mp.fused_h;
   const int k0 = (int)(((int64_t)a.k0 + (int64_t)call * mp.fused_h) % a.n_t) + s_glob % mp.fused_h;
   const int row0 = k0 - mp.ktab_lo;  // table row of sample i - 2 (centre i = k0 + 2)
@@ -270,6 +294,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
 #define LDBG(slot, val, n) do {} while (0)
 #endif
 
+  STAMP(0);
   // ---- K and D: the limb's links and its chain body (limb lanes), the torso (lane 7) ----
   // Liveness drives the order (the step's peak registers are here): the outer samples' pos / ust first,
   // then the centre link by link, each link's finite differences as soon as its centre values exist
@@ -290,31 +315,34 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
     {
       real P[3][3], U[3][3];
       const hs_topo* Ts = opaque_s(T);
-      limb_outer(Ts, L, limb_frame(Ts, L, straight, own, W, row, u, tv[0], om), W.ktab[row][L], P, U, big);
+      limb_outer(Ts, sh.k.links[L], limb_frame(Ts, L, straight, own, W, row, u, tv[0], om), W.ktab[row][L], P, U, big);
 #pragma unroll
       for (int kk = 0; kk < 3; kk++)
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-          sh.outer[3 * kk + j][lane] = P[kk][j];
-          sh.outer[9 + 3 * kk + j][lane] = U[kk][j];
+          sh.k.outer[3 * kk + j][ol] = P[kk][j];
+          sh.k.outer[9 + 3 * kk + j][ol] = U[kk][j];
         }
     }
+    STAMP(1);
     // (sched_barrier: the machine scheduler would interleave the independent samples for ILP, holding
     // two samples' FK working sets at once)
     __builtin_amdgcn_sched_barrier(0);
     {
       real P[3][3], U[3][3];
       const hs_topo* Ts = opaque_s(T);
-      limb_outer(Ts, L, limb_frame(Ts, L, straight, own, W, row + 4, u, tv[4], op), W.ktab[row + 4][L], P, U, big);
+      limb_outer(Ts, sh.k.links[L], limb_frame(Ts, L, straight, own, W, row + 4, u, tv[4], op), W.ktab[row + 4][L], P, U,
+                 big);
 #pragma unroll
       for (int kk = 0; kk < 3; kk++)
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-          sh.outer[18 + 3 * kk + j][lane] = P[kk][j];
-          sh.outer[27 + 3 * kk + j][lane] = U[kk][j];
+          sh.k.outer[18 + 3 * kk + j][ol] = P[kk][j];
+          sh.k.outer[27 + 3 * kk + j][ol] = U[kk][j];
         }
     }
     __builtin_amdgcn_sched_barrier(0);
+    STAMP(2);
     {
       const hs_topo* T = opaque_s(T_);
       const A34 J = limb_frame(T, L, straight, own, W, row + 2, u, tv[2], oc);
@@ -333,7 +361,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
 #pragma unroll
       for (int kk = 0; kk < 3; kk++) {
         real P0[3], U0[3];
-        fk_link<true>(T, L, kk, Jv, H, sq[kk], cq[kk], P0, U0, Jp[kk], Jz[kk], fp, contact);
+        fk_link<true>(T, sh.k.links[L][kk], kk, Jv, H, sq[kk], cq[kk], P0, U0, Jp[kk], Jz[kk], fp, contact);
         opaque_vals<3>(P0);  // the features as hs_rollout_kernel's later phases read them (LDS)
         opaque_vals<3>(U0);
         opaque_vals<3>(Jp[kk]);
@@ -343,10 +371,10 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
         __builtin_amdgcn_sched_barrier(0);  // the link's outer values read here, not hoisted above its FK
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-          Pm[j] = sh.outer[3 * kk + j][lane];
-          Um[j] = sh.outer[9 + 3 * kk + j][lane];
-          Pp[j] = sh.outer[18 + 3 * kk + j][lane];
-          Up[j] = sh.outer[27 + 3 * kk + j][lane];
+          Pm[j] = sh.k.outer[3 * kk + j][ol];
+          Um[j] = sh.k.outer[9 + 3 * kk + j][ol];
+          Pp[j] = sh.k.outer[18 + 3 * kk + j][ol];
+          Up[j] = sh.k.outer[27 + 3 * kk + j][ol];
         }
         part_dyn((real)T->mass[T->limb_node[L][kk]], inv, Pm, P0, Pp, Um, U0, Up, g3[kk]);
         LDBG(T->limb_node[L][kk], P0[0], 1);
@@ -375,6 +403,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       jvel[kk] = dd / (2 * dt);
     }
   }
+  STAMP(3);
   BodyS tb[3];
   if (tlane) {  // the torso (node 0): its joint frame J = I * J_A_parent (node_features)
 #pragma unroll
@@ -383,7 +412,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       else tb[k] = body_frame(load34r(W.ktor[row0 + 2 * k] + 6), n0.com);
     }
   }
-  wave_sync();  // S.g overlays sh.outer: every lane's outer reads first
+  wave_sync();  // S.g overlays sh.k: every lane's outer and link reads first
   if (limb) {
     // g to LDS (the chain bodies' and the root's subtree sums read them)
 #pragma unroll
@@ -399,10 +428,12 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   }
   wave_sync();
 
+  STAMP(4);
   // ---- S1: subtree sums (particular_sub's stage 2) ----
-  // links: their own range (the limb's links are consecutive in preorder, sizes 3, 2, 1)
+  // links: their own range in registers (the limb's links are consecutive in preorder, sizes 3, 2, 1); the
+  // root on the torso lane: its own g plus each kid's subtree sum (the kid's preorder range, in order),
+  // particular_sub's two levels of sums
   real xt[3][3];  // the links' x torque rows
-  real rawF[2][3], rawV[2][3];  // [0]: the chain body's subtree sums, [1]: the top link's
   if (limb) {
 #pragma unroll
     for (int kk = 0; kk < 3; kk++) {
@@ -410,9 +441,6 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
 #pragma unroll
       for (int m = kk; m < 3; m++)
         for (int j = 0; j < 3; j++) { F[j] += g3[m][j]; V[j] += g3[m][3 + j]; }
-      if (kk == 0) {  // the limb's top link: a root kid when its chain has no body (its sums for the root)
-        for (int j = 0; j < 3; j++) { rawF[1][j] = F[j]; rawV[1][j] = V[j]; }
-      }
       // particular_sub applies stage 3 in a block of its own (after a wavefront barrier): F, V enter it
       // as opaque values
       opaque_vals<3>(F);
@@ -428,35 +456,18 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       LDBG(T->limb_node[L][kk], F[0], 18);
       LDBG(T->limb_node[L][kk], d[0], 17);
     }
-    // the chain body this limb owns: its preorder range, read from LDS
-    if (own) {
-      const int vv = T->limb_own[L][0], sz = T->node[vv].size;
-      real F[3] = {0, 0, 0}, V[3] = {0, 0, 0};
-      for (int r = 0; r < sz; r++)
-        for (int j = 0; j < 3; j++) { F[j] += S.g[vv + r][j]; V[j] += S.g[vv + r][3 + j]; }
-      for (int j = 0; j < 3; j++) { rawF[0][j] = F[j]; rawV[0][j] = V[j]; }
-    }
   }
-  wave_sync();  // every range read above precedes the root kids' writes below
-  if (limb) {
-    if (own) {
-      const int vv = T->limb_own[L][0];
-      if (T->node[vv].parent == 0)
-        for (int j = 0; j < 3; j++) { S.g[vv][j] = rawF[0][j]; S.g[vv][3 + j] = rawV[0][j]; }
-    }
-    const int top = T->limb_node[L][0];
-    if (T->node[top].parent == 0)
-      for (int j = 0; j < 3; j++) { S.g[top][j] = rawF[1][j]; S.g[top][3 + j] = rawV[1][j]; }
-  }
-  wave_sync();
-  if (tlane) {  // the root: its own g plus its children's sums, in kids order; x_0 = (F, V - 0 x F)
+  if (tlane) {  // x_0 = (F, V - 0 x F)
     real F[3], V[3];
     for (int j = 0; j < 3; j++) { F[j] = S.g[0][j]; V[j] = S.g[0][3 + j]; }
     const int nk = T->node[0].nkids;
     for (int kk = 0; kk < HS_CMAX; kk++) {
       if (kk >= nk) break;
-      const int c = T->node[0].kids[kk];
-      for (int j = 0; j < 3; j++) { F[j] += S.g[c][j]; V[j] += S.g[c][3 + j]; }
+      const int c = T->node[0].kids[kk], sz = T->node[c].size;
+      real Fk[3] = {0, 0, 0}, Vk[3] = {0, 0, 0};
+      for (int r = 0; r < sz; r++)
+        for (int j = 0; j < 3; j++) { Fk[j] += S.g[c + r][j]; Vk[j] += S.g[c + r][3 + j]; }
+      for (int j = 0; j < 3; j++) { F[j] += Fk[j]; V[j] += Vk[j]; }
     }
     const real d[3] = {0, 0, 0};
     V[0] -= d[1] * F[2] - d[2] * F[1];
@@ -466,6 +477,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   }
   wave_sync();  // S.a before the Schur system reads it
 
+  STAMP(5);
   // ---- contact list in foot order (ftsolver's contact columns) ----
   const int fiL = T->link[L][2].foot;
   const uint32_t cm = grp_or((limb && contact) ? 1u << fiL : 0u);
@@ -510,6 +522,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       const bool nearz = c2 >= t / float(kNearBand) && c2 <= t * float(kNearBand);
       defer |= !well || nearz;  // the same on every lane of the group (group8_sum)
     }
+    STAMP(6);
     // the contact's first-order block D_c, g_c (fast_solve_lanes: joint m of the foot's chain, foot link
     // first, on lane m of a quad, summed ((m0 + m1) + (m2 + m3)); the chain's jointless bodies add zeros)
     real sch[27];
@@ -595,6 +608,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       real vv = grp_get(sch[e], src);
       Ssum[e] = rank8_sum(slot ? vv : real(0));
     }
+    STAMP(7);
     // the 6 x 6 Schur complement system (every lane of the group: the same values)
     real lam[6];
     {
@@ -633,6 +647,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       opaque_vals<3>(y3);  // sv.y
     }
   }
+  STAMP(8);
   if (defer) {  // the whole step to the fixup launch (hs_rollout_kernel FIX_SOLVE)
     if (l == 0 && live) {
       const int it = atomicAdd(mp.fix_count, 1);
@@ -693,4 +708,6 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
     for (int jj = 0; jj < nmj; jj++) work_dt += S.wd[jj];
     reinterpret_cast<real*>(mp.fused_work)[(size_t)s_glob * a.n_rollouts + b] = work_dt;
   }
+  STAMP(9);
+  RSTAMP(17);
 }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes for hs_rollout_kernel (run under gpurun), one counter group per pass, on the bench's
+# PMC passes for the fused step launch (run under gpurun), one counter group per pass, on the bench's
 # own command (default: the driver's, fused launches). tools/pmc_summary.py divides each fused
 # dispatch's counts by the steps it ran (grid / wavefronts per step) and skips the setup-only pass.
 #   PMC_SET=traffic (default: HBM bytes + instruction mix) | diag (stall/i-cache breakdown)

@@ -18,19 +18,24 @@ import os
 import statistics
 from collections import defaultdict
 
-KERNEL = "hs_rollout_kernel"
-STEP_LAUNCH = re.compile(r"hs_rollout_kernel<\d+, false, 1>")  # the fused step launch (hs::FIX_DEFER)
+KERNEL = "the fused step launch"
+# the fused step launch: the limb-lane kernel (round 6: 8 rollouts per wavefront) or hs_rollout_kernel's
+# FIX_DEFER instantiation (2 per wavefront)
+STEP_LAUNCH = re.compile(r"hs_limb_kernel<\d+>|hs_rollout_kernel<\d+, false, 1>")
 FORCES_LAUNCH = re.compile(r"hs_rollout_kernel<\d+, true, 0>")  # solve_forces' step launches (--forces)
 
 
-def collect(root, n_waves, step_launch=STEP_LAUNCH):
+def collect(root, n_rollouts, step_launch=STEP_LAUNCH):
     """counter -> per-step values of the step launches of the timed job: in each pass, the dispatches with
     the most steps (the bench's warm-up job runs fewer steps per launch and is left out)"""
     vals = defaultdict(dict)  # counter -> dispatch -> per-step value
     for path in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
         with open(path) as f:
             rows = [r for r in csv.DictReader(f) if step_launch.search(r["Kernel_Name"])]
-        steps_of = {r["Dispatch_Id"]: int(r.get("Grid_Size") or r.get("Grid_Size_X")) // 64 // n_waves for r in rows}
+        def waves_per_step(name):
+            return (n_rollouts + 7) // 8 if "hs_limb_kernel" in name else (n_rollouts + 1) // 2
+        steps_of = {r["Dispatch_Id"]: int(r.get("Grid_Size") or r.get("Grid_Size_X")) // 64 // waves_per_step(r["Kernel_Name"])
+                    for r in rows}
         most = max(steps_of.values(), default=0)
         for row in rows:
             steps = steps_of[row["Dispatch_Id"]]
@@ -81,8 +86,7 @@ def main():
     ap.add_argument("--forces", action="store_true", help="solve_forces' step launches (bench.py --forces)")
     ap.add_argument("--job-steps", type=int, default=20, help="steps per job: the per-job kernels' share")
     a = ap.parse_args()
-    n_waves = (a.rollouts + 1) // 2
-    v = collect(a.root, n_waves, FORCES_LAUNCH if a.forces else STEP_LAUNCH)
+    v = collect(a.root, a.rollouts, FORCES_LAUNCH if a.forces else STEP_LAUNCH)
     med = {c: statistics.median(x) for c, x in v.items()}
     sha = lib_of(a.root)
     lines = [f"{KERNEL}, {a.workload} ({a.cmd}), rocprofv3 --pmc, one group per pass, library {sha}",
