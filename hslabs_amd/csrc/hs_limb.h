@@ -64,6 +64,7 @@ __device__ inline real rank8_sum(real v) {
 // instruction selector would contract into the consuming add (-ffp-contract=fast), rounding once where
 // hs_rollout_kernel rounds twice (f's torque = amr * inv added into particular_sub's cross term, g's
 // force = mr * inv added into the subtree sums: 1e-14 differences). The asm emits nothing.
+// (not volatile: a volatile asm is a scheduling boundary, and the step has dozens of these)
 template <int N>
 __device__ inline void opaque_vals(real* v) {
 #pragma unroll
@@ -294,6 +295,19 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
 #define LDBG(slot, val, n) do {} while (0)
 #endif
 
+  // the torso's g (node 0; its joint frame J = I * J_A_parent, node_features), on every lane: its loads and
+  // arithmetic overlap the limbs' (a torso-lane branch after them would expose its load latency)
+  real g0[6];
+  {
+    BodyS tb[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (straight) tb[k] = body_straight(W.kf.torso, u, tv[2 * k]);
+      else tb[k] = body_frame(load34r(W.ktor[row0 + 2 * k] + 6), n0.com);
+    }
+    part_dyn((real)T->mass[0], inv, tb[0].P, tb[1].P, tb[2].P, tb[0].U, tb[1].U, tb[2].U, g0);
+    part_g(tb[1].P, o, g0);
+  }
   STAMP(0);
   // ---- K and D: the limb's links and its chain body (limb lanes), the torso (lane 7) ----
   // Liveness drives the order (the step's peak registers are here): the outer samples' pos / ust first,
@@ -404,14 +418,6 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
     }
   }
   STAMP(3);
-  BodyS tb[3];
-  if (tlane) {  // the torso (node 0): its joint frame J = I * J_A_parent (node_features)
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      if (straight) tb[k] = body_straight(W.kf.torso, u, tv[2 * k]);
-      else tb[k] = body_frame(load34r(W.ktor[row0 + 2 * k] + 6), n0.com);
-    }
-  }
   wave_sync();  // S.g overlays sh.k: every lane's outer and link reads first
   if (limb) {
     // g to LDS (the chain bodies' and the root's subtree sums read them)
@@ -421,9 +427,6 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
     if (own)
       for (int j = 0; j < 6; j++) S.g[T->limb_own[L][0]][j] = gown[j];
   } else if (tlane) {
-    real g0[6];
-    part_dyn((real)T->mass[0], inv, tb[0].P, tb[1].P, tb[2].P, tb[0].U, tb[1].U, tb[2].U, g0);
-    part_g(tb[1].P, o, g0);
     for (int j = 0; j < 6; j++) S.g[0][j] = g0[j];
   }
   wave_sync();
@@ -465,7 +468,12 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       if (kk >= nk) break;
       const int c = T->node[0].kids[kk], sz = T->node[c].size;
       real Fk[3] = {0, 0, 0}, Vk[3] = {0, 0, 0};
-      for (int r = 0; r < sz; r++)
+      // the range's loads issued together (ranges of up to 8 parts unrolled: hexapod 7, spider 3, myant 4)
+#pragma unroll
+      for (int r = 0; r < 8; r++)
+        if (r < sz)
+          for (int j = 0; j < 3; j++) { Fk[j] += S.g[c + r][j]; Vk[j] += S.g[c + r][3 + j]; }
+      for (int r = 8; r < sz; r++)
         for (int j = 0; j < 3; j++) { Fk[j] += S.g[c + r][j]; Vk[j] += S.g[c + r][3 + j]; }
       for (int j = 0; j < 3; j++) { F[j] += Fk[j]; V[j] += Vk[j]; }
     }
