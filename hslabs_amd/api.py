@@ -207,6 +207,13 @@ def limb_launches() -> int:
     return int(capi.load().hs_limb_launches())
 
 
+def limb_deferred() -> int:
+    """steps the limb-lane kernel deferred to the fixup launch in this process (hs_limb_stats; synchronous)"""
+    d = ctypes.c_int64()
+    capi.check(capi.load().hs_limb_stats(None, ctypes.byref(d)), "hs_limb_stats")
+    return int(d.value)
+
+
 def params_array(params) -> np.ndarray:
     """list[PgsConfigParams] | structured array -> contiguous GAIT_DTYPE array."""
     if isinstance(params, np.ndarray) and params.dtype == GAIT_DTYPE:

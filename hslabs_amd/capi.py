@@ -43,7 +43,7 @@ EXPORTS = [
     "hs_batch_best_key_device", "hs_batch_free", "hs_comm_unique_id", "hs_comm_init", "hs_comm_free", "hs_comm_size",
     "hs_comm_reduce_best", "hs_select_best_comm", "hs_pergen_rec", "hs_pergen_rec_host", "hs_model_lik",
     "hs_model_lik_host", "hs_model_fk", "hs_model_fk_host", "hs_model_get_node", "hs_model_set_torso_penalty",
-    "hs_model_get_torso_penalty", "hs_model_limb_lane", "hs_limb_launches",
+    "hs_model_get_torso_penalty", "hs_model_limb_lane", "hs_limb_launches", "hs_limb_stats",
 ]
 HS_FLAG_LIK_FAILED = 128
 SIM_BODY_STRIDE = 13
@@ -249,6 +249,7 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.hs_model_limb_lane.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)]
     L.hs_limb_launches.argtypes = []
     L.hs_limb_launches.restype = ctypes.c_int64
+    L.hs_limb_stats.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     L.hs_abi_version.argtypes = []
     L.hs_abi_version.restype = ctypes.c_int
     if L.hs_abi_version() != ABI_VERSION:

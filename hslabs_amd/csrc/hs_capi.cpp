@@ -378,6 +378,21 @@ int hs_model_limb_lane(hs_model_t m, int32_t* ok) {
 
 int64_t hs_limb_launches(void) { return g_limb_launches.load(); }
 
+extern "C" int hs_limb_deferred_f64(unsigned long long* out);
+extern "C" int hs_limb_deferred_f32(unsigned long long* out);
+
+int hs_limb_stats(int64_t* launches, int64_t* deferred) {
+  if (launches) *launches = g_limb_launches.load();
+  if (deferred) {
+    unsigned long long a = 0, b = 0;
+    hipError_t e = (hipError_t)hs_limb_deferred_f64(&a);
+    if (e == hipSuccess) e = (hipError_t)hs_limb_deferred_f32(&b);
+    if (e != hipSuccess) return hip_fail(e, "hs_limb_stats");
+    *deferred = (int64_t)(a + b);
+  }
+  return HS_OK;
+}
+
 const char* hs_last_error(void) { return g_err.c_str(); }
 
 int hs_model_load_ex(const char* xml_path, int lik_variant, hs_model_t* out) {

@@ -3490,6 +3490,15 @@ __global__ __launch_bounds__(WAVE) void hs_pergen_rec_kernel(const hs_topo* __re
 
 }  // namespace
 
+#if HS_REAL_IS_FLOAT
+extern "C" int hs_limb_deferred_f32(unsigned long long* out) {
+#else
+extern "C" int hs_limb_deferred_f64(unsigned long long* out) {
+#endif
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_limb_deferred), sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+}
+
 #if defined(HS_DBG) && !HS_REAL_IS_FLOAT
 extern "C" int hs_debug_read_dbg(double* out, int n) {
   if (n > (1 << 22)) n = 1 << 22;

@@ -21,6 +21,15 @@
 // computes it with hs_rollout_kernel's whole machinery (1 and 2 contacts, tier 2, the Eigen-style path,
 // HS_FLAG_NEAR_RANK): the same (step, rollout) items the fused step launch defers.
 
+#ifndef HS_LIMB_ROOT_BRANCHFREE
+#define HS_LIMB_ROOT_BRANCHFREE 0
+#endif
+#ifndef HS_LIMB_WORK_UNROLL
+#define HS_LIMB_WORK_UNROLL 0
+#endif
+#ifndef HS_LIMB_SAMPLE_BARRIER
+#define HS_LIMB_SAMPLE_BARRIER 1  // scheduling barriers between the stencil's samples (register pressure)
+#endif
 #ifndef HS_LIMB_LINK_BARRIER
 #define HS_LIMB_LINK_BARRIER 0  // 1: within noise at the driver command, 3 % slower at K = 200 (r06_t5)
 #endif
@@ -30,6 +39,10 @@
 
 constexpr int LG = 8;           // lanes per rollout group
 constexpr int LGR = WAVE / LG;  // rollouts per wavefront
+
+// steps this process's limb-lane launches deferred to the fixup launch (hs_limb_stats; one atomic per
+// deferred step, rare)
+__device__ unsigned long long g_limb_deferred;
 
 template <int NM>
 struct LimbLds {
@@ -68,7 +81,7 @@ __device__ inline real rank8_sum(real v) {
 template <int N>
 __device__ inline void opaque_vals(real* v) {
 #pragma unroll
-  for (int j = 0; j < N; j++) asm volatile("" : "+v"(v[j]));
+  for (int j = 0; j < N; j++) asm("" : "+v"(v[j]));
 }
 
 // The same pointer, opaque to the optimizer: the three samples' FK read the same topology entries (a
@@ -341,7 +354,9 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
     STAMP(1);
     // (sched_barrier: the machine scheduler would interleave the independent samples for ILP, holding
     // two samples' FK working sets at once)
+#if HS_LIMB_SAMPLE_BARRIER
     __builtin_amdgcn_sched_barrier(0);
+#endif
     {
       real P[3][3], U[3][3];
       const hs_topo* Ts = opaque_s(T);
@@ -355,7 +370,9 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
           sh.k.outer[27 + 3 * kk + j][ol] = U[kk][j];
         }
     }
+#if HS_LIMB_SAMPLE_BARRIER
     __builtin_amdgcn_sched_barrier(0);
+#endif
     STAMP(2);
     {
       const hs_topo* T = opaque_s(T_);
@@ -382,7 +399,9 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
         opaque_vals<3>(Jz[kk]);
         if (kk == 2) opaque_vals<3>(fp);
         real Pm[3], Um[3], Pp[3], Up[3];
+#if HS_LIMB_SAMPLE_BARRIER
         __builtin_amdgcn_sched_barrier(0);  // the link's outer values read here, not hoisted above its FK
+#endif
 #pragma unroll
         for (int j = 0; j < 3; j++) {
           Pm[j] = sh.k.outer[3 * kk + j][ol];
@@ -468,11 +487,26 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       if (kk >= nk) break;
       const int c = T->node[0].kids[kk], sz = T->node[c].size;
       real Fk[3] = {0, 0, 0}, Vk[3] = {0, 0, 0};
-      // the range's loads issued together (ranges of up to 8 parts unrolled: hexapod 7, spider 3, myant 4)
+#if HS_LIMB_ROOT_BRANCHFREE
+      // the range's loads issued together, without a branch per part (ranges of up to 8 parts unrolled:
+      // hexapod 7, spider 3, myant 4; a part past the range is loaded from a valid row and not added)
+#pragma unroll
+      for (int r = 0; r < 8; r++) {
+        const int rr = c + r < NM ? c + r : NM - 1;
+        real gv[6];
+        for (int j = 0; j < 6; j++) gv[j] = S.g[rr][j];
+        for (int j = 0; j < 3; j++) {
+          Fk[j] = r < sz ? Fk[j] + gv[j] : Fk[j];
+          Vk[j] = r < sz ? Vk[j] + gv[3 + j] : Vk[j];
+        }
+      }
+#else
+      // ranges of up to 8 parts unrolled (hexapod 7, spider 3, myant 4)
 #pragma unroll
       for (int r = 0; r < 8; r++)
         if (r < sz)
           for (int j = 0; j < 3; j++) { Fk[j] += S.g[c + r][j]; Vk[j] += S.g[c + r][3 + j]; }
+#endif
       for (int r = 8; r < sz; r++)
         for (int j = 0; j < 3; j++) { Fk[j] += S.g[c + r][j]; Vk[j] += S.g[c + r][3 + j]; }
       for (int j = 0; j < 3; j++) { F[j] += Fk[j]; V[j] += Vk[j]; }
@@ -658,6 +692,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   STAMP(8);
   if (defer) {  // the whole step to the fixup launch (hs_rollout_kernel FIX_SOLVE)
     if (l == 0 && live) {
+      atomicAdd(&g_limb_deferred, 1ull);  // hs_limb_stats
       const int it = atomicAdd(mp.fix_count, 1);
       mp.fix_items[2 * it] = fstep;
       mp.fix_items[2 * it + 1] = b;  // 2 * wavefront + half of hs_rollout_kernel's layout
@@ -713,7 +748,15 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
     // the joints' positive work in joint order (work_over_period's loop, periodic.cpp:294-300), summed over
     // the steps in order by the reduce
     real work_dt = real(0);
+#if HS_LIMB_WORK_UNROLL
+    real wdv[HS_NMAX];
+#pragma unroll
+    for (int jj = 0; jj < HS_NMAX; jj++) wdv[jj] = S.wd[jj];  // issued together; only the nmj terms summed
+#pragma unroll
+    for (int jj = 0; jj < HS_NMAX; jj++) work_dt = jj < nmj ? work_dt + wdv[jj] : work_dt;
+#else
     for (int jj = 0; jj < nmj; jj++) work_dt += S.wd[jj];
+#endif
     reinterpret_cast<real*>(mp.fused_work)[(size_t)s_glob * a.n_rollouts + b] = work_dt;
   }
   STAMP(9);

@@ -545,6 +545,10 @@ void hs_sim_free(hs_sim_t sim);
  * environment keeps hs_rollout_kernel. hs_limb_launches: the limb-lane launches this process has made. */
 int hs_model_limb_lane(hs_model_t model, int32_t* ok);
 int64_t hs_limb_launches(void);
+/* Diagnostics of the limb-lane kernel: its launches and the steps it deferred to the fixup launch (one,
+ * two contacts, guards near their thresholds, ...) in this process; *deferred is read from the device
+ * (synchronous on the current device). Either pointer may be NULL. */
+int hs_limb_stats(int64_t* launches, int64_t* deferred);
 
 const char* hs_last_error(void);
 int hs_abi_version(void);
