@@ -785,6 +785,7 @@ __device__ __attribute__((always_inline)) inline void limb_fk(const hs_topo* T, 
         mulp(H, c, fp);
         real* F = w.fpos(k, lk.foot);
         for (int i = 0; i < 3; i++) F[i] = fp[i];
+        if (k == 0) DBG(24 + lk.foot, fp[2], 25);
         w.contact(k, lk.foot) = fp[2] < (real)(T->rcap + 1e-4);
       }
     }
@@ -2334,10 +2335,13 @@ __device__ __attribute__((always_inline)) inline bool fast_solve_lanes(const hs_
         for (int r = 0; r < 6; r++) b[i] -= a_entry(d0, r, i) * a[r];
       }
       real rl[3];
+      DBG(24 + sv.cfoot[0], M[4], 19);
+      DBG(24 + sv.cfoot[0], b[1], 20);
       ok = chol_n<3>(M, kFastPivotGuard, rl, lnear);
       if (ok) {
         chol_solve_n<3>(M, rl, b);
         for (int i = 0; i < 3; i++) sv.y[i] = b[i];
+        DBG(24 + sv.cfoot[0], b[0], 21);
       }
       fl.ok[0] = ok;
     }
@@ -2352,6 +2356,7 @@ __device__ __attribute__((always_inline)) inline bool fast_solve_lanes(const hs_
       real nv[6], M[36], b[6], rl[6];
       if (ok) {
         for (int r = 0; r < 3; r++) { nv[r] = u[r] / un / sqrt(real(2)); nv[3 + r] = -nv[r]; }
+        DBG(24 + sv.cfoot[0], nv[2], 26);
         for (int i = 0; i < 6; i++) {
           const real* di = fl.d0[i / 3];
           for (int j = 0; j < 6; j++) {
@@ -2364,10 +2369,15 @@ __device__ __attribute__((always_inline)) inline bool fast_solve_lanes(const hs_
           for (int r = 0; r < 6; r++) s += a_entry(di, r, i % 3) * a[r];
           b[i] = -s;
         }
+        DBG(24 + sv.cfoot[0], M[5], 27);
+        opaque_vals<36>(M);  // the assembled system (hs_limb_kernel fences the same values)
+        opaque_vals<6>(b);
+        opaque_vals<6>(nv);
         ok = chol_n<6>(M, kFastPivotGuard, rl, lnear);
       }
       if (ok) {
         chol_solve_n<6>(M, rl, b);
+        opaque_vals<6>(b);
         real nDn = 0, nr = 0;
         for (int c = 0; c < 2; c++)
           for (int i = 0; i < 3; i++) {
@@ -2380,6 +2390,9 @@ __device__ __attribute__((always_inline)) inline bool fast_solve_lanes(const hs_
         if (ok) {
           real t = -nr / nDn;
           for (int i = 0; i < 6; i++) sv.y[i] = b[i] + t * nv[i];
+          DBG(24 + sv.cfoot[0], sv.y[0], 22);
+          DBG(24 + sv.cfoot[0], b[0], 23);
+          DBG(24 + sv.cfoot[0], t, 24);
         }
       }
       fl.ok[0] = ok;

@@ -72,17 +72,7 @@ __device__ inline real rank8_sum(real v) {
   return v;
 }
 
-// Values made opaque to the optimizer where hs_rollout_kernel passes them through LDS: there a product
-// stored to LDS and loaded back is a rounded operand, here a register whose defining multiply the
-// instruction selector would contract into the consuming add (-ffp-contract=fast), rounding once where
-// hs_rollout_kernel rounds twice (f's torque = amr * inv added into particular_sub's cross term, g's
-// force = mr * inv added into the subtree sums: 1e-14 differences). The asm emits nothing.
-// (not volatile: a volatile asm is a scheduling boundary, and the step has dozens of these)
-template <int N>
-__device__ inline void opaque_vals(real* v) {
-#pragma unroll
-  for (int j = 0; j < N; j++) asm("" : "+v"(v[j]));
-}
+// opaque_vals (hs_math.h): values made opaque where hs_rollout_kernel passes them through LDS
 
 // The same pointer, opaque to the optimizer: the three samples' FK read the same topology entries (a
 // limb's link products, rotations, COMs: 80 reals) and frames, and merged loads would keep them live
@@ -239,6 +229,41 @@ __device__ __attribute__((always_inline)) inline void limb_outer(const hs_topo* 
   bool nc = false;
 #pragma unroll
   for (int kk = 0; kk < 3; kk++) fk_link<false>(T, LK[kk], kk, Jv, H, sq[kk], cq[kk], P[kk], U[kk], nul, nul, nul, nc);
+}
+
+// A contact's first-order block D_c (packed lower: 00 10 11 20 21 22) and g_c on its limb lane
+// (fast_solve_lanes: joint m of the foot's chain, foot link first, on lane m of a quad, summed
+// ((m0 + m1) + (m2 + m3)); the chain's jointless bodies add exact zeros)
+__device__ __attribute__((always_inline)) inline void contact_block(const real (&Jp)[3][3], const real (&Jz)[3][3],
+                                                                    const real (&xt)[3][3], const real* fp, real* Dp6,
+                                                                    real* gc) {
+  real tD[3][6], tg[3][3];
+#pragma unroll
+  for (int m = 0; m < 3; m++) {
+    const int p = 2 - m;
+    real Dp[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+    real da[3], va[3][3];
+    for (int r = 0; r < 3; r++) da[r] = Jp[p][r] - fp[r];
+    cross_rows(da, va);
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      const real w2 = Jz[p][r] * Jz[p][r];
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        if (i == r) continue;
+#pragma unroll
+        for (int j = 0; j <= i; j++)
+          if (j != r) Dp[i * (i + 1) / 2 + j] += w2 * va[r][i] * va[r][j];
+        g[i] += w2 * va[r][i] * xt[p][r];
+      }
+    }
+    for (int e = 0; e < 6; e++) tD[m][e] = Dp[e];
+    for (int i = 0; i < 3; i++) tg[m][i] = g[i];
+  }
+#pragma unroll
+  for (int e = 0; e < 6; e++) Dp6[e] = (tD[0][e] + tD[1][e]) + (tD[2][e] + real(0));
+#pragma unroll
+  for (int i = 0; i < 3; i++) gc[i] = (tg[0][i] + tg[1][i]) + (tg[2][i] + real(0));
 }
 
 template <int NM>
@@ -525,6 +550,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   const uint32_t cm = grp_or((limb && contact) ? 1u << fiL : 0u);
   const int nc = __popc(cm);
   const bool mine = limb && contact;
+  if (limb) LDBG(24 + fiL, fp[2], 25);
   // the limb lane holding contact rank l (lane l < nc of the group gathers that contact's values)
   int src = 0;
   for (int L2 = 0; L2 < nl; L2++) {
@@ -533,10 +559,13 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   }
   src += gbase;
   const bool slot = l < nc;
-  // the one- and two-contact closed forms and joint values outside sincos_k_small's range: the fixup's
-  bool defer = nc == 1 || nc == 2 || grp_any(big, gbase);
+  // joint values outside sincos_k_small's range: the fixup's
+  bool defer = grp_any(big, gbase);
   real y3[3] = {0, 0, 0};
-  real d0[3] = {0, 0, 0}, Dinv[9], gc[3];
+  real d0[3] = {0, 0, 0}, Dinv[9], gc[3], Dp6[6];
+  if (mine)
+    for (int r = 0; r < 3; r++) d0[r] = o[r] - fp[r];  // A_c = [-I; [d0_c]x]
+  if (mine && nc >= 2) contact_block(Jp, Jz, xt, fp, Dp6, gc);
 #ifdef HS_LIMB_EXP_NOSOLVE
   defer |= nc >= 3;
   if (false) {
@@ -544,8 +573,6 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   if (nc >= 3) {
 #endif
     // zeroth_well_posed: the feet's scatter, in single precision, the contacts' d0 on lanes 0 .. nc - 1
-    if (mine)
-      for (int r = 0; r < 3; r++) d0[r] = o[r] - fp[r];
     float e0 = grp_getf(float(o[0] - fp[0]), src), e1 = grp_getf(float(o[1] - fp[1]), src),
           e2 = grp_getf(float(o[2] - fp[2]), src);
     if (!slot) e0 = e1 = e2 = 0.f;
@@ -565,41 +592,13 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       defer |= !well || nearz;  // the same on every lane of the group (group8_sum)
     }
     STAMP(6);
-    // the contact's first-order block D_c, g_c (fast_solve_lanes: joint m of the foot's chain, foot link
-    // first, on lane m of a quad, summed ((m0 + m1) + (m2 + m3)); the chain's jointless bodies add zeros)
+    // the contact's Schur block of its first-order block D_c (contact_block)
     real sch[27];
 #pragma unroll
     for (int e = 0; e < 27; e++) sch[e] = 0;
     bool lnear = false, ok = true;
     if (mine) {
-      real tD[3][6], tg[3][3];
-#pragma unroll
-      for (int m = 0; m < 3; m++) {
-        const int p = 2 - m;
-        real Dp[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-        real da[3], va[3][3];
-        for (int r = 0; r < 3; r++) da[r] = Jp[p][r] - fp[r];
-        cross_rows(da, va);
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-          const real w2 = Jz[p][r] * Jz[p][r];
-#pragma unroll
-          for (int i = 0; i < 3; i++) {
-            if (i == r) continue;
-#pragma unroll
-            for (int j = 0; j <= i; j++)
-              if (j != r) Dp[i * (i + 1) / 2 + j] += w2 * va[r][i] * va[r][j];
-            g[i] += w2 * va[r][i] * xt[p][r];
-          }
-        }
-        for (int e = 0; e < 6; e++) tD[m][e] = Dp[e];
-        for (int i = 0; i < 3; i++) tg[m][i] = g[i];
-      }
-      real Dp[6];
-#pragma unroll
-      for (int e = 0; e < 6; e++) Dp[e] = (tD[0][e] + tD[1][e]) + (tD[2][e] + real(0));
-#pragma unroll
-      for (int i = 0; i < 3; i++) gc[i] = (tg[0][i] + tg[1][i]) + (tg[2][i] + real(0));
+      const real* Dp = Dp6;
       opaque_vals<3>(d0);
       const real D[9] = {Dp[0], Dp[1], Dp[3], Dp[1], Dp[2], Dp[4], Dp[3], Dp[4], Dp[5]};
       LDBG(24 + fiL, Dp[0], 6);
@@ -689,6 +688,112 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       opaque_vals<3>(y3);  // sv.y
     }
   }
+  if (nc == 1 || nc == 2) {
+    // fast_solve_lanes' one- and two-contact closed forms (its lane 0, from FastL): here on every lane of
+    // the group, the contacts' values gathered from their limb lanes
+    int s0 = 0, s1 = 0;
+    for (int L2 = 0; L2 < nl; L2++) {
+      const int f2 = T->link[L2][2].foot;
+      if ((cm >> f2) & 1) {
+        const int r2 = __popc(cm & ((1u << f2) - 1));
+        if (r2 == 0) s0 = L2;
+        if (r2 == 1) s1 = L2;
+      }
+    }
+    s0 += gbase;
+    s1 += gbase;
+    const real a[6] = {S.a[0], S.a[1], S.a[2], S.a[3], S.a[4], S.a[5]};
+    bool lnear = false, ok;
+    real y[6];
+    if (nc == 1) {  // unique least-squares solution (A^T A) w = -A^T a
+      real dd[3];
+      for (int r = 0; r < 3; r++) dd[r] = grp_get(d0[r], s0);
+      real M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bv[3] = {0, 0, 0};
+      for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++)
+          for (int r = 0; r < 6; r++) M[3 * i + j] += a_entry(dd, r, i) * a_entry(dd, r, j);
+        for (int r = 0; r < 6; r++) bv[i] -= a_entry(dd, r, i) * a[r];
+      }
+      real rl[3];
+      if (mine) LDBG(24 + fiL, M[4], 19);
+      if (mine) LDBG(24 + fiL, bv[1], 20);
+      ok = chol_n<3>(M, kFastPivotGuard, rl, lnear);
+      if (ok) chol_solve_n<3>(M, rl, bv);
+      for (int i = 0; i < 3; i++) y[i] = bv[i];
+      if (mine && ok) LDBG(24 + fiL, bv[0], 21);
+    } else {  // rank 5: kernel n = (u,-u)/sqrt2 along the line between the feet
+      real f0[3], f1[3], dA[2][3], Dc[2][6], gg[2][3];
+      for (int r = 0; r < 3; r++) {
+        f0[r] = grp_get(fp[r], s0);
+        f1[r] = grp_get(fp[r], s1);
+        dA[0][r] = grp_get(d0[r], s0);
+        dA[1][r] = grp_get(d0[r], s1);
+        gg[0][r] = grp_get(gc[r], s0);
+        gg[1][r] = grp_get(gc[r], s1);
+      }
+      for (int e = 0; e < 6; e++) {
+        Dc[0][e] = grp_get(Dp6[e], s0);
+        Dc[1][e] = grp_get(Dp6[e], s1);
+      }
+      const real Dm[2][9] = {{Dc[0][0], Dc[0][1], Dc[0][3], Dc[0][1], Dc[0][2], Dc[0][4], Dc[0][3], Dc[0][4], Dc[0][5]},
+                             {Dc[1][0], Dc[1][1], Dc[1][3], Dc[1][1], Dc[1][2], Dc[1][4], Dc[1][3], Dc[1][4], Dc[1][5]}};
+      real u[3], un = 0;
+      for (int r = 0; r < 3; r++) { u[r] = f0[r] - f1[r]; un += u[r] * u[r]; }
+      un = sqrt(un);
+      ok = un > real(1e-12);
+      real nv[6], M[36], bv[6], rl[6];
+      if (ok) {
+        for (int r = 0; r < 3; r++) { nv[r] = u[r] / un / sqrt(real(2)); nv[3 + r] = -nv[r]; }
+        const bool first = mine && __popc(cm & ((1u << fiL) - 1)) == 0;
+        if (first) LDBG(24 + fiL, nv[2], 26);
+        for (int i = 0; i < 6; i++) {
+          const real* di = dA[i / 3];
+          for (int j = 0; j < 6; j++) {
+            const real* dj = dA[j / 3];
+            real sv = 0;
+            for (int r = 0; r < 6; r++) sv += a_entry(di, r, i % 3) * a_entry(dj, r, j % 3);
+            M[6 * i + j] = sv + nv[i] * nv[j];
+          }
+          real sv = 0;
+          for (int r = 0; r < 6; r++) sv += a_entry(di, r, i % 3) * a[r];
+          bv[i] = -sv;
+        }
+        if (first) LDBG(24 + fiL, M[5], 27);
+        opaque_vals<36>(M);  // as hs_rollout_kernel's fast_solve_lanes fences them
+        opaque_vals<6>(bv);
+        opaque_vals<6>(nv);
+        ok = chol_n<6>(M, kFastPivotGuard, rl, lnear);
+      }
+      if (ok) {
+        chol_solve_n<6>(M, rl, bv);
+        opaque_vals<6>(bv);
+        real nDn = 0, nr = 0;
+        for (int c = 0; c < 2; c++)
+          for (int i = 0; i < 3; i++) {
+            real Dw = 0, Dn = 0;
+            for (int j = 0; j < 3; j++) { Dw += Dm[c][3 * i + j] * bv[3 * c + j]; Dn += Dm[c][3 * i + j] * nv[3 * c + j]; }
+            nr += nv[3 * c + i] * (Dw + gg[c][i]);
+            nDn += nv[3 * c + i] * Dn;
+          }
+        ok = nDn > 0;
+        if (ok) {
+          real t = -nr / nDn;
+          for (int i = 0; i < 6; i++) y[i] = bv[i] + t * nv[i];
+          if (mine && __popc(cm & ((1u << fiL) - 1)) == 0) {
+            LDBG(24 + fiL, y[0], 22);
+            LDBG(24 + fiL, bv[0], 23);
+            LDBG(24 + fiL, t, 24);
+          }
+        }
+      }
+    }
+    defer |= !ok || lnear;  // the same on every lane of the group
+    if (mine && ok) {
+      const int rk = __popc(cm & ((1u << fiL) - 1));
+      for (int i = 0; i < 3; i++) y3[i] = rk == 0 ? y[i] : y[3 + i];
+      opaque_vals<3>(y3);  // sv.y
+    }
+  }
   STAMP(8);
   if (defer) {  // the whole step to the fixup launch (hs_rollout_kernel FIX_SOLVE)
     if (l == 0 && live) {
@@ -742,6 +847,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   if (l == 0 && live) {
     uint32_t flags = 0;
     if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
+    if (nc == 1) flags |= HS_FLAG_FULL_RANK;
     if (any_nan) flags |= HS_FLAG_NAN;
     if (any_bad) flags |= HS_FLAG_UNREACH;
     if (a.flags) a.flags[orow] = flags;

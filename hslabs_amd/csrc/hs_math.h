@@ -89,6 +89,20 @@ __device__ inline A34 invert(const A34& A) {
   return I;
 }
 
+// Values made opaque to the optimizer where hs_rollout_kernel passes them through LDS: there a product
+// stored to LDS and loaded back is a rounded operand, here a register whose defining multiply the
+// instruction selector would contract into the consuming add (-ffp-contract=fast), rounding once where
+// hs_rollout_kernel rounds twice (f's torque = amr * inv added into particular_sub's cross term, g's
+// force = mr * inv added into the subtree sums: 1e-14 differences). The asm emits nothing.
+// hs_rollout_kernel's two-contact closed form fences its assembled system the same way (both kernels: the
+// contraction across the assembly and the factorization depends on the surrounding code)
+// (not volatile: a volatile asm is a scheduling boundary, and the step has dozens of these)
+template <int N>
+__device__ inline void opaque_vals(real* v) {
+#pragma unroll
+  for (int j = 0; j < N; j++) asm("" : "+v"(v[j]));
+}
+
 // sines / cosines of three Euler angles (one shared range reduction per angle:
 // sincos is bitwise identical to sin and cos, tools/sincos_check.hip)
 struct SC3 {

@@ -12,7 +12,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NAMES = {1: "P0[0] link pos", 2: "f[0] link force", 3: "g torque[0]", 4: "x torque[0] (subtree)", 5: "U0[0] link ust",
          6: "D_c[0]", 7: "g_c[0]", 8: "y[0]", 9: "Um[0] link ust t-2dt", 10: "amr[0] link", 11: "Up[0] link ust t+2dt",
-         12: "Pm[0] link pos t-2dt", 13: "f[1]", 14: "f[2] (gravity added)", 15: "o[0], o[1] (slots 31, 30)", 16: "amr[1]", 17: "d[0] = Jp - o (subtree stage)", 18: "F[0] subtree force"}
+         12: "Pm[0] link pos t-2dt", 13: "f[1]", 14: "f[2] (gravity added)", 15: "o[0], o[1] (slots 31, 30)", 16: "amr[1]", 17: "d[0] = Jp - o (subtree stage)", 18: "F[0] subtree force",
+         19: "nc=1 M[4]", 20: "nc=1 b[1] before solve", 21: "nc=1 y[0]", 22: "nc=2 y[0]", 23: "nc=2 b[0] (after solve)",
+         24: "nc=2 t", 25: "foot fp[2]", 26: "nc=2 nv[2]", 27: "nc=2 M[5]"}
 
 
 def child(n):
@@ -23,9 +25,10 @@ def child(n):
     from hslabs_amd import capi, synth
     L = capi.load()
     L.hs_debug_read_dbg.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    m = H.KinematicModel(os.path.join(ROOT, "models", "hexapod.xml"))
+    model = os.environ.get("MODEL", "hexapod")
+    m = H.KinematicModel(os.path.join(ROOT, "models", f"{model}.xml"))
     B, K = 256, 20
-    p = synth.gen_params(B, "hexapod", id0=4321)
+    p = synth.gen_params(B, model, id0=4321)
     out = []
     for limb in ("1", "0"):
         os.environ["HS_LIMB"] = limb
