@@ -221,10 +221,17 @@ int check_args(const hs_model_s* m, const hs_run_args* a) {
 // writes tau, cf, flags and the work terms), and the preparation pass holds the IK table (the kernel reads
 // its rows); HS_LIMB=0 in the environment keeps hs_rollout_kernel's fused step launch (A/B, tests)
 std::atomic<int64_t> g_limb_launches{0};
+// hs_run_steps' calls up to this horizon take the limb-lane kernel (a launch per call holds the call's
+// horizon steps; longer calls keep hs_rollout_kernel's launch)
+#define HS_ONLINE_MAX_H 64
 
 bool limb_kernel_wanted() {
   const char* e = getenv("HS_LIMB");  // read per call: a test switches kernels within one process
   return !(e && e[0] == '0');
+}
+bool limb_online_wanted() {
+  const char* e = getenv("HS_LIMB_ONLINE");
+  return e && e[0] == '1';
 }
 bool limb_eligible(const hs_topo& host, const hs_run_args& a) {
   // fp32: not yet bitwise hs_rollout_kernel's (1e-6 differences: float contraction), so not taken
@@ -232,11 +239,15 @@ bool limb_eligible(const hs_topo& host, const hs_run_args& a) {
          a.precision == HS_PREC_F64;
 }
 
+// online (hs_run_steps through the limb-lane kernel): a launch per call over its horizon steps, each call
+// writing output rows [0, horizon) like hs_run_steps' launches, its declined steps fixed and its work
+// added to work_cot (in step order, the reduce's two roundings) by one fixup + reduce launch before the
+// next call's launch, the best key by the last call's reduce
 int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map mp, ws_pool& gen_pool,
               ws_pool& work_pool, ws_pool& fix_pool, std::mutex& mu, double total_mass, const double* rollout_mass,
-              int32_t n_calls, bool limb = false) {
-  const int64_t S = (int64_t)n_calls * a.horizon;  // steps, one output row each
-  if (S > (1 << 24)) return fail(HS_E_ARG, "too many steps");
+              int32_t n_calls, bool limb = false, bool online = false, void* const* kernel_events = nullptr) {
+  const int64_t S = online ? a.horizon : (int64_t)n_calls * a.horizon;  // output rows per rollout
+  if (S > (1 << 24) || (int64_t)n_calls * a.horizon > INT32_MAX) return fail(HS_E_ARG, "too many steps");
   // steps per launch: the launch refills the SIMDs from its queue of wavefronts (the batch's last
   // wavefronts no longer end every step). Up to 512k wavefronts per launch (256 rounds of a full
   // MI355X at 2 per SIMD; measured B = 4096, 200 steps, interleaved A/B: 16 steps -2.5 %, 32 steps
@@ -252,8 +263,9 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
 #define HS_FUSED_RESERVE_STEPS 1024
 #endif
   const int32_t B = a.n_rollouts;
-  const int32_t CHUNK = std::max(1, std::min(HS_FUSED_MAX_STEPS, HS_FUSED_WAVES / std::max(1, mp.n_waves)));
-  const int32_t n_chunks = (int32_t)((S + CHUNK - 1) / CHUNK);
+  const int32_t CHUNK = online ? a.horizon
+                               : std::max(1, std::min(HS_FUSED_MAX_STEPS, HS_FUSED_WAVES / std::max(1, mp.n_waves)));
+  const int32_t n_chunks = online ? n_calls : (int32_t)((S + CHUNK - 1) / CHUNK);
   const size_t gwb = ws_slot_bytes();
   // steps the closed form declines (every step in HS_SOLVE_REFERENCE) are deferred to a fixup launch
   // after each step launch, so the step kernel carries no call to the general path; one counter per
@@ -282,8 +294,8 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   hs_run_args c = a;
   c.horizon = (int32_t)S;  // output rows per rollout
   c.best_key = nullptr;    // taken by the reduce, after the last step
-  hs_run_args r = a;       // the reduce: its key covers the call's S steps unless told otherwise
-  if (r.key_steps == 0) r.key_steps = (int32_t)S;
+  hs_run_args r = a;       // the reduce: its key covers the call's steps unless told otherwise
+  if (r.key_steps == 0) r.key_steps = (int32_t)((int64_t)n_calls * a.horizon);
   mp.fused_h = a.horizon;
   mp.fused_work = work;
   mp.fused_gen = gen;
@@ -300,6 +312,40 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   mp.fix_n_counts = 0;
   mp.fix_items = fix_items;
   bool reduced = false;
+  if (online) {
+    hipStream_t st = (hipStream_t)a.stream;
+    for (int32_t i = 0; le == 0 && i < n_calls; i++) {
+      c.k0 = (int32_t)(((int64_t)a.k0 + (int64_t)i * a.horizon) % a.n_t);
+      mp.fused_s0 = 0;
+      mp.fused_n = a.horizon;
+      mp.fix_mode = hs::FIX_DEFER;
+      mp.fix_count = fix_counts + i;
+      mp.fix_reduce = 0;
+      hipError_t e = kernel_events ? hipEventRecord((hipEvent_t)kernel_events[2 * i], st) : hipSuccess;
+      if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+      if (limb) {  // (no IK table for the call: hs_rollout_kernel's fused step launch, the same shape)
+        le = f32 ? hs::launch_limb_f32(d, c, ws, mp) : hs::launch_limb(d, c, ws, mp);
+        g_limb_launches++;
+      } else {
+        le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+      }
+      if (le != 0) break;
+      mp.fix_mode = hs::FIX_SOLVE;
+      mp.fix_reduce = a.work_cot != nullptr;
+      if (mp.fix_reduce) {
+        mp.red_total_mass = total_mass;
+        mp.red_rollout_mass = rollout_mass;
+        mp.red_n_steps = a.horizon;
+        mp.red_key_steps = r.key_steps;
+        mp.red_best_key = i + 1 == n_calls ? r.best_key : nullptr;
+      }
+      le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+      if (le == 0 && kernel_events) e = hipEventRecord((hipEvent_t)kernel_events[2 * i + 1], st);
+      if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+    }
+    if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
+    return HS_OK;
+  }
   for (int64_t s0 = 0, ci = 0; le == 0 && s0 < S; s0 += CHUNK, ci++) {
     mp.fused_s0 = (int32_t)s0;
     mp.fused_n = (int32_t)std::min<int64_t>(CHUNK, S - s0);
@@ -518,8 +564,17 @@ int hs_run_steps(hs_model_t m, const hs_run_args* a, int32_t n_calls, void* cons
   void* ws = nullptr;
   rc = device_state(m, a->n_rollouts + 1, a->stream, &d, &ws);  // + the idle half-wave of an odd batch
   if (rc != HS_OK) return rc;
-  return launch_steps(d, routed(*a, m->host.torso_mask), ws, hs::single_model_map(m->host, a->n_rollouts), n_calls,
-                      kernel_events, m->host.total_mass, nullptr);
+  const hs_run_args r = routed(*a, m->host.torso_mask);
+  // HS_LIMB_ONLINE=1, the limb-lane kernel's class: a launch per call and a fixup + reduce launch after it
+  // (run_fused's online shape, the same outputs, work and key bitwise). Not the default: its launch of
+  // B / 8 wavefronts lasts one wavefront's life, 18.2-18.7 us at B = 4096 (the limb lanes' dependent
+  // chain), and the fixup + reduce adds 4.7-5.2 us: 155 M steps/s against hs_rollout_kernel's launch per
+  // call with the general path inline, 20 us at 32 lanes per rollout (profiles/r06_t7_steps_trace_tail.txt)
+  if (limb_online_wanted() && limb_eligible(m->host, r) && a->horizon <= HS_ONLINE_MAX_H)
+    return run_fused(d, r, ws, hs::single_model_map(m->host, a->n_rollouts), m->fused_gen, m->fused_work,
+                     m->fused_fix, m->mu, m->host.total_mass, nullptr, n_calls, true, true, kernel_events);
+  return launch_steps(d, r, ws, hs::single_model_map(m->host, a->n_rollouts), n_calls, kernel_events,
+                      m->host.total_mass, nullptr);
 }
 
 int hs_run_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls) {

@@ -34,23 +34,31 @@ def hmodels(gpu):
     return {n: gpu.KinematicModel(os.path.join(MODELS, f"{n}.xml")) for n in ("hexapod", "spider", "myant")}
 
 
-def run(gpu, model, params, limb, K=20, Hc=1, k0=0, best=True, dtype=None, rollout_id_base=0):
+def run(gpu, model, params, limb, K=20, Hc=1, k0=0, best=True, dtype=None, rollout_id_base=0, steps=False,
+        accumulate=True):
+    """K calls of Hc steps: fused (hs_run_calls, K * Hc output rows) or steps=True (hs_run_steps, a launch
+    per call, each call writing rows [0, Hc); limb: its opt-in online shape, HS_LIMB_ONLINE=1)"""
     import torch
 
     old = os.environ.get("HS_LIMB")
     os.environ["HS_LIMB"] = "1" if limb else "0"
+    os.environ["HS_LIMB_ONLINE"] = "1" if limb and steps else "0"
     try:
-        b = gpu.DeviceBatch(model, params, n_t=20, k0=k0, horizon=K * Hc, outputs=OUTS, dtype=dtype,
+        b = gpu.DeviceBatch(model, params, n_t=20, k0=k0, horizon=Hc if steps else K * Hc, outputs=OUTS, dtype=dtype,
                             rollout_id_base=rollout_id_base)
         b.key_steps = K * Hc
         b.work_cot.zero_()
         b.reset_best()
-        b.run_calls(K, call_horizon=Hc, best=best, accumulate=True)
+        if steps:
+            b.run_steps(K, best=best, accumulate=accumulate)
+        else:
+            b.run_calls(K, call_horizon=Hc, best=best, accumulate=accumulate)
         torch.cuda.synchronize()
         out = {k: getattr(b, k).cpu().numpy() for k in OUTS}
         out["best_key"] = int(b.best_key.item())
         return out
     finally:
+        os.environ.pop("HS_LIMB_ONLINE")
         if old is None:
             os.environ.pop("HS_LIMB")
         else:
@@ -120,6 +128,23 @@ def test_limb_kernel_configs3_shard(gpu, hmodels):
     p = synth.gen_params(32768, "hexapod", id0=229376)
     same(run(gpu, hmodels["hexapod"], p, True, rollout_id_base=229376),
          run(gpu, hmodels["hexapod"], p, False, rollout_id_base=229376), "configs[3] shard")
+
+
+@pytest.mark.parametrize("name,K,Hc,k0,acc", [("hexapod", 20, 1, 0, True), ("hexapod", 6, 4, 17, True),
+                                               ("myant", 9, 1, 3, False), ("spider", 1, 20, 0, True)])
+def test_limb_kernel_online_calls(gpu, hmodels, name, K, Hc, k0, acc):
+    """hs_run_steps through the limb-lane kernel (HS_LIMB_ONLINE=1: a launch per call, then its fixup + work
+    reduce; opt-in, slower than the default at B = 4096, hs_capi.cpp hs_run_steps): the call's rows,
+    the accumulated (or last call's) work and COT, and the key after the last call, bitwise equal to
+    hs_rollout_kernel's launch per call with the general path inline"""
+    from hslabs_amd import synth
+
+    p = synth.gen_params(1000, name, id0=31, curved=True)
+    n0 = gpu.api.limb_launches()
+    a = run(gpu, hmodels[name], p, True, K=K, Hc=Hc, k0=k0, steps=True, accumulate=acc)
+    assert gpu.api.limb_launches() == n0 + K
+    b = run(gpu, hmodels[name], p, False, K=K, Hc=Hc, k0=k0, steps=True, accumulate=acc)
+    same(a, b, f"online {name} K={K} H={Hc}")
 
 
 def test_limb_kernel_not_taken_in_fp32(gpu, hmodels):
