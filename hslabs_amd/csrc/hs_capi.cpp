@@ -233,10 +233,15 @@ bool limb_online_wanted() {
   const char* e = getenv("HS_LIMB_ONLINE");
   return e && e[0] == '1';
 }
+bool limb_f32_wanted() {
+  const char* e = getenv("HS_LIMB_F32");
+  return !(e && e[0] == '0');
+}
 bool limb_eligible(const hs_topo& host, const hs_run_args& a) {
-  // fp32: not yet bitwise hs_rollout_kernel's (1e-6 differences: float contraction), so not taken
+  // fp32: within the single-precision build's bound of hs_rollout_kernel's float results, not bitwise
+  // (float contraction differs by context: ~1e-6 relative); HS_LIMB_F32=0 keeps hs_rollout_kernel there
   return limb_kernel_wanted() && host.limb_lane_ok && a.solve_mode == HS_SOLVE_AUTO && !a.x && !a.q && !a.dq &&
-         a.precision == HS_PREC_F64;
+         (a.precision == HS_PREC_F64 || limb_f32_wanted());
 }
 
 // online (hs_run_steps through the limb-lane kernel): a launch per call over its horizon steps, each call

@@ -147,13 +147,27 @@ def test_limb_kernel_online_calls(gpu, hmodels, name, K, Hc, k0, acc):
     same(a, b, f"online {name} K={K} H={Hc}")
 
 
-def test_limb_kernel_not_taken_in_fp32(gpu, hmodels):
-    """the single-precision build keeps hs_rollout_kernel (the limb-lane kernel's float build is not bitwise
-    its equal yet)"""
+@pytest.mark.parametrize("name,B,K,Hc,curved", [("spider", 16384, 2, 32, False), ("hexapod", 2048, 20, 1, True),
+                                                 ("myant", 1024, 20, 1, False)])
+def test_limb_kernel_fp32_close_to_rollout_kernel(gpu, hmodels, name, B, K, Hc, curved):
+    """the single-precision build (configs[2]'s shape first) takes the limb-lane kernel too; float contraction
+    differs by context, so its results are within the fp32 build's stated bound of hs_rollout_kernel's
+    float results, not bitwise: the same flags on all but a few near-threshold steps, and torques within
+    FP32_TOL (tests/test_gpu.py) relative wherever the flags agree"""
     import torch
     from hslabs_amd import synth
 
-    p = synth.gen_params(2048, "spider", id0=5)
+    p = synth.gen_params(B, name, id0=5, curved=curved)
     n0 = gpu.api.limb_launches()
-    run(gpu, hmodels["spider"], p, True, K=2, Hc=32, dtype=torch.float32)
-    assert gpu.api.limb_launches() == n0
+    a = run(gpu, hmodels[name], p, True, K=K, Hc=Hc, dtype=torch.float32)
+    assert gpu.api.limb_launches() > n0
+    b = run(gpu, hmodels[name], p, False, K=K, Hc=Hc, dtype=torch.float32)
+    same_flags = a["flags"] == b["flags"]
+    ok = same_flags[..., None] & np.isfinite(a["tau"]) & np.isfinite(b["tau"])
+    err = np.abs(a["tau"].astype(np.float64) - b["tau"]) / np.maximum(1.0, np.abs(b["tau"].astype(np.float64)))
+    print(f"{name} fp32: flags differ on {int((~same_flags).sum())} of {same_flags.size} steps, "
+          f"max rel torque difference {err[ok].max():.2e}")
+    assert same_flags.mean() > 0.999
+    assert err[ok].max() < 1e-3
+    wa, wb = a["work_cot"][:, 0].astype(np.float64), b["work_cot"][:, 0].astype(np.float64)
+    assert np.allclose(wa, wb, rtol=1e-3, atol=1e-6)
