@@ -275,7 +275,8 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   // steps the closed form declines (every step in HS_SOLVE_REFERENCE) are deferred to a fixup launch
   // after each step launch, so the step kernel carries no call to the general path; one counter per
   // launch (zeroed by the setup pass), then the items
-  const size_t fix_counts_bytes = ((size_t)n_chunks * sizeof(int32_t) + 255) / 256 * 256;
+  // (then as many grid-barrier counters for the fixup + reduce launches, hs_internal.h fix_barrier)
+  const size_t fix_counts_bytes = ((size_t)2 * n_chunks * sizeof(int32_t) + 255) / 256 * 256;
   const size_t fix_bytes = fix_counts_bytes + (size_t)CHUNK * mp.n_waves * 2 * 2 * sizeof(int32_t);
   void *gen = nullptr, *work = nullptr, *fix = nullptr;
   {
@@ -307,9 +308,12 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
   mp.setup_only = 1;  // gait setup once per rollout, stored for every step
   mp.setup_io = hs::SETUP_STORE;
   mp.fix_count = fix_counts;
-  mp.fix_n_counts = n_chunks;
+  mp.fix_n_counts = 2 * n_chunks;  // the fixup counters and the barrier counters
+  // the fixup + reduce launch's grid barrier: its ceil(B / 64) workgroups must be resident together
+  const char* fb = getenv("HS_FIX_BARRIER");  // 0: each workgroup fixes its own rollouts' items (A/B)
+  const bool barrier_ok = (B + 63) / 64 <= 1024 && !(fb && fb[0] == '0');
   hs::ktab_range(a.k0, a.n_t, a.horizon, n_calls, &mp.ktab_lo, &mp.ktab_n, &mp.ttab_n);  // the preparation pass's rows
-  limb = limb && mp.ktab_n > 0 && !mp.wave_rollouts;
+  limb = limb && mp.ktab_n > 0 && (!mp.wave_rollouts || mp.limb_rollouts);
   mp.prep_unit = limb ? 8 : 2;  // the rollouts' records written on the XCD whose step launches read them
   int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   mp.setup_only = 0;
@@ -337,6 +341,7 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
       if (le != 0) break;
       mp.fix_mode = hs::FIX_SOLVE;
       mp.fix_reduce = a.work_cot != nullptr;
+      mp.fix_barrier = barrier_ok ? fix_counts + n_chunks + i : nullptr;
       if (mp.fix_reduce) {
         mp.red_total_mass = total_mass;
         mp.red_rollout_mass = rollout_mass;
@@ -366,6 +371,7 @@ int run_fused(const hs_topo* d, const hs_run_args& a, void* ws, hs::launch_map m
     // launch of an HS_SOLVE_AUTO call (few items, if any) together with the work reduce
     mp.fix_mode = hs::FIX_SOLVE;
     mp.fix_reduce = s0 + CHUNK >= S && a.solve_mode == HS_SOLVE_AUTO && a.work_cot;
+    mp.fix_barrier = barrier_ok ? fix_counts + n_chunks + ci : nullptr;
     if (mp.fix_reduce) {
       mp.red_total_mass = total_mass;
       mp.red_rollout_mass = rollout_mass;
@@ -410,6 +416,10 @@ struct hs_mixed_s {
   hs_topo* d_topos = nullptr;  // the models' topologies, contiguous (wave_model indexes it)
   int32_t* d_wave_model = nullptr;
   int32_t* d_wave_rollouts = nullptr;
+  // the limb-lane kernel's layout (every model of the plan of its class): 8 rollouts of one model per
+  // wavefront, [model], [8 * wave] rollout ids (-1 idle) and their hs_rollout_kernel slots
+  int32_t limb_waves = 0;
+  int32_t *d_limb_model = nullptr, *d_limb_rollouts = nullptr;
   double* d_rollout_mass = nullptr;  // total mass of each rollout's model (the fused reduce's COT)
   int32_t torso_mask = 3;            // 3 unless a model's switch_torso_penalty (at plan creation) differs
   ws_pool ws;
@@ -686,6 +696,8 @@ int hs_mixed_create(const hs_model_t* models, int32_t n_models, const int32_t* m
   p->models.assign(models, models + n_models);
   std::vector<hs_topo> topos;
   std::vector<int32_t> wave_model, wave_rollouts;
+  std::vector<int32_t> limb_model, limb_rollouts, limb_slots;
+  bool limb_ok = true;
   hs_model_dims& md = p->max_dims;
   memset(&md, 0, sizeof(md));
   int32_t max_cf = 0, max_x = 0;
@@ -702,10 +714,19 @@ int hs_mixed_create(const hs_model_t* models, int32_t n_models, const int32_t* m
     p->st_tau = std::max(p->st_tau, t.nmj);
     p->st_q = std::max(p->st_q, t.cfg);
     const std::vector<int32_t>& g = groups[(size_t)k];
+    const int32_t slot0 = (int32_t)wave_rollouts.size();
     for (size_t i = 0; i < g.size(); i += 2) {  // two rollouts of one model per wavefront
       wave_model.push_back(k);
       wave_rollouts.push_back(g[i]);
       wave_rollouts.push_back(i + 1 < g.size() ? g[i + 1] : -1);
+    }
+    limb_ok = limb_ok && t.limb_lane_ok;
+    for (size_t i = 0; i < g.size(); i += 8) {  // the limb-lane kernel: eight per wavefront, the same order
+      limb_model.push_back(k);
+      for (size_t j = i; j < i + 8; j++) {
+        limb_rollouts.push_back(j < g.size() ? g[j] : -1);
+        limb_slots.push_back(j < g.size() ? slot0 + (int32_t)j : -1);
+      }
     }
   }
   md.nmj = p->st_tau;
@@ -722,6 +743,18 @@ int hs_mixed_create(const hs_model_t* models, int32_t n_models, const int32_t* m
   if (e == hipSuccess) e = hipMemcpy(p->d_topos, topos.data(), nt, hipMemcpyHostToDevice);
   if (e == hipSuccess && nw) e = hipMemcpy(p->d_wave_model, wave_model.data(), nw, hipMemcpyHostToDevice);
   if (e == hipSuccess && nw) e = hipMemcpy(p->d_wave_rollouts, wave_rollouts.data(), 2 * nw, hipMemcpyHostToDevice);
+  if (e == hipSuccess && limb_ok && !limb_model.empty()) {
+    // [model][rollouts][slots] in one allocation
+    const size_t nl = limb_model.size();
+    e = hipMalloc(&p->d_limb_model, (nl + 16 * nl) * sizeof(int32_t));
+    p->limb_waves = (int32_t)nl;
+    p->d_limb_rollouts = p->d_limb_model + nl;
+    if (e == hipSuccess) e = hipMemcpy(p->d_limb_model, limb_model.data(), nl * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_limb_rollouts, limb_rollouts.data(), 8 * nl * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy(p->d_limb_rollouts + 8 * nl, limb_slots.data(), 8 * nl * sizeof(int32_t), hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess && n_rollouts > 0) {
     std::vector<double> mass((size_t)n_rollouts);
     for (int32_t r = 0; r < n_rollouts; r++) mass[(size_t)r] = models[model_index[r]]->host.total_mass;
@@ -741,6 +774,7 @@ void hs_mixed_free(hs_mixed_t p) {
   if (p->d_topos) free_on_device(p->dev, p->d_topos);
   if (p->d_wave_model) free_on_device(p->dev, p->d_wave_model);
   if (p->d_wave_rollouts) free_on_device(p->dev, p->d_wave_rollouts);
+  if (p->d_limb_model) free_on_device(p->dev, p->d_limb_model);
   if (p->d_rollout_mass) free_on_device(p->dev, p->d_rollout_mass);
   p->ws.release();
   p->fused_gen.release();
@@ -812,9 +846,17 @@ int hs_run_mixed_calls(hs_mixed_t p, const hs_run_args* a, int32_t n_calls) {
     e = (hipError_t)p->ws.get(a->stream, (size_t)p->n_rollouts + 1, &ws);
   }
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
-  return run_fused(p->d_topos, routed(*a, p->torso_mask), ws, mp, p->fused_gen, p->fused_work, p->fused_fix, p->mu, 0.0,
-                   p->d_rollout_mass,
-                   n_calls);
+  const hs_run_args r = routed(*a, p->torso_mask);
+  bool limb = false;
+  if (p->d_limb_model) {  // every model of the plan is of the limb-lane kernel's class
+    mp.limb_model = p->d_limb_model;
+    mp.limb_rollouts = p->d_limb_rollouts;
+    mp.limb_slots = p->d_limb_rollouts + 8 * (size_t)p->limb_waves;
+    mp.limb_waves = p->limb_waves;
+    limb = limb_eligible(p->models[0]->host, r);
+  }
+  return run_fused(p->d_topos, r, ws, mp, p->fused_gen, p->fused_work, p->fused_fix, p->mu, 0.0, p->d_rollout_mass,
+                   n_calls, limb);
 }
 
 int hs_complete_traj(hs_model_t m, const hs_gait_params* params, int32_t B, int32_t n_t, int32_t ignore_reach,

@@ -63,6 +63,11 @@ struct launch_map {
   // FIX_SOLVE with fix_reduce: the call's last fixup and the work reduce in one launch (a workgroup per
   // 64 rollouts fixes their items, then sums their work); red_*: the reduce's own arguments
   int32_t fix_reduce, red_key_steps, red_n_steps;
+  // fix_reduce with fix_barrier (a counter zeroed by the setup pass; null when the reduce grid is too large to
+  // be resident at once): the items are spread over all the launch's workgroups, which meet at a grid
+  // barrier before the reduce (a rollout's items may sit on another workgroup); otherwise each workgroup
+  // fixes its own rollouts' items in turn
+  int32_t* fix_barrier;
   double red_total_mass;
   const double* red_rollout_mass;
   uint64_t* red_best_key;
@@ -75,6 +80,11 @@ struct launch_map {
   // u % 8, where the step launches read them (0 or 2: hs_rollout_kernel's two rollouts per wavefront; 8:
   // the limb-lane kernel's eight)
   int32_t prep_unit;
+  // the limb-lane kernel over a mixed plan: wavefront w runs model limb_model[w] for the rollouts
+  // limb_rollouts[8 w .. 8 w + 7] (-1: an idle group), whose slots in hs_rollout_kernel's layout (the fixup's
+  // items) are limb_slots[...]; limb_waves wavefronts per step (null: one model, rollouts 8 w + group)
+  const int32_t *limb_model, *limb_rollouts, *limb_slots;
+  int32_t limb_waves;
 };
 
 // Kernel launcher (hs_kernels.hip). `workspace` holds general_workspace_bytes()

@@ -16,10 +16,12 @@
 // (the same helpers, the same expressions), so the outputs are bitwise those of that kernel
 // (tests/test_gpu_limb.py). The kernel takes the common case: a call with the preparation pass's IK
 // table, a model of the limb-lane class (hs_topo::limb_lane_ok), HS_SOLVE_AUTO, no x / q / dq outputs,
-// a step with no contact or with >= 3 contacts that the closed form's tier 1 solves with no guard near
-// its threshold. Every other step is deferred to the fixup launch (hs_rollout_kernel FIX_SOLVE), which
-// computes it with hs_rollout_kernel's whole machinery (1 and 2 contacts, tier 2, the Eigen-style path,
-// HS_FLAG_NEAR_RANK): the same (step, rollout) items the fused step launch defers.
+// a step the closed form's tier 1 solves (0 to 6 contacts; a guard near its threshold sets
+// HS_FLAG_NEAR_RANK as fast_solve does). Every other step -- a singular contact block (tier 2), nearly
+// collinear feet (the Eigen-style path), a joint value past sincos_k_small's range -- is deferred to the
+// fixup launch (hs_rollout_kernel FIX_SOLVE), which computes it with hs_rollout_kernel's whole machinery:
+// the same (step, rollout) items the fused step launch defers. A mixed plan of limb-lane models runs
+// eight rollouts of one model per wavefront (launch_map::limb_model / limb_rollouts).
 
 #ifndef HS_LIMB_ROOT_BRANCHFREE
 #define HS_LIMB_ROOT_BRANCHFREE 0
@@ -267,7 +269,7 @@ __device__ __attribute__((always_inline)) inline void contact_block(const real (
 }
 
 template <int NM>
-__global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_topo* __restrict__ T, hs_run_args a,
+__global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
                                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
   // the outer samples' pos / ust of every lane's links (kinematics), then the groups' exchange arrays:
   // 18 KB per wavefront, 8 per CU at 2 waves / SIMD
@@ -282,6 +284,9 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
     LimbLds<NM> g[LGR];
   } sh;
   LimbLds<NM>* lds = sh.g;
+  int fstep = 0, q = (int)blockIdx.x;
+  fused_coords((int)blockIdx.x, mp.fused_w, mp.fused_n, fstep, q);
+  const hs_topo* __restrict__ T = mp.limb_model ? T0 + mp.limb_model[q] : T0;  // a mixed plan's wavefront model
   {  // the link records, 8 bytes per lane and load
     const uint64_t* src = reinterpret_cast<const uint64_t*>(&T->link[0][0]);
     uint64_t* dst = reinterpret_cast<uint64_t*>(&sh.k.links[0][0]);
@@ -292,11 +297,10 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   RSTAMP(16);
   STAMP(15);
   const int lane = (int)threadIdx.x, grp = lane >> 3, l = lane & 7, gbase = lane & ~7;
-  int fstep = 0, q = (int)blockIdx.x;
-  fused_coords((int)blockIdx.x, mp.fused_w, mp.fused_n, fstep, q);
-  const int b = q * LGR + grp;
-  const bool live = b < a.n_rollouts;
-  const int bb = live ? b : a.n_rollouts - 1;  // an idle group computes a copy and stores nothing
+  const int b = mp.limb_rollouts ? mp.limb_rollouts[q * LGR + grp] : q * LGR + grp;
+  const bool live = b >= 0 && b < a.n_rollouts;
+  // an idle group computes a copy of a rollout of its wavefront's model and stores nothing
+  const int bb = live ? b : (mp.limb_rollouts ? mp.limb_rollouts[q * LGR] : a.n_rollouts - 1);
   LimbLds<NM>& S = lds[grp];
   const int ol = grp * HS_LMAX + (l < HS_LMAX ? l : 0);  // this limb lane's column of sh.k.outer
   const int s_glob = mp.fused_s0 + fstep, call = s_glob / mp.fused_h;
@@ -561,6 +565,9 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   const bool slot = l < nc;
   // joint values outside sincos_k_small's range: the fixup's
   bool defer = grp_any(big, gbase);
+  // a routing decision within kNearBand of its guard: HS_FLAG_NEAR_RANK, as fast_solve sets it (the values
+  // are hs_rollout_kernel's bitwise, so the decisions are its own)
+  bool nearf = false;
   real y3[3] = {0, 0, 0};
   real d0[3] = {0, 0, 0}, Dinv[9], gc[3], Dp6[6];
   if (mine)
@@ -589,7 +596,8 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       const float t = kZerothGuard * k * (c00 + c11 + c22) * md;
       const bool well = c2 >= t;
       const bool nearz = c2 >= t / float(kNearBand) && c2 <= t * float(kNearBand);
-      defer |= !well || nearz;  // the same on every lane of the group (group8_sum)
+      defer |= !well;  // the same on every lane of the group (group8_sum)
+      nearf |= nearz;
     }
     STAMP(6);
     // the contact's Schur block of its first-order block D_c (contact_block)
@@ -638,7 +646,8 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
         }
       }
     }
-    defer |= grp_any(mine && (!ok || lnear), gbase);
+    defer |= grp_any(mine && !ok, gbase);  // a singular D_c: tier 2's
+    nearf |= grp_any(mine && lnear, gbase);
     // what fast_solve_lanes stores in FastL and reads back for y (LDS): g_c, d0_c, D_c^-1
     opaque_vals<3>(gc);
     opaque_vals<9>(Dinv);
@@ -662,7 +671,8 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       for (int r = 0; r < 6; r++) lam[r] = S.a[r] - Ssum[SCH_H + r];
       bool near6 = false;
       const bool ok6 = ldl_n<6>(Sm, kFastPivotGuard, rl6, near6);
-      defer |= !ok6 || near6;
+      defer |= !ok6;
+      nearf |= near6;
       if (ok6) ldl_solve_n<6>(Sm, rl6, lam);
       opaque_vals<6>(lam);  // FastL::sc.lam
     }
@@ -787,7 +797,8 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
         }
       }
     }
-    defer |= !ok || lnear;  // the same on every lane of the group
+    defer |= !ok;  // the same on every lane of the group
+    nearf |= lnear;
     if (mine && ok) {
       const int rk = __popc(cm & ((1u << fiL) - 1));
       for (int i = 0; i < 3; i++) y3[i] = rk == 0 ? y[i] : y[3 + i];
@@ -800,7 +811,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       atomicAdd(&g_limb_deferred, 1ull);  // hs_limb_stats
       const int it = atomicAdd(mp.fix_count, 1);
       mp.fix_items[2 * it] = fstep;
-      mp.fix_items[2 * it + 1] = b;  // 2 * wavefront + half of hs_rollout_kernel's layout
+      mp.fix_items[2 * it + 1] = mp.limb_slots ? mp.limb_slots[q * LGR + grp] : b;  // 2 * wavefront + half of hs_rollout_kernel's layout
     }
     return;
   }
@@ -842,12 +853,19 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
         outp(a.cf)[orow * mp.st_cf + 3 * fiL + j] = zv;
       }
   }
+  if (live) {  // a mixed plan's rows past this model's joints and feet (hs_rollout_kernel writes them 0)
+    if (a.tau)
+      for (int c = nmj + l; c < mp.st_tau; c += LG) outp(a.tau)[orow * mp.st_tau + c] = real(0);
+    if (a.cf)
+      for (int c = 3 * T->nf + l; c < mp.st_cf; c += LG) outp(a.cf)[orow * mp.st_cf + c] = real(0);
+  }
   const bool any_nan = grp_any(nan, gbase), any_bad = grp_any(limb && bad, gbase);
   wave_sync();
   if (l == 0 && live) {
     uint32_t flags = 0;
     if (nc == 0) flags |= HS_FLAG_NO_CONTACT;
     if (nc == 1) flags |= HS_FLAG_FULL_RANK;
+    if (nearf) flags |= HS_FLAG_NEAR_RANK;
     if (any_nan) flags |= HS_FLAG_NAN;
     if (any_bad) flags |= HS_FLAG_UNREACH;
     if (a.flags) a.flags[orow] = flags;

@@ -130,6 +130,53 @@ def test_limb_kernel_configs3_shard(gpu, hmodels):
          run(gpu, hmodels["hexapod"], p, False, rollout_id_base=229376), "configs[3] shard")
 
 
+@pytest.mark.parametrize("B,K,Hc,dtype", [(4096, 20, 1, "f64"), (1001, 3, 7, "f64"), (2048, 2, 32, "f32")])
+def test_limb_kernel_mixed_plan(gpu, hmodels, B, K, Hc, dtype):
+    """configs[4]'s mixed plan (myant + hexapod interleaved, one launch: eight rollouts of one model per
+    wavefront, the fixup's items in hs_rollout_kernel's slots): fp64 bitwise, fp32 within the bound; the
+    rows past myant's joints and feet written 0 (the output buffers start as NaN here)"""
+    import torch
+    from hslabs_amd import synth
+
+    params, idx = synth.gen_mixed(B)
+    ms = [hmodels[n] for n in synth.MIXED_MODELS]
+    f32 = dtype == "f32"
+
+    def go(limb):
+        old = os.environ.get("HS_LIMB")
+        os.environ["HS_LIMB"] = "1" if limb else "0"
+        try:
+            mb = gpu.MixedBatch(ms, idx, params, n_t=20, k0=0, horizon=K * Hc, outputs=OUTS,
+                                dtype=torch.float32 if f32 else None)
+            for k in ("tau", "cf"):
+                getattr(mb, k).fill_(float("nan"))
+            mb.key_steps = K * Hc
+            mb.work_cot.zero_()
+            mb.reset_best()
+            mb.run_calls(K, call_horizon=Hc, best=True, accumulate=True)
+            torch.cuda.synchronize()
+            out = {k: getattr(mb, k).cpu().numpy() for k in OUTS}
+            out["best_key"] = int(mb.best_key.item())
+            return out
+        finally:
+            if old is None:
+                os.environ.pop("HS_LIMB")
+            else:
+                os.environ["HS_LIMB"] = old
+
+    n0 = gpu.api.limb_launches()
+    a = go(True)
+    assert gpu.api.limb_launches() > n0
+    b = go(False)
+    assert np.isfinite(a["tau"]).all() and np.isfinite(a["cf"]).all()
+    if not f32:
+        same(a, b, f"mixed B={B} K={K} H={Hc}")
+    else:
+        assert (a["flags"] == b["flags"]).mean() > 0.999
+        err = np.abs(a["tau"].astype(np.float64) - b["tau"]) / np.maximum(1.0, np.abs(b["tau"].astype(np.float64)))
+        assert err.max() < 1e-3
+
+
 @pytest.mark.parametrize("name,K,Hc,k0,acc", [("hexapod", 20, 1, 0, True), ("hexapod", 6, 4, 17, True),
                                                ("myant", 9, 1, 3, False), ("spider", 1, 20, 0, True)])
 def test_limb_kernel_online_calls(gpu, hmodels, name, K, Hc, k0, acc):
