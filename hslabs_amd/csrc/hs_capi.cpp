@@ -660,21 +660,57 @@ int hs_run_forces_calls(hs_model_t m, const hs_run_args* a, int32_t n_calls, con
   c.horizon = (int32_t)S;  // output (and tau_in) rows per rollout
   c.tau = c.x = c.work_cot = nullptr;
   c.best_key = nullptr;
-  // the run_fused scheme without the fixup and the work reduce: solve_forces has no declined steps
-  // to defer (its own solve covers every step) and no work. Its LDS layout runs 3 wavefronts / SIMD.
+  // the run_fused scheme without the work reduce: hs_rollout_kernel's forces mode solves every step
+  // itself (its LDS layout runs 3 wavefronts / SIMD). The limb-lane kernel's forces mode (the model of
+  // its class, HS_SOLVE_AUTO, no q rows, fp64, the preparation pass's table) takes forces_solve's fast
+  // path and defers a step whose foot block B_f is near singular (the dense normal equations) to a
+  // fixup launch of hs_rollout_kernel's forces mode after each step launch
   const int32_t CHUNK = std::max(1, std::min(HS_FUSED_MAX_STEPS, HS_FUSED_WAVES / std::max(1, mp.n_waves)));
+  const int32_t n_chunks = (int32_t)((S + CHUNK - 1) / CHUNK);
   const bool f32 = a->precision == HS_PREC_F32;
   mp.fused_h = a->horizon;
   mp.setup_only = 1;
   mp.setup_io = hs::SETUP_STORE;
   hs::ktab_range(a->k0, a->n_t, a->horizon, n_calls, &mp.ktab_lo, &mp.ktab_n, &mp.ttab_n);
+  const bool limb = limb_kernel_wanted() && m->host.limb_lane_ok && a->solve_mode == HS_SOLVE_AUTO && !a->q &&
+                    !f32 && mp.ktab_n > 0;
+  int32_t* fix_counts = nullptr;
+  if (limb) {
+    const size_t counts_bytes = ((size_t)n_chunks * sizeof(int32_t) + 255) / 256 * 256;
+    const size_t bytes = counts_bytes + (size_t)CHUNK * mp.n_waves * 2 * 2 * sizeof(int32_t);
+    const size_t gwb = ws_slot_bytes();
+    void* fix = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(m->mu);
+      const hipError_t e = (hipError_t)m->fused_fix.get(a->stream, (bytes + gwb - 1) / gwb, &fix);
+      if (e != hipSuccess) return hip_fail(e, "hipMalloc(forces fixup items)");
+    }
+    fix_counts = (int32_t*)fix;
+    mp.fix_count = fix_counts;
+    mp.fix_n_counts = n_chunks;
+    mp.fix_items = (int32_t*)((char*)fix + counts_bytes);
+    mp.prep_unit = 8;
+  }
   int le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
   mp.setup_only = 0;
   mp.setup_io = hs::SETUP_LOAD;
-  for (int64_t s0 = 0; le == 0 && s0 < S; s0 += CHUNK) {
+  mp.fix_n_counts = 0;
+  for (int64_t s0 = 0, ci = 0; le == 0 && s0 < S; s0 += CHUNK, ci++) {
     mp.fused_s0 = (int32_t)s0;
     mp.fused_n = (int32_t)std::min<int64_t>(CHUNK, S - s0);
-    le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+    if (limb) {
+      mp.fix_count = fix_counts + ci;
+      mp.fix_mode = hs::FIX_DEFER;
+      le = hs::launch_limb(d, c, ws, mp);
+      g_limb_launches++;
+      if (le != 0) break;
+      mp.fix_mode = hs::FIX_SOLVE;
+      mp.fix_reduce = 0;
+      le = hs::launch_fused(d, c, ws, mp);
+      mp.fix_mode = hs::FIX_NONE;
+    } else {
+      le = f32 ? hs::launch_fused_f32(d, c, ws, mp) : hs::launch_fused(d, c, ws, mp);
+    }
   }
   if (le != 0) return hip_fail((hipError_t)le, "kernel launch");
   return HS_OK;

@@ -2725,6 +2725,109 @@ __device__ inline real wtt_entry(int e, const real* ts, int n) {
   return ((a == b) ? real(n) + q[0] + q[1] + q[2] : real(0)) - qab;
 }
 
+// One limb's blocks of forces_solve (lane = limb; hs_limb_kernel's forces mode calls it on its limb lanes):
+// J, Z, P: its three links' joint positions, axes and part positions at the centre sample, fp its foot, P0
+// the torso's position, X the links' x torque rows, zz the motors' torques. fa: S_l (packed lower) and
+// e_l; fb (when B_f factors): K_f and q_f; Ct, Bd, Bl / rdB, rb: C~_f, B_f raw and its LDL^T, r_f.
+__device__ __attribute__((always_inline)) inline bool forces_limb_block(const real (&J)[3][3], const real (&Z)[3][3],
+                                                                        const real (&P)[3][3], const real* fp,
+                                                                        const real* P0, const real (&X)[3][3],
+                                                                        const real* zz, real* fa, real* fb, real* Ct,
+                                                                        real* Bd, real* Bl, real* rdB, real* rb,
+                                                                        real* dbgv = nullptr) {
+  // raw rows of motor k: R[k] = (W_mt row (6), C_m row vs foot f (3), d_m (1)); M lower (k' <= k)
+  real R[3][10], M[9];
+  for (int k = 0; k < 3; k++) {
+    for (int c = 0; c < 10; c++) R[k][c] = 0;
+    for (int c = 0; c < 3; c++) M[3 * k + c] = (c == k) ? real(1) : real(0);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; i++) {  // part p[i] lies in the subtrees of motors 0 .. i
+    real ri[3], u[3][3];
+    for (int t = 0; t < 3; t++) ri[t] = P[i][t] - P0[t];
+#pragma unroll
+    for (int k = 0; k <= i; k++) {
+      real a3[3], ru[3];
+      for (int t = 0; t < 3; t++) a3[t] = J[k][t] - P[i][t];
+      cross3(a3, Z[k], u[k]);
+      cross3(ri, u[k], ru);
+      for (int c = 0; c < 3; c++) R[k][c] += -u[k][c];
+      for (int c = 0; c < 3; c++) R[k][3 + c] += -(ru[c] + Z[k][c]);
+#pragma unroll
+      for (int k2 = 0; k2 <= k; k2++)
+        M[3 * k + k2] += (u[k][0] * u[k2][0] + u[k][1] * u[k2][1] + u[k][2] * u[k2][2]) +
+                         (Z[k][0] * Z[k2][0] + Z[k][1] * Z[k2][1] + Z[k][2] * Z[k2][2]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    real dd[3];
+    for (int t = 0; t < 3; t++) dd[t] = J[k][t] - fp[t];
+    for (int jj = 0; jj < 3; jj++) {
+      real v = 0;
+      for (int t = 0; t < 3; t++) v += Z[k][t] * cross_e(dd, jj, t);
+      R[k][6 + jj] = v;
+    }
+    real t0 = 0;
+    for (int t = 0; t < 3; t++) t0 += Z[k][t] * X[k][t];
+    R[k][9] = zz[k] - t0;
+    if (dbgv && k == 0) { dbgv[0] = t0; dbgv[1] = zz[k]; dbgv[2] = X[k][0]; dbgv[3] = Z[k][0]; }
+  }
+  real rdM[3];
+  ldl_n<3>(M, real(0), rdM);  // M >= I
+#pragma unroll
+  for (int c = 0; c < 10; c++) {  // Y = L^-1 R
+    R[1][c] -= M[3] * R[0][c];
+    R[2][c] -= M[6] * R[0][c] + M[7] * R[1][c];
+  }
+  auto prod = [&](int a, int b) {  // (L^-1 R)_a^T D^-1 (L^-1 R)_b
+    return R[0][a] * rdM[0] * R[0][b] + R[1][a] * rdM[1] * R[1][b] + R[2][a] * rdM[2] * R[2][b];
+  };
+#pragma unroll
+  for (int e = 0; e < 21; e++) {  // S_l = W_tm M^-1 W_mt (packed lower)
+    const TriWalk<> t(e);
+    fa[e] = prod(t.r, t.c);
+  }
+#pragma unroll
+  for (int r = 0; r < 6; r++) fa[21 + r] = prod(r, 9);  // e_l = W_tm M^-1 d_m
+  real d[3];
+  for (int t = 0; t < 3; t++) d[t] = fp[t] - P0[t];
+#pragma unroll
+  for (int r = 0; r < 6; r++)
+#pragma unroll
+    for (int jj = 0; jj < 3; jj++) {
+      const real ct = (r < 3) ? ((r == jj) ? real(1) : real(0)) : cross_e(d, jj, r - 3);
+      Ct[3 * r + jj] = ct - prod(r, 6 + jj);
+    }
+  Bd[0] = prod(6, 6); Bd[1] = prod(7, 6); Bd[2] = prod(7, 7);
+  Bd[3] = prod(8, 6); Bd[4] = prod(8, 7); Bd[5] = prod(8, 8);
+  for (int jj = 0; jj < 3; jj++) rb[jj] = prod(6 + jj, 9);
+  Bl[0] = Bd[0]; Bl[3] = Bd[1]; Bl[4] = Bd[2]; Bl[6] = Bd[3]; Bl[7] = Bd[4]; Bl[8] = Bd[5];
+  const bool okB = ldl_n<3>(Bl, kForcesBlockGuard, rdB);
+  if (okB) {  // K_f = C~ B^-1 C~^T, q_f = C~ B^-1 r_f, through V = L_B^-1 [C~^T | r_f]
+    real V[3][7];
+    for (int c = 0; c < 6; c++)
+      for (int k = 0; k < 3; k++) V[k][c] = Ct[3 * c + k];
+    for (int k = 0; k < 3; k++) V[k][6] = rb[k];
+#pragma unroll
+    for (int c = 0; c < 7; c++) {
+      V[1][c] -= Bl[3] * V[0][c];
+      V[2][c] -= Bl[6] * V[0][c] + Bl[7] * V[1][c];
+    }
+    auto vp = [&](int a, int b) {
+      return V[0][a] * rdB[0] * V[0][b] + V[1][a] * rdB[1] * V[1][b] + V[2][a] * rdB[2] * V[2][b];
+    };
+#pragma unroll
+    for (int e = 0; e < 21; e++) {
+      const TriWalk<> t(e);
+      fb[e] = vp(t.r, t.c);
+    }
+#pragma unroll
+    for (int r = 0; r < 6; r++) fb[21 + r] = vp(r, 6);
+  }
+  return okB;
+}
+
 template <class W, class SV>
 __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_topo* T, SV& sv, ForceL& fr, const W& w,
                                                                        const real* z, bool dense, int lane) {
@@ -2741,6 +2844,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
       s += (b < 0) ? ra : ra * (Pi[b] - P0[b]);
     }
     ts[lane] = s;
+    if (lane == 3) DBG(0, s, 30);
   }
   // per limb: C~_f (6 x 3), B_f (raw and LDL^T), r_f stay in registers to the end
   real Ct[18], Bd[6], Bl[9], rdB[3], rb[3];
@@ -2751,104 +2855,31 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     int p[3];
     for (int k = 0; k < 3; k++) p[k] = T->limb_node[L][k];
     f = T->node[p[2]].foot;
-    const real* fp = w.fpos(0, f);
-    real J[3][3], Z[3][3], P[3][3];
-    for (int k = 0; k < 3; k++)
+    real J[3][3], Z[3][3], P[3][3], X[3][3], zz[3];
+    for (int k = 0; k < 3; k++) {
       for (int t = 0; t < 3; t++) {
         J[k][t] = w.jpos(0, p[k])[t];
         Z[k][t] = w.jz(0, p[k])[t];
         P[k][t] = w.pos(0, p[k])[t];
+        X[k][t] = sv.x[3 * n + 3 * p[k] + t];
       }
-    // raw rows of motor k: R[k] = (W_mt row (6), C_m row vs foot f (3), d_m (1)); M lower (k' <= k)
-    real R[3][10], M[9];
-    for (int k = 0; k < 3; k++) {
-      for (int c = 0; c < 10; c++) R[k][c] = 0;
-      for (int c = 0; c < 3; c++) M[3 * k + c] = (c == k) ? real(1) : real(0);
+      zz[k] = z[T->node[p[k]].hinge];
     }
-#pragma unroll
-    for (int i = 0; i < 3; i++) {  // part p[i] lies in the subtrees of motors 0 .. i
-      real ri[3], u[3][3];
-      for (int t = 0; t < 3; t++) ri[t] = P[i][t] - P0[t];
-#pragma unroll
-      for (int k = 0; k <= i; k++) {
-        real a3[3], ru[3];
-        for (int t = 0; t < 3; t++) a3[t] = J[k][t] - P[i][t];
-        cross3(a3, Z[k], u[k]);
-        cross3(ri, u[k], ru);
-        for (int c = 0; c < 3; c++) R[k][c] += -u[k][c];
-        for (int c = 0; c < 3; c++) R[k][3 + c] += -(ru[c] + Z[k][c]);
-#pragma unroll
-        for (int k2 = 0; k2 <= k; k2++)
-          M[3 * k + k2] += (u[k][0] * u[k2][0] + u[k][1] * u[k2][1] + u[k][2] * u[k2][2]) +
-                           (Z[k][0] * Z[k2][0] + Z[k][1] * Z[k2][1] + Z[k][2] * Z[k2][2]);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      real dd[3];
-      for (int t = 0; t < 3; t++) dd[t] = J[k][t] - fp[t];
-      for (int jj = 0; jj < 3; jj++) {
-        real v = 0;
-        for (int t = 0; t < 3; t++) v += Z[k][t] * cross_e(dd, jj, t);
-        R[k][6 + jj] = v;
-      }
-      const int h = p[k], j = T->node[h].hinge;
-      real t0 = 0;
-      for (int t = 0; t < 3; t++) t0 += Z[k][t] * sv.x[3 * n + 3 * h + t];
-      R[k][9] = z[j] - t0;
-    }
-    real rdM[3];
-    ldl_n<3>(M, real(0), rdM);  // M >= I
-#pragma unroll
-    for (int c = 0; c < 10; c++) {  // Y = L^-1 R
-      R[1][c] -= M[3] * R[0][c];
-      R[2][c] -= M[6] * R[0][c] + M[7] * R[1][c];
-    }
-    auto prod = [&](int a, int b) {  // (L^-1 R)_a^T D^-1 (L^-1 R)_b
-      return R[0][a] * rdM[0] * R[0][b] + R[1][a] * rdM[1] * R[1][b] + R[2][a] * rdM[2] * R[2][b];
-    };
-#pragma unroll
-    for (int e = 0; e < 21; e++) {  // S_l = W_tm M^-1 W_mt (packed lower)
-      const TriWalk<> t(e);
-      fr.a[L][e] = prod(t.r, t.c);
-    }
-#pragma unroll
-    for (int r = 0; r < 6; r++) fr.a[L][21 + r] = prod(r, 9);  // e_l = W_tm M^-1 d_m
-    real d[3];
-    for (int t = 0; t < 3; t++) d[t] = fp[t] - P0[t];
-#pragma unroll
-    for (int r = 0; r < 6; r++)
-#pragma unroll
-      for (int jj = 0; jj < 3; jj++) {
-        const real ct = (r < 3) ? ((r == jj) ? real(1) : real(0)) : cross_e(d, jj, r - 3);
-        Ct[3 * r + jj] = ct - prod(r, 6 + jj);
-      }
-    Bd[0] = prod(6, 6); Bd[1] = prod(7, 6); Bd[2] = prod(7, 7);
-    Bd[3] = prod(8, 6); Bd[4] = prod(8, 7); Bd[5] = prod(8, 8);
-    for (int jj = 0; jj < 3; jj++) rb[jj] = prod(6 + jj, 9);
-    Bl[0] = Bd[0]; Bl[3] = Bd[1]; Bl[4] = Bd[2]; Bl[6] = Bd[3]; Bl[7] = Bd[4]; Bl[8] = Bd[5];
-    okB = ldl_n<3>(Bl, kForcesBlockGuard, rdB);
-    if (okB) {  // K_f = C~ B^-1 C~^T, q_f = C~ B^-1 r_f, through V = L_B^-1 [C~^T | r_f]
-      real V[3][7];
-      for (int c = 0; c < 6; c++)
-        for (int k = 0; k < 3; k++) V[k][c] = Ct[3 * c + k];
-      for (int k = 0; k < 3; k++) V[k][6] = rb[k];
-#pragma unroll
-      for (int c = 0; c < 7; c++) {
-        V[1][c] -= Bl[3] * V[0][c];
-        V[2][c] -= Bl[6] * V[0][c] + Bl[7] * V[1][c];
-      }
-      auto vp = [&](int a, int b) {
-        return V[0][a] * rdB[0] * V[0][b] + V[1][a] * rdB[1] * V[1][b] + V[2][a] * rdB[2] * V[2][b];
-      };
-#pragma unroll
-      for (int e = 0; e < 21; e++) {
-        const TriWalk<> t(e);
-        fr.b[L][e] = vp(t.r, t.c);
-      }
-#pragma unroll
-      for (int r = 0; r < 6; r++) fr.b[L][21 + r] = vp(r, 6);
-    }
+    real dbgv[4] = {0, 0, 0, 0};
+    okB = forces_limb_block(J, Z, P, w.fpos(0, f), P0, X, zz, fr.a[L], fr.b[L], Ct, Bd, Bl, rdB, rb
+#ifdef HS_DBG
+                            , dbgv
+#endif
+    );
+    DBG(24 + f, dbgv[0], 40);
+    DBG(24 + f, dbgv[1], 41);
+    DBG(24 + f, dbgv[2], 42);
+    DBG(24 + f, dbgv[3], 43);
+    DBG(24 + f, fr.a[L][0], 31);
+    DBG(24 + f, fr.b[L][0], 32);
+    DBG(24 + f, Ct[0], 36);
+    DBG(24 + f, rb[0], 37);
+    DBG(24 + f, fr.a[L][21], 38);
   }
   const bool fast = !dense && half_ballot(lane < nl && !okB) == 0;
   wave_sync();
@@ -2862,6 +2893,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     const real v = (lane < 21) ? (fast ? wtt_entry(lane, ts, n) + s : wtt_entry(lane, ts, n) - s)
                                : (fast ? s - dt : dt - s);
     fr.a[0][lane] = v;  // lane reads column `lane` only, so slot 0 takes the sums in place
+    if (lane == 0) DBG(1, v, 33);
   }
   wave_sync();
   STAMP(5);
@@ -2876,6 +2908,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
     }
     ldl_n<6>(K, real(0), rd);  // >= I
     ldl_solve_n<6>(K, rd, lam);
+    if (lane == 0) DBG(2, lam[0], 34);
     if (lane < nl) {  // y_f = B_f^-1 (r_f - C~_f^T lam)
       real t[3];
       for (int k = 0; k < 3; k++) {
@@ -2884,6 +2917,7 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
         t[k] = s;
       }
       ldl_solve_n<3>(Bl, rdB, t);
+      DBG(24 + f, t[0], 35);
       for (int k = 0; k < 3; k++) sv.y[3 * f + k] = t[k];
     }
     wave_sync();
@@ -3595,7 +3629,9 @@ int launch_pergen_rec(const hs_topo* d_topo, const hs_gait_params* params, int32
 
 template <int NM>
 void launch_nm(const hs_topo* d_topo, const hs_run_args& a, RolloutWS* ws, const launch_map& mp, hipStream_t st) {
-  if (mp.tau_in)
+  if (mp.tau_in && mp.fix_mode == FIX_SOLVE)  // the limb-lane forces launch's deferred items
+    hipLaunchKernelGGL((hs_rollout_kernel<NM, true, FIX_SOLVE>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
+  else if (mp.tau_in)
     hipLaunchKernelGGL((hs_rollout_kernel<NM, true, FIX_NONE>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
   else if (mp.fix_mode == FIX_DEFER)
     hipLaunchKernelGGL((hs_rollout_kernel<NM, false, FIX_DEFER>), dim3(mp.n_waves), dim3(WAVE), 0, st, d_topo, a, ws, mp);
@@ -3676,9 +3712,15 @@ int launch_limb(const hs_topo* d_topo, const hs_run_args& a, void* workspace, co
   launch_map m = mp;
   m.fused_w = mp.limb_rollouts ? mp.limb_waves : (a.n_rollouts + LGR - 1) / LGR;  // wavefronts per step: 8 rollouts each
   const dim3 grid((unsigned)((int64_t)m.fused_w * mp.fused_n));
-  if (mp.max_parts <= 18) hipLaunchKernelGGL((hs_limb_kernel<18>), grid, dim3(WAVE), 0, st, d_topo, a, ws, m);
-  else if (mp.max_parts <= 22) hipLaunchKernelGGL((hs_limb_kernel<22>), grid, dim3(WAVE), 0, st, d_topo, a, ws, m);
-  else hipLaunchKernelGGL((hs_limb_kernel<HS_NMAX>), grid, dim3(WAVE), 0, st, d_topo, a, ws, m);
+  if (mp.tau_in) {  // solve_forces (hs_run_forces_calls)
+    if (mp.max_parts <= 18) hipLaunchKernelGGL((hs_limb_kernel<18, true>), grid, dim3(WAVE), 0, st, d_topo, a, ws, m);
+    else if (mp.max_parts <= 22) hipLaunchKernelGGL((hs_limb_kernel<22, true>), grid, dim3(WAVE), 0, st, d_topo, a, ws, m);
+    else hipLaunchKernelGGL((hs_limb_kernel<HS_NMAX, true>), grid, dim3(WAVE), 0, st, d_topo, a, ws, m);
+  } else {
+    if (mp.max_parts <= 18) hipLaunchKernelGGL((hs_limb_kernel<18, false>), grid, dim3(WAVE), 0, st, d_topo, a, ws, m);
+    else if (mp.max_parts <= 22) hipLaunchKernelGGL((hs_limb_kernel<22, false>), grid, dim3(WAVE), 0, st, d_topo, a, ws, m);
+    else hipLaunchKernelGGL((hs_limb_kernel<HS_NMAX, false>), grid, dim3(WAVE), 0, st, d_topo, a, ws, m);
+  }
   return (int)hipGetLastError();
 }
 

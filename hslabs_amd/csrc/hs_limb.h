@@ -51,6 +51,7 @@ struct LimbLds {
   real g[NM][6];     // per part g_i = (f_i, t_i + (P_i - p0) x f_i); a root kid's slot then its subtree sums
   real a[6];         // the root's x (torso force, torque): the zeroth-order right-hand side
   real wd[HS_NMAX];  // the motors' positive work of the step, in joint order
+  real p[NM][3];     // forces mode: the parts' positions at the centre sample (forces_solve's s, Q sums)
 };
 
 // a value of lane `src` of this lane's group (ds_bpermute)
@@ -268,7 +269,135 @@ __device__ __attribute__((always_inline)) inline void contact_block(const real (
   for (int i = 0; i < 3; i++) gc[i] = (tg[0][i] + tg[1][i]) + (tg[2][i] + real(0));
 }
 
+// hs_limb_kernel's forces mode after S1 (forces_solve's fast path, every value by its operations in its
+// order): the parts' s, Q sums over nodes 1 .. n - 1 in node order (every lane of the group), the limb's
+// blocks on its lane (forces_limb_block), the sums over the limbs in limb order (a DPP chain: lane l adds
+// its term to lane l - 1's partial sum, the total on lane nl - 1), the 6 x 6 system on every lane, each
+// limb's foot forces on its lane
 template <int NM>
+__device__ __attribute__((always_inline)) inline void limb_forces(const hs_topo* T, const hs_run_args& a,
+                                                                  const hs::launch_map& mp, LimbLds<NM>& S, bool limb,
+                                                                  int l, int L, int gbase, int nl, bool live, int b,
+                                                                  int fstep, int s_glob, const real* o,
+                                                                  const real (&Jp)[3][3], const real (&Jz)[3][3],
+                                                                  const real (&Pc)[3][3], const real* fp,
+                                                                  const real (&xt)[3][3], bool bad, bool big) {
+  const int n = T->n;
+#ifdef HS_DBG
+  const int dbg_r = live ? b * a.horizon + s_glob : -1;
+#define FDBG(slot, val, n_)                                                                                      \
+  do {                                                                                                           \
+    if (HS_DBG == (n_) && dbg_r >= 0 && (size_t)dbg_r * 32 + (slot) < (1u << 22)) g_dbg[(size_t)dbg_r * 32 + (slot)] = (double)(val); \
+  } while (0)
+#else
+#define FDBG(slot, val, n_) do {} while (0)
+#endif
+  real ts[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) ts[q] = 0;
+  for (int i = 1; i < n; i++) {
+    real r[3];
+    for (int t = 0; t < 3; t++) r[t] = S.p[i][t] - o[t];
+    // forces_solve's lanes select between r_a and the product r_a r_b before adding (a lane-dependent
+    // select): the product is rounded, then added -- not one FMA
+    real q[6] = {r[0] * r[0], r[1] * r[1], r[2] * r[2], r[0] * r[1], r[0] * r[2], r[1] * r[2]};
+    opaque_vals<6>(q);
+    ts[0] += r[0];
+    ts[1] += r[1];
+    ts[2] += r[2];
+    for (int j = 0; j < 6; j++) ts[3 + j] += q[j];
+  }
+  opaque_vals<9>(ts);  // forces_solve keeps them in LDS (sv.y)
+  const int dbg_f = T->link[L][2].foot;
+  (void)dbg_f;
+  if (l == 0) FDBG(0, ts[3], 30);
+  const size_t orow = (size_t)b * a.horizon + s_glob;
+  real Ct[18], Bd[6], Bl[9], rdB[3], rb[3], fa[27], fb[27];
+  bool okB = true;
+  if (limb) {
+    const real* z = inp(mp.tau_in) + (live ? orow : 0) * mp.st_tau;
+    real zz[3];
+    for (int kk = 0; kk < 3; kk++) zz[kk] = z[T->node[T->limb_node[L][kk]].hinge];
+    real dbgv[4] = {0, 0, 0, 0};
+    okB = forces_limb_block(Jp, Jz, Pc, fp, o, xt, zz, fa, fb, Ct, Bd, Bl, rdB, rb
+#ifdef HS_DBG
+                            , dbgv
+#endif
+    );
+    FDBG(24 + dbg_f, dbgv[0], 40);
+    FDBG(24 + dbg_f, dbgv[1], 41);
+    FDBG(24 + dbg_f, dbgv[2], 42);
+    FDBG(24 + dbg_f, dbgv[3], 43);
+    FDBG(24 + dbg_f, fa[0], 31);
+    FDBG(24 + dbg_f, fb[0], 32);
+    FDBG(24 + dbg_f, Ct[0], 36);
+    FDBG(24 + dbg_f, rb[0], 37);
+    FDBG(24 + dbg_f, fa[21], 38);
+    opaque_vals<27>(fa);  // fr.a / fr.b (LDS)
+    if (okB) opaque_vals<27>(fb);
+  }
+  const bool fast = !grp_any(limb && !okB, gbase);
+  if (!fast || grp_any(big, gbase)) {  // the dense normal equations: the forces fixup's (forces_solve)
+    if (l == 0 && live) {
+      atomicAdd(&g_limb_deferred, 1ull);
+      const int it = atomicAdd(mp.fix_count, 1);
+      mp.fix_items[2 * it] = fstep;
+      mp.fix_items[2 * it + 1] = b;  // 2 * wavefront + half of hs_rollout_kernel's layout
+    }
+    return;
+  }
+  // K = W_tt - sum S_l + sum K_f, rhs = sum (q_f + e_l) - d_t
+  real kv[27];
+#pragma unroll
+  for (int e = 0; e < 27; e++) {
+    const real v = limb ? ((e < 21) ? fb[e] - fa[e] : fb[e] + fa[e]) : real(0);
+    real s = real(0) + v;
+    for (int k = 1; k < nl; k++) {
+      const real prev = dpp_r<0x111>(s);  // row_shr 1: lane l - 1's partial sum
+      if (l >= 1) s = prev + v;
+    }
+    const real tot = grp_get(s, gbase + nl - 1);
+    const real dtv = (e < 21) ? real(0) : (e < 24 ? S.a[e - 21] : S.a[e - 21]);
+    kv[e] = (e < 21) ? wtt_entry(e, ts, n) + tot : tot - dtv;
+  }
+  opaque_vals<27>(kv);  // fr.a[0] (LDS)
+  if (l == 0) FDBG(1, kv[0], 33);
+  real K[36], rd[6], lam[6];
+#pragma unroll
+  for (int r = 0; r < 6; r++) {
+#pragma unroll
+    for (int c = 0; c < 6; c++) K[6 * r + c] = (c <= r) ? kv[pk(r, c)] : real(0);
+    lam[r] = kv[21 + r];
+  }
+  ldl_n<6>(K, real(0), rd);  // >= I
+  ldl_solve_n<6>(K, rd, lam);
+  if (l == 0) FDBG(2, lam[0], 34);
+  bool nan = false;
+  real t[3] = {0, 0, 0};
+  if (limb) {  // y_f = B_f^-1 (r_f - C~_f^T lam)
+    for (int k = 0; k < 3; k++) {
+      real s = rb[k];
+      for (int r = 0; r < 6; r++) s -= Ct[3 * r + k] * lam[r];
+      t[k] = s;
+    }
+    ldl_solve_n<3>(Bl, rdB, t);
+    FDBG(24 + dbg_f, t[0], 35);
+    for (int k = 0; k < 3; k++) nan |= t[k] != t[k];
+    const int f = T->link[L][2].foot;
+    if (live && a.cf)
+      for (int k = 0; k < 3; k++) outp(a.cf)[orow * mp.st_cf + 3 * f + k] = t[k];
+  }
+  if (live && a.cf)  // a mixed plan's columns past this model's feet
+    for (int c = 3 * T->nf + l; c < mp.st_cf; c += LG) outp(a.cf)[orow * mp.st_cf + c] = real(0);
+  const bool any_nan = grp_any(nan, gbase), any_bad = grp_any(limb && bad, gbase);
+  if (l == 0 && live && a.flags) a.flags[orow] = (any_nan ? HS_FLAG_NAN : 0u) | (any_bad ? HS_FLAG_UNREACH : 0u);
+}
+#undef FDBG
+
+// FORCES: hs_run_forces_calls' solve_forces step (contact forces given motor torques, forces_solve's fast
+// path: a limb's blocks on its lane, the sums over the limbs in limb order by a DPP chain, the 6 x 6 on
+// every lane of the group; a B_f near singular defers the step to the forces fixup launch)
+template <int NM, bool FORCES>
 __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
                                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
   // the outer samples' pos / ust of every lane's links (kinematics), then the groups' exchange arrays:
@@ -360,6 +489,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   bool own = false;  // this limb computes a chain body (limb_own_n = 1)
   real gown[6];
   real jvel[3];
+  real Pc[3][3], Pown[3];  // forces mode: the links' and the chain body's positions at the centre
   bool bad = false, big = false;
   const hs_topo* const T_ = T;
   if (limb) {
@@ -409,6 +539,8 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       if (own) {  // the chain body's differences first: its three samples are dead before the links' FK
         part_dyn((real)T->mass[T->limb_own[L][0]], inv, om.P, oc.P, op.P, om.U, oc.U, op.U, gown);
         part_g(oc.P, o, gown);
+        if constexpr (FORCES)
+          for (int j = 0; j < 3; j++) Pown[j] = oc.P[j];
       }
       const real* ja = W.ktab[row + 2][L];
       real sq[3], cq[3];
@@ -423,6 +555,8 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
         real P0[3], U0[3];
         fk_link<true>(T, sh.k.links[L][kk], kk, Jv, H, sq[kk], cq[kk], P0, U0, Jp[kk], Jz[kk], fp, contact);
         opaque_vals<3>(P0);  // the features as hs_rollout_kernel's later phases read them (LDS)
+        if constexpr (FORCES)
+          for (int j = 0; j < 3; j++) Pc[kk][j] = P0[j];
         opaque_vals<3>(U0);
         opaque_vals<3>(Jp[kk]);
         opaque_vals<3>(Jz[kk]);
@@ -459,6 +593,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
     // the motors' joint rates at the centre (compute_vel_traj's wrapped difference of q at t +- dt)
 #pragma unroll
     for (int kk = 0; kk < 3; kk++) {
+      if constexpr (FORCES) break;
       real dd = W.ktab[row + 3][L][kk] - W.ktab[row + 1][L][kk];
       if (dd > kPi) dd -= 2 * kPi;
       else if (dd < -kPi) dd += 2 * kPi;
@@ -474,6 +609,13 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       for (int j = 0; j < 6; j++) S.g[T->limb_node[L][kk]][j] = g3[kk][j];
     if (own)
       for (int j = 0; j < 6; j++) S.g[T->limb_own[L][0]][j] = gown[j];
+    if constexpr (FORCES) {
+#pragma unroll
+      for (int kk = 0; kk < 3; kk++)
+        for (int j = 0; j < 3; j++) S.p[T->limb_node[L][kk]][j] = Pc[kk][j];
+      if (own)
+        for (int j = 0; j < 3; j++) S.p[T->limb_own[L][0]][j] = Pown[j];
+    }
   } else if (tlane) {
     for (int j = 0; j < 6; j++) S.g[0][j] = g0[j];
   }
@@ -549,6 +691,10 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   wave_sync();  // S.a before the Schur system reads it
 
   STAMP(5);
+  if constexpr (FORCES) {
+    limb_forces<NM>(T, a, mp, S, limb, l, L, gbase, nl, live, b, fstep, s_glob, o, Jp, Jz, Pc, fp, xt, bad, big);
+    return;
+  }
   // ---- contact list in foot order (ftsolver's contact columns) ----
   const int fiL = T->link[L][2].foot;
   const uint32_t cm = grp_or((limb && contact) ? 1u << fiL : 0u);

@@ -177,6 +177,59 @@ def test_limb_kernel_mixed_plan(gpu, hmodels, B, K, Hc, dtype):
         assert err.max() < 1e-3
 
 
+@pytest.mark.parametrize("name,B,K,Hc,curved,straight_legs", [("hexapod", 4096, 20, 1, False, False),
+                                                               ("spider", 1003, 4, 5, True, False),
+                                                               ("myant", 640, 20, 1, False, False),
+                                                               ("hexapod", 512, 10, 1, False, True)])
+def test_limb_kernel_forces_bitwise(gpu, hmodels, name, B, K, Hc, curved, straight_legs):
+    """solve_forces (hs_run_forces_calls, bench.py --forces' shape first) through the limb-lane kernel's
+    forces mode against hs_rollout_kernel's: flags bitwise, contact forces within 1e-12 * max(1, |f|) (not
+    bitwise: hs_rollout_kernel's forces instantiation rounds the particular solution's torque rows x
+    differently from its control instantiation -- FMA contraction follows the LDS layout, SolveXY there,
+    PostL here -- by up to 1.8e-15, tools/limb_dbg.py FORCES=1 40-43; the limb-lane kernel computes the
+    control instantiation's x, bitwise), the steps whose foot block is near singular (straight legs: the
+    dense normal equations) deferred to the forces fixup"""
+    import torch
+    from hslabs_amd import synth
+
+    m = hmodels[name]
+    p = synth.gen_params(B, name, id0=11, curved=curved)
+    if straight_legs:  # long steps and a high torso: legs stretched to the IK's reach
+        p["step_length"] *= 2.5
+    ctl = gpu.DeviceBatch(m, p, n_t=20, k0=0, horizon=K * Hc, outputs=("tau",))
+    ctl.run_calls(K, call_horizon=Hc)
+    i = torch.arange(K * Hc, device=ctl.tau.device)[None, :, None]
+    j = torch.arange(m.nmj, device=ctl.tau.device)[None, None, :]
+    tau = ctl.tau + 0.2 * torch.sin(0.7 * i + 1.3 * j)
+
+    def go(limb):
+        old = os.environ.get("HS_LIMB")
+        os.environ["HS_LIMB"] = "1" if limb else "0"
+        try:
+            fb = gpu.DeviceBatch(m, p, n_t=20, k0=0, horizon=K * Hc, outputs=("cf", "flags"))
+            fb.cf.fill_(float("nan"))
+            fb.forces_launcher(tau, K, call_horizon=Hc)()
+            torch.cuda.synchronize()
+            return fb.cf.cpu().numpy(), fb.flags.cpu().numpy()
+        finally:
+            if old is None:
+                os.environ.pop("HS_LIMB")
+            else:
+                os.environ["HS_LIMB"] = old
+
+    n0, d0 = gpu.api.limb_launches(), gpu.api.limb_deferred()
+    ca, fa = go(True)
+    n1, d1 = gpu.api.limb_launches(), gpu.api.limb_deferred()
+    cb, fb_ = go(False)
+    assert n1 > n0
+    print(f"forces {name}: {d1 - d0} of {B * K * Hc} steps deferred to the forces fixup")
+    assert np.array_equal(fa, fb_), f"flags differ on {int((fa != fb_).sum())} steps"
+    assert np.isfinite(ca).all()
+    err = np.abs(ca - cb) / np.maximum(1.0, np.abs(cb))
+    print(f"forces {name}: {int((ca != cb).sum())} of {ca.size} entries differ, max relative {err.max():.2e}")
+    assert err.max() < 1e-12
+
+
 @pytest.mark.parametrize("name,K,Hc,k0,acc", [("hexapod", 20, 1, 0, True), ("hexapod", 6, 4, 17, True),
                                                ("myant", 9, 1, 3, False), ("spider", 1, 20, 0, True)])
 def test_limb_kernel_online_calls(gpu, hmodels, name, K, Hc, k0, acc):

@@ -14,7 +14,10 @@ NAMES = {1: "P0[0] link pos", 2: "f[0] link force", 3: "g torque[0]", 4: "x torq
          6: "D_c[0]", 7: "g_c[0]", 8: "y[0]", 9: "Um[0] link ust t-2dt", 10: "amr[0] link", 11: "Up[0] link ust t+2dt",
          12: "Pm[0] link pos t-2dt", 13: "f[1]", 14: "f[2] (gravity added)", 15: "o[0], o[1] (slots 31, 30)", 16: "amr[1]", 17: "d[0] = Jp - o (subtree stage)", 18: "F[0] subtree force",
          19: "nc=1 M[4]", 20: "nc=1 b[1] before solve", 21: "nc=1 y[0]", 22: "nc=2 y[0]", 23: "nc=2 b[0] (after solve)",
-         24: "nc=2 t", 25: "foot fp[2]", 26: "nc=2 nv[2]", 27: "nc=2 M[5]"}
+         24: "nc=2 t", 25: "foot fp[2]", 26: "nc=2 nv[2]", 27: "nc=2 M[5]",
+         30: "forces ts[3]", 31: "forces S_l[0]", 32: "forces K_f[0]", 33: "forces K[0]", 34: "forces lam[0]",
+         35: "forces y_f[0]", 36: "forces Ct[0]", 37: "forces r_f[0]", 38: "forces e_l[0]",
+         40: "forces t0 = jz.x (motor 0)", 41: "forces z (motor 0)", 42: "forces X[0][0]", 43: "forces Z[0][0]"}
 
 
 def child(n):
@@ -30,11 +33,21 @@ def child(n):
     B, K = 256, 20
     p = synth.gen_params(B, model, id0=4321)
     out = []
+    forces = os.environ.get("FORCES") == "1"  # solve_forces (hs_run_forces_calls) instead of the control step
+    if forces:
+        ctl = H.DeviceBatch(m, p, n_t=20, k0=0, horizon=K, outputs=("tau",))
+        ctl.run_calls(K, call_horizon=1)
+        tau_in = ctl.tau + 0.1
     for limb in ("1", "0"):
         os.environ["HS_LIMB"] = limb
-        b = H.DeviceBatch(m, p, n_t=20, k0=0, horizon=K, outputs=("tau", "cf", "flags", "work_cot"))
-        b.work_cot.zero_()
-        b.run_calls(K, call_horizon=1, best=False, accumulate=True)
+        if forces:
+            b = H.DeviceBatch(m, p, n_t=20, k0=0, horizon=K, outputs=("cf", "flags"))
+            b.forces_launcher(tau_in, K)()
+            b.tau = b.cf
+        else:
+            b = H.DeviceBatch(m, p, n_t=20, k0=0, horizon=K, outputs=("tau", "cf", "flags", "work_cot"))
+            b.work_cot.zero_()
+            b.run_calls(K, call_horizon=1, best=False, accumulate=True)
         torch.cuda.synchronize()
         buf = np.zeros(B * K * 32)
         capi.check(L.hs_debug_read_dbg(buf.ctypes.data, buf.size), "read")

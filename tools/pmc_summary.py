@@ -21,7 +21,7 @@ from collections import defaultdict
 KERNEL = "the fused step launch"
 # the fused step launch: the limb-lane kernel (round 6: 8 rollouts per wavefront) or hs_rollout_kernel's
 # FIX_DEFER instantiation (2 per wavefront)
-STEP_LAUNCH = re.compile(r"hs_limb_kernel<\d+>|hs_rollout_kernel<\d+, false, 1>")
+STEP_LAUNCH = re.compile(r"hs_limb_kernel<\d+, false>|hs_rollout_kernel<\d+, false, 1>")
 FORCES_LAUNCH = re.compile(r"hs_rollout_kernel<\d+, true, 0>")  # solve_forces' step launches (--forces)
 
 
