@@ -185,6 +185,22 @@ def _oracle_gaits(O, arr):
                          foot_shift=float(r["foot_shift"])) for r in arr]
 
 
+def step_kernel(models, fused=True, fp32=False, forces=False):
+    """the step launch's kernel for this workload, as the native library routes it (hs_capi.cpp
+    limb_eligible, hs_run_steps, hs_run_forces_calls): the limb-lane kernel for the models of its class"""
+    env = os.environ
+    limb = env.get("HS_LIMB", "1") != "0" and all(m.limb_lane_ok for m in models)
+    if fp32:
+        limb = limb and env.get("HS_LIMB_F32", "1") != "0" and not forces
+    if not fused:
+        limb = limb and env.get("HS_LIMB_ONLINE") == "1"
+    if forces:
+        return "hs_limb_kernel<NM, true>" if limb else "hs_rollout_kernel<NM, true, 0>"
+    if limb:
+        return "hs_limb_kernel<NM, false>"
+    return "hs_rollout_kernel<NM, false, 1>" if fused else "hs_rollout_kernel<NM, false, 0>"
+
+
 def cpu_baseline(model_names, n_t, horizon, seconds, threads=None):
     """Oracle (CPU restatement, tree basis: the reference's FullPivLU / ColPivQR rank loop on the
     tree-built null basis) on a bounded sample, model_names = one model or a mixed batch's models in
@@ -432,7 +448,7 @@ def main_forces(args, torch, dist, world, rank, dev):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_over_algorithmic": None if traffic is None else round(traffic / alg_bytes, 3),
-                         "traffic_note": pmc_note, "kernel": "hs_rollout_kernel<NM, true, 0>",
+                         "traffic_note": pmc_note, "kernel": step_kernel([model], forces=True),
                          "kernel_ms": round(kern_ms, 5), "alg_bytes_per_launch": alg_bytes,
                          "alg_bytes_per_step": step_bytes},
             "check": {"max_rel_cf_vs_control_loop": err, "general_steps": general},
@@ -626,6 +642,7 @@ def main():
     else:
         model_names = [args.model]
         model = H.KinematicModel(os.path.join(ROOT, "models", f"{args.model}.xml"))
+        models = [model]
         params = synth.gen_params(B, args.model, id0=id0, curved=args.curved)
         batch = H.DeviceBatch(model, params, n_t=n_t, k0=0, horizon=rows, outputs=outs, device=dev,
                               rollout_id_base=id0, dtype=dtype)
@@ -754,7 +771,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_over_algorithmic": None if traffic is None else round(traffic / alg_bytes, 3),
                          "traffic_note": pmc_note,
-                         "kernel": "hs_rollout_kernel (+ the preparation pass (setup and IK table) and the work reduce, one step of the batch)",
+                         "kernel": step_kernel(models, fused, args.fp32) + " (+ the preparation pass (setup and IK table) "
+                                   "and the fixup + work reduce; kernel_ms: the call's event-timed GPU time per step of the batch)",
                          "kernel_ms": round(kern_ms, 5), "alg_bytes_per_launch": alg_bytes},
             # the bound that binds: FP64 VALU issue/latency
             "fp64_valu": fp64,

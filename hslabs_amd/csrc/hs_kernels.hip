@@ -3476,38 +3476,30 @@ __global__ __launch_bounds__(WAVE, FORCES ? HS_MIN_WAVES_FORCES
   if constexpr (MODE == hs::FIX_SOLVE) {  // the deferred (step, rollout) items
     const int n = *mp.fix_count;           // written by the previous launch on this stream
     if (mp.fix_reduce) {  // workgroup w: the work reduce of rollouts 64 w .. 64 w + 63 after the items
-      if (mp.fix_barrier && n > 0) {
-        // the items over every workgroup (a rollout whose legs stay straight defers many of its steps: one
-        // workgroup fixing them in turn ran 200 us, configs[4]), then a grid barrier: the launch's
-        // ceil(B / 64) <= 1024 one-wavefront workgroups are resident together (the host passes no barrier
-        // otherwise); n is the same for all, so every workgroup arrives
-        for (int it = blockIdx.x; it < n; it += gridDim.x) {
-          const int fstep = mp.fix_items[2 * it], ws = mp.fix_items[2 * it + 1];
-          rollout_wave<NM, FORCES, false>(T0, a, rws, mp, smem, fstep, ws >> 1, ws & 1);
-          wave_sync();
-        }
-        __threadfence();  // the fixed steps' rows and work terms, before this workgroup's arrival
-        if (threadIdx.x == 0) {
-          atomicAdd(mp.fix_barrier, 1);
-          // bounded (~2^24 polls): a barrier that never fills ends the wait instead of hanging the device
-          for (int spin = 0; spin < (1 << 24); spin++) {
-            if (__hip_atomic_load(mp.fix_barrier, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= (int)gridDim.x) break;
-            __builtin_amdgcn_s_sleep(2);
-          }
-        }
-        __syncthreads();
-        __threadfence();
-      } else {
-        for (int it = 0; it < n; it++) {
-          const int fstep = mp.fix_items[2 * it], ws = mp.fix_items[2 * it + 1];
-          const int rb = mp.wave_rollouts ? mp.wave_rollouts[ws] : ws;
-          if (rb / WAVE != (int)blockIdx.x) continue;
-          rollout_wave<NM, FORCES, false>(T0, a, rws, mp, smem, fstep, ws >> 1, ws & 1);
-          wave_sync();
-        }
-        if (n > 0) __threadfence();  // the fixed steps' work terms, read back by the other lanes
-        __syncthreads();
+      // fix_barrier: the items over every workgroup (a rollout whose legs stay straight defers many of its
+      // steps: one workgroup fixing them in turn ran 200 us, configs[4]), then a grid barrier: the launch's
+      // ceil(B / 64) <= 1024 one-wavefront workgroups are resident together (the host passes no barrier
+      // otherwise); n is the same for all, so every workgroup arrives. Otherwise each workgroup fixes its
+      // own rollouts' items in turn. (One call site of the step: a second inlined copy doubled the code.)
+      const bool spread = mp.fix_barrier != nullptr;
+      for (int it = spread ? (int)blockIdx.x : 0; it < n; it += spread ? (int)gridDim.x : 1) {
+        const int fstep = mp.fix_items[2 * it], ws = mp.fix_items[2 * it + 1];
+        const int rb = mp.wave_rollouts ? mp.wave_rollouts[ws] : ws;
+        if (!spread && rb / WAVE != (int)blockIdx.x) continue;
+        rollout_wave<NM, FORCES, false>(T0, a, rws, mp, smem, fstep, ws >> 1, ws & 1);
+        wave_sync();
       }
+      if (n > 0) __threadfence();  // the fixed steps' rows and work terms, before this workgroup's arrival
+      if (spread && n > 0 && threadIdx.x == 0) {
+        atomicAdd(mp.fix_barrier, 1);
+        // bounded (~2^24 polls): a barrier that never fills ends the wait instead of hanging the device
+        for (int spin = 0; spin < (1 << 24); spin++) {
+          if (__hip_atomic_load(mp.fix_barrier, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= (int)gridDim.x) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      __syncthreads();
+      if (spread && n > 0) __threadfence();
       reduce_rollouts(a, (real)mp.red_total_mass, mp.red_rollout_mass, reinterpret_cast<const real*>(mp.fused_work),
                       mp.red_n_steps, mp.red_best_key, mp.red_key_steps);
       return;

@@ -35,6 +35,15 @@
 #ifndef HS_LIMB_LINK_BARRIER
 #define HS_LIMB_LINK_BARRIER 0  // 1: within noise at the driver command, 3 % slower at K = 200 (r06_t5)
 #endif
+#ifndef HS_LIMB_PAD
+#define HS_LIMB_PAD 1
+#endif
+#ifndef HS_LIMB_NEAR_DEFER
+#define HS_LIMB_NEAR_DEFER 0
+#endif
+#ifndef HS_LIMB_MIXED_T
+#define HS_LIMB_MIXED_T 1
+#endif
 #ifndef HS_LIMB_WAVES
 #define HS_LIMB_WAVES 2  // waves per SIMD the limb kernel is built for
 #endif
@@ -46,12 +55,12 @@ constexpr int LGR = WAVE / LG;  // rollouts per wavefront
 // deferred step, rare)
 __device__ unsigned long long g_limb_deferred;
 
-template <int NM>
+template <int NM, bool FORCES = false>
 struct LimbLds {
   real g[NM][6];     // per part g_i = (f_i, t_i + (P_i - p0) x f_i); a root kid's slot then its subtree sums
   real a[6];         // the root's x (torso force, torque): the zeroth-order right-hand side
   real wd[HS_NMAX];  // the motors' positive work of the step, in joint order
-  real p[NM][3];     // forces mode: the parts' positions at the centre sample (forces_solve's s, Q sums)
+  real p[FORCES ? NM : 1][3];  // forces mode: the parts' positions at the centre sample (forces_solve's s, Q sums)
 };
 
 // a value of lane `src` of this lane's group (ds_bpermute)
@@ -276,7 +285,7 @@ __device__ __attribute__((always_inline)) inline void contact_block(const real (
 // limb's foot forces on its lane
 template <int NM>
 __device__ __attribute__((always_inline)) inline void limb_forces(const hs_topo* T, const hs_run_args& a,
-                                                                  const hs::launch_map& mp, LimbLds<NM>& S, bool limb,
+                                                                  const hs::launch_map& mp, LimbLds<NM, true>& S, bool limb,
                                                                   int l, int L, int gbase, int nl, bool live, int b,
                                                                   int fstep, int s_glob, const real* o,
                                                                   const real (&Jp)[3][3], const real (&Jz)[3][3],
@@ -410,12 +419,16 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       real outer[36][LGR * HS_LMAX];  // [Pm, Um, Pp, Up][link][component][limb lane]: one conflict-free row per value
       hs_link links[HS_LMAX][3];
     } k;
-    LimbLds<NM> g[LGR];
+    LimbLds<NM, FORCES> g[LGR];
   } sh;
-  LimbLds<NM>* lds = sh.g;
+  LimbLds<NM, FORCES>* lds = sh.g;
   int fstep = 0, q = (int)blockIdx.x;
   fused_coords((int)blockIdx.x, mp.fused_w, mp.fused_n, fstep, q);
+#if HS_LIMB_MIXED_T
   const hs_topo* __restrict__ T = mp.limb_model ? T0 + mp.limb_model[q] : T0;  // a mixed plan's wavefront model
+#else
+  const hs_topo* __restrict__ T = T0;
+#endif
   {  // the link records, 8 bytes per lane and load
     const uint64_t* src = reinterpret_cast<const uint64_t*>(&T->link[0][0]);
     uint64_t* dst = reinterpret_cast<uint64_t*>(&sh.k.links[0][0]);
@@ -430,7 +443,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   const bool live = b >= 0 && b < a.n_rollouts;
   // an idle group computes a copy of a rollout of its wavefront's model and stores nothing
   const int bb = live ? b : (mp.limb_rollouts ? mp.limb_rollouts[q * LGR] : a.n_rollouts - 1);
-  LimbLds<NM>& S = lds[grp];
+  LimbLds<NM, FORCES>& S = lds[grp];
   const int ol = grp * HS_LMAX + (l < HS_LMAX ? l : 0);  // this limb lane's column of sh.k.outer
   const int s_glob = mp.fused_s0 + fstep, call = s_glob / mp.fused_h;
   const int k0 = (int)(((int64_t)a.k0 + (int64_t)call * mp.fused_h) % a.n_t) + s_glob % mp.fused_h;
@@ -952,6 +965,9 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
     }
   }
   STAMP(8);
+#if HS_LIMB_NEAR_DEFER
+  defer |= nearf;
+#endif
   if (defer) {  // the whole step to the fixup launch (hs_rollout_kernel FIX_SOLVE)
     if (l == 0 && live) {
       atomicAdd(&g_limb_deferred, 1ull);  // hs_limb_stats
@@ -999,7 +1015,9 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
         outp(a.cf)[orow * mp.st_cf + 3 * fiL + j] = zv;
       }
   }
-  if (live) {  // a mixed plan's rows past this model's joints and feet (hs_rollout_kernel writes them 0)
+  // a mixed plan's rows past this model's joints and feet (hs_rollout_kernel writes them 0; a single model's
+  // rows have none: the loops' code is kept off its path, ~1 % at K = 200, r06_t17)
+  if (HS_LIMB_PAD && live && mp.limb_rollouts) {
     if (a.tau)
       for (int c = nmj + l; c < mp.st_tau; c += LG) outp(a.tau)[orow * mp.st_tau + c] = real(0);
     if (a.cf)

@@ -22,7 +22,7 @@ KERNEL = "the fused step launch"
 # the fused step launch: the limb-lane kernel (round 6: 8 rollouts per wavefront) or hs_rollout_kernel's
 # FIX_DEFER instantiation (2 per wavefront)
 STEP_LAUNCH = re.compile(r"hs_limb_kernel<\d+, false>|hs_rollout_kernel<\d+, false, 1>")
-FORCES_LAUNCH = re.compile(r"hs_rollout_kernel<\d+, true, 0>")  # solve_forces' step launches (--forces)
+FORCES_LAUNCH = re.compile(r"hs_limb_kernel<\d+, true>|hs_rollout_kernel<\d+, true, 0>")  # solve_forces' step launches (--forces)
 
 
 def collect(root, n_rollouts, step_launch=STEP_LAUNCH):
