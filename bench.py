@@ -480,6 +480,8 @@ def pmc_for(traffic_key, lib_sha, name="pmc_traffic.json"):
     (tools/gpu_pmc.sh + tools/pmc_summary.py), only when it was taken on the library this process
     loaded (same sha256 prefix); else None and the reason."""
     j = _profile_json(name)
+    if j and "workloads" in j:  # one summary per workload (configs[1], [2], [4]), each keyed to its library
+        j = j["workloads"].get(traffic_key)
     if not j or j.get("workload") != traffic_key:
         return None, "no PMC summary for this workload"
     if j.get("lib_sha256") != lib_sha:

@@ -85,8 +85,11 @@ def main():
     ap.add_argument("--cmd", default="bench.py --steps 20 --warmup 5 --no-cpu")
     ap.add_argument("--forces", action="store_true", help="solve_forces' step launches (bench.py --forces)")
     ap.add_argument("--job-steps", type=int, default=20, help="steps per job: the per-job kernels' share")
+    ap.add_argument("--rows-per-step", type=int, default=1,
+                    help="output rows (fused steps) per bench step: the call horizon H (configs[2]: 32)")
     a = ap.parse_args()
     v = collect(a.root, a.rollouts, FORCES_LAUNCH if a.forces else STEP_LAUNCH)
+    v = {c: [x * a.rows_per_step for x in xs] for c, xs in v.items()}  # per bench step (H rows)
     med = {c: statistics.median(x) for c, x in v.items()}
     sha = lib_of(a.root)
     lines = [f"{KERNEL}, {a.workload} ({a.cmd}), rocprofv3 --pmc, one group per pass, library {sha}",
@@ -133,11 +136,19 @@ def main():
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
     if a.traffic_json and traffic is not None:
+        # one entry per workload (bench.py pmc_for looks its own up), merged into the file's others
+        try:
+            j = json.load(open(a.traffic_json))
+        except (OSError, ValueError):
+            j = {}
+        if "workloads" not in j:
+            j = {"workloads": {j["workload"]: j} if j.get("workload") else {}}
+        j["workloads"][a.workload] = {
+            "workload": a.workload, "rollouts": a.rollouts, "lib_sha256": sha,
+            "hbm_bytes_per_step": traffic, "fp64_lane_flops_per_step": fp64,
+            "source": f"{a.out} (FETCH_SIZE x2 + WRITE_SIZE per step of the batch; FP64 instruction counts; {a.cmd})"}
         with open(a.traffic_json, "w") as f:
-            json.dump({"workload": a.workload, "rollouts": a.rollouts, "lib_sha256": sha,
-                       "hbm_bytes_per_step": traffic, "fp64_lane_flops_per_step": fp64,
-                       "source": f"{a.out} (FETCH_SIZE x2 + WRITE_SIZE per step of the batch; FP64 instruction "
-                                 f"counts; {a.cmd})"}, f, indent=1)
+            json.dump(j, f, indent=1)
             f.write("\n")
 
 
