@@ -2865,16 +2865,16 @@ __device__ __attribute__((always_inline)) inline uint32_t forces_solve(const hs_
       }
       zz[k] = z[T->node[p[k]].hinge];
     }
-    real dbgv[4] = {0, 0, 0, 0};
-    okB = forces_limb_block(J, Z, P, w.fpos(0, f), P0, X, zz, fr.a[L], fr.b[L], Ct, Bd, Bl, rdB, rb
 #ifdef HS_DBG
-                            , dbgv
-#endif
-    );
+    real dbgv[4] = {0, 0, 0, 0};
+    okB = forces_limb_block(J, Z, P, w.fpos(0, f), P0, X, zz, fr.a[L], fr.b[L], Ct, Bd, Bl, rdB, rb, dbgv);
     DBG(24 + f, dbgv[0], 40);
     DBG(24 + f, dbgv[1], 41);
     DBG(24 + f, dbgv[2], 42);
     DBG(24 + f, dbgv[3], 43);
+#else
+    okB = forces_limb_block(J, Z, P, w.fpos(0, f), P0, X, zz, fr.a[L], fr.b[L], Ct, Bd, Bl, rdB, rb);
+#endif
     DBG(24 + f, fr.a[L][0], 31);
     DBG(24 + f, fr.b[L][0], 32);
     DBG(24 + f, Ct[0], 36);

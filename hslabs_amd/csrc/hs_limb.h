@@ -327,16 +327,16 @@ __device__ __attribute__((always_inline)) inline void limb_forces(const hs_topo*
     const real* z = inp(mp.tau_in) + (live ? orow : 0) * mp.st_tau;
     real zz[3];
     for (int kk = 0; kk < 3; kk++) zz[kk] = z[T->node[T->limb_node[L][kk]].hinge];
-    real dbgv[4] = {0, 0, 0, 0};
-    okB = forces_limb_block(Jp, Jz, Pc, fp, o, xt, zz, fa, fb, Ct, Bd, Bl, rdB, rb
 #ifdef HS_DBG
-                            , dbgv
-#endif
-    );
+    real dbgv[4] = {0, 0, 0, 0};
+    okB = forces_limb_block(Jp, Jz, Pc, fp, o, xt, zz, fa, fb, Ct, Bd, Bl, rdB, rb, dbgv);
     FDBG(24 + dbg_f, dbgv[0], 40);
     FDBG(24 + dbg_f, dbgv[1], 41);
     FDBG(24 + dbg_f, dbgv[2], 42);
     FDBG(24 + dbg_f, dbgv[3], 43);
+#else
+    okB = forces_limb_block(Jp, Jz, Pc, fp, o, xt, zz, fa, fb, Ct, Bd, Bl, rdB, rb);
+#endif
     FDBG(24 + dbg_f, fa[0], 31);
     FDBG(24 + dbg_f, fb[0], 32);
     FDBG(24 + dbg_f, Ct[0], 36);
