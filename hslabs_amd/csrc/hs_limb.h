@@ -41,6 +41,9 @@
 #ifndef HS_LIMB_NEAR_DEFER
 #define HS_LIMB_NEAR_DEFER 0
 #endif
+#ifndef HS_LIMB_EARLY_LOADS
+#define HS_LIMB_EARLY_LOADS 0
+#endif
 #ifndef HS_LIMB_MIXED_T
 #define HS_LIMB_MIXED_T 1
 #endif
@@ -429,6 +432,50 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
 #else
   const hs_topo* __restrict__ T = T0;
 #endif
+#if HS_LIMB_EARLY_LOADS
+  // the rollout's first loads (its records, sample times, torso) issued before the link records' copy and
+  // its barrier, so their latency overlaps the copy
+  RSTAMP(16);
+  STAMP(15);
+  const int lane = (int)threadIdx.x, grp = lane >> 3, l = lane & 7, gbase = lane & ~7;
+  const int b = mp.limb_rollouts ? mp.limb_rollouts[q * LGR + grp] : q * LGR + grp;
+  const bool live = b >= 0 && b < a.n_rollouts;
+  // an idle group computes a copy of a rollout of its wavefront's model and stores nothing
+  const int bb = live ? b : (mp.limb_rollouts ? mp.limb_rollouts[q * LGR] : a.n_rollouts - 1);
+  LimbLds<NM, FORCES>& S = lds[grp];
+  const int ol = grp * HS_LMAX + (l < HS_LMAX ? l : 0);  // this limb lane's column of sh.k.outer
+  const int s_glob = mp.fused_s0 + fstep, call = s_glob / mp.fused_h;
+  const int k0 = (int)(((int64_t)a.k0 + (int64_t)call * mp.fused_h) % a.n_t) + s_glob % mp.fused_h;
+  const int row0 = k0 - mp.ktab_lo;  // table row of sample i - 2 (centre i = k0 + 2)
+  const int nl = T->n_limbs, nmj = T->nmj;
+  const bool limb = l < nl, tlane = l == LG - 1;
+  const int L = limb ? l : 0;
+  const RolloutWS& W = rws[bb];
+  const hs_gait_params& gp = a.params[bb];
+  const bool straight = (real)gp.curvature == 0 && !gp.rec_transform_flag;
+  const real dt = W.st.dt;
+  const real v = W.st.v;
+  const NodeK n0 = load_nodek(T, 0);
+  const real u[3] = {n0.Jp(0, 0), n0.Jp(1, 0), n0.Jp(2, 0)};
+  real tv[5];
+#pragma unroll
+  for (int k = 0; k < 5; k += 2) tv[k] = W.t_tab[row0 + k] * v;  // gait_record's torso advance
+  // the torso COM at the centre sample (particular_sub's origin o = pos(0, 0)), on every lane
+  real o[3];
+  if (straight) {
+    for (int i = 0; i < 3; i++) o[i] = fma(tv[2], u[i], W.kf.torso[i]);
+  } else {
+    mulp(load34r(W.ktor[row0 + 2] + 6), n0.com, o);
+  }
+  const real inv = real(1) / (2 * dt);
+  {  // the link records, 8 bytes per lane and load
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(&T->link[0][0]);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(&sh.k.links[0][0]);
+    constexpr int NW = sizeof(sh.k.links) / sizeof(uint64_t);
+    for (int e = (int)threadIdx.x; e < NW; e += WAVE) dst[e] = src[e];
+    wave_sync();
+  }
+#else
   {  // the link records, 8 bytes per lane and load
     const uint64_t* src = reinterpret_cast<const uint64_t*>(&T->link[0][0]);
     uint64_t* dst = reinterpret_cast<uint64_t*>(&sh.k.links[0][0]);
@@ -469,6 +516,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
     mulp(load34r(W.ktor[row0 + 2] + 6), n0.com, o);
   }
   const real inv = real(1) / (2 * dt);
+#endif
 #ifdef HS_DBG
   const int dbg_r = live ? b * a.horizon + s_glob : -1;
 #define LDBG(slot, val, n)                                                                                       \
