@@ -588,6 +588,13 @@ int hs_run_steps(hs_model_t m, const hs_run_args* a, int32_t n_calls, void* cons
   if (limb_online_wanted() && limb_eligible(m->host, r) && a->horizon <= HS_ONLINE_MAX_H)
     return run_fused(d, r, ws, hs::single_model_map(m->host, a->n_rollouts), m->fused_gen, m->fused_work,
                      m->fused_fix, m->mu, m->host.total_mass, nullptr, n_calls, true, true, kernel_events);
+  // HS_ONLINE_DEFER=1: the same online shape on hs_rollout_kernel's fused instantiation (FIX_DEFER, 4
+  // waves/SIMD, no general-path call) and its fixup + reduce per call (VERDICT r05 item 4's variant;
+  // measured)
+  const char* od = getenv("HS_ONLINE_DEFER");
+  if (od && od[0] == '1' && r.solve_mode == HS_SOLVE_AUTO && a->horizon <= HS_ONLINE_MAX_H)
+    return run_fused(d, r, ws, hs::single_model_map(m->host, a->n_rollouts), m->fused_gen, m->fused_work,
+                     m->fused_fix, m->mu, m->host.total_mass, nullptr, n_calls, false, true, kernel_events);
   return launch_steps(d, r, ws, hs::single_model_map(m->host, a->n_rollouts), n_calls, kernel_events,
                       m->host.total_mass, nullptr);
 }

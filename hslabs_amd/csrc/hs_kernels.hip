@@ -2725,18 +2725,31 @@ __device__ inline real wtt_entry(int e, const real* ts, int n) {
   return ((a == b) ? real(n) + q[0] + q[1] + q[2] : real(0)) - qab;
 }
 
-// One limb's blocks of forces_solve (lane = limb; hs_limb_kernel's forces mode calls it on its limb lanes):
-// J, Z, P: its three links' joint positions, axes and part positions at the centre sample, fp its foot, P0
-// the torso's position, X the links' x torque rows, zz the motors' torques. fa: S_l (packed lower) and
-// e_l; fb (when B_f factors): K_f and q_f; Ct, Bd, Bl / rdB, rb: C~_f, B_f raw and its LDL^T, r_f.
-__device__ __attribute__((always_inline)) inline bool forces_limb_block(const real (&J)[3][3], const real (&Z)[3][3],
-                                                                        const real (&P)[3][3], const real* fp,
-                                                                        const real* P0, const real (&X)[3][3],
-                                                                        const real* zz, real* fa, real* fb, real* Ct,
-                                                                        real* Bd, real* Bl, real* rdB, real* rb,
-                                                                        real* dbgv = nullptr) {
+// One limb's blocks of forces_solve (lane = limb), in stages both kernels share: the raw rows and M's
+// LDL^T (forces_rows), the foot's C~_f / B_f / r_f (forces_foot), B_f's factor and V = L_B^-1 [C~^T | r_f]
+// (forces_v). J, Z, P: the limb's three links' joint positions, axes and part positions at the centre
+// sample, fp its foot, P0 the torso's position, X the links' x torque rows, zz the motors' torques.
+// After forces_rows, prod(a, b) = (L^-1 R)_a^T D^-1 (L^-1 R)_b: S_l (packed lower) and e_l are prod(r, c)
+// and prod(r, 9); after forces_v, vprod(a, b): K_f and q_f.
+struct ForcesRows {
+  real R[3][10], rdM[3];
+  __device__ real prod(int a, int b) const {
+    return R[0][a] * rdM[0] * R[0][b] + R[1][a] * rdM[1] * R[1][b] + R[2][a] * rdM[2] * R[2][b];
+  }
+};
+struct ForcesV {
+  real V[3][7], rdB[3];
+  __device__ real vprod(int a, int b) const {
+    return V[0][a] * rdB[0] * V[0][b] + V[1][a] * rdB[1] * V[1][b] + V[2][a] * rdB[2] * V[2][b];
+  }
+};
+__device__ __attribute__((always_inline)) inline void forces_rows(ForcesRows& F, const real (&J)[3][3],
+                                                                  const real (&Z)[3][3], const real (&P)[3][3],
+                                                                  const real* fp, const real* P0,
+                                                                  const real (&X)[3][3], const real* zz) {
   // raw rows of motor k: R[k] = (W_mt row (6), C_m row vs foot f (3), d_m (1)); M lower (k' <= k)
-  real R[3][10], M[9];
+  real M[9];
+  auto& R = F.R;
   for (int k = 0; k < 3; k++) {
     for (int c = 0; c < 10; c++) R[k][c] = 0;
     for (int c = 0; c < 3; c++) M[3 * k + c] = (c == k) ? real(1) : real(0);
@@ -2771,25 +2784,17 @@ __device__ __attribute__((always_inline)) inline bool forces_limb_block(const re
     real t0 = 0;
     for (int t = 0; t < 3; t++) t0 += Z[k][t] * X[k][t];
     R[k][9] = zz[k] - t0;
-    if (dbgv && k == 0) { dbgv[0] = t0; dbgv[1] = zz[k]; dbgv[2] = X[k][0]; dbgv[3] = Z[k][0]; }
   }
-  real rdM[3];
-  ldl_n<3>(M, real(0), rdM);  // M >= I
+  ldl_n<3>(M, real(0), F.rdM);  // M >= I
 #pragma unroll
   for (int c = 0; c < 10; c++) {  // Y = L^-1 R
     R[1][c] -= M[3] * R[0][c];
     R[2][c] -= M[6] * R[0][c] + M[7] * R[1][c];
   }
-  auto prod = [&](int a, int b) {  // (L^-1 R)_a^T D^-1 (L^-1 R)_b
-    return R[0][a] * rdM[0] * R[0][b] + R[1][a] * rdM[1] * R[1][b] + R[2][a] * rdM[2] * R[2][b];
-  };
-#pragma unroll
-  for (int e = 0; e < 21; e++) {  // S_l = W_tm M^-1 W_mt (packed lower)
-    const TriWalk<> t(e);
-    fa[e] = prod(t.r, t.c);
-  }
-#pragma unroll
-  for (int r = 0; r < 6; r++) fa[21 + r] = prod(r, 9);  // e_l = W_tm M^-1 d_m
+}
+// C~_f (Ct), B_f raw (Bd) and its LDL^T (Bl / rdB), r_f (rb); returns whether B_f factors
+__device__ __attribute__((always_inline)) inline bool forces_foot(const ForcesRows& F, const real* fp, const real* P0,
+                                                                  real* Ct, real* Bd, real* Bl, real* rdB, real* rb) {
   real d[3];
   for (int t = 0; t < 3; t++) d[t] = fp[t] - P0[t];
 #pragma unroll
@@ -2797,33 +2802,56 @@ __device__ __attribute__((always_inline)) inline bool forces_limb_block(const re
 #pragma unroll
     for (int jj = 0; jj < 3; jj++) {
       const real ct = (r < 3) ? ((r == jj) ? real(1) : real(0)) : cross_e(d, jj, r - 3);
-      Ct[3 * r + jj] = ct - prod(r, 6 + jj);
+      Ct[3 * r + jj] = ct - F.prod(r, 6 + jj);
     }
-  Bd[0] = prod(6, 6); Bd[1] = prod(7, 6); Bd[2] = prod(7, 7);
-  Bd[3] = prod(8, 6); Bd[4] = prod(8, 7); Bd[5] = prod(8, 8);
-  for (int jj = 0; jj < 3; jj++) rb[jj] = prod(6 + jj, 9);
+  Bd[0] = F.prod(6, 6); Bd[1] = F.prod(7, 6); Bd[2] = F.prod(7, 7);
+  Bd[3] = F.prod(8, 6); Bd[4] = F.prod(8, 7); Bd[5] = F.prod(8, 8);
+  for (int jj = 0; jj < 3; jj++) rb[jj] = F.prod(6 + jj, 9);
   Bl[0] = Bd[0]; Bl[3] = Bd[1]; Bl[4] = Bd[2]; Bl[6] = Bd[3]; Bl[7] = Bd[4]; Bl[8] = Bd[5];
-  const bool okB = ldl_n<3>(Bl, kForcesBlockGuard, rdB);
-  if (okB) {  // K_f = C~ B^-1 C~^T, q_f = C~ B^-1 r_f, through V = L_B^-1 [C~^T | r_f]
-    real V[3][7];
-    for (int c = 0; c < 6; c++)
-      for (int k = 0; k < 3; k++) V[k][c] = Ct[3 * c + k];
-    for (int k = 0; k < 3; k++) V[k][6] = rb[k];
+  return ldl_n<3>(Bl, kForcesBlockGuard, rdB);
+}
+// K_f = C~ B^-1 C~^T, q_f = C~ B^-1 r_f, through V = L_B^-1 [C~^T | r_f]
+__device__ __attribute__((always_inline)) inline void forces_v(ForcesV& G, const real* Ct, const real* Bl,
+                                                               const real* rdB, const real* rb) {
+  auto& V = G.V;
+  for (int c = 0; c < 6; c++)
+    for (int k = 0; k < 3; k++) V[k][c] = Ct[3 * c + k];
+  for (int k = 0; k < 3; k++) V[k][6] = rb[k];
 #pragma unroll
-    for (int c = 0; c < 7; c++) {
-      V[1][c] -= Bl[3] * V[0][c];
-      V[2][c] -= Bl[6] * V[0][c] + Bl[7] * V[1][c];
-    }
-    auto vp = [&](int a, int b) {
-      return V[0][a] * rdB[0] * V[0][b] + V[1][a] * rdB[1] * V[1][b] + V[2][a] * rdB[2] * V[2][b];
-    };
+  for (int c = 0; c < 7; c++) {
+    V[1][c] -= Bl[3] * V[0][c];
+    V[2][c] -= Bl[6] * V[0][c] + Bl[7] * V[1][c];
+  }
+  for (int k = 0; k < 3; k++) G.rdB[k] = rdB[k];
+}
+// hs_rollout_kernel's form: S_l / e_l to fa, K_f / q_f to fb (its LDS ForceL rows)
+__device__ __attribute__((always_inline)) inline bool forces_limb_block(const real (&J)[3][3], const real (&Z)[3][3],
+                                                                        const real (&P)[3][3], const real* fp,
+                                                                        const real* P0, const real (&X)[3][3],
+                                                                        const real* zz, real* fa, real* fb, real* Ct,
+                                                                        real* Bd, real* Bl, real* rdB, real* rb,
+                                                                        real* dbgv = nullptr) {
+  ForcesRows F;
+  forces_rows(F, J, Z, P, fp, P0, X, zz);
+  if (dbgv) { dbgv[0] = zz[0] - F.R[0][9]; dbgv[1] = zz[0]; dbgv[2] = X[0][0]; dbgv[3] = Z[0][0]; }
+#pragma unroll
+  for (int e = 0; e < 21; e++) {  // S_l = W_tm M^-1 W_mt (packed lower)
+    const TriWalk<> t(e);
+    fa[e] = F.prod(t.r, t.c);
+  }
+#pragma unroll
+  for (int r = 0; r < 6; r++) fa[21 + r] = F.prod(r, 9);  // e_l = W_tm M^-1 d_m
+  const bool okB = forces_foot(F, fp, P0, Ct, Bd, Bl, rdB, rb);
+  if (okB) {
+    ForcesV G;
+    forces_v(G, Ct, Bl, rdB, rb);
 #pragma unroll
     for (int e = 0; e < 21; e++) {
       const TriWalk<> t(e);
-      fb[e] = vp(t.r, t.c);
+      fb[e] = G.vprod(t.r, t.c);
     }
 #pragma unroll
-    for (int r = 0; r < 6; r++) fb[21 + r] = vp(r, 6);
+    for (int r = 0; r < 6; r++) fb[21 + r] = G.vprod(r, 6);
   }
   return okB;
 }

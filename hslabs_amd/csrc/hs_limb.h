@@ -324,29 +324,33 @@ __device__ __attribute__((always_inline)) inline void limb_forces(const hs_topo*
   (void)dbg_f;
   if (l == 0) FDBG(0, ts[3], 30);
   const size_t orow = (size_t)b * a.horizon + s_glob;
-  real Ct[18], Bd[6], Bl[9], rdB[3], rb[3], fa[27], fb[27];
+  // the limb's blocks (forces_solve's stages), its 27 terms of the sums over the limbs formed as soon as
+  // both factors exist: K_f - S_l (packed lower), q_f + e_l -- forces_solve's fr.b - fr.a / fr.b + fr.a,
+  // each product rounded as its LDS rows hold it (the two 27-entry blocks are never live together)
+  real Ct[18], Bd[6], Bl[9], rdB[3], rb[3], vl[27];
   bool okB = true;
   if (limb) {
     const real* z = inp(mp.tau_in) + (live ? orow : 0) * mp.st_tau;
     real zz[3];
     for (int kk = 0; kk < 3; kk++) zz[kk] = z[T->node[T->limb_node[L][kk]].hinge];
-#ifdef HS_DBG
-    real dbgv[4] = {0, 0, 0, 0};
-    okB = forces_limb_block(Jp, Jz, Pc, fp, o, xt, zz, fa, fb, Ct, Bd, Bl, rdB, rb, dbgv);
-    FDBG(24 + dbg_f, dbgv[0], 40);
-    FDBG(24 + dbg_f, dbgv[1], 41);
-    FDBG(24 + dbg_f, dbgv[2], 42);
-    FDBG(24 + dbg_f, dbgv[3], 43);
-#else
-    okB = forces_limb_block(Jp, Jz, Pc, fp, o, xt, zz, fa, fb, Ct, Bd, Bl, rdB, rb);
-#endif
-    FDBG(24 + dbg_f, fa[0], 31);
-    FDBG(24 + dbg_f, fb[0], 32);
+    ForcesRows F;
+    forces_rows(F, Jp, Jz, Pc, fp, o, xt, zz);
+    okB = forces_foot(F, fp, o, Ct, Bd, Bl, rdB, rb);
     FDBG(24 + dbg_f, Ct[0], 36);
     FDBG(24 + dbg_f, rb[0], 37);
-    FDBG(24 + dbg_f, fa[21], 38);
-    opaque_vals<27>(fa);  // fr.a / fr.b (LDS)
-    if (okB) opaque_vals<27>(fb);
+    if (okB) {
+      ForcesV G;
+      forces_v(G, Ct, Bl, rdB, rb);
+#pragma unroll
+      for (int e = 0; e < 27; e++) {
+        const TriWalk<> t(e < 21 ? e : 0);
+        real pa = e < 21 ? F.prod(t.r, t.c) : F.prod(e - 21, 9);
+        real pb = e < 21 ? G.vprod(t.r, t.c) : G.vprod(e - 21, 6);
+        opaque_vals<1>(&pa);  // fr.a / fr.b (LDS)
+        opaque_vals<1>(&pb);
+        vl[e] = (e < 21) ? pb - pa : pb + pa;
+      }
+    }
   }
   const bool fast = !grp_any(limb && !okB, gbase);
   if (!fast || grp_any(big, gbase)) {  // the dense normal equations: the forces fixup's (forces_solve)
@@ -362,7 +366,7 @@ __device__ __attribute__((always_inline)) inline void limb_forces(const hs_topo*
   real kv[27];
 #pragma unroll
   for (int e = 0; e < 27; e++) {
-    const real v = limb ? ((e < 21) ? fb[e] - fa[e] : fb[e] + fa[e]) : real(0);
+    const real v = limb ? vl[e] : real(0);
     real s = real(0) + v;
     for (int k = 1; k < nl; k++) {
       const real prev = dpp_r<0x111>(s);  // row_shr 1: lane l - 1's partial sum

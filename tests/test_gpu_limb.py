@@ -247,6 +247,26 @@ def test_limb_kernel_online_calls(gpu, hmodels, name, K, Hc, k0, acc):
     same(a, b, f"online {name} K={K} H={Hc}")
 
 
+@pytest.mark.parametrize("K,Hc,acc", [(20, 1, True), (5, 3, False)])
+def test_online_defer_variant_bitwise(gpu, hmodels, K, Hc, acc):
+    """HS_ONLINE_DEFER=1 (hs_run_steps on hs_rollout_kernel's fused FIX_DEFER instantiation, a launch per
+    call and its fixup + reduce): bitwise the default launch per call with the general path inline"""
+    import torch
+    from hslabs_amd import synth
+
+    m = hmodels["hexapod"]
+    p = synth.gen_params(777, "hexapod", id0=3, curved=True)
+
+    def go(defer):
+        os.environ["HS_ONLINE_DEFER"] = "1" if defer else "0"
+        try:
+            return run(gpu, m, p, False, K=K, Hc=Hc, steps=True, accumulate=acc)
+        finally:
+            os.environ.pop("HS_ONLINE_DEFER")
+
+    same(go(True), go(False), f"online defer K={K} H={Hc}")
+
+
 @pytest.mark.parametrize("name,B,K,Hc,curved", [("spider", 16384, 2, 32, False), ("hexapod", 2048, 20, 1, True),
                                                  ("myant", 1024, 20, 1, False)])
 def test_limb_kernel_fp32_close_to_rollout_kernel(gpu, hmodels, name, B, K, Hc, curved):
