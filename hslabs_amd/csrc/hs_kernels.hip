@@ -3476,17 +3476,18 @@ __device__ __attribute__((always_inline)) inline void rollout_wave(const hs_topo
 #ifndef HS_FUSED_GROUP
 #define HS_FUSED_GROUP 256
 #endif
+template <int GROUP = HS_FUSED_GROUP>
 __device__ inline void fused_coords(int blk, int W, int n, int& fstep, int& wid) {
-#if HS_FUSED_GROUP > 0
-  const int q = blk / (HS_FUSED_GROUP * n), g0 = q * HS_FUSED_GROUP;
-  const int gw = W - g0 < HS_FUSED_GROUP ? W - g0 : HS_FUSED_GROUP;  // the last group may be narrower
-  const int r = blk - g0 * n;
-  fstep = r / gw;
-  wid = g0 + r % gw;
-#else
-  fstep = blk / W;
-  wid = blk % W;
-#endif
+  if constexpr (GROUP > 0) {
+    const int q = blk / (GROUP * n), g0 = q * GROUP;
+    const int gw = W - g0 < GROUP ? W - g0 : GROUP;  // the last group may be narrower
+    const int r = blk - g0 * n;
+    fstep = r / gw;
+    wid = g0 + r % gw;
+  } else {
+    fstep = blk / W;
+    wid = blk % W;
+  }
 }
 
 // MODE (hs::FIX_*): NONE, the step with the general path out of line; DEFER, the fused step launch

@@ -41,6 +41,14 @@
 #ifndef HS_LIMB_NEAR_DEFER
 #define HS_LIMB_NEAR_DEFER 0
 #endif
+#ifndef HS_LIMB_GROUP
+// the fused launch's block order for the limb kernel (fused_coords): groups of this many batch wavefronts
+// (8 rollouts each), each group's steps in order
+#define HS_LIMB_GROUP HS_FUSED_GROUP
+#endif
+#ifndef HS_LIMB_NC12
+#define HS_LIMB_NC12 1  // one and two contacts solved here (0: deferred, A/B)
+#endif
 #ifndef HS_LIMB_EARLY_LOADS
 #define HS_LIMB_EARLY_LOADS 0
 #endif
@@ -430,7 +438,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   } sh;
   LimbLds<NM, FORCES>* lds = sh.g;
   int fstep = 0, q = (int)blockIdx.x;
-  fused_coords((int)blockIdx.x, mp.fused_w, mp.fused_n, fstep, q);
+  fused_coords<HS_LIMB_GROUP>((int)blockIdx.x, mp.fused_w, mp.fused_n, fstep, q);
 #if HS_LIMB_MIXED_T
   const hs_topo* __restrict__ T = mp.limb_model ? T0 + mp.limb_model[q] : T0;  // a mixed plan's wavefront model
 #else
@@ -783,7 +791,7 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
   real d0[3] = {0, 0, 0}, Dinv[9], gc[3], Dp6[6];
   if (mine)
     for (int r = 0; r < 3; r++) d0[r] = o[r] - fp[r];  // A_c = [-I; [d0_c]x]
-  if (mine && nc >= 2) contact_block(Jp, Jz, xt, fp, Dp6, gc);
+  if (mine && nc >= (HS_LIMB_NC12 ? 2 : 3)) contact_block(Jp, Jz, xt, fp, Dp6, gc);
 #ifdef HS_LIMB_EXP_NOSOLVE
   defer |= nc >= 3;
   if (false) {
@@ -909,7 +917,12 @@ __global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_t
       opaque_vals<3>(y3);  // sv.y
     }
   }
+#if !HS_LIMB_NC12
+  defer |= nc == 1 || nc == 2;  // (A/B: one and two contacts to the fixup launch)
+  if (false) {
+#else
   if (nc == 1 || nc == 2) {
+#endif
     // fast_solve_lanes' one- and two-contact closed forms (its lane 0, from FastL): here on every lane of
     // the group, the contacts' values gathered from their limb lanes
     int s0 = 0, s1 = 0;
