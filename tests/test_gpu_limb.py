@@ -3,10 +3,12 @@
 hs_run_calls takes the limb-lane kernel for its fused step launches when the model is of its class
 (hs_topo::limb_lane_ok: hexapod, spider, myant), the call solves in HS_SOLVE_AUTO with the IK table and
 asks for no x / q / dq rows; HS_LIMB=0 in the environment keeps hs_rollout_kernel. The limb-lane kernel
-computes every value with the same operations in the same order, and defers to the fixup launch (the
-old kernel's general machinery) every step it does not take -- one or two contacts, tier 2, the
-Eigen-style path, a guard near its threshold -- so the two kernels' outputs are BITWISE equal: torques,
-contact forces, flags, the accumulated work and COT, and the best key. Parity with the oracle then
+computes every value with the same operations in the same order (0 to 6 contacts; a guard near its
+threshold flagged HS_FLAG_NEAR_RANK as the old kernel flags it), and defers to the fixup launch (the
+old kernel's general machinery) every step it does not take -- tier 2, the Eigen-style path, a joint
+value past sincos_k_small's range -- so the two kernels' fp64 outputs are BITWISE equal: torques,
+contact forces, flags, the accumulated work and COT, and the best key (mixed plans included). The fp32
+build and solve_forces' forces mode are held to stated tolerances instead. Parity with the oracle then
 follows from tests/test_gpu_parity.py, which runs the default (limb-lane) path.
 """
 import os
@@ -81,8 +83,8 @@ def test_models_are_of_the_limb_lane_class(gpu, hmodels):
                                             ("myant", False, 1024), ("spider", False, 517)])
 def test_limb_kernel_bitwise_equals_rollout_kernel(gpu, hmodels, name, curved, B):
     """configs[1]'s shape (K = 20 calls of H = 1) and odd batches (idle lanes in the last wavefront):
-    straight and turning gaits (the torso record's frames), myant's one- and two-contact steps (deferred to
-    the fixup launch)"""
+    straight and turning gaits (the torso record's frames), myant's one- and two-contact steps (solved in
+    the limb kernel by fast_solve_lanes' closed forms)"""
     from hslabs_amd import synth
 
     p = synth.gen_params(B, name, id0=4321, curved=curved)
