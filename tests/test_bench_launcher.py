@@ -75,18 +75,24 @@ def test_world_size_mismatch_is_an_error():
 
 
 def test_committed_pmc_summary_is_keyed_to_the_driver_workload():
-    """bench.py attaches the committed PMC traffic (profiles/pmc_traffic.json) only to the workload
-    key it was taken on and only for the library hash it records: the committed summary is the
-    driver's configs[1] run (bench.py --gpus 1 --steps 20 --warmup 5)."""
+    """bench.py attaches the committed PMC traffic (profiles/pmc_traffic.json: one summary per workload)
+    only to the workload key it was taken on and only for the library hash it records: configs[1] (the
+    driver's run, bench.py --gpus 1 --steps 20 --warmup 5), configs[2] and configs[4]."""
     sys.path.insert(0, ROOT)
     import bench
 
-    j = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
-    assert j["workload"] == "hexapod B=4096 H=1"  # bench.py's traffic_key for configs[1]
-    assert len(j["lib_sha256"]) == 16 and j["hbm_bytes_per_step"] > 1_572_864  # >= the algorithmic bytes
-    got, why = bench.pmc_for("hexapod B=4096 H=1", j["lib_sha256"])
-    assert got is not None, why
-    assert bench.pmc_for("hexapod B=4096 H=1", "0" * 16)[0] is None  # another library: refused
+    j = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))["workloads"]
+    # bench.py's traffic keys, with each workload's algorithmic bytes per bench step (SURVEY.md 8d)
+    for key, alg in (("hexapod B=4096 H=1", 1_572_864), ("spider B=16384 H=32 fp32", None),
+                     ("mixed B=4096 H=1 fp64", None)):
+        e = j[key]
+        assert e["workload"] == key and len(e["lib_sha256"]) == 16
+        if alg:
+            assert e["hbm_bytes_per_step"] > alg  # >= the algorithmic bytes
+        got, why = bench.pmc_for(key, e["lib_sha256"])
+        assert got is not None and got["hbm_bytes_per_step"] == e["hbm_bytes_per_step"], why
+        assert bench.pmc_for(key, "0" * 16)[0] is None  # another library: refused
+    assert bench.pmc_for("hexapod B=1 H=1", j["hexapod B=4096 H=1"]["lib_sha256"])[0] is None  # no summary
 
 
 def test_every_bench_mode_times_through_timed_window():
