@@ -58,6 +58,9 @@
 #ifndef HS_LIMB_WAVES
 #define HS_LIMB_WAVES 2  // waves per SIMD the limb kernel is built for
 #endif
+#ifndef HS_LIMB_WAVES_F32
+#define HS_LIMB_WAVES_F32 HS_LIMB_WAVES  // the single-precision build's (140 VGPRs, 10.9 KB: 3 fit)
+#endif
 
 constexpr int LG = 8;           // lanes per rollout group
 constexpr int LGR = WAVE / LG;  // rollouts per wavefront
@@ -422,7 +425,7 @@ __device__ __attribute__((always_inline)) inline void limb_forces(const hs_topo*
 // path: a limb's blocks on its lane, the sums over the limbs in limb order by a DPP chain, the 6 x 6 on
 // every lane of the group; a B_f near singular defers the step to the forces fixup launch)
 template <int NM, bool FORCES>
-__global__ __launch_bounds__(WAVE, HS_LIMB_WAVES) void hs_limb_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
+__global__ __launch_bounds__(WAVE, HS_REAL_IS_FLOAT ? HS_LIMB_WAVES_F32 : HS_LIMB_WAVES) void hs_limb_kernel(const hs_topo* __restrict__ T0, hs_run_args a,
                                                                       RolloutWS* __restrict__ rws, hs::launch_map mp) {
   // the outer samples' pos / ust of every lane's links (kinematics), then the groups' exchange arrays:
   // 18 KB per wavefront, 8 per CU at 2 waves / SIMD
