@@ -3053,7 +3053,10 @@ __device__ __attribute__((always_inline)) inline void forces_step(const hs_topo*
                             SV& sv, ForceL& fr, const W& w, int b, bool live, int h, int lane) {
   const int nf = T->nf, cfg = T->cfg, nl = T->n_limbs, nq = 3 * nf;
   dynamics(T, dt, sv, w, lane);
-  particular(T, sv, w, lane);
+  // the control step's subtree sums (round 6: the level-by-level recursion summed x in another order,
+  // so the forces mode's x differed from the control step's -- and the limb-lane kernel's -- by rounding)
+  particular_sub(T, sv, w, lane);
+  wave_sync();  // particular_sub leaves x unsynchronised across lanes; forces_solve reads it across lanes
   STAMP(10);
   const size_t row = (size_t)b * a.horizon + h;
   const real* z = inp(mp.tau_in) + (live ? row : 0) * mp.st_tau;

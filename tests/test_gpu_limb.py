@@ -229,7 +229,10 @@ def test_limb_kernel_forces_bitwise(gpu, hmodels, name, B, K, Hc, curved, straig
     assert np.isfinite(ca).all()
     err = np.abs(ca - cb) / np.maximum(1.0, np.abs(cb))
     print(f"forces {name}: {int((ca != cb).sum())} of {ca.size} entries differ, max relative {err.max():.2e}")
-    assert err.max() < 1e-12
+    if curved:  # turning gaits: ULP-level differences remain on some steps
+        assert err.max() < 1e-13
+    else:
+        assert np.array_equal(ca, cb), f"forces differ on {int((ca != cb).sum())} entries (max relative {err.max():.2e})"
 
 
 @pytest.mark.parametrize("name,K,Hc,k0,acc", [("hexapod", 20, 1, 0, True), ("hexapod", 6, 4, 17, True),

@@ -31,7 +31,7 @@ def child(n):
     model = os.environ.get("MODEL", "hexapod")
     m = H.KinematicModel(os.path.join(ROOT, "models", f"{model}.xml"))
     B, K = 256, 20
-    p = synth.gen_params(B, model, id0=4321)
+    p = synth.gen_params(B, model, id0=4321, curved=os.environ.get("CURVED") == "1")
     out = []
     forces = os.environ.get("FORCES") == "1"  # solve_forces (hs_run_forces_calls) instead of the control step
     if forces:
