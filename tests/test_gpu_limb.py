@@ -185,12 +185,9 @@ def test_limb_kernel_mixed_plan(gpu, hmodels, B, K, Hc, dtype):
                                                                ("hexapod", 512, 10, 1, False, True)])
 def test_limb_kernel_forces_bitwise(gpu, hmodels, name, B, K, Hc, curved, straight_legs):
     """solve_forces (hs_run_forces_calls, bench.py --forces' shape first) through the limb-lane kernel's
-    forces mode against hs_rollout_kernel's: flags bitwise, contact forces within 1e-12 * max(1, |f|) (not
-    bitwise: hs_rollout_kernel's forces instantiation rounds the particular solution's torque rows x
-    differently from its control instantiation -- FMA contraction follows the LDS layout, SolveXY there,
-    PostL here -- by up to 1.8e-15, tools/limb_dbg.py FORCES=1 40-43; the limb-lane kernel computes the
-    control instantiation's x, bitwise), the steps whose foot block is near singular (straight legs: the
-    dense normal equations) deferred to the forces fixup"""
+    forces mode against hs_rollout_kernel's: flags and contact forces bitwise on straight gaits (both take
+    the control step's subtree sums for x), within 1e-13 relative on turning gaits; the steps whose foot
+    block is near singular (straight legs: the dense normal equations) deferred to the forces fixup"""
     import torch
     from hslabs_amd import synth
 
