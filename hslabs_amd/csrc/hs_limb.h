@@ -41,6 +41,9 @@
 #ifndef HS_LIMB_NEAR_DEFER
 #define HS_LIMB_NEAR_DEFER 0
 #endif
+#ifndef HS_LIMB_KID_LANES
+#define HS_LIMB_KID_LANES 1  // the root's kids' range sums on lanes 0 .. nk - 1 (K = 200 +4 %, r06_t32)
+#endif
 #ifndef HS_LIMB_GROUP
 // the fused launch's block order for the limb kernel (fused_coords): groups of this many batch wavefronts
 // (8 rollouts each), each group's steps in order
@@ -726,6 +729,40 @@ __global__ __launch_bounds__(WAVE, HS_REAL_IS_FLOAT ? HS_LIMB_WAVES_F32 : HS_LIM
       LDBG(T->limb_node[L][kk], d[0], 17);
     }
   }
+#if HS_LIMB_KID_LANES
+  // the root's kids' range sums on lanes 0 .. nk - 1 of the group, in parallel (each range in preorder, as
+  // the torso lane would sum it), into the kid's own slot (ranges are disjoint: no lane reads another's)
+  {
+    const int nk = T->node[0].nkids;
+    if (l < nk && l < HS_CMAX) {
+      const int c = T->node[0].kids[l], sz = T->node[c].size;
+      real Fk[3] = {0, 0, 0}, Vk[3] = {0, 0, 0};
+#pragma unroll
+      for (int r = 0; r < 8; r++)
+        if (r < sz)
+          for (int j = 0; j < 3; j++) { Fk[j] += S.g[c + r][j]; Vk[j] += S.g[c + r][3 + j]; }
+      for (int r = 8; r < sz; r++)
+        for (int j = 0; j < 3; j++) { Fk[j] += S.g[c + r][j]; Vk[j] += S.g[c + r][3 + j]; }
+      for (int j = 0; j < 3; j++) { S.g[c][j] = Fk[j]; S.g[c][3 + j] = Vk[j]; }
+    }
+  }
+  wave_sync();
+  if (tlane) {  // x_0 = (F, V - 0 x F): its own g plus the kids' sums, in kid order
+    real F[3], V[3];
+    for (int j = 0; j < 3; j++) { F[j] = S.g[0][j]; V[j] = S.g[0][3 + j]; }
+    const int nk = T->node[0].nkids;
+    for (int kk = 0; kk < HS_CMAX; kk++) {
+      if (kk >= nk) break;
+      const int c = T->node[0].kids[kk];
+      for (int j = 0; j < 3; j++) { F[j] += S.g[c][j]; V[j] += S.g[c][3 + j]; }
+    }
+    const real d[3] = {0, 0, 0};
+    V[0] -= d[1] * F[2] - d[2] * F[1];
+    V[1] -= d[2] * F[0] - d[0] * F[2];
+    V[2] -= d[0] * F[1] - d[1] * F[0];
+    for (int j = 0; j < 3; j++) { S.a[j] = F[j]; S.a[3 + j] = V[j]; }
+  }
+#else
   if (tlane) {  // x_0 = (F, V - 0 x F)
     real F[3], V[3];
     for (int j = 0; j < 3; j++) { F[j] = S.g[0][j]; V[j] = S.g[0][3 + j]; }
@@ -764,6 +801,7 @@ __global__ __launch_bounds__(WAVE, HS_REAL_IS_FLOAT ? HS_LIMB_WAVES_F32 : HS_LIM
     V[2] -= d[0] * F[1] - d[1] * F[0];
     for (int j = 0; j < 3; j++) { S.a[j] = F[j]; S.a[3 + j] = V[j]; }
   }
+#endif
   wave_sync();  // S.a before the Schur system reads it
 
   STAMP(5);
