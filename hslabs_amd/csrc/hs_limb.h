@@ -41,6 +41,9 @@
 #ifndef HS_LIMB_NEAR_DEFER
 #define HS_LIMB_NEAR_DEFER 0
 #endif
+#ifndef HS_LIMB_WORK_DPP
+#define HS_LIMB_WORK_DPP 0  // the joint-order work sum as a DPP chain across the limb lanes (A/B)
+#endif
 #ifndef HS_LIMB_KID_LANES
 #define HS_LIMB_KID_LANES 1  // the root's kids' range sums on lanes 0 .. nk - 1 (K = 200 +4 %, r06_t32)
 #endif
@@ -1087,6 +1090,8 @@ __global__ __launch_bounds__(WAVE, HS_REAL_IS_FLOAT ? HS_LIMB_WAVES_F32 : HS_LIM
   // ---- S4: motor torques, contact forces, work (step()'s outputs) ----
   const size_t orow = (size_t)b * a.horizon + s_glob;
   bool nan = false;
+  real wl[3] = {0, 0, 0};  // this limb's three work terms, its motors in link order
+  bool lm = true;          // its motors are joints 3 L, 3 L + 1, 3 L + 2 (limb-major joint order)
   if (limb) {
 #pragma unroll
     for (int kk = 0; kk < 3; kk++) {
@@ -1109,6 +1114,8 @@ __global__ __launch_bounds__(WAVE, HS_REAL_IS_FLOAT ? HS_LIMB_WAVES_F32 : HS_LIM
       }
       real dw = tq * jvel[kk];
       S.wd[hh] = (dw > 0) ? dw : 0;
+      wl[kk] = (dw > 0) ? dw : 0;
+      lm &= hh == 3 * L + kk;
       nan |= tq != tq;
       if (live && a.tau) outp(a.tau)[orow * mp.st_tau + hh] = tq;
     }
@@ -1130,6 +1137,21 @@ __global__ __launch_bounds__(WAVE, HS_REAL_IS_FLOAT ? HS_LIMB_WAVES_F32 : HS_LIM
       for (int c = 3 * T->nf + l; c < mp.st_cf; c += LG) outp(a.cf)[orow * mp.st_cf + c] = real(0);
   }
   const bool any_nan = grp_any(nan, gbase), any_bad = grp_any(limb && bad, gbase);
+#if HS_LIMB_WORK_DPP
+  // the joint-order sum work_over_period takes, as a chain across the limb lanes when the joints are
+  // limb-major (lane l adds its three terms, in order, to lane l - 1's partial sum: the same additions in
+  // the same order as the loop over S.wd), else the loop
+  const bool chain = !grp_any(limb && !lm, gbase) && nmj == 3 * nl;
+  real wsum = 0;
+  if (chain) {
+    real sacc = ((real(0) + wl[0]) + wl[1]) + wl[2];
+    for (int k = 1; k < nl; k++) {
+      const real prev = dpp_r<0x111>(sacc);  // row_shr 1: lane l - 1's partial sum
+      if (l >= 1) sacc = ((prev + wl[0]) + wl[1]) + wl[2];
+    }
+    wsum = grp_get(sacc, gbase + nl - 1);
+  }
+#endif
   wave_sync();
   if (l == 0 && live) {
     uint32_t flags = 0;
@@ -1148,6 +1170,10 @@ __global__ __launch_bounds__(WAVE, HS_REAL_IS_FLOAT ? HS_LIMB_WAVES_F32 : HS_LIM
     for (int jj = 0; jj < HS_NMAX; jj++) wdv[jj] = S.wd[jj];  // issued together; only the nmj terms summed
 #pragma unroll
     for (int jj = 0; jj < HS_NMAX; jj++) work_dt = jj < nmj ? work_dt + wdv[jj] : work_dt;
+#elif HS_LIMB_WORK_DPP
+    if (chain) work_dt = wsum;
+    else
+      for (int jj = 0; jj < nmj; jj++) work_dt += S.wd[jj];
 #else
     for (int jj = 0; jj < nmj; jj++) work_dt += S.wd[jj];
 #endif
